@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""bench.py — frames/sec of the MI355X 3DGS rasterizer (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|1]
+
+One step = one full frame through the native pipeline (preprocess -> depth
+sort -> pair emission -> tile sort -> ranges -> blend) on the synthetic scene
+of BASELINE config 2 (1M Gaussians, 1920x1080, seed 2, camera at (0,0,4),
+fovY 50, k = 3), with the scene and the output image resident in HBM.
+
+Multi-GPU (config 4 semantics, launched by torch.distributed.run): one process
+per GPU, each rank renders its own orbit camera (azimuth 45 deg * rank) of the
+replicated scene; frames shard with no data-path collective (weak scaling).
+Finished frames are gathered to rank 0 over RCCL (torch.distributed, backend
+nccl) once after the timed region — the offline-render hand-off — and the
+gather time is reported separately.
+
+Rank 0 prints ONE JSON line (contract in the task statement), including the
+blend kernel's roofline (HIP events around every blend launch inside the timed
+region) and the CPU-oracle baseline (rank 0, N = 1 only, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (n, W, H, seed)
+    1: (10_000, 640, 480, 1),
+    2: (1_000_000, 1920, 1080, 2),
+    3: (5_000_000, 1600, 1063, 3),
+}
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--k", type=float, default=3.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-oracle sample length")
+    ap.add_argument("--scene-dir", default=None)
+    return ap.parse_args()
+
+
+def algorithmic_blend_bytes(ntiles: int, consumed: int, W: int, H: int) -> int:
+    """SURVEY.md 8d blend row: T*8 (tile ranges) + Pc*(8 pair + 48 record) + 12*W*H (image)."""
+    return 8 * ntiles + 56 * consumed + 12 * W * H
+
+
+def cpu_baseline(soa, cam, W, H, k, seconds):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle  # test infrastructure: CPU baseline leg only
+    threads = min(16, os.cpu_count() or 1)
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        _oracle.render(soa, cam, W, H, k, threads=threads)
+        frames += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or frames >= 50:
+            break
+    return {"value": frames / el, "unit": "frames/sec", "cores": threads, "kind": "port",
+            "sample": f"{frames} full frame(s) of the same workload by the C oracle (oracle/gsr_oracle.c, "
+                      f"OpenMP {threads} threads), {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    import torch  # noqa: E402  (before gaussianrenderer_amd: one HIP runtime)
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    import gaussianrenderer_amd as gsr
+
+    n, W, H, seed = CONFIGS[args.config]
+    scene_dir = args.scene_dir or os.path.join(tempfile.gettempdir(), "gsr_bench")
+    os.makedirs(scene_dir, exist_ok=True)
+    ply = os.path.join(scene_dir, f"config{args.config}_n{n}_s{seed}.ply")
+    if local_rank == 0 and not os.path.exists(ply):
+        tmp = ply + f".tmp{os.getpid()}"
+        gsr.write_synthetic_ply(tmp, n, seed)
+        os.replace(tmp, ply)
+    if dist:
+        dist.barrier()
+    scene = gsr.Scene.from_ply(ply)           # the drop-in loader path (misc.cu:13-134)
+    cam = gsr.make_camera(position=(0, 0, 4), fov_y=50, aspect=W / H)
+    if world > 1:
+        gsr.orbit(cam, 45.0 * rank, 0.0)         # config 4: one orbit camera per GPU
+
+    r = gsr.Renderer()
+    out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def frame():
+        r.render(scene, cam, W, H, out.data_ptr(), k=args.k, stream=stream)
+
+    # warmup (+ grow the pair buffer to the high-water mark)
+    for _ in range(max(1, args.warmup)):
+        frame()
+    while r.sync() != 0:
+        frame()
+
+    # untimed diagnostic frame: per-stage breakdown, P and Pc
+    r.set_timing(2)
+    r.set_diagnostics(True)
+    frame()
+    r.sync()
+    stages, _ = r.stage_times()
+    pairs = r.pair_count()
+    consumed = r.blend_records_loaded()
+    r.set_diagnostics(False)
+    tiles_x, tiles_y = r.tile_grid()
+
+    # timed region: K frames, HIP events around every blend launch
+    r.set_timing(1)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frame()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    blend_times, timed_frames = r.stage_times()
+    r.set_timing(0)
+    overflow = r.sync()
+
+    elapsed_t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    gather_ms = None
+    if dist:
+        dist.all_reduce(elapsed_t, op=dist.ReduceOp.MAX)
+        # offline-render hand-off: finished frames to rank 0 over RCCL (xGMI)
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        gl = [torch.empty_like(out) for _ in range(world)] if rank == 0 else None
+        dist.gather(out, gl, dst=0)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - g0) * 1e3
+    max_elapsed = float(elapsed_t.item())
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    ms_per_step = max_elapsed / args.steps * 1e3
+    value = world * args.steps / max_elapsed
+    blend_avg_ms = blend_times["blend"] / max(1, timed_frames)
+    ntiles = tiles_x * tiles_y
+    bytes_blend = algorithmic_blend_bytes(ntiles, consumed, W, H)
+    achieved = bytes_blend / (blend_avg_ms * 1e-3) / 1e9
+    img = out.view(3, H, W)
+    result = {
+        "metric": "frames/sec at 1920x1080, 1M Gaussians (config %d)" % args.config if args.config == 2
+        else f"frames/sec (config {args.config})",
+        "value": round(value, 3),
+        "unit": "frames/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded 3DGS .ply, SURVEY.md 8d)",
+        "config": {"workload": f"config{args.config}: {n} Gaussians, {W}x{H}, k={args.k}, "
+                               f"{'one orbit camera per GPU' if world > 1 else 'camera (0,0,4) fovY 50'}",
+                   "gaussians": n, "width": W, "height": H, "parallelism": f"frames{world}"},
+        "roofline": {"bound": "hbm", "kernel": "k_blend", "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "avg_launch_ms": round(blend_avg_ms, 4),
+                     "algorithmic_bytes": bytes_blend},
+        "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+        "pairs": pairs,
+        "pairs_consumed": consumed,
+        "image_mean": float(img.mean().item()),
+        "overflow_after_timed": overflow,
+    }
+    if gather_ms is not None:
+        result["gather_ms"] = round(gather_ms, 3)
+    if world == 1 and not args.no_cpu_baseline:
+        soa = gsr.read_ply(ply)
+        result["cpu_baseline"] = cpu_baseline(soa, cam, W, H, args.k, args.cpu_seconds)
+    print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,268 @@
+"""gaussianrenderer_amd — MI355X-native 3D Gaussian splatting rasterizer.
+
+Host-side mirror of the reference's interface (wwangg22/GaussianRenderer):
+
+* :func:`loadGaussianCudaFromPly`  — misc.cu:13-134 (device scene block)
+* :func:`preprocessCUDAGaussians`  — render.cu:871-1157 (whole frame, host image)
+* :class:`TilingInformation`       — utils/gaussians.hpp:38-60
+* :func:`make_camera` / :func:`orbit` — scene/camera.cpp
+
+and the native stream-ordered API (:class:`Renderer`) used by the bench.
+Everything that renders runs in libgsr.so (hand-written gfx950 HIP kernels);
+there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_float, c_int, c_int64
+
+import numpy as np
+
+from . import _native
+from ._native import (Camera, GsrError, LAYOUT_AOS, LAYOUT_SCENE_BLOCK, NUM_STAGES, SCENE_NARRAYS,
+                      SPLAT_RECORD_BYTES, STAGES, TILE_PX, check, lib)
+
+__all__ = [
+    "Camera", "GsrError", "Renderer", "Scene", "TilingInformation", "make_camera", "orbit",
+    "loadGaussianCudaFromPly", "preprocessCUDAGaussians", "read_ply", "write_synthetic_ply",
+    "SPLAT_DTYPE", "STAGES", "TILE_PX", "lib",
+]
+
+# gsr_read_splats record (include/gsr.h).
+SPLAT_DTYPE = np.dtype([
+    ("inv_covar", "<f4", 4), ("opacity", "<f4"), ("color", "<f4", 3),
+    ("px_x", "<i4"), ("px_y", "<i4"), ("x_range", "<u4"), ("y_range", "<u4"),
+    ("tile_x_range", "<u4"), ("tile_y_range", "<u4"), ("tile_count", "<u4"), ("depth_key", "<u4"),
+])
+assert SPLAT_DTYPE.itemsize == SPLAT_RECORD_BYTES
+
+
+class TilingInformation:
+    """utils/gaussians.hpp:38-60 — ctor argument order (ny, nx, h, w)."""
+
+    def __init__(self, ny: int, nx: int, h: int, w: int):
+        self.num_tile_y, self.num_tile_x, self.H, self.W = ny, nx, h, w
+        self._strides()
+
+    def _strides(self):
+        self.width_stride = max(1, (self.W + self.num_tile_x - 1) // self.num_tile_x)
+        self.height_stride = max(1, (self.H + self.num_tile_y - 1) // self.num_tile_y)
+
+    def resize(self, h: int, w: int, num_tile_x: int, num_tile_y: int):
+        self.H, self.W, self.num_tile_x, self.num_tile_y = h, w, num_tile_x, num_tile_y
+        self._strides()
+
+
+def make_camera(position=(0.0, 0.0, 4.0), look_at=(0.0, 0.0, 0.0), up=(0.0, 1.0, 0.0), fov_y=50.0,
+                aspect=16.0 / 9.0, near=0.1, far=100.0) -> Camera:
+    """Camera() + setters + updateCameraMatrices() + updateFrustumPlanes() (camera.cpp)."""
+    cam = Camera()
+    L = lib()
+    L.gsr_camera_default(byref(cam))
+    cam.position[:] = [float(v) for v in position]
+    cam.lookAt[:] = [float(v) for v in look_at]
+    cam.w_up[:] = [float(v) for v in up]
+    cam.fovY, cam.aspectRatio, cam.nearClip, cam.farClip = fov_y, aspect, near, far
+    L.gsr_camera_update(byref(cam))
+    L.gsr_camera_update_frustum(byref(cam))
+    return cam
+
+
+def orbit(cam: Camera, azimuth_deg: float, elevation_deg: float = 0.0) -> Camera:
+    """Camera::orbit (camera.cpp:130-158), in place; returns cam."""
+    lib().gsr_camera_orbit(byref(cam), azimuth_deg, elevation_deg)
+    return cam
+
+
+def camera_intrinsics(cam: Camera):
+    fx, fy = c_float(), c_float()
+    lib().gsr_camera_intrinsics(byref(cam), byref(fx), byref(fy))
+    return fx.value, fy.value
+
+
+def read_ply(path: str) -> np.ndarray:
+    """Host PLY parse with the reference loader's semantics -> (38, n) float32 SoA."""
+    L = lib()
+    n = c_int64(-1)
+    check(L.gsr_ply_read_host(path.encode(), None, 0, byref(n)), "gsr_ply_read_host")
+    soa = np.zeros((SCENE_NARRAYS, n.value), dtype=np.float32)
+    check(L.gsr_ply_read_host(path.encode(), soa.ctypes.data, n.value, byref(n)), "gsr_ply_read_host")
+    return soa
+
+
+def write_synthetic_ply(path: str, n: int, seed: int) -> None:
+    """Seeded synthetic 62-property 3DGS PLY."""
+    check(lib().gsr_synth_write_ply(path.encode(), int(n), int(seed)), "gsr_synth_write_ply")
+
+
+class Scene:
+    """A device scene block (one hipMalloc: header + SoA arrays)."""
+
+    def __init__(self, ptr: int, n: int, owned: bool = True):
+        self.ptr, self.n, self.owned = ptr, n, owned
+
+    @classmethod
+    def from_soa(cls, soa: np.ndarray) -> "Scene":
+        soa = np.ascontiguousarray(soa, dtype=np.float32)
+        assert soa.shape[0] == SCENE_NARRAYS
+        ptr = lib().gsr_scene_upload(soa.ctypes.data, soa.shape[1])
+        if not ptr:
+            raise GsrError(-2, "gsr_scene_upload")
+        return cls(ptr, soa.shape[1])
+
+    @classmethod
+    def from_ply(cls, path: str) -> "Scene":
+        ptr, n = loadGaussianCudaFromPly(path)
+        if not ptr:
+            raise GsrError(-3, f"loadGaussianCudaFromPly({path})")
+        return cls(ptr, n)
+
+    def download(self) -> np.ndarray:
+        soa = np.zeros((SCENE_NARRAYS, self.n), dtype=np.float32)
+        check(lib().gsr_scene_download(self.ptr, soa.ctypes.data, self.n), "gsr_scene_download")
+        return soa
+
+    def free(self):
+        if self.ptr and self.owned:
+            lib().gsr_scene_free(self.ptr)
+        self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def loadGaussianCudaFromPly(path: str):
+    """misc.cu:13-134 -> (device pointer or 0, numGaussians)."""
+    n = c_int(0)
+    ptr = lib().gsr_load_ply_device(path.encode(), byref(n))
+    return (ptr or 0), n.value
+
+
+def preprocessCUDAGaussians(d_gaussians: int, num_gaussians: int, cam: Camera, num_tile_y: int, num_tile_x: int,
+                            width_stride: int, height_stride: int, tile_W: int, tile_H: int,
+                            k: float) -> np.ndarray:
+    """render.cu:871-1157 through the drop-in C symbol; returns the host image (3, H, W)."""
+    out = np.zeros((3, tile_H, tile_W), dtype=np.float32)
+    lib().preprocessCUDAGaussians(d_gaussians, out.ctypes.data_as(ctypes.POINTER(c_float)), num_gaussians, cam,
+                                  num_tile_y, num_tile_x, width_stride, height_stride, tile_W, tile_H, k)
+    return out
+
+
+class Renderer:
+    """Persistent render context (stream-ordered, device-resident)."""
+
+    def __init__(self):
+        self.ctx = lib().gsr_create()
+
+    def close(self):
+        if self.ctx:
+            lib().gsr_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reserve(self, n: int, pairs: int):
+        check(lib().gsr_reserve(self.ctx, n, pairs), "gsr_reserve")
+
+    def render(self, scene, cam: Camera, W: int, H: int, out_ptr: int, k: float = 3.0, tiling=None,
+               stream: int = 0, layout: int = LAYOUT_SCENE_BLOCK, n: int | None = None) -> int:
+        """Enqueue one frame into the device buffer out_ptr (3*W*H float32).
+
+        Returns GSR_OK, or GSR_E_OVERFLOW when an earlier frame overflowed the
+        pair buffer (it has been grown; that frame must be re-rendered)."""
+        ptr = scene.ptr if isinstance(scene, Scene) else int(scene)
+        n = scene.n if n is None else n
+        t = tiling or TilingInformation(1, 1, H, W)
+        rc = lib().gsr_render(self.ctx, ptr, layout, n, byref(cam), W, H, t.num_tile_x, t.num_tile_y,
+                              t.width_stride, t.height_stride, k, out_ptr, stream or None)
+        if rc not in (_native.GSR_OK, _native.GSR_E_OVERFLOW):
+            raise GsrError(rc, "gsr_render")
+        return rc
+
+    def preprocess(self, scene, cam: Camera, W: int, H: int, k: float = 3.0, tiling=None, stream: int = 0,
+                   layout: int = LAYOUT_SCENE_BLOCK, n: int | None = None):
+        ptr = scene.ptr if isinstance(scene, Scene) else int(scene)
+        n = scene.n if n is None else n
+        t = tiling or TilingInformation(1, 1, H, W)
+        rc = lib().gsr_preprocess(self.ctx, ptr, layout, n, byref(cam), W, H, t.num_tile_x, t.num_tile_y,
+                                  t.width_stride, t.height_stride, k, stream or None)
+        if rc not in (_native.GSR_OK, _native.GSR_E_OVERFLOW):
+            raise GsrError(rc, "gsr_preprocess")
+
+    def sort(self, stream: int = 0):
+        check(lib().gsr_sort(self.ctx, stream or None), "gsr_sort")
+
+    def blend(self, out_ptr: int, stream: int = 0):
+        check(lib().gsr_blend(self.ctx, out_ptr, stream or None), "gsr_blend")
+
+    def sync(self) -> int:
+        rc = lib().gsr_sync(self.ctx)
+        if rc not in (_native.GSR_OK, _native.GSR_E_OVERFLOW):
+            raise GsrError(rc, "gsr_sync")
+        return rc
+
+    def pair_count(self) -> int:
+        return int(lib().gsr_pair_count(self.ctx))
+
+    def read_splats(self, n: int) -> np.ndarray:
+        out = np.zeros(n, dtype=SPLAT_DTYPE)
+        check(lib().gsr_read_splats(self.ctx, out.ctypes.data, n), "gsr_read_splats")
+        return out
+
+    def read_depth_order(self, n: int) -> np.ndarray:
+        out = np.zeros(n, dtype=np.uint64)
+        check(lib().gsr_read_depth_order(self.ctx, out.ctypes.data, n), "gsr_read_depth_order")
+        return out
+
+    def read_pairs(self) -> np.ndarray:
+        cap = max(self.pair_count(), 0)
+        out = np.zeros(max(cap, 1), dtype=np.uint64)
+        m = lib().gsr_read_pairs(self.ctx, out.ctypes.data, cap)
+        if m < 0:
+            raise GsrError(int(m), "gsr_read_pairs")
+        return out[:m]
+
+    def tile_grid(self):
+        tx, ty = c_int(), c_int()
+        check(lib().gsr_tile_grid(self.ctx, byref(tx), byref(ty)), "gsr_tile_grid")
+        return tx.value, ty.value
+
+    def read_tile_ranges(self) -> np.ndarray:
+        tx, ty = self.tile_grid()
+        out = np.zeros((tx * ty, 2), dtype=np.uint32)
+        check(lib().gsr_read_tile_ranges(self.ctx, out.ctypes.data, tx * ty), "gsr_read_tile_ranges")
+        return out
+
+    def set_timing(self, mode: int):
+        check(lib().gsr_set_timing(self.ctx, mode), "gsr_set_timing")
+
+    def set_diagnostics(self, on: bool):
+        check(lib().gsr_set_diagnostics(self.ctx, int(on)), "gsr_set_diagnostics")
+
+    def blend_records_loaded(self) -> int:
+        return int(lib().gsr_blend_records_loaded(self.ctx))
+
+    def stage_times(self):
+        ms = (ctypes.c_double * NUM_STAGES)()
+        frames = c_int64()
+        check(lib().gsr_stage_times(self.ctx, ms, byref(frames)), "gsr_stage_times")
+        return dict(zip(STAGES, list(ms))), frames.value
+
+
+def device_available() -> bool:
+    return bool(lib().gsr_device_available())
+
+
+def math_probe(xy: np.ndarray) -> np.ndarray:
+    """Evaluate the gsr_detmath functions on the GPU (see include/gsr.h)."""
+    xy = np.ascontiguousarray(xy, dtype=np.float32).reshape(-1, 2)
+    out = np.zeros((xy.shape[0], 8), dtype=np.float32)
+    check(lib().gsr_math_probe(xy.ctypes.data, xy.shape[0], out.ctypes.data), "gsr_math_probe")
+    return out

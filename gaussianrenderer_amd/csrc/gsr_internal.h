@@ -1,0 +1,61 @@
+// gsr_internal.h — shared between the host runtime (gsr_runtime.cpp) and the
+// gfx950 kernels (gsr_kernels.hip).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gsr_types.h"
+
+namespace gsr {
+
+// Per-frame constants, passed by value to the kernels.
+struct Frame {
+    float V[16];        // view matrix (camera.cpp:53, row-major)
+    float P[16];        // projection (math.cpp:91-97)
+    float Rc[9];        // r_cam
+    float RcT[9];       // r_cam_T
+    float campos[3];
+    float znear;
+    float fx, fy;       // render.cu:620-621 (host-computed, shared with the oracle)
+    float k;            // sigma multiplier
+    int W, H;           // image size (tile_W, tile_H of the reference ABI)
+    int cover_w, cover_h;   // pixels covered by the reference tile grid
+    int tiles_x, tiles_y;   // internal GSR_TILE_PX tiles
+};
+
+// Radix-sort geometry.
+constexpr int kSortThreads = 256;
+constexpr int kSortItems = 16;                          // per thread per tile
+constexpr int kSortTile = kSortThreads * kSortItems;    // 4096 items per tile
+constexpr int kMaxSortGroups = 1024;                    // fixed grid upper bound
+
+// Device-side frame statistics block (device memory).
+struct Stats {
+    unsigned long long pairs_total;   // P before the capacity clamp
+    uint32_t pairs_eff;               // min(P, capacity): what sort/ranges/blend consume
+    uint32_t overflow;                // 1 if P > capacity
+};
+
+// ---- launch wrappers (gsr_kernels.hip) ----
+hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, int64_t stride,
+                             hipStream_t s);
+hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
+                             uint4* rec, uint64_t* items, hipStream_t s);
+// One stable LSD pass over u64 items on bits [shift, shift + bits) (bits <= 8).
+// n = n_dev ? *n_dev : n_host.  hist: 256 * groups u32, totals: 256 u32.
+hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
+                             int shift, int bits, int groups, uint32_t* hist, uint32_t* totals,
+                             hipStream_t s);
+hipError_t launch_emit(const uint64_t* depth_sorted, uint32_t n, const uint4* rec, int groups,
+                       unsigned long long* wg_scratch, Stats* stats, Stats* host_mapped_stats,
+                       uint32_t pair_capacity, int tiles_x, uint64_t* pairs, hipStream_t s);
+hipError_t launch_tile_ranges(const uint64_t* pairs, const Stats* stats, uint2* ranges, int num_tiles,
+                              hipStream_t s);
+// consumed: optional device counter of splat records loaded (diagnostics).
+hipError_t launch_blend(const uint64_t* pairs, const uint2* ranges, const uint4* rec, const Frame& fr,
+                        float* out, unsigned long long* consumed, hipStream_t s);
+// Device math probe for the detmath GPU parity test.
+hipError_t launch_math_probe(const float* in, int n, float* out, hipStream_t s);
+
+}  // namespace gsr

@@ -1,0 +1,723 @@
+// gsr_kernels.hip — gfx950 (CDNA4) kernels of the 3DGS rasterizer.
+//
+// Pipeline per frame (all stream-ordered, no host round trip):
+//   k_preprocess      one thread per Gaussian, SoA coalesced loads: cull + SH
+//                     colour + view/clip + 2D covariance + extent + AABB, writes a
+//                     64-B splat record and the (depth_key << 32 | index) item
+//                     [render.cu:472-786]
+//   radix passes      stable LSD sort of the N items by depth key (4 x 8 bits)
+//   k_emit_*          scan of per-Gaussian tile counts in depth order, then one
+//                     (tile << 32 | index) pair per covered 16x16 tile
+//                     [render.cu:811-857, 788-809]
+//   radix passes      stable LSD sort of the pairs by tile id (2 x <= 8 bits)
+//   k_tile_ranges     [start, end) of each tile from adjacent-key boundaries
+//   k_blend           one workgroup per 16x16 tile, one pixel per lane, 8x8 pixel
+//                     block per wave64; LDS-staged batches of 256 splat records;
+//                     exact per-pixel early termination [render.cu:266-367]
+//
+// Every float expression restates render.cu / math.cu in the same operation
+// order; the file is compiled with -ffp-contract=off so no FMA is formed
+// implicitly, and the transcendental functions come from gsr_detmath.h, so the
+// results are bit-identical to the CPU oracle (oracle/gsr_oracle.c).
+#include <hip/hip_runtime.h>
+
+#include "gsr_detmath.h"
+#include "gsr.h"
+#include "gsr_internal.h"
+
+namespace gsr {
+
+namespace {
+
+__constant__ float kShC0 = 0.28209479177387814f;      // render.cu:369-377
+__constant__ float kShC1 = 0.4886025119029199f;
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// ------------------------------------------------------------------ helpers
+
+// Exclusive scan across a 256-thread workgroup (4 waves).  `scratch` holds 4
+// entries.  Contains two barriers; every thread of the block must call it.
+template <typename T>
+__device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
+    const uint32_t lane = lane_id();
+    const uint32_t w = threadIdx.x >> 6;
+    T x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        T y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) scratch[w] = x;
+    __syncthreads();
+    T pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const T s = scratch[k];
+        if ((uint32_t)k < w) pre += s;
+        tot += s;
+    }
+    __syncthreads();
+    total = tot;
+    return pre + x - v;
+}
+
+// [begin, end) of workgroup g when n items are split over `groups` workgroups in
+// chunks that are multiples of `gran`.
+__device__ __forceinline__ void chunk_range(uint64_t n, int groups, int g, uint64_t gran,
+                                            uint64_t& b, uint64_t& e) {
+    uint64_t per = (n + (uint64_t)groups - 1) / (uint64_t)groups;
+    per = (per + gran - 1) / gran * gran;
+    b = per * (uint64_t)g;
+    if (b > n) b = n;
+    e = b + per;
+    if (e > n) e = n;
+}
+
+// --------------------------------------------------------------- AoS -> SoA
+
+// Accepts the reference's Gaussian[] (gaussians.hpp:16-30) as input.
+__global__ __launch_bounds__(256) void k_aos_to_soa(const gsr_gaussian* __restrict__ g, int64_t n,
+                                                    float* __restrict__ a, int64_t stride) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const gsr_gaussian& q = g[i];
+    a[GSR_A_X * stride + i] = q.x;
+    a[GSR_A_Y * stride + i] = q.y;
+    a[GSR_A_Z * stride + i] = q.z;
+    a[GSR_A_OPACITY * stride + i] = q.opacity;
+#pragma unroll
+    for (int c = 0; c < 3; c++) a[(GSR_A_SCALE0 + c) * stride + i] = q.scale[c];
+#pragma unroll
+    for (int c = 0; c < 4; c++) a[(GSR_A_ROT0 + c) * stride + i] = q.rot[c];
+#pragma unroll
+    for (int c = 0; c < 27; c++) a[(GSR_A_SH0 + c) * stride + i] = q.sh[c];
+}
+
+// ------------------------------------------------------------------ preprocess
+
+// math.cu:120-129 (matMul3D_cuda): out = 0; out += A[ik]*B[kj], k ascending.
+__device__ __forceinline__ void mm3(const float* A, const float* B, float* out) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            float acc = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) acc += A[i * 3 + k] * B[k * 3 + j];
+            out[i * 3 + j] = acc;
+        }
+}
+
+// math.cu:172-186 (geMatMul_cuda), A MxK, B KxN.
+template <int M, int N, int K>
+__device__ __forceinline__ void gemm(const float* A, const float* B, float* out) {
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            float acc = 0.0f;
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc += A[i * K + k] * B[k * N + j];
+            out[i * N + j] = acc;
+        }
+}
+
+// math.cu:131-138 (matVecMul4D_cuda).
+__device__ __forceinline__ void mv4(const float* M, const float* v, float* out) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc += M[i * 4 + j] * v[j];
+        out[i] = acc;
+    }
+}
+
+__device__ __forceinline__ uint4 dead_record_d() {
+    // tile ranges empty, count 0, depth key 0xFFFFFFFF (sorts last)
+    return make_uint4(0u, 0u, 0u, 0xffffffffu);
+}
+
+__global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ arr, int64_t stride,
+                                                    int64_t n, Frame fr, uint4* __restrict__ rec,
+                                                    uint64_t* __restrict__ items) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float gx = arr[GSR_A_X * stride + i];
+    const float gy = arr[GSR_A_Y * stride + i];
+    const float gz = arr[GSR_A_Z * stride + i];
+    uint4* R = rec + 4 * i;
+    items[i] = ((uint64_t)0xffffffffu << 32) | (uint64_t)(uint32_t)i;
+
+    // ---- view + clip transform and cull (render.cu:535-556) ----
+    const float old_xyz[4] = {gx, gy, gz, 1.0f};
+    float tmp_xyz[4], new_xyz[4];
+    mv4(fr.V, old_xyz, tmp_xyz);
+    if (!isfinite(tmp_xyz[0]) || !isfinite(tmp_xyz[1]) || !isfinite(tmp_xyz[2])) {
+        R[3] = dead_record_d();
+        return;
+    }
+    mv4(fr.P, tmp_xyz, new_xyz);
+    new_xyz[0] = new_xyz[0] / new_xyz[3];
+    new_xyz[1] = new_xyz[1] / new_xyz[3];
+    new_xyz[2] = new_xyz[2] / new_xyz[3];
+    if (!isfinite(new_xyz[0]) || !isfinite(new_xyz[1]) || !isfinite(new_xyz[2]) ||
+        tmp_xyz[2] >= -fr.znear || new_xyz[2] < -1.0f || new_xyz[2] > 1.0f) {
+        R[3] = dead_record_d();
+        return;
+    }
+
+    // ---- 2D covariance (render.cu:655-686) ----
+    const float X = tmp_xyz[0], Y = tmp_xyz[1], Z = tmp_xyz[2];
+    const float fx = fr.fx, fy = fr.fy;
+    float jac[6], jacT[6];
+    jac[0] = fx / Z; jac[1] = 0.0f;
+    jac[2] = -fx * X / (Z * Z); jac[3] = 0.0f;
+    jac[4] = fy / Z; jac[5] = -fy * Y / (Z * Z);
+    jacT[0] = jac[0]; jacT[1] = jac[3]; jacT[2] = jac[1];
+    jacT[3] = jac[4]; jacT[4] = jac[2]; jacT[5] = jac[5];
+
+    // buildRotMatFromQuat_cuda (math.cu:153-164)
+    float qw = arr[(GSR_A_ROT0 + 0) * stride + i];
+    float qx = arr[(GSR_A_ROT0 + 1) * stride + i];
+    float qy = arr[(GSR_A_ROT0 + 2) * stride + i];
+    float qz = arr[(GSR_A_ROT0 + 3) * stride + i];
+    const float qn = sqrtf(qx * qx + qy * qy + qz * qz + qw * qw);
+    qx /= qn; qy /= qn; qz /= qn; qw /= qn;
+    float Rm[9], RT[9], S[9], tmp[9], cov[9];
+    Rm[0] = 1 - 2 * qy * qy - 2 * qz * qz; Rm[1] = 2 * qx * qy - 2 * qw * qz;     Rm[2] = 2 * qx * qz + 2 * qw * qy;
+    Rm[3] = 2 * qx * qy + 2 * qw * qz;     Rm[4] = 1 - 2 * qx * qx - 2 * qz * qz; Rm[5] = 2 * qy * qz - 2 * qw * qx;
+    Rm[6] = 2 * qx * qz - 2 * qw * qy;     Rm[7] = 2 * qy * qz + 2 * qw * qx;     Rm[8] = 1 - 2 * qx * qx - 2 * qy * qy;
+    RT[0] = Rm[0]; RT[1] = Rm[3]; RT[2] = Rm[6];
+    RT[3] = Rm[1]; RT[4] = Rm[4]; RT[5] = Rm[7];
+    RT[6] = Rm[2]; RT[7] = Rm[5]; RT[8] = Rm[8];
+    const float scale_mod = 1.0f;
+    S[0] = scale_mod * arr[(GSR_A_SCALE0 + 0) * stride + i]; S[1] = 0.0f; S[2] = 0.0f;
+    S[3] = 0.0f; S[4] = scale_mod * arr[(GSR_A_SCALE0 + 1) * stride + i]; S[5] = 0.0f;
+    S[6] = 0.0f; S[7] = 0.0f; S[8] = scale_mod * arr[(GSR_A_SCALE0 + 2) * stride + i];
+    mm3(Rm, S, tmp);
+    mm3(tmp, S, Rm);
+    mm3(Rm, RT, cov);
+    mm3(fr.Rc, cov, tmp);
+    mm3(tmp, fr.RcT, cov);
+    gemm<2, 3, 3>(jac, cov, tmp);
+    float S2[4];
+    gemm<2, 2, 3>(tmp, jacT, S2);
+    const int W = fr.W, H = fr.H;
+    S2[0] = (W * 0.5f) * (W * 0.5f) * S2[0];
+    S2[1] = (W * 0.5f) * (H * 0.5f) * S2[1];
+    S2[2] = (H * 0.5f) * (W * 0.5f) * S2[2];
+    S2[3] = (H * 0.5f) * (H * 0.5f) * S2[3];
+    const float det = S2[0] * S2[3] - S2[1] * S2[2];
+    if (!isfinite(det) || det < 1e-8f) {                        // render.cu:690
+        R[3] = dead_record_d();
+        return;
+    }
+    const float invDet = 1.0f / det;
+    const float ic0 = S2[3] * invDet, ic1 = -S2[1] * invDet;
+    const float ic2 = -S2[2] * invDet, ic3 = S2[0] * invDet;
+
+    // ---- extent (render.cu:704-764) ----
+    const float sxy = 0.5f * (S2[1] + S2[2]);
+    const float tr = S2[0] + S2[3];
+    const float dif = S2[0] - S2[3];
+    const float rad = sqrtf(fmaxf(0.0f, dif * dif + 4 * sxy * sxy));
+    float l1 = 0.5f * (tr + rad);
+    float l2 = 0.5f * (tr - rad);
+    l1 = fmaxf(l1, 1e-8f);
+    l2 = fmaxf(l2, 1e-8f);
+    const float theta = 0.5f * gsr_atan2f(2 * sxy, dif);
+    const float r1 = fr.k * sqrtf(l1);
+    const float r2 = fr.k * sqrtf(l2);
+    const float c = gsr_cosf(theta);
+    const float sn = gsr_sinf(theta);
+    float ex = fabsf(r1 * c) + fabsf(r2 * sn);
+    float ey = fabsf(r1 * sn) + fabsf(r2 * c);
+    ex /= W / 2.0f;
+    ey /= H / 2.0f;
+    float xmin = new_xyz[0] - ex, xmax = new_xyz[0] + ex;
+    float ymin = new_xyz[1] - ey, ymax = new_xyz[1] + ey;
+    if (xmax < -0.99f || xmin > 0.99f || ymax < -0.99f || ymin > 0.99f) {   // render.cu:737
+        R[3] = dead_record_d();
+        return;
+    }
+    xmin = fmaxf(xmin, -1.0f);
+    xmax = fminf(xmax, 1.0f);
+    ymin = fmaxf(ymin, -1.0f);
+    ymax = fminf(ymax, 1.0f);
+    const int xmin_px = gsr_f2i_sat(floorf(((xmin + 1.0f) * 0.5f) * W));
+    const int xmax_px = gsr_f2i_sat(ceilf(((xmax + 1.0f) * 0.5f) * W));
+    const int ymin_px = gsr_f2i_sat(floorf(((ymin + 1.0f) * 0.5f) * H));
+    const int ymax_px = gsr_f2i_sat(ceilf(((ymax + 1.0f) * 0.5f) * H));
+    const int px_x = gsr_f2i_sat(roundf(((new_xyz[0] + 1.0f) * 0.5f) * W));
+    const int px_y = gsr_f2i_sat(roundf(((new_xyz[1] + 1.0f) * 0.5f) * H));
+    const uint32_t key = gsr_f2u_sat(-Z * 1e6f);                // render.cu:850
+
+    // internal GSR_TILE_PX tiles covered (output is tile-invariant)
+    const int tx0 = xmin_px / GSR_TILE_PX;
+    const int tx1 = min(fr.tiles_x - 1, xmax_px / GSR_TILE_PX);
+    const int ty0 = ymin_px / GSR_TILE_PX;
+    const int ty1 = min(fr.tiles_y - 1, ymax_px / GSR_TILE_PX);
+    const uint32_t count = (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1));
+
+    // ---- SH colour, bands 0..2 (render.cu:500-534), only for survivors ----
+    float dir[3] = {gx - fr.campos[0], gy - fr.campos[1], gz - fr.campos[2]};
+    {
+        const float nn = sqrtf(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);  // math.cu:7-18
+        if (nn > 1e-8f) {
+            dir[0] /= nn; dir[1] /= nn; dir[2] /= nn;
+        } else {
+            dir[0] = 0.0f; dir[1] = 0.0f; dir[2] = 0.0f;
+        }
+    }
+    const float x = dir[0], y = dir[1], z = dir[2];
+    const float xx = x * x, yy = y * y, zz = z * z;
+    const float xy = x * y, yz = y * z, xz = x * z;
+    const float C2_0 = 1.0925484305920792f, C2_1 = -1.0925484305920792f, C2_2 = 0.31539156525252005f,
+                C2_3 = -1.0925484305920792f, C2_4 = 0.5462742152960396f;
+    float col[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        const float* sh = arr + (GSR_A_SH0 + ch) * stride + i;   // sh[ch], sh[3+ch], ...
+        float cc = sh[0] * kShC0;
+        cc += kShC1 * z * sh[6 * stride];
+        cc -= kShC1 * y * sh[3 * stride];
+        cc -= kShC1 * x * sh[9 * stride];
+        cc += C2_0 * xy * sh[12 * stride];
+        cc += C2_1 * yz * sh[15 * stride];
+        cc += C2_2 * (2.0f * zz - xx - yy) * sh[18 * stride];
+        cc += C2_3 * xz * sh[21 * stride];
+        cc += C2_4 * (xx - yy) * sh[24 * stride];
+        cc += 0.5f;
+        col[ch] = fminf(fmaxf(cc, 0.0f), 1.0f);
+    }
+    const float opacity = arr[GSR_A_OPACITY * stride + i];
+
+    R[0] = make_uint4(__float_as_uint(ic0), __float_as_uint(ic1), __float_as_uint(ic2), __float_as_uint(ic3));
+    R[1] = make_uint4(__float_as_uint(opacity), __float_as_uint(col[0]), __float_as_uint(col[1]),
+                      __float_as_uint(col[2]));
+    R[2] = make_uint4((uint32_t)px_x, (uint32_t)px_y, (uint32_t)xmin_px | ((uint32_t)xmax_px << 16),
+                      (uint32_t)ymin_px | ((uint32_t)ymax_px << 16));
+    R[3] = make_uint4((uint32_t)tx0 | ((uint32_t)tx1 << 16), (uint32_t)ty0 | ((uint32_t)ty1 << 16), count, key);
+    items[i] = ((uint64_t)key << 32) | (uint64_t)(uint32_t)i;
+}
+
+// ------------------------------------------------------------------ radix sort
+//
+// Stable LSD pass, reduce-then-scan (no inter-workgroup spin waits, so no
+// forward-progress assumption): upsweep histograms per workgroup chunk,
+// per-digit scan over workgroups, downsweep that ranks each 4096-item tile with
+// wave64 ballot matching (the AMD stand-in for __match_any), scatters into LDS
+// in digit order and writes runs out coalesced.
+
+__global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* __restrict__ in,
+                                                                const uint32_t* __restrict__ n_dev,
+                                                                uint32_t n_host, int shift, uint32_t mask,
+                                                                int groups, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[4][256];
+    const uint32_t t = threadIdx.x;
+    const uint32_t w = t >> 6;
+#pragma unroll
+    for (int k = 0; k < 4; k++) h[k][t] = 0;
+    __syncthreads();
+    const uint64_t n = n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
+    uint64_t b, e;
+    chunk_range(n, groups, blockIdx.x, kSortTile, b, e);
+    uint64_t i = b + t;
+    for (; i + 3 * kSortThreads < e; i += 4 * kSortThreads) {
+        const uint64_t v0 = in[i], v1 = in[i + kSortThreads], v2 = in[i + 2 * kSortThreads],
+                       v3 = in[i + 3 * kSortThreads];
+        atomicAdd(&h[w][(uint32_t)(v0 >> shift) & mask], 1u);
+        atomicAdd(&h[w][(uint32_t)(v1 >> shift) & mask], 1u);
+        atomicAdd(&h[w][(uint32_t)(v2 >> shift) & mask], 1u);
+        atomicAdd(&h[w][(uint32_t)(v3 >> shift) & mask], 1u);
+    }
+    for (; i < e; i += kSortThreads) atomicAdd(&h[w][(uint32_t)(in[i] >> shift) & mask], 1u);
+    __syncthreads();
+    hist[t * (uint32_t)groups + blockIdx.x] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
+}
+
+// One workgroup per digit: exclusive scan of hist[d][0..groups) in place.
+__global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist, int groups,
+                                                     uint32_t* __restrict__ totals) {
+    __shared__ uint32_t scratch[4];
+    uint32_t* row = hist + (size_t)blockIdx.x * groups;
+    const int per = (groups + 255) / 256;
+    const int b = threadIdx.x * per;
+    uint32_t local = 0;
+    for (int k = 0; k < per; k++)
+        if (b + k < groups) local += row[b + k];
+    uint32_t total;
+    uint32_t run = block_exclusive_scan<uint32_t>(local, scratch, total);
+    for (int k = 0; k < per; k++)
+        if (b + k < groups) {
+            const uint32_t v = row[b + k];
+            row[b + k] = run;
+            run += v;
+        }
+    if (threadIdx.x == 0) totals[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
+    const uint64_t* __restrict__ in, uint64_t* __restrict__ out, const uint32_t* __restrict__ n_dev,
+    uint32_t n_host, int shift, int bits, int groups, const uint32_t* __restrict__ hist,
+    const uint32_t* __restrict__ totals) {
+    __shared__ uint64_t s_items[kSortTile];     // 32 KB
+    __shared__ uint32_t s_wc[4][256];           // per-wave digit counters, then wave bases
+    __shared__ uint32_t s_gbase[256];           // running global offset per digit
+    __shared__ uint32_t s_lbase[256];           // tile-local exclusive base per digit
+    __shared__ uint32_t s_scr[4];
+    const uint32_t t = threadIdx.x;
+    const uint32_t lane = lane_id();
+    const uint32_t w = t >> 6;
+    const uint32_t mask = (1u << bits) - 1u;
+    const uint64_t n = n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
+    uint64_t b, e;
+    chunk_range(n, groups, blockIdx.x, kSortTile, b, e);
+    if (b >= e) return;                          // uniform per workgroup
+
+    // global base of each digit for this workgroup
+    {
+        uint32_t tot;
+        const uint32_t dig_excl = block_exclusive_scan<uint32_t>(totals[t], s_scr, tot);
+        s_gbase[t] = dig_excl + hist[t * (uint32_t)groups + blockIdx.x];
+    }
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+    for (uint64_t tb = b; tb < e; tb += kSortTile) {
+        const uint32_t tn = (uint32_t)min((uint64_t)kSortTile, e - tb);
+#pragma unroll
+        for (int k = 0; k < 4; k++) s_wc[k][t] = 0;
+        __syncthreads();
+
+        uint64_t it[kSortItems];
+        uint32_t rk[kSortItems];
+        const uint32_t wbase = w * 64 * kSortItems;
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            it[k] = (el < tn) ? in[tb + el] : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            const bool valid = el < tn;
+            const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
+            uint64_t peers = __ballot(valid);
+            for (int bit = 0; bit < bits; bit++) {
+                const bool on = (d >> bit) & 1u;
+                const uint64_t bm = __ballot(on);
+                peers &= on ? bm : ~bm;
+            }
+            uint32_t r = 0;
+            if (valid) {
+                const uint32_t before = s_wc[w][d];
+                r = before + (uint32_t)__popcll(peers & lt_mask);
+                if ((uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
+                    s_wc[w][d] = before + (uint32_t)__popcll(peers);
+            }
+            rk[k] = r;
+        }
+        __syncthreads();
+        // per digit t: exclusive prefix over the four waves, tile count, tile-local base
+        uint32_t tcount;
+        {
+            const uint32_t c0 = s_wc[0][t], c1 = s_wc[1][t], c2 = s_wc[2][t], c3 = s_wc[3][t];
+            s_wc[0][t] = 0;
+            s_wc[1][t] = c0;
+            s_wc[2][t] = c0 + c1;
+            s_wc[3][t] = c0 + c1 + c2;
+            tcount = c0 + c1 + c2 + c3;
+            uint32_t tot;
+            s_lbase[t] = block_exclusive_scan<uint32_t>(tcount, s_scr, tot);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            if (el < tn) {
+                const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
+                s_items[s_lbase[d] + s_wc[w][d] + rk[k]] = it[k];
+            }
+        }
+        __syncthreads();
+        for (uint32_t q = t; q < tn; q += kSortThreads) {
+            const uint64_t v = s_items[q];
+            const uint32_t d = (uint32_t)(v >> shift) & mask;
+            out[(uint64_t)s_gbase[d] + (q - s_lbase[d])] = v;
+        }
+        __syncthreads();
+        s_gbase[t] += tcount;
+        // next iteration's first barrier orders this update before its use
+    }
+}
+
+// ------------------------------------------------------------------ emission
+
+__global__ __launch_bounds__(256) void k_emit_count(const uint64_t* __restrict__ sorted, uint32_t n,
+                                                     const uint4* __restrict__ rec, int groups,
+                                                     unsigned long long* __restrict__ wg_sum) {
+    __shared__ unsigned long long scr[4];
+    uint64_t b, e;
+    chunk_range(n, groups, blockIdx.x, 256, b, e);
+    unsigned long long s = 0;
+    for (uint64_t j = b + threadIdx.x; j < e; j += 256) {
+        const uint32_t i = (uint32_t)sorted[j];
+        s += rec[4 * (uint64_t)i + 3].z;
+    }
+    unsigned long long tot;
+    block_exclusive_scan<unsigned long long>(s, scr, tot);
+    if (threadIdx.x == 0) wg_sum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_emit_scan(unsigned long long* __restrict__ wg, int groups,
+                                                    uint32_t cap, Stats* __restrict__ st,
+                                                    Stats* host_st) {
+    __shared__ unsigned long long scr[4];
+    const int per = (groups + 255) / 256;
+    const int b = threadIdx.x * per;
+    unsigned long long local = 0;
+    for (int k = 0; k < per; k++)
+        if (b + k < groups) local += wg[b + k];
+    unsigned long long total;
+    unsigned long long run = block_exclusive_scan<unsigned long long>(local, scr, total);
+    for (int k = 0; k < per; k++)
+        if (b + k < groups) {
+            const unsigned long long v = wg[b + k];
+            wg[b + k] = run;
+            run += v;
+        }
+    if (threadIdx.x == 0) {
+        Stats s;
+        s.pairs_total = total;
+        s.pairs_eff = (uint32_t)(total < cap ? total : cap);
+        s.overflow = total > cap ? 1u : 0u;
+        st[0] = s;
+        // st[1]: sticky record (max P, overflow seen) until the host clears it
+        Stats k = st[1];
+        if (s.pairs_total > k.pairs_total) k.pairs_total = s.pairs_total;
+        k.pairs_eff = s.pairs_eff;
+        k.overflow |= s.overflow;
+        st[1] = k;
+        if (host_st) {
+            host_st->pairs_total = k.pairs_total;
+            host_st->pairs_eff = k.pairs_eff;
+            host_st->overflow = k.overflow;
+            __threadfence_system();
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_emit_pairs(const uint64_t* __restrict__ sorted, uint32_t n,
+                                                     const uint4* __restrict__ rec, int groups,
+                                                     const unsigned long long* __restrict__ wg_base,
+                                                     uint32_t cap, int tiles_x,
+                                                     uint64_t* __restrict__ pairs) {
+    __shared__ unsigned long long scr[4];
+    uint64_t b, e;
+    chunk_range(n, groups, blockIdx.x, 256, b, e);
+    unsigned long long run = wg_base[blockIdx.x];
+    for (uint64_t rb = b; rb < e; rb += 256) {
+        const uint64_t j = rb + threadIdx.x;
+        uint32_t cnt = 0, i = 0;
+        uint4 D = make_uint4(0, 0, 0, 0);
+        if (j < e) {
+            i = (uint32_t)sorted[j];
+            D = rec[4 * (uint64_t)i + 3];
+            cnt = D.z;
+        }
+        unsigned long long tot;
+        unsigned long long pos = run + block_exclusive_scan<unsigned long long>(cnt, scr, tot);
+        if (cnt) {
+            const uint32_t tx0 = D.x & 0xffffu, tx1 = D.x >> 16;
+            const uint32_t ty0 = D.y & 0xffffu, ty1 = D.y >> 16;
+            for (uint32_t ty = ty0; ty <= ty1; ty++)
+                for (uint32_t tx = tx0; tx <= tx1; tx++) {
+                    if (pos < cap) pairs[pos] = ((uint64_t)(ty * (uint32_t)tiles_x + tx) << 32) | i;
+                    pos++;
+                }
+        }
+        run += tot;
+    }
+}
+
+// ------------------------------------------------------------------ tile ranges
+
+__global__ __launch_bounds__(256) void k_tile_ranges(const uint64_t* __restrict__ pairs,
+                                                      const Stats* __restrict__ st,
+                                                      uint2* __restrict__ ranges) {
+    const uint32_t n = st->pairs_eff;
+    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) {
+        const uint32_t tl = (uint32_t)(pairs[p] >> 32);
+        if (p == 0 || (uint32_t)(pairs[p - 1] >> 32) != tl) ranges[tl].x = p;
+        if (p == n - 1 || (uint32_t)(pairs[p + 1] >> 32) != tl) ranges[tl].y = p + 1;
+    }
+}
+
+// ------------------------------------------------------------------ blend
+
+constexpr int kBatch = 256;
+
+// Bijective XCD-aware remap: blocks that share an XCD (b % 8) get one
+// contiguous run of tiles, so neighbouring tiles' shared splats hit one L2.
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+    const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+__global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pairs,
+                                                const uint2* __restrict__ ranges,
+                                                const uint4* __restrict__ rec, int tiles_x, int tiles_y,
+                                                int W, int H, int cover_w, int cover_h,
+                                                float* __restrict__ out,
+                                                unsigned long long* __restrict__ consumed) {
+    __shared__ uint4 sA[kBatch], sB[kBatch], sC[kBatch];
+    const int ntiles = tiles_x * tiles_y;
+    const int tile = xcd_remap(blockIdx.x, ntiles);
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int bx = tx * GSR_TILE_PX + (w & 1) * 8;
+    const int by = ty * GSR_TILE_PX + (w >> 1) * 8;
+    const int px = bx + (lane & 7), py = by + (lane >> 3);
+    const bool inside = px < cover_w && py < cover_h;
+    const float fpx = (float)px, fpy = (float)py;
+    float T = 1.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    bool done = !inside;
+    const uint2 rg = ranges[tile];
+    uint32_t loaded = 0;
+    for (uint32_t base = rg.x; base < rg.y; base += kBatch) {
+        const uint32_t cnt = min((uint32_t)kBatch, rg.y - base);
+        loaded += cnt;
+        __syncthreads();
+        if ((uint32_t)t < cnt) {
+            const uint32_t gi = (uint32_t)pairs[base + t];
+            const uint4* R = rec + 4 * (uint64_t)gi;
+            sA[t] = R[0];
+            sB[t] = R[1];
+            sC[t] = R[2];
+        }
+        __syncthreads();
+        if (__ballot(!done) != 0ull) {
+            for (uint32_t s = 0; s < cnt; s++) {
+                const uint4 C = sC[s];
+                const int xmin = (int)(C.z & 0xffffu), xmax = (int)(C.z >> 16);
+                const int ymin = (int)(C.w & 0xffffu), ymax = (int)(C.w >> 16);
+                if (xmax < bx || xmin > bx + 7 || ymax < by || ymin > by + 7) continue;  // wave-uniform
+                if (!done && px >= xmin && px <= xmax && py >= ymin && py <= ymax) {
+                    const uint4 A = sA[s];
+                    const uint4 B = sB[s];
+                    const float dx = fpx - (float)(int)C.x;
+                    const float dy = fpy - (float)(int)C.y;
+                    const float md2 = dx * (__uint_as_float(A.x) * dx + __uint_as_float(A.y) * dy) +
+                                      dy * (__uint_as_float(A.z) * dx + __uint_as_float(A.w) * dy);
+                    float alpha = __uint_as_float(B.x) * gsr_expf(-0.5f * md2);
+                    alpha = fminf(alpha, 0.99f);
+                    if (!(alpha < 1e-3f)) {
+                        cr += __uint_as_float(B.y) * alpha * T;
+                        cg += __uint_as_float(B.z) * alpha * T;
+                        cb += __uint_as_float(B.w) * alpha * T;
+                        T *= (1.0f - alpha);
+                        done = T < 1e-3f;
+                    }
+                }
+                if (__ballot(!done) == 0ull) break;
+            }
+        }
+        if (__syncthreads_and(done ? 1 : 0)) break;
+    }
+    if (consumed && t == 0 && loaded) atomicAdd(consumed, (unsigned long long)loaded);
+    if (px < W && py < H) {
+        const size_t o = (size_t)py * (size_t)W + (size_t)px;
+        const size_t hw = (size_t)W * (size_t)H;
+        out[o] = inside ? cr : 0.0f;
+        out[hw + o] = inside ? cg : 0.0f;
+        out[2 * hw + o] = inside ? cb : 0.0f;
+    }
+}
+
+// ------------------------------------------------------------------ math probe
+
+__global__ void k_math_probe(const float* __restrict__ in, int n, float* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = in[2 * i], y = in[2 * i + 1];
+    float* o = out + 8 * i;
+    o[0] = gsr_expf(x);
+    o[1] = gsr_sinf(x);
+    o[2] = gsr_cosf(x);
+    o[3] = gsr_atan2f(x, y);
+    o[4] = sqrtf(x);
+    o[5] = x / y;
+    o[6] = roundf(x);
+    o[7] = __int_as_float(gsr_f2i_sat(x * 1000.0f));
+}
+
+inline int grid_for(int64_t n, int block) { return (int)((n + block - 1) / block); }
+
+}  // namespace
+
+// ------------------------------------------------------------------ launchers
+
+hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, int64_t stride,
+                             hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_aos_to_soa, dim3(grid_for(n, 256)), dim3(256), 0, s, aos, n, arrays, stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
+                             uint4* rec, uint64_t* items, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_preprocess, dim3(grid_for(n, 256)), dim3(256), 0, s, arrays, stride, n, fr, rec,
+                       items);
+    return hipGetLastError();
+}
+
+hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
+                             int shift, int bits, int groups, uint32_t* hist, uint32_t* totals,
+                             hipStream_t s) {
+    const uint32_t mask = (1u << bits) - 1u;
+    hipLaunchKernelGGL(k_radix_upsweep, dim3(groups), dim3(kSortThreads), 0, s, in, n_dev, n_host, shift,
+                       mask, groups, hist);
+    hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, hist, groups, totals);
+    hipLaunchKernelGGL(k_radix_downsweep, dim3(groups), dim3(kSortThreads), 0, s, in, out, n_dev, n_host,
+                       shift, bits, groups, hist, totals);
+    return hipGetLastError();
+}
+
+hipError_t launch_emit(const uint64_t* depth_sorted, uint32_t n, const uint4* rec, int groups,
+                       unsigned long long* wg_scratch, Stats* stats, Stats* host_mapped_stats,
+                       uint32_t pair_capacity, int tiles_x, uint64_t* pairs, hipStream_t s) {
+    hipLaunchKernelGGL(k_emit_count, dim3(groups), dim3(256), 0, s, depth_sorted, n, rec, groups, wg_scratch);
+    hipLaunchKernelGGL(k_emit_scan, dim3(1), dim3(256), 0, s, wg_scratch, groups, pair_capacity, stats,
+                       host_mapped_stats);
+    hipLaunchKernelGGL(k_emit_pairs, dim3(groups), dim3(256), 0, s, depth_sorted, n, rec, groups, wg_scratch,
+                       pair_capacity, tiles_x, pairs);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_ranges(const uint64_t* pairs, const Stats* stats, uint2* ranges, int num_tiles,
+                              hipStream_t s) {
+    hipError_t e = hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)num_tiles, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_tile_ranges, dim3(2048), dim3(256), 0, s, pairs, stats, ranges);
+    return hipGetLastError();
+}
+
+hipError_t launch_blend(const uint64_t* pairs, const uint2* ranges, const uint4* rec, const Frame& fr,
+                        float* out, unsigned long long* consumed, hipStream_t s) {
+    const int nt = fr.tiles_x * fr.tiles_y;
+    if (nt <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_blend, dim3(nt), dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x, fr.tiles_y, fr.W,
+                       fr.H, fr.cover_w, fr.cover_h, out, consumed);
+    return hipGetLastError();
+}
+
+hipError_t launch_math_probe(const float* in, int n, float* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_math_probe, dim3(grid_for(n, 256)), dim3(256), 0, s, in, n, out);
+    return hipGetLastError();
+}
+
+}  // namespace gsr

@@ -1,0 +1,209 @@
+/*
+ * gsr.h — C ABI of the MI355X-native 3D Gaussian splatting rasterizer.
+ *
+ * Two groups of entry points:
+ *
+ *  1. DROP-IN BOUNDARY — the exact symbols the reference viewer links
+ *     against.  A viewer built against the reference's
+ *     render.cuh / misc.cuh links against libgsr.so unchanged:
+ *
+ *       preprocessCUDAGaussians   replaces render.cu:871-1157 (decl render.cuh:27-37)
+ *       loadGaussianCudaFromPly   replaces misc.cu:13-134     (decl misc.cuh:4, C++ linkage)
+ *       oneSweep3DGaussianSort    replaces render.cu:194-264  (decl render.cuh:8-11)
+ *       oneSweepSort              replaces onesweep.cu:190-250 (decl onesweep.cuh:8)
+ *
+ *  2. NATIVE API (gsr_*) — stream-ordered, device-resident, no per-frame
+ *     allocation: a persistent context (workspace sized by high-water mark),
+ *     the three pipeline stages the reference names "Preprocess + Sort +
+ *     Render" as separate calls, readback hooks used by the parity tests, and
+ *     the host-side camera / PLY helpers that mirror the reference's
+ *     camera.cpp and gaussians.cpp so tests and benches can build inputs
+ *     exactly like the viewer does.
+ *
+ * Errors: every int-returning function returns 0 on success and a negative
+ * GSR_E* code on failure; gsr_last_error() returns the message.  The void
+ * drop-in functions keep the reference's behaviour (print the error to
+ * stderr and return, render.cu:914-923).
+ */
+#ifndef GSR_H
+#define GSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "gsr_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    GSR_OK = 0,
+    GSR_E_ARG = -1,        /* invalid argument */
+    GSR_E_HIP = -2,        /* HIP runtime error (no device, OOM, launch failure) */
+    GSR_E_IO = -3,         /* file missing / unreadable / truncated */
+    GSR_E_FORMAT = -4,     /* unsupported PLY format */
+    GSR_E_OVERFLOW = -5    /* pair buffer overflowed in the previous frame (grown; re-render) */
+};
+
+/* Scene layout accepted by the render entry points. */
+enum {
+    GSR_LAYOUT_SCENE_BLOCK = 0,   /* our SoA block (gsr_scene_header + arrays) */
+    GSR_LAYOUT_AOS = 1            /* reference Gaussian[] (240 B records) */
+};
+
+/* Stage indices for gsr_stage_times(). */
+enum {
+    GSR_STAGE_PREPROCESS = 0,     /* cull + SH colour + projection + covariance + AABB */
+    GSR_STAGE_DEPTH_SORT = 1,     /* stable radix sort of (depth, index) */
+    GSR_STAGE_EMIT = 2,           /* scan of tile counts + (tile, index) pair emission */
+    GSR_STAGE_TILE_SORT = 3,      /* stable radix sort of pairs by tile */
+    GSR_STAGE_RANGES = 4,         /* per-tile [start, end) from sorted pairs */
+    GSR_STAGE_BLEND = 5,          /* front-to-back alpha compositing */
+    GSR_NUM_STAGES = 6
+};
+
+#define GSR_TILE_PX 16            /* internal tile edge (pixels); output is tile-invariant */
+#define GSR_SPLAT_RECORD_BYTES 64 /* per-Gaussian splat record written by preprocess */
+
+/* ---------------------------------------------------------------- drop-in */
+
+/* render.cu:871-881.  d_gaussians: a device scene block from
+ * loadGaussianCudaFromPly (our SoA layout) OR a device Gaussian[] array in
+ * the reference's AoS layout (detected by the header magic).  out_pixels:
+ * HOST buffer of 3*tile_W*tile_H floats, planar RGB, row 0 = bottom (NDC -1).
+ * tile_W/tile_H are the image size; the num_tile / stride arguments follow
+ * TilingInformation (gaussians.hpp:47-58) and only bound which pixels are
+ * covered (pixels at x >= num_tile_x*width_stride or y >= num_tile_y*
+ * height_stride stay 0 as in renderGaussians, render.cu:285-363).
+ * Synchronous; uses a process-wide context guarded by a mutex. */
+void preprocessCUDAGaussians(gsr_gaussian* d_gaussians, float* out_pixels, int num_gaussians,
+                             gsr_camera cam, int num_tile_y, int num_tile_x, int width_stride,
+                             int height_stride, int tile_W, int tile_H, float k);
+
+/* C twin of loadGaussianCudaFromPly (misc.cu:13-134) for FFI callers:
+ * returns a device scene block (free with hipFree or gsr_scene_free), or
+ * NULL on failure; *out_numGaussians is set once the header is parsed. */
+gsr_gaussian* gsr_load_ply_device(const char* filename, int* out_numGaussians);
+
+/* render.cu:194-264: stable sort of N host-side lightWeightGaussian records
+ * by the low num_bits bits of radix_id, in place; *kernel_ms = device time. */
+void oneSweep3DGaussianSort(gsr_lwg* d_in, int N, int num_bits, float* kernel_ms);
+
+/* onesweep.cu:190-250: sort N host ints (keys in [0, maxVal], non-negative)
+ * ascending into output; *kernel_ms = device time of the sort passes. */
+void oneSweepSort(int* input, int* output, int N, int maxVal, float* kernel_ms);
+
+/* ---------------------------------------------------------------- context */
+
+typedef struct gsr_context gsr_context;
+
+gsr_context* gsr_create(void);
+void gsr_destroy(gsr_context* ctx);
+
+/* Pre-size the workspace for n Gaussians and `pairs` (tile, Gaussian) pairs. */
+int gsr_reserve(gsr_context* ctx, int64_t n, int64_t pairs);
+
+/* Whole frame, stream-ordered (stream = hipStream_t or NULL for the default
+ * stream).  d_out: DEVICE buffer of 3*W*H floats (planar, row 0 = bottom).
+ * Reference tiling arguments as in preprocessCUDAGaussians; pass
+ * num_tile_x = num_tile_y = 1 and strides = W, H for "cover the image".
+ * Returns GSR_E_OVERFLOW if an earlier frame overflowed the pair buffer
+ * (the buffer has been grown; that earlier frame's image was incomplete). */
+int gsr_render(gsr_context* ctx, const void* d_scene, int layout, int64_t n,
+               const gsr_camera* cam, int W, int H, int num_tile_x, int num_tile_y,
+               int width_stride, int height_stride, float k, float* d_out, void* stream);
+
+/* The three stages of gsr_render, callable separately (same stream). */
+int gsr_preprocess(gsr_context* ctx, const void* d_scene, int layout, int64_t n,
+                   const gsr_camera* cam, int W, int H, int num_tile_x, int num_tile_y,
+                   int width_stride, int height_stride, float k, void* stream);
+int gsr_sort(gsr_context* ctx, void* stream);
+int gsr_blend(gsr_context* ctx, float* d_out, void* stream);
+
+/* Wait for all work of the context; returns GSR_E_OVERFLOW if the last frame
+ * overflowed (and grows the buffer). */
+int gsr_sync(gsr_context* ctx);
+
+/* ---- readback (synchronous; for tests and tooling) ---- */
+
+/* Number of (tile, Gaussian) pairs of the last frame (before capacity clamp). */
+int64_t gsr_pair_count(gsr_context* ctx);
+/* Per-Gaussian splat records (n * GSR_SPLAT_RECORD_BYTES bytes):
+ *   float inv_covar[4]; float opacity; float color[3];
+ *   int32 px_x, px_y; uint32 x_range (xmin | xmax<<16); uint32 y_range;
+ *   uint32 tile_x_range; uint32 tile_y_range; uint32 tile_count; uint32 depth_key.
+ * Culled / invalid Gaussians have tile_count 0 and depth_key 0xFFFFFFFF;
+ * their other fields are unspecified. */
+int gsr_read_splats(gsr_context* ctx, void* host_records, int64_t n);
+/* (depth_key << 32 | index) items after the depth sort, n of them. */
+int gsr_read_depth_order(gsr_context* ctx, uint64_t* host_items, int64_t n);
+/* (tile << 32 | index) pairs after the tile sort; returns the count copied. */
+int64_t gsr_read_pairs(gsr_context* ctx, uint64_t* host_pairs, int64_t cap);
+/* Internal tile grid of the last frame and its [start, end) ranges. */
+int gsr_tile_grid(gsr_context* ctx, int* tiles_x, int* tiles_y);
+int gsr_read_tile_ranges(gsr_context* ctx, uint32_t* host_ranges, int64_t num_tiles);
+
+/* ---- per-stage device timing with hipEvents on the render stream ----
+ * mode 0 = off, 1 = blend only (two events per frame), 2 = every stage. */
+int gsr_set_timing(gsr_context* ctx, int mode);
+/* Sums of per-stage device milliseconds and the number of frames timed since
+ * the last call (synchronises, then resets). */
+int gsr_stage_times(gsr_context* ctx, double* ms_out /* GSR_NUM_STAGES */, int64_t* frames);
+
+/* Diagnostics (off by default): when on, the blend counts the splat records
+ * it actually loads (Pc of SURVEY.md 8d: pairs consumed before every pixel of
+ * a tile saturates); gsr_blend_records_loaded() returns the last frame's Pc. */
+int gsr_set_diagnostics(gsr_context* ctx, int on);
+int64_t gsr_blend_records_loaded(gsr_context* ctx);
+
+/* ---------------------------------------------------------------- scenes */
+
+/* Upload a host SoA scene (GSR_SCENE_NARRAYS arrays of n floats, contiguous,
+ * already activated as by the loader) into a new device scene block. */
+void* gsr_scene_upload(const float* host_soa, int64_t n);
+void gsr_scene_free(void* d_scene);
+/* Copy a device scene block back into host SoA form (38 * n floats). */
+int gsr_scene_download(const void* d_scene, float* host_soa, int64_t n);
+
+/* ---------------------------------------------------------------- host helpers */
+
+/* PLY reader with the semantics of loadGaussianCudaFromPly (misc.cu:13-134 +
+ * storeGaussianFromProperty gaussians.cpp:17-30), host side only.  Call with
+ * host_soa == NULL to get the count; then with a buffer of 38*n floats. */
+int gsr_ply_read_host(const char* path, float* host_soa, int64_t capacity, int64_t* n_out);
+
+/* Seeded synthetic scene: writes a standard 62-property
+ * binary_little_endian 3DGS .ply, or fills raw (pre-activation) property
+ * values.  Same generator, same values, for a given (n, seed). */
+int gsr_synth_write_ply(const char* path, int64_t n, uint64_t seed);
+
+/* Camera (camera.cpp): Camera() ctor 8-13, updateCameraMatrices 36-57,
+ * updateFrustumPlanes 59-121, zoom 123-128, orbit 130-158. */
+void gsr_camera_default(gsr_camera* cam);
+void gsr_camera_update(gsr_camera* cam);
+void gsr_camera_update_frustum(gsr_camera* cam);
+void gsr_camera_zoom(gsr_camera* cam, float delta);
+void gsr_camera_orbit(gsr_camera* cam, float azimuth_deg, float elevation_deg);
+/* fx, fy exactly as render.cu:620-621 (tanf computed correctly rounded). */
+void gsr_camera_intrinsics(const gsr_camera* cam, float* fx, float* fy);
+
+/* Device self-test used by the parity tests: for each (x, y) pair of host_in
+ * (2n floats) evaluates on the GPU {gsr_expf(x), gsr_sinf(x), gsr_cosf(x),
+ * gsr_atan2f(x, y), sqrtf(x), x / y, roundf(x), bits(gsr_f2i_sat(1000x))}
+ * into host_out (8n floats), so the CPU twins can be compared bit for bit. */
+int gsr_math_probe(const float* host_in, int n, float* host_out);
+
+const char* gsr_last_error(void);
+const char* gsr_version(void);
+/* 1 if a HIP device is usable, else 0 (never aborts). */
+int gsr_device_available(void);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+
+#include <string>
+/* misc.cuh:4 — C++ linkage, same mangled name as the reference's loader. */
+gsr_gaussian* loadGaussianCudaFromPly(const std::string& filename, int* out_numGaussians);
+#endif
+
+#endif /* GSR_H */

@@ -1,0 +1,104 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so) — TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_float, c_int, c_int64, c_void_p
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+REF_DRIVER = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+
+SPLAT_DTYPE = np.dtype([
+    ("status", "<i4"), ("color", "<f4", 3), ("ndc", "<f4", 3), ("view", "<f4", 3),
+    ("inv_covar", "<f4", 4), ("aabb", "<i4", 4), ("px_x", "<i4"), ("px_y", "<i4"),
+    ("depth_key", "<u4"), ("opacity", "<f4"),
+])
+
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        if not os.path.exists(ORACLE_SO):
+            raise ImportError(f"{ORACLE_SO} missing: run `make -C oracle`")
+        from gaussianrenderer_amd._native import Camera
+        L = ctypes.CDLL(ORACLE_SO)
+        cam = POINTER(Camera)
+        L.orc_ply_read.argtypes = [ctypes.c_char_p, c_void_p, c_int64, POINTER(c_int64)]
+        L.orc_ply_read.restype = c_int
+        L.orc_intrinsics.argtypes = [cam, POINTER(c_float), POINTER(c_float)]
+        L.orc_preprocess.argtypes = [c_void_p, c_int64, cam, c_int, c_int, c_float, c_void_p]
+        L.orc_preprocess.restype = c_int
+        L.orc_render.argtypes = [c_void_p, c_int64, cam, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+                                 c_void_p, c_int]
+        L.orc_render.restype = c_int
+        L.orc_render_tiled.argtypes = [c_void_p, c_int64, cam, c_int, c_int, c_int, c_int, c_int, c_int,
+                                       c_float, c_void_p]
+        L.orc_render_tiled.restype = c_int
+        L.orc_project.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+        L.orc_covariance_chain.argtypes = [c_void_p, c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p,
+                                           c_void_p]
+        for f in ("orc_expf", "orc_sinf", "orc_cosf"):
+            getattr(L, f).argtypes = [c_float]
+            getattr(L, f).restype = c_float
+        L.orc_atan2f.argtypes = [c_float, c_float]
+        L.orc_atan2f.restype = c_float
+        assert SPLAT_DTYPE.itemsize == 88
+        _L = L
+    return _L
+
+
+def ply_read(path: str) -> np.ndarray:
+    n = c_int64(-1)
+    rc = lib().orc_ply_read(path.encode(), None, 0, ctypes.byref(n))
+    if rc:
+        raise IOError(f"orc_ply_read({path}) = {rc}")
+    soa = np.zeros((38, n.value), dtype=np.float32)
+    rc = lib().orc_ply_read(path.encode(), soa.ctypes.data, n.value, ctypes.byref(n))
+    if rc:
+        raise IOError(f"orc_ply_read({path}) = {rc}")
+    return soa
+
+
+def preprocess(soa: np.ndarray, cam, W: int, H: int, k: float) -> np.ndarray:
+    soa = np.ascontiguousarray(soa, dtype=np.float32)
+    n = soa.shape[1]
+    out = np.zeros(n, dtype=SPLAT_DTYPE)
+    lib().orc_preprocess(soa.ctypes.data, n, ctypes.byref(cam), W, H, k, out.ctypes.data)
+    return out
+
+
+def render(soa: np.ndarray, cam, W: int, H: int, k: float, tiling=None, threads: int = 0) -> np.ndarray:
+    soa = np.ascontiguousarray(soa, dtype=np.float32)
+    nx, ny, ws, hs = tiling if tiling else (1, 1, W, H)
+    out = np.zeros((3, H, W), dtype=np.float32)
+    rc = lib().orc_render(soa.ctypes.data, soa.shape[1], ctypes.byref(cam), W, H, nx, ny, ws, hs, k,
+                          out.ctypes.data, threads)
+    assert rc == 0
+    return out
+
+
+def render_tiled(soa: np.ndarray, cam, W: int, H: int, k: float, tiling) -> np.ndarray:
+    soa = np.ascontiguousarray(soa, dtype=np.float32)
+    nx, ny, ws, hs = tiling
+    out = np.zeros((3, H, W), dtype=np.float32)
+    rc = lib().orc_render_tiled(soa.ctypes.data, soa.shape[1], ctypes.byref(cam), W, H, nx, ny, ws, hs, k,
+                                out.ctypes.data)
+    assert rc == 0
+    return out
+
+
+def expected_depth_order(spl: np.ndarray) -> np.ndarray:
+    """(depth_key << 32 | index) of every Gaussian, stable-sorted by key (index tie-break);
+    culled / dropped Gaussians carry key 0xFFFFFFFF."""
+    n = spl.shape[0]
+    keys = np.where(spl["status"] == 2, spl["depth_key"], np.uint32(0xFFFFFFFF)).astype(np.uint64)
+    items = (keys << np.uint64(32)) | np.arange(n, dtype=np.uint64)
+    return np.sort(items, kind="stable")

@@ -1,0 +1,86 @@
+"""The C-ABI library loads on a CPU-only host and exports every symbol that
+include/*.h declares; host-only helpers behave like the reference on errors."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("gsr.h", "gsr_types.h")]
+
+
+def declared_functions():
+    names = set()
+    for h in HEADERS:
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\([^;{]*\)\s*;", src, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def exported_symbols(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_every_declared_symbol_is_exported(gsr):
+    from gaussianrenderer_amd import _native
+    decl = declared_functions()
+    assert {"preprocessCUDAGaussians", "oneSweepSort", "oneSweep3DGaussianSort", "gsr_render",
+            "loadGaussianCudaFromPly"} <= decl
+    syms = exported_symbols(_native.LIB_PATH)
+    missing = [d for d in decl if d != "loadGaussianCudaFromPly" and d not in syms]
+    assert not missing, missing
+    for s in _native.CXX_SYMBOLS:   # C++-linkage loader, misc.cuh:4
+        assert s in syms
+    bound = {name for name, _, _ in _native.SIGNATURES}
+    assert decl - {"loadGaussianCudaFromPly"} <= bound
+
+
+def test_struct_layouts(gsr):
+    from gaussianrenderer_amd import _native
+    assert ctypes.sizeof(_native.Camera) == 484
+    assert _native.Camera.P_matrix.offset == 88 and _native.Camera.r_cam.offset == 316
+    assert gsr.SPLAT_DTYPE.itemsize == 64
+
+
+def test_ply_errors(gsr, tmp_path):
+    L = gsr.lib()
+    n = ctypes.c_int64(-1)
+    assert L.gsr_ply_read_host(str(tmp_path / "nope.ply").encode(), None, 0, ctypes.byref(n)) == -3
+    asc = tmp_path / "a.ply"
+    asc.write_text("ply\nformat ascii 1.0\nelement vertex 1\nproperty float x\nend_header\n1.0\n")
+    assert L.gsr_ply_read_host(str(asc).encode(), None, 0, ctypes.byref(n)) == -4
+    assert n.value == 1     # count is published before the format check, as misc.cu:38
+    assert b"Unsupported PLY format" in L.gsr_last_error()
+    p = tmp_path / "t.ply"
+    gsr.write_synthetic_ply(str(p), 10, 3)
+    data = p.read_bytes()
+    p.write_bytes(data[:-100])
+    soa = np.zeros((38, 10), np.float32)
+    assert L.gsr_ply_read_host(str(p).encode(), soa.ctypes.data, 10, ctypes.byref(n)) == -3
+
+
+def test_synthetic_generator_is_seeded(gsr, tmp_path):
+    a, b, c = (tmp_path / f"{i}.ply" for i in range(3))
+    gsr.write_synthetic_ply(str(a), 100, 5)
+    gsr.write_synthetic_ply(str(b), 100, 5)
+    gsr.write_synthetic_ply(str(c), 100, 6)
+    assert a.read_bytes() == b.read_bytes() != c.read_bytes()
+    soa = gsr.read_ply(str(a))
+    assert soa.shape == (38, 100)
+    assert (soa[0] >= -3).all() and (soa[0] <= 3).all()
+    assert ((soa[3] > 0.26) & (soa[3] < 0.96)).all()          # sigmoid(U(-1, 3))
+    assert ((soa[4:7] > np.exp(-5.66)) & (soa[4:7] < np.exp(-4.06))).all()
+
+
+def test_tiling_information_matches_reference(gsr):
+    t = gsr.TilingInformation(50, 50, 1080, 1920)          # gaussians.hpp:47-49
+    assert (t.width_stride, t.height_stride) == (39, 22)
+    t.resize(480, 640, 50, 50)
+    assert (t.width_stride, t.height_stride) == (13, 10)

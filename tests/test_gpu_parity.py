@@ -1,0 +1,290 @@
+"""GPU parity: the HIP pipeline (through the C ABI) against the CPU oracle on
+the same seeded inputs.  Integer / index outputs (AABBs, pixel centres, depth
+keys, sort orders, tile ranges) must be bit-exact; the image gate is the
+north-star per-pixel L-inf <= 1e-4 (the pipeline is in fact bit-exact, which
+is asserted separately so a regression is visible)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from conftest import scene_soa
+
+pytestmark = pytest.mark.gpu
+
+LINF_TOL = 1e-4          # BASELINE.json north_star: per-pixel L-inf <= 1e-4
+
+
+@pytest.fixture(scope="module")
+def torch(gpu):
+    import torch as t
+    assert t.cuda.is_available()
+    return t
+
+
+@pytest.fixture(scope="module")
+def c1(gpu, tmp_path_factory):
+    return scene_soa(gpu, tmp_path_factory, 10_000, 1)
+
+
+def cam_for(gsr, W, H, pos=(0, 0, 4), look=(0, 0, 0), fov=50):
+    return gsr.make_camera(position=pos, look_at=look, fov_y=fov, aspect=W / H)
+
+
+def render_gpu(gsr, torch, scene, cam, W, H, k=3.0, tiling=None, renderer=None, layout=0, n=None):
+    r = renderer or gsr.Renderer()
+    out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    for _ in range(3):
+        rc = r.render(scene, cam, W, H, out.data_ptr(), k=k, tiling=tiling, layout=layout, n=n)
+        if r.sync() == 0:
+            break
+    return out.view(3, H, W).cpu().numpy(), r
+
+
+def assert_image_parity(got, want):
+    diff = np.abs(got.astype(np.float64) - want.astype(np.float64))
+    linf = float(diff.max()) if diff.size else 0.0
+    assert np.isfinite(got).all()
+    assert linf <= LINF_TOL, f"L-inf {linf} > {LINF_TOL} at {np.unravel_index(diff.argmax(), diff.shape)}"
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"not bit-exact (L-inf {linf})"
+
+
+def test_math_probe_bitwise(gpu, orc):
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.uniform(-100, 90, 40000), rng.uniform(-4, 4, 40000),
+                        rng.standard_normal(20000) * 1e3,
+                        [0.0, -0.0, 0.5, -0.5, 1.5, 2.5, np.inf, -np.inf, np.nan, 1e-40, 88.7, -103.9]])
+    y = np.concatenate([rng.uniform(-5, 5, 100000), np.ones(12)])
+    y[y == 0] = 1.0
+    xy = np.stack([x, y], 1).astype(np.float32)
+    got = gpu.math_probe(xy)
+    L = orc.lib()
+    xs, ys = xy[:, 0], xy[:, 1]
+    ref = np.zeros_like(got)
+    ref[:, 0] = [L.orc_expf(v) for v in xs]
+    ref[:, 1] = [L.orc_sinf(v) for v in xs]
+    ref[:, 2] = [L.orc_cosf(v) for v in xs]
+    ref[:, 3] = [L.orc_atan2f(a, b) for a, b in zip(xs, ys)]
+    with np.errstate(all="ignore"):
+        ref[:, 4] = np.sqrt(xs)
+        ref[:, 5] = xs / ys
+        tr = np.trunc(xs)
+        ref[:, 6] = np.where(np.abs(xs - tr) >= np.float32(0.5), tr + np.sign(xs), tr).astype(np.float32)
+    same = (got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref))
+    for col, name in enumerate(["exp", "sin", "cos", "atan2", "sqrt", "div", "round"]):
+        bad = np.where(~same[:, col])[0]
+        assert bad.size == 0, f"{name}: {bad.size} mismatches, e.g. x={xs[bad[:3]]} y={ys[bad[:3]]} got={got[bad[:3], col]} ref={ref[bad[:3], col]}"
+
+
+CAMS = [dict(pos=(0, 0, 4)), dict(pos=(1.0, 0.5, 3.0), look=(0.2, 0, 0), fov=70), dict(pos=(0, 0, 1.5), fov=90),
+        dict(pos=(-2.5, -1.0, -3.0))]
+
+
+@pytest.mark.parametrize("ci", range(len(CAMS)))
+def test_preprocess_records_bit_exact(gpu, orc, torch, c1, ci):
+    path, soa = c1
+    W, H = 640, 480
+    cam = cam_for(gpu, W, H, **CAMS[ci])
+    scene = gpu.Scene.from_soa(soa)
+    r = gpu.Renderer()
+    r.preprocess(scene, cam, W, H, k=3.0)
+    r.sort()
+    got = r.read_splats(soa.shape[1])
+    want = orc.preprocess(soa, cam, W, H, 3.0)
+    vis = want["status"] == 2
+    assert vis.sum() > 0
+    assert np.array_equal(got["tile_count"][~vis], np.zeros((~vis).sum(), np.uint32))
+    assert (got["depth_key"][~vis] == 0xFFFFFFFF).all()
+    g = got[vis]
+    w = want[vis]
+    assert np.array_equal(g["inv_covar"].view(np.uint32), w["inv_covar"].view(np.uint32))
+    assert np.array_equal(g["color"].view(np.uint32), w["color"].view(np.uint32))
+    assert np.array_equal(g["opacity"].view(np.uint32), w["opacity"].view(np.uint32))
+    assert np.array_equal(g["px_x"], w["px_x"]) and np.array_equal(g["px_y"], w["px_y"])
+    assert np.array_equal(g["x_range"] & 0xFFFF, w["aabb"][:, 0]) and np.array_equal(g["x_range"] >> 16, w["aabb"][:, 2])
+    assert np.array_equal(g["y_range"] & 0xFFFF, w["aabb"][:, 1]) and np.array_equal(g["y_range"] >> 16, w["aabb"][:, 3])
+    assert np.array_equal(g["depth_key"], w["depth_key"])
+    tx, ty = (W + 15) // 16, (H + 15) // 16
+    tx0, tx1 = w["aabb"][:, 0] // 16, np.minimum(tx - 1, w["aabb"][:, 2] // 16)
+    ty0, ty1 = w["aabb"][:, 1] // 16, np.minimum(ty - 1, w["aabb"][:, 3] // 16)
+    assert np.array_equal(g["tile_count"], ((tx1 - tx0 + 1) * (ty1 - ty0 + 1)).astype(np.uint32))
+
+    # depth order: stable by key, index tie-break
+    order = r.read_depth_order(soa.shape[1])
+    assert np.array_equal(order, orc.expected_depth_order(want))
+
+    # pairs: (tile << 32 | index), stable by tile over the depth order
+    idx_sorted = (order & 0xFFFFFFFF).astype(np.int64)
+    idx_sorted = idx_sorted[want["status"][idx_sorted] == 2]
+    a = want["aabb"]
+    ex_tiles = []
+    for i in idx_sorted:
+        x0, x1 = a[i, 0] // 16, min(tx - 1, a[i, 2] // 16)
+        y0, y1 = a[i, 1] // 16, min(ty - 1, a[i, 3] // 16)
+        for yy in range(y0, y1 + 1):
+            for xx in range(x0, x1 + 1):
+                ex_tiles.append((yy * tx + xx, i))
+    ex = np.array(ex_tiles, dtype=np.uint64).reshape(-1, 2)
+    ex_pairs = (ex[:, 0] << np.uint64(32)) | ex[:, 1]
+    ex_pairs = ex_pairs[np.argsort(ex[:, 0], kind="stable")]
+    pairs = r.read_pairs()
+    assert r.pair_count() == ex_pairs.size
+    assert np.array_equal(pairs, ex_pairs)
+    ranges = r.read_tile_ranges()
+    t_of = (ex_pairs >> np.uint64(32)).astype(np.int64)
+    counts = np.bincount(t_of, minlength=tx * ty)
+    nz = counts > 0
+    assert np.array_equal((ranges[nz, 1] - ranges[nz, 0]).astype(np.int64), counts[nz])
+    assert (ranges[~nz, 1] == ranges[~nz, 0]).all()
+
+
+@pytest.mark.parametrize("ci", range(len(CAMS)))
+def test_image_config1_parity(gpu, orc, torch, c1, ci):
+    path, soa = c1
+    W, H = 640, 480
+    cam = cam_for(gpu, W, H, **CAMS[ci])
+    scene = gpu.Scene.from_soa(soa)
+    got, _ = render_gpu(gpu, torch, scene, cam, W, H)
+    want = orc.render(soa, cam, W, H, 3.0)
+    assert (want != 0).sum() > 1000
+    assert_image_parity(got, want)
+
+
+def test_dropin_scene_block_reference_tiling(gpu, orc, torch, c1):
+    """loadGaussianCudaFromPly + preprocessCUDAGaussians (the viewer's calls),
+    reference 50x50 tiling (cull_sort_test.cpp:44-45)."""
+    path, soa = c1
+    W, H = 640, 480
+    ptr, n = gpu.loadGaussianCudaFromPly(path)
+    assert ptr and n == 10_000
+    t = gpu.TilingInformation(50, 50, H, W)
+    cam = cam_for(gpu, W, H)
+    got = gpu.preprocessCUDAGaussians(ptr, n, cam, t.num_tile_y, t.num_tile_x, t.width_stride, t.height_stride,
+                                      W, H, 3.0)
+    want = orc.render(soa, cam, W, H, 3.0, tiling=(50, 50, t.width_stride, t.height_stride))
+    assert_image_parity(got, want)
+    gpu.lib().gsr_scene_free(ptr)
+
+
+def aos_records(soa):
+    n = soa.shape[1]
+    rec = np.zeros((n, 60), dtype=np.float32)           # 240 B (gaussians.hpp:16-30)
+    rec[:, 0:3] = soa[0:3].T                            # x, y, z
+    rec[:, 6:33] = soa[11:38].T                         # sh[27]
+    rec[:, 36] = soa[3]                                 # opacity
+    rec[:, 37:40] = soa[4:7].T                          # scale
+    rec[:, 40:44] = soa[7:11].T                         # rot
+    rec[:, 3:6] = 7.0                                   # normals: ignored
+    rec[:, 33:36] = -1.0                                # color: recomputed
+    return rec
+
+
+def test_dropin_aos_input(gpu, orc, torch, c1):
+    """A reference-layout Gaussian[] device array (e.g. from the reference's own loader)."""
+    path, soa = c1
+    W, H = 320, 240
+    rec = aos_records(soa[:, :4000])
+    dev = torch.from_numpy(rec).cuda()
+    cam = cam_for(gpu, W, H, pos=(0.3, 0.2, 3.5))
+    t = gpu.TilingInformation(40, 40, H, W)
+    got = gpu.preprocessCUDAGaussians(dev.data_ptr(), 4000, cam, t.num_tile_y, t.num_tile_x, t.width_stride,
+                                      t.height_stride, W, H, 3.0)
+    torch.cuda.synchronize()
+    want = orc.render(soa[:, :4000], cam, W, H, 3.0, tiling=(40, 40, t.width_stride, t.height_stride))
+    assert_image_parity(got, want)
+
+
+@pytest.mark.parametrize("tiling", [(8, 8, 40, 30), (7, 3, 92, 160), (3, 5, 100, 100)])
+def test_partial_coverage_tiling(gpu, orc, torch, c1, tiling):
+    path, soa = c1
+    W, H = 640, 480
+    cam = cam_for(gpu, W, H)
+    t = gpu.TilingInformation(1, 1, H, W)
+    t.num_tile_x, t.num_tile_y, t.width_stride, t.height_stride = tiling
+    got, _ = render_gpu(gpu, torch, gpu.Scene.from_soa(soa), cam, W, H, tiling=t)
+    want = orc.render(soa, cam, W, H, 3.0, tiling=tiling)
+    assert_image_parity(got, want)
+
+
+@pytest.mark.parametrize("W,H,k", [(1, 1, 3.0), (37, 23, 3.0), (640, 480, 0.0), (640, 480, 8.0), (17, 300, 2.0)])
+def test_odd_sizes_and_k(gpu, orc, torch, c1, W, H, k):
+    path, soa = c1
+    cam = cam_for(gpu, W, H, fov=60)
+    got, _ = render_gpu(gpu, torch, gpu.Scene.from_soa(soa), cam, W, H, k=k)
+    want = orc.render(soa, cam, W, H, k)
+    assert_image_parity(got, want)
+
+
+def test_empty_and_all_culled(gpu, orc, torch, c1):
+    path, soa = c1
+    W, H = 64, 48
+    cam = cam_for(gpu, W, H)
+    empty = gpu.Scene.from_soa(np.zeros((38, 0), np.float32))
+    got, _ = render_gpu(gpu, torch, empty, cam, W, H)
+    assert not got.any()
+    away = cam_for(gpu, W, H, pos=(0, 0, 4), look=(0, 0, 8))     # looking away from the cloud
+    got, _ = render_gpu(gpu, torch, gpu.Scene.from_soa(soa), away, W, H)
+    want = orc.render(soa, away, W, H, 3.0)
+    assert not want.any()
+    assert_image_parity(got, want)
+
+
+def test_pair_overflow_grows_and_rerenders(gpu, orc, torch):
+    """Huge splats: every one covers the whole image -> P >> the initial capacity."""
+    n = 3000
+    rng = np.random.default_rng(9)
+    soa = np.zeros((38, n), np.float32)
+    soa[0] = rng.uniform(-0.2, 0.2, n); soa[1] = rng.uniform(-0.2, 0.2, n); soa[2] = rng.uniform(-0.2, 0.2, n)
+    soa[3] = rng.uniform(0.01, 0.05, n)
+    soa[4:7] = rng.uniform(1.0, 2.0, (3, n))
+    soa[7] = 1.0
+    soa[11:38] = rng.normal(0, 0.3, (27, n))
+    W, H = 640, 480
+    cam = cam_for(gpu, W, H)
+    r = gpu.Renderer()
+    scene = gpu.Scene.from_soa(soa)
+    out = torch.empty(3 * W * H, device="cuda")
+    r.render(scene, cam, W, H, out.data_ptr())
+    assert r.sync() == -5                      # overflow reported and buffer grown
+    r.render(scene, cam, W, H, out.data_ptr())
+    assert r.sync() == 0
+    assert r.pair_count() > 1_000_000
+    want = orc.render(soa, cam, W, H, 3.0)
+    assert_image_parity(out.view(3, H, W).cpu().numpy(), want)
+
+
+def test_deterministic_and_reusable_context(gpu, torch, c1):
+    path, soa = c1
+    W, H = 640, 480
+    scene = gpu.Scene.from_soa(soa)
+    r = gpu.Renderer()
+    cams = [cam_for(gpu, W, H, **c) for c in CAMS]
+    first = [render_gpu(gpu, torch, scene, c, W, H, renderer=r)[0] for c in cams]
+    second = [render_gpu(gpu, torch, scene, c, W, H, renderer=r)[0] for c in cams]
+    for a, b in zip(first, second):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_orbit_cameras_parity(gpu, orc, torch, tmp_path_factory):
+    """Config-4 shape at reduced size: 8 orbit cameras (azimuth 45 deg * i)."""
+    path, soa = scene_soa(gpu, tmp_path_factory, 20_000, 4)
+    W, H = 480, 270
+    scene = gpu.Scene.from_soa(soa)
+    r = gpu.Renderer()
+    for i in range(8):
+        cam = cam_for(gpu, W, H)
+        gpu.orbit(cam, 45.0 * i, 0.0)
+        got, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
+        want = orc.render(soa, cam, W, H, 3.0)
+        assert_image_parity(got, want)
+
+
+def test_config2_full_parity(gpu, orc, torch, tmp_path_factory):
+    """BASELINE config 2 at full size: 1M Gaussians, 1920x1080."""
+    path, soa = scene_soa(gpu, tmp_path_factory, 1_000_000, 2)
+    W, H = 1920, 1080
+    cam = cam_for(gpu, W, H)
+    got, r = render_gpu(gpu, torch, gpu.Scene.from_ply(path), cam, W, H)
+    want = orc.render(soa, cam, W, H, 3.0, threads=min(16, os.cpu_count() or 1))
+    assert_image_parity(got, want)
