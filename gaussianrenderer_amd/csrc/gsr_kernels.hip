@@ -577,6 +577,7 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
     const int tile = xcd_remap(blockIdx.x, ntiles);
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // each wave owns one 8x8 pixel block of the 16x16 tile, one pixel per lane
     const int bx = tx * GSR_TILE_PX + (w & 1) * 8;
     const int by = ty * GSR_TILE_PX + (w >> 1) * 8;
     const int px = bx + (lane & 7), py = by + (lane >> 3);
@@ -589,7 +590,7 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
     for (uint32_t base = rg.x; base < rg.y; base += kBatch) {
         const uint32_t cnt = min((uint32_t)kBatch, rg.y - base);
         loaded += cnt;
-        __syncthreads();
+        __syncthreads();                                   // previous batch fully consumed
         if ((uint32_t)t < cnt) {
             const uint32_t gi = (uint32_t)pairs[base + t];
             const uint4* R = rec + 4 * (uint64_t)gi;
@@ -599,30 +600,56 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
         }
         __syncthreads();
         if (__ballot(!done) != 0ull) {
-            for (uint32_t s = 0; s < cnt; s++) {
-                const uint4 C = sC[s];
-                const int xmin = (int)(C.z & 0xffffu), xmax = (int)(C.z >> 16);
-                const int ymin = (int)(C.w & 0xffffu), ymax = (int)(C.w >> 16);
-                if (xmax < bx || xmin > bx + 7 || ymax < by || ymin > by + 7) continue;  // wave-uniform
-                if (!done && px >= xmin && px <= xmax && py >= ymin && py <= ymax) {
+            // wave-parallel cull: which splats of the batch touch this wave's 8x8 block
+            uint64_t hit[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t s = q * 64 + lane;
+                bool h = false;
+                if (s < cnt) {
+                    const uint4 C = sC[s];
+                    const int xmin = (int)(C.z & 0xffffu), xmax = (int)(C.z >> 16);
+                    const int ymin = (int)(C.w & 0xffffu), ymax = (int)(C.w >> 16);
+                    h = !(xmax < bx || xmin > bx + 7 || ymax < by || ymin > by + 7);
+                }
+                hit[q] = __ballot(h);
+            }
+            // splats in list order; predicated (branch-free) per-pixel body
+            bool alive = true;
+            auto run = [&](uint64_t m, int q0) {
+                while (m && alive) {
+                    const int s = q0 + __builtin_ctzll(m);
+                    m &= m - 1;
+                    const uint4 C = sC[s];
                     const uint4 A = sA[s];
                     const uint4 B = sB[s];
+                    const int xmin = (int)(C.z & 0xffffu), xmax = (int)(C.z >> 16);
+                    const int ymin = (int)(C.w & 0xffffu), ymax = (int)(C.w >> 16);
+                    const bool in_box = (px >= xmin) & (px <= xmax) & (py >= ymin) & (py <= ymax);
+                    // render.cu:329-340, same operation order
                     const float dx = fpx - (float)(int)C.x;
                     const float dy = fpy - (float)(int)C.y;
                     const float md2 = dx * (__uint_as_float(A.x) * dx + __uint_as_float(A.y) * dy) +
                                       dy * (__uint_as_float(A.z) * dx + __uint_as_float(A.w) * dy);
                     float alpha = __uint_as_float(B.x) * gsr_expf(-0.5f * md2);
                     alpha = fminf(alpha, 0.99f);
-                    if (!(alpha < 1e-3f)) {
-                        cr += __uint_as_float(B.y) * alpha * T;
-                        cg += __uint_as_float(B.z) * alpha * T;
-                        cb += __uint_as_float(B.w) * alpha * T;
-                        T *= (1.0f - alpha);
-                        done = T < 1e-3f;
-                    }
+                    const bool take = in_box & !done & !(alpha < 1e-3f);
+                    const float wr = __uint_as_float(B.y) * alpha * T;
+                    const float wg = __uint_as_float(B.z) * alpha * T;
+                    const float wb = __uint_as_float(B.w) * alpha * T;
+                    const float Tn = T * (1.0f - alpha);
+                    cr = take ? cr + wr : cr;
+                    cg = take ? cg + wg : cg;
+                    cb = take ? cb + wb : cb;
+                    T = take ? Tn : T;
+                    done = done | (take & (Tn < 1e-3f));
+                    alive = __ballot(!done) != 0ull;       // whole block saturated -> stop
                 }
-                if (__ballot(!done) == 0ull) break;
-            }
+            };
+            run(hit[0], 0);
+            run(hit[1], 64);
+            run(hit[2], 128);
+            run(hit[3], 192);
         }
         if (__syncthreads_and(done ? 1 : 0)) break;
     }

@@ -84,13 +84,14 @@ GSR_HD float gsr_pow2i(int e) {
  * subnormal results) is covered with IEEE rounding only.
  */
 GSR_HD float gsr_expf(float x) {
-    if (x != x) return x + x;                 /* NaN */
-    if (x > 88.75f) return gsr_bits_to_float(0x7f800000u);  /* +inf */
-    if (x < -104.0f) return 0.0f;             /* below half the smallest subnormal */
-    const float t = x * 1.44269504088896341f; /* log2(e) */
+    /* Branch-free: evaluate on x clamped into the finite range, then select the
+     * special results (the GPU blend runs this per pixel-splat, where exec-mask
+     * branches cost more than the arithmetic). */
+    const float xc = fminf(fmaxf(x, -104.0f), 88.75f);   /* NaN -> -104 (replaced below) */
+    const float t = xc * 1.44269504088896341f;            /* log2(e) */
     const float n = rintf(t);
-    float r = __builtin_fmaf(-n, 0.693359375f, x);       /* ln2 hi part (exact product) */
-    r = __builtin_fmaf(-n, -2.12194440e-4f, r);          /* ln2 lo part */
+    float r = __builtin_fmaf(-n, 0.693359375f, xc);       /* ln2 hi part (exact product) */
+    r = __builtin_fmaf(-n, -2.12194440e-4f, r);           /* ln2 lo part */
     float p = 1.9875691500e-4f;
     p = __builtin_fmaf(p, r, 1.3981999507e-3f);
     p = __builtin_fmaf(p, r, 8.3334519073e-3f);
@@ -99,10 +100,14 @@ GSR_HD float gsr_expf(float x) {
     p = __builtin_fmaf(p, r, 5.0000001201e-1f);
     const float r2 = r * r;
     const float y = __builtin_fmaf(p, r2, r) + 1.0f;
-    const int ni = (int)n;                    /* |n| <= 151 here */
+    const int ni = (int)n;                                /* n in [-150, 128] */
     const int e1 = ni / 2;
     const int e2 = ni - e1;
-    return (y * gsr_pow2i(e1)) * gsr_pow2i(e2);
+    float res = (y * gsr_pow2i(e1)) * gsr_pow2i(e2);
+    res = (x < -104.0f) ? 0.0f : res;                     /* below half the smallest subnormal */
+    res = (x > 88.75f) ? gsr_bits_to_float(0x7f800000u) : res;
+    res = (x != x) ? x + x : res;                         /* NaN */
+    return res;
 }
 
 /* Polynomial cores on |r| <= pi/4 (Cephes sinf / cosf). */
