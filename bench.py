@@ -124,7 +124,8 @@ def main():
     r.sync()
     stages, _ = r.stage_times()
     pairs = r.pair_count()
-    consumed = r.blend_records_loaded()
+    counters = r.blend_counters()
+    consumed = counters["records_loaded"]
     r.set_diagnostics(False)
     tiles_x, tiles_y = r.tile_grid()
 
@@ -194,6 +195,8 @@ def main():
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
         "pairs": pairs,
         "pairs_consumed": consumed,
+        "blend_counters": counters,
+        "blend_lane_efficiency": round(counters["active_lanes"] / max(1, 64 * counters["wave_splat_iters"]), 4),
         "image_mean": float(img.mean().item()),
         "overflow_after_timed": overflow,
     }

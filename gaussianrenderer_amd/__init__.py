@@ -249,6 +249,13 @@ class Renderer:
     def blend_records_loaded(self) -> int:
         return int(lib().gsr_blend_records_loaded(self.ctx))
 
+    def blend_counters(self) -> dict:
+        v = np.zeros(8, dtype=np.int64)
+        check(lib().gsr_blend_counters(self.ctx, v.ctypes.data), "gsr_blend_counters")
+        keys = ("records_loaded", "wave_splat_iters", "active_lanes", "taken_lanes", "iters_no_active",
+                "iters_skipped_cutoff")
+        return dict(zip(keys, (int(x) for x in v)))
+
     def stage_times(self):
         ms = (ctypes.c_double * NUM_STAGES)()
         frames = c_int64()

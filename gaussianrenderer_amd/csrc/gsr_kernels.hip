@@ -566,13 +566,27 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
+// md2 cutoff of one splat: alpha = fminf(op * exp(-md2/2), 0.99) < 1e-3 holds
+// for every md2 > 2 ln(1000 op) (exp and the product are within a few ulp), so
+// lanes beyond the returned bound can never composite.  The bound is padded by
+// 1e-5 relative + 1e-3 absolute — orders of magnitude above the rounding of
+// gsr_expf, the product and the hardware log2 used here — and is NaN (never
+// skip) for NaN opacity, +inf for infinite opacity, -inf for op <= 0.  It only
+// decides whether a wave may SKIP work; it never changes a composited value.
+__device__ __forceinline__ float md2_cutoff(float op) {
+    const float l = __log2f(op * 1000.0f);                   // v_log_f32
+    return (l * 1.38629436111989061f) * 1.00001f + 1e-3f;     // 2 ln2 log2(1000 op)
+}
+
+template <bool DIAG>
 __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pairs,
                                                 const uint2* __restrict__ ranges,
                                                 const uint4* __restrict__ rec, int tiles_x, int tiles_y,
                                                 int W, int H, int cover_w, int cover_h,
                                                 float* __restrict__ out,
-                                                unsigned long long* __restrict__ consumed) {
+                                                unsigned long long* __restrict__ counters) {
     __shared__ uint4 sA[kBatch], sB[kBatch], sC[kBatch];
+    __shared__ float sCut[kBatch];
     const int ntiles = tiles_x * tiles_y;
     const int tile = xcd_remap(blockIdx.x, ntiles);
     const int tx = tile % tiles_x, ty = tile / tiles_x;
@@ -583,23 +597,27 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
     const int px = bx + (lane & 7), py = by + (lane >> 3);
     const bool inside = px < cover_w && py < cover_h;
     const float fpx = (float)px, fpy = (float)py;
-    float T = 1.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f;
-    bool done = !inside;
+    // transmittance; a pixel is saturated ("done", render.cu:328) iff T < 1e-3.
+    // Pixels outside the covered area start saturated (T = 0) and write 0.
+    float T = inside ? 1.0f : 0.0f;
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
     const uint2 rg = ranges[tile];
-    uint32_t loaded = 0;
+    uint64_t d_loaded = 0, d_iter = 0, d_active = 0, d_taken = 0, d_zero_active = 0, d_skipped = 0;
     for (uint32_t base = rg.x; base < rg.y; base += kBatch) {
         const uint32_t cnt = min((uint32_t)kBatch, rg.y - base);
-        loaded += cnt;
+        if (DIAG) d_loaded += cnt;
         __syncthreads();                                   // previous batch fully consumed
         if ((uint32_t)t < cnt) {
             const uint32_t gi = (uint32_t)pairs[base + t];
             const uint4* R = rec + 4 * (uint64_t)gi;
+            const uint4 b4 = R[1];
             sA[t] = R[0];
-            sB[t] = R[1];
+            sB[t] = b4;
             sC[t] = R[2];
+            sCut[t] = md2_cutoff(__uint_as_float(b4.x));
         }
         __syncthreads();
-        if (__ballot(!done) != 0ull) {
+        if (__ballot(!(T < 1e-3f)) != 0ull) {
             // wave-parallel cull: which splats of the batch touch this wave's 8x8 block
             uint64_t hit[4];
 #pragma unroll
@@ -622,18 +640,30 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
                     m &= m - 1;
                     const uint4 C = sC[s];
                     const uint4 A = sA[s];
-                    const uint4 B = sB[s];
+                    const float cut = sCut[s];
                     const int xmin = (int)(C.z & 0xffffu), xmax = (int)(C.z >> 16);
                     const int ymin = (int)(C.w & 0xffffu), ymax = (int)(C.w >> 16);
-                    const bool in_box = (px >= xmin) & (px <= xmax) & (py >= ymin) & (py <= ymax);
+                    const bool live = (px >= xmin) & (px <= xmax) & (py >= ymin) & (py <= ymax) &
+                                      !(T < 1e-3f);
                     // render.cu:329-340, same operation order
                     const float dx = fpx - (float)(int)C.x;
                     const float dy = fpy - (float)(int)C.y;
                     const float md2 = dx * (__uint_as_float(A.x) * dx + __uint_as_float(A.y) * dy) +
                                       dy * (__uint_as_float(A.z) * dx + __uint_as_float(A.w) * dy);
+                    if (DIAG) {
+                        d_iter += 1;
+                        const uint64_t act = __ballot(live);
+                        d_active += (uint64_t)__popcll(act);
+                        d_zero_active += act == 0ull;
+                    }
+                    if (__ballot(live & !(md2 > cut)) == 0ull) {   // no lane can reach alpha >= 1e-3
+                        if (DIAG) d_skipped += 1;
+                        continue;
+                    }
+                    const uint4 B = sB[s];
                     float alpha = __uint_as_float(B.x) * gsr_expf(-0.5f * md2);
                     alpha = fminf(alpha, 0.99f);
-                    const bool take = in_box & !done & !(alpha < 1e-3f);
+                    const bool take = live & !(alpha < 1e-3f);
                     const float wr = __uint_as_float(B.y) * alpha * T;
                     const float wg = __uint_as_float(B.z) * alpha * T;
                     const float wb = __uint_as_float(B.w) * alpha * T;
@@ -642,8 +672,8 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
                     cg = take ? cg + wg : cg;
                     cb = take ? cb + wb : cb;
                     T = take ? Tn : T;
-                    done = done | (take & (Tn < 1e-3f));
-                    alive = __ballot(!done) != 0ull;       // whole block saturated -> stop
+                    if (DIAG) d_taken += (uint64_t)__popcll(__ballot(take));
+                    alive = __ballot(!(T < 1e-3f)) != 0ull;   // whole block saturated -> stop
                 }
             };
             run(hit[0], 0);
@@ -651,9 +681,18 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
             run(hit[2], 128);
             run(hit[3], 192);
         }
-        if (__syncthreads_and(done ? 1 : 0)) break;
+        if (__syncthreads_and((T < 1e-3f) ? 1 : 0)) break;
     }
-    if (consumed && t == 0 && loaded) atomicAdd(consumed, (unsigned long long)loaded);
+    if (DIAG) {
+        if (t == 0 && d_loaded) atomicAdd(counters, (unsigned long long)d_loaded);
+        if (lane == 0) {
+            atomicAdd(counters + 1, (unsigned long long)d_iter);
+            atomicAdd(counters + 2, (unsigned long long)d_active);
+            atomicAdd(counters + 3, (unsigned long long)d_taken);
+            atomicAdd(counters + 4, (unsigned long long)d_zero_active);
+            atomicAdd(counters + 5, (unsigned long long)d_skipped);
+        }
+    }
     if (px < W && py < H) {
         const size_t o = (size_t)py * (size_t)W + (size_t)px;
         const size_t hw = (size_t)W * (size_t)H;
@@ -736,8 +775,12 @@ hipError_t launch_blend(const uint64_t* pairs, const uint2* ranges, const uint4*
                         float* out, unsigned long long* consumed, hipStream_t s) {
     const int nt = fr.tiles_x * fr.tiles_y;
     if (nt <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_blend, dim3(nt), dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x, fr.tiles_y, fr.W,
-                       fr.H, fr.cover_w, fr.cover_h, out, consumed);
+    if (consumed)
+        hipLaunchKernelGGL(k_blend<true>, dim3(nt), dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x, fr.tiles_y,
+                           fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
+    else
+        hipLaunchKernelGGL(k_blend<false>, dim3(nt), dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x,
+                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
     return hipGetLastError();
 }
 

@@ -729,9 +729,9 @@ static int blend_locked(gsr_context* c, float* d_out) {
     mark(c, GSR_STAGE_BLEND);
     if (c->diagnostics) {
         if (!c->consumed) {
-            if (int rc = realloc_dev(&c->consumed, 1)) return rc;
+            if (int rc = realloc_dev(&c->consumed, 8)) return rc;
         }
-        HIP_TRY(hipMemsetAsync(c->consumed, 0, sizeof(unsigned long long), c->stream));
+        HIP_TRY(hipMemsetAsync(c->consumed, 0, 8 * sizeof(unsigned long long), c->stream));
     }
     HIP_TRY(gsr::launch_blend(c->pairs[c->pair_buf], c->ranges, c->rec, c->fr, d_out,
                               c->diagnostics ? c->consumed : nullptr, c->stream));
@@ -875,12 +875,19 @@ extern "C" int gsr_set_diagnostics(gsr_context* c, int on) {
 }
 
 extern "C" int64_t gsr_blend_records_loaded(gsr_context* c) {
-    if (!c || !c->consumed) return -1;
+    int64_t v[8];
+    if (gsr_blend_counters(c, v)) return -1;
+    return v[0];
+}
+
+extern "C" int gsr_blend_counters(gsr_context* c, int64_t* out4) {
+    if (!c || !c->consumed || !out4) return set_err(GSR_E_ARG, "gsr_blend_counters: diagnostics were off");
     std::lock_guard<std::mutex> lk(c->mu);
-    unsigned long long v = 0;
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
-    if (hipMemcpy(&v, c->consumed, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    return (int64_t)v;
+    unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(v, c->consumed, sizeof v, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 8; i++) out4[i] = (int64_t)v[i];
+    return GSR_OK;
 }
 
 // ------------------------------------------------------------------ math probe

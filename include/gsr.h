@@ -155,6 +155,12 @@ int gsr_stage_times(gsr_context* ctx, double* ms_out /* GSR_NUM_STAGES */, int64
  * a tile saturates); gsr_blend_records_loaded() returns the last frame's Pc. */
 int gsr_set_diagnostics(gsr_context* ctx, int on);
 int64_t gsr_blend_records_loaded(gsr_context* ctx);
+/* All blend counters of the last diagnostics frame (8 values): {records
+ * loaded (Pc), wave-splat iterations, active lanes (in AABB and not
+ * saturated), lanes that composited, iterations with no active lane,
+ * iterations skipped by the per-splat md2 cutoff, 0, 0};
+ * lane efficiency = active / (64 * iterations). */
+int gsr_blend_counters(gsr_context* ctx, int64_t* out8);
 
 /* ---------------------------------------------------------------- scenes */
 

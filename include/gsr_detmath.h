@@ -84,9 +84,10 @@ GSR_HD float gsr_pow2i(int e) {
  * subnormal results) is covered with IEEE rounding only.
  */
 GSR_HD float gsr_expf(float x) {
-    /* Branch-free: evaluate on x clamped into the finite range, then select the
-     * special results (the GPU blend runs this per pixel-splat, where exec-mask
-     * branches cost more than the arithmetic). */
+    /* Branch-free: evaluate on x clamped into [-104, 88.75].  The clamp alone
+     * yields the right special results: 2^-150 * e^(-104 + 150 ln2) rounds to
+     * +0 for every x <= -104, and 2^128 * e^(88.75 - 128 ln2) overflows to +inf
+     * for every x >= 88.75 (ln FLT_MAX = 88.7228); only NaN needs a select. */
     const float xc = fminf(fmaxf(x, -104.0f), 88.75f);   /* NaN -> -104 (replaced below) */
     const float t = xc * 1.44269504088896341f;            /* log2(e) */
     const float n = rintf(t);
@@ -103,11 +104,8 @@ GSR_HD float gsr_expf(float x) {
     const int ni = (int)n;                                /* n in [-150, 128] */
     const int e1 = ni / 2;
     const int e2 = ni - e1;
-    float res = (y * gsr_pow2i(e1)) * gsr_pow2i(e2);
-    res = (x < -104.0f) ? 0.0f : res;                     /* below half the smallest subnormal */
-    res = (x > 88.75f) ? gsr_bits_to_float(0x7f800000u) : res;
-    res = (x != x) ? x + x : res;                         /* NaN */
-    return res;
+    const float res = (y * gsr_pow2i(e1)) * gsr_pow2i(e2);
+    return (x != x) ? x + x : res;                        /* NaN */
 }
 
 /* Polynomial cores on |r| <= pi/4 (Cephes sinf / cosf). */

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run (rocprofv3 csv) into a text table.
+
+Per kernel: calls, average duration (kernel trace), and per-launch HBM traffic
+from the separate FETCH_SIZE / WRITE_SIZE passes.  Units and gfx950
+corrections follow MI355X_MICROARCH.md section HBM: the counters are in KiB
+(x1024) and FETCH_SIZE reads half the bytes of a wide coalesced stream, so the
+corrected read traffic is reported as 2 x FETCH_SIZE next to the raw value.
+
+    python tools/summarize_prof.py gpurun_out/prof > profiles/r01_rocprof_summary.txt
+"""
+import collections
+import csv
+import os
+import re
+import sys
+
+
+def short(name: str) -> str:
+    m = re.search(r"(k_\w+)", name)
+    if m:
+        return m.group(1)
+    return name.split("(")[0][:60]
+
+
+def main(d):
+    stats = list(csv.DictReader(open(os.path.join(d, "kt", "kt_kernel_stats.csv"))))
+    pmc = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        p = os.path.join(d, f"pmc_{c}", "pmc_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        agg = collections.defaultdict(list)
+        for r in csv.DictReader(open(p)):
+            agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)
+        pmc[c] = {k: sum(v) / len(v) for k, v in agg.items()}
+    print("rocprofv3 --kernel-trace --stats; PMC FETCH_SIZE and WRITE_SIZE in separate passes")
+    print(f"{'kernel':<34}{'calls':>7}{'avg_us':>10}{'pct':>7}{'FETCH_MB':>10}{'2xFETCH_MB':>12}{'WRITE_MB':>10}{'GB/s(2xF+W)':>13}")
+    for r in stats:
+        k = short(r["Name"])
+        avg_us = float(r["AverageNs"]) / 1e3
+        f = pmc.get("FETCH_SIZE", {}).get(k)
+        w = pmc.get("WRITE_SIZE", {}).get(k)
+        fmt = lambda v: f"{v / 1e6:10.2f}" if v is not None else f"{'-':>10}"
+        gbs = (2 * f + w) / (avg_us * 1e-6) / 1e9 if (f is not None and w is not None and avg_us > 0) else None
+        print(f"{k:<34}{int(r['Calls']):>7}{avg_us:>10.2f}{float(r['Percentage']):>7.2f}{fmt(f)}"
+              f"{(f'{2 * f / 1e6:12.2f}' if f is not None else f'{chr(45):>12}')}{fmt(w)}"
+              f"{(f'{gbs:13.1f}' if gbs is not None else f'{chr(45):>13}')}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof")
