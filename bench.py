@@ -10,10 +10,12 @@ fovY 50, k = 3), with the scene and the output image resident in HBM.
 
 Multi-GPU (config 4 semantics, launched by torch.distributed.run): one process
 per GPU, each rank renders its own orbit camera (azimuth 45 deg * rank) of the
-replicated scene; frames shard with no data-path collective (weak scaling).
-Finished frames are gathered to rank 0 over RCCL (torch.distributed, backend
-nccl) once after the timed region — the offline-render hand-off — and the
-gather time is reported separately.
+replicated scene; frames shard with no collective inside the render (weak
+scaling).  With --gather step (default for N > 1) every finished frame is
+handed to rank 0 by an RCCL gather over xGMI (torch.distributed, backend
+nccl), issued asynchronously and overlapped with the next frame's render
+(double-buffered); --gather end hands over only the last frame, after the
+timed region.  gaussianrenderer_amd/multi.py holds the per-rank logic.
 
 Rank 0 prints ONE JSON line (contract in the task statement), including the
 blend kernel's roofline (HIP events around every blend launch inside the timed
@@ -50,6 +52,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-oracle sample length")
     ap.add_argument("--scene-dir", default=None)
+    ap.add_argument("--gather", choices=("step", "end", "none"), default="step",
+                    help="N>1: RCCL gather of finished frames to rank 0 every step (overlapped) or once at the end")
     return ap.parse_args()
 
 
@@ -76,12 +80,10 @@ def cpu_baseline(soa, cam, W, H, k, seconds):
 
 def main():
     args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-
-    import numpy as np
     import torch  # noqa: E402  (before gaussianrenderer_amd: one HIP runtime)
+    from gaussianrenderer_amd import multi
+    info = multi.rank_info()
+    rank, world, local_rank = info.rank, info.world, info.local_rank
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
@@ -100,27 +102,40 @@ def main():
     if dist:
         dist.barrier()
     scene = gsr.Scene.from_ply(ply)           # the drop-in loader path (misc.cu:13-134)
-    cam = gsr.make_camera(position=(0, 0, 4), fov_y=50, aspect=W / H)
-    if world > 1:
-        gsr.orbit(cam, 45.0 * rank, 0.0)         # config 4: one orbit camera per GPU
+    cam = multi.orbit_camera(rank, W, H)      # rank 0: camera (0,0,4); config 4: orbit 45 deg * rank
 
     r = gsr.Renderer()
-    out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    nbuf = 2 if (dist and args.gather == "step") else 1
+    outs = [torch.empty(3 * W * H, dtype=torch.float32, device="cuda") for _ in range(nbuf)]
+    recv = ([[torch.empty_like(outs[0]) for _ in range(world)] for _ in range(nbuf)]
+            if (dist and rank == 0 and args.gather == "step") else None)
     stream = torch.cuda.current_stream().cuda_stream
+    pending = [None] * nbuf
 
-    def frame():
-        r.render(scene, cam, W, H, out.data_ptr(), k=args.k, stream=stream)
+    def frame(i=0):
+        b = i % nbuf
+        if pending[b] is not None:
+            pending[b].wait()                   # stream-wait: gather of this buffer done
+            pending[b] = None
+        r.render(scene, cam, W, H, outs[b].data_ptr(), k=args.k, stream=stream)
+        if dist and args.gather == "step":
+            pending[b] = dist.gather(outs[b], recv[b] if recv else None, dst=0, async_op=True)
 
     # warmup (+ grow the pair buffer to the high-water mark)
-    for _ in range(max(1, args.warmup)):
-        frame()
+    for i in range(max(1, args.warmup)):
+        frame(i)
     while r.sync() != 0:
         frame()
+    for b in range(nbuf):
+        if pending[b] is not None:
+            pending[b].wait()
+            pending[b] = None
+    torch.cuda.synchronize()
 
-    # untimed diagnostic frame: per-stage breakdown, P and Pc
+    # untimed diagnostic frame: per-stage breakdown, P, Pc and blend counters
     r.set_timing(2)
     r.set_diagnostics(True)
-    frame()
+    r.render(scene, cam, W, H, outs[0].data_ptr(), k=args.k, stream=stream)
     r.sync()
     stages, _ = r.stage_times()
     pairs = r.pair_count()
@@ -135,8 +150,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        frame()
+    for i in range(args.steps):
+        frame(i)
+    for b in range(nbuf):
+        if pending[b] is not None:
+            pending[b].wait()
+            pending[b] = None
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -146,18 +165,14 @@ def main():
     r.set_timing(0)
     overflow = r.sync()
 
-    elapsed_t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    max_elapsed = multi.max_over_ranks(dist, elapsed, "cuda")
     gather_ms = None
-    if dist:
-        dist.all_reduce(elapsed_t, op=dist.ReduceOp.MAX)
-        # offline-render hand-off: finished frames to rank 0 over RCCL (xGMI)
+    if dist and args.gather == "end":
         torch.cuda.synchronize()
         g0 = time.perf_counter()
-        gl = [torch.empty_like(out) for _ in range(world)] if rank == 0 else None
-        dist.gather(out, gl, dst=0)
+        multi.gather_frames(dist, outs[0])
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) * 1e3
-    max_elapsed = float(elapsed_t.item())
 
     if rank != 0:
         if dist:
@@ -170,7 +185,7 @@ def main():
     ntiles = tiles_x * tiles_y
     bytes_blend = algorithmic_blend_bytes(ntiles, consumed, W, H)
     achieved = bytes_blend / (blend_avg_ms * 1e-3) / 1e9
-    img = out.view(3, H, W)
+    img = outs[0].view(3, H, W)
     result = {
         "metric": "frames/sec at 1920x1080, 1M Gaussians (config %d)" % args.config if args.config == 2
         else f"frames/sec (config {args.config})",
@@ -186,7 +201,8 @@ def main():
         "dtype": "f32",
         "data": "synthetic (seeded 3DGS .ply, SURVEY.md 8d)",
         "config": {"workload": f"config{args.config}: {n} Gaussians, {W}x{H}, k={args.k}, "
-                               f"{'one orbit camera per GPU' if world > 1 else 'camera (0,0,4) fovY 50'}",
+                               + (f"one orbit camera per GPU, RCCL gather to rank 0 ({args.gather})" if world > 1
+                                  else "camera (0,0,4) fovY 50"),
                    "gaussians": n, "width": W, "height": H, "parallelism": f"frames{world}"},
         "roofline": {"bound": "hbm", "kernel": "k_blend", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
