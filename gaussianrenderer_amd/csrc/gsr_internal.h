@@ -26,8 +26,7 @@ struct Frame {
 
 // Radix-sort geometry.
 constexpr int kSortThreads = 256;
-constexpr int kSortItems = 16;                          // per thread per tile
-constexpr int kSortTile = kSortThreads * kSortItems;    // 4096 items per tile
+constexpr int kSortTile = kSortThreads * 16;           // largest tile (items = 16 per thread)
 constexpr int kMaxSortGroups = 1024;                    // fixed grid upper bound
 
 // Device-side frame statistics block (device memory).
@@ -44,14 +43,15 @@ hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, con
                              uint4* rec, uint64_t* items, hipStream_t s);
 // One stable LSD pass over u64 items on bits [shift, shift + bits) (bits <= 8).
 // n = n_dev ? *n_dev : n_host.  hist: 256 * groups u32, totals: 256 u32.
+// ranges (nullable, final tile-sort pass): per-tile {~start, end} of key (item >> 32),
+// zeroed beforehand.
+// items: 8 or 16 per thread (tile = 256 * items); groups from sort_groups().
 hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
-                             int shift, int bits, int groups, uint32_t* hist, uint32_t* totals,
-                             hipStream_t s);
+                             int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
+                             uint2* ranges, hipStream_t s);
 hipError_t launch_emit(const uint64_t* depth_sorted, uint32_t n, const uint4* rec, int groups,
                        unsigned long long* wg_scratch, Stats* stats, Stats* host_mapped_stats,
                        uint32_t pair_capacity, int tiles_x, uint64_t* pairs, hipStream_t s);
-hipError_t launch_tile_ranges(const uint64_t* pairs, const Stats* stats, uint2* ranges, int num_tiles,
-                              hipStream_t s);
 // consumed: optional device counter of splat records loaded (diagnostics).
 hipError_t launch_blend(const uint64_t* pairs, const uint2* ranges, const uint4* rec, const Frame& fr,
                         float* out, unsigned long long* consumed, hipStream_t s);

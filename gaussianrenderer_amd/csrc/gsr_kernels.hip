@@ -10,7 +10,7 @@
 //                     (tile << 32 | index) pair per covered 16x16 tile
 //                     [render.cu:811-857, 788-809]
 //   radix passes      stable LSD sort of the pairs by tile id (2 x <= 8 bits)
-//   k_tile_ranges     [start, end) of each tile from adjacent-key boundaries
+//                     (the last tile pass also records each tile's [start, end))
 //   k_blend           one workgroup per 16x16 tile, one pixel per lane, 8x8 pixel
 //                     block per wave64; LDS-staged batches of 256 splat records;
 //                     exact per-pixel early termination [render.cu:266-367]
@@ -311,6 +311,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
 // wave64 ballot matching (the AMD stand-in for __match_any), scatters into LDS
 // in digit order and writes runs out coalesced.
 
+template <int ITEMS>
 __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* __restrict__ in,
                                                                 const uint32_t* __restrict__ n_dev,
                                                                 uint32_t n_host, int shift, uint32_t mask,
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
     __syncthreads();
     const uint64_t n = n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
     uint64_t b, e;
-    chunk_range(n, groups, blockIdx.x, kSortTile, b, e);
+    chunk_range(n, groups, blockIdx.x, kSortThreads * ITEMS, b, e);
     uint64_t i = b + t;
     for (; i + 3 * kSortThreads < e; i += 4 * kSortThreads) {
         const uint64_t v0 = in[i], v1 = in[i + kSortThreads], v2 = in[i + 2 * kSortThreads],
@@ -359,11 +360,13 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
     if (threadIdx.x == 0) totals[blockIdx.x] = total;
 }
 
+template <int ITEMS>
 __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const uint64_t* __restrict__ in, uint64_t* __restrict__ out, const uint32_t* __restrict__ n_dev,
     uint32_t n_host, int shift, int bits, int groups, const uint32_t* __restrict__ hist,
-    const uint32_t* __restrict__ totals) {
-    __shared__ uint64_t s_items[kSortTile];     // 32 KB
+    const uint32_t* __restrict__ totals, uint2* __restrict__ ranges) {
+    constexpr int kTile = kSortThreads * ITEMS;
+    __shared__ uint64_t s_items[kTile];
     __shared__ uint32_t s_wc[4][256];           // per-wave digit counters, then wave bases
     __shared__ uint32_t s_gbase[256];           // running global offset per digit
     __shared__ uint32_t s_lbase[256];           // tile-local exclusive base per digit
@@ -374,7 +377,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const uint32_t mask = (1u << bits) - 1u;
     const uint64_t n = n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
     uint64_t b, e;
-    chunk_range(n, groups, blockIdx.x, kSortTile, b, e);
+    chunk_range(n, groups, blockIdx.x, kTile, b, e);
     if (b >= e) return;                          // uniform per workgroup
 
     // global base of each digit for this workgroup
@@ -385,22 +388,22 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     }
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
-    for (uint64_t tb = b; tb < e; tb += kSortTile) {
-        const uint32_t tn = (uint32_t)min((uint64_t)kSortTile, e - tb);
+    for (uint64_t tb = b; tb < e; tb += kTile) {
+        const uint32_t tn = (uint32_t)min((uint64_t)kTile, e - tb);
 #pragma unroll
         for (int k = 0; k < 4; k++) s_wc[k][t] = 0;
         __syncthreads();
 
-        uint64_t it[kSortItems];
-        uint32_t rk[kSortItems];
-        const uint32_t wbase = w * 64 * kSortItems;
+        uint64_t it[ITEMS];
+        uint32_t rk[ITEMS];
+        const uint32_t wbase = w * 64 * ITEMS;
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
+        for (int k = 0; k < ITEMS; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             it[k] = (el < tn) ? in[tb + el] : 0ull;
         }
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
+        for (int k = 0; k < ITEMS; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             const bool valid = el < tn;
             const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
@@ -434,7 +437,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
+        for (int k = 0; k < ITEMS; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             if (el < tn) {
                 const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
@@ -445,7 +448,17 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
         for (uint32_t q = t; q < tn; q += kSortThreads) {
             const uint64_t v = s_items[q];
             const uint32_t d = (uint32_t)(v >> shift) & mask;
-            out[(uint64_t)s_gbase[d] + (q - s_lbase[d])] = v;
+            const uint32_t dst = s_gbase[d] + (q - s_lbase[d]);
+            out[dst] = v;
+            if (ranges) {
+                // final pass of the tile sort: the LDS tile is fully sorted, so each
+                // run of one tile key is contiguous; record its global [start, end)
+                // as {~start, end} with atomicMax, so a zeroed array means "empty"
+                // (replaces a separate boundary-detection kernel).
+                const uint32_t key = (uint32_t)(v >> 32);
+                if (q == 0 || (uint32_t)(s_items[q - 1] >> 32) != key) atomicMax(&ranges[key].x, ~dst);
+                if (q == tn - 1 || (uint32_t)(s_items[q + 1] >> 32) != key) atomicMax(&ranges[key].y, dst + 1);
+            }
         }
         __syncthreads();
         s_gbase[t] += tcount;
@@ -542,19 +555,6 @@ __global__ __launch_bounds__(256) void k_emit_pairs(const uint64_t* __restrict__
     }
 }
 
-// ------------------------------------------------------------------ tile ranges
-
-__global__ __launch_bounds__(256) void k_tile_ranges(const uint64_t* __restrict__ pairs,
-                                                      const Stats* __restrict__ st,
-                                                      uint2* __restrict__ ranges) {
-    const uint32_t n = st->pairs_eff;
-    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) {
-        const uint32_t tl = (uint32_t)(pairs[p] >> 32);
-        if (p == 0 || (uint32_t)(pairs[p - 1] >> 32) != tl) ranges[tl].x = p;
-        if (p == n - 1 || (uint32_t)(pairs[p + 1] >> 32) != tl) ranges[tl].y = p + 1;
-    }
-}
-
 // ------------------------------------------------------------------ blend
 
 constexpr int kBatch = 256;
@@ -601,7 +601,8 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
     // Pixels outside the covered area start saturated (T = 0) and write 0.
     float T = inside ? 1.0f : 0.0f;
     float cr = 0.0f, cg = 0.0f, cb = 0.0f;
-    const uint2 rg = ranges[tile];
+    const uint2 rr = ranges[tile];                       // {~start, end}, zero = empty
+    const uint2 rg = make_uint2(rr.y ? ~rr.x : 0u, rr.y);
     uint64_t d_loaded = 0, d_iter = 0, d_active = 0, d_taken = 0, d_zero_active = 0, d_skipped = 0;
     for (uint32_t base = rg.x; base < rg.y; base += kBatch) {
         const uint32_t cnt = min((uint32_t)kBatch, rg.y - base);
@@ -740,15 +741,24 @@ hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, con
     return hipGetLastError();
 }
 
-hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
-                             int shift, int bits, int groups, uint32_t* hist, uint32_t* totals,
-                             hipStream_t s) {
+template <int ITEMS>
+static void radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host, int shift,
+                       int bits, int groups, uint32_t* hist, uint32_t* totals, uint2* ranges, hipStream_t s) {
     const uint32_t mask = (1u << bits) - 1u;
-    hipLaunchKernelGGL(k_radix_upsweep, dim3(groups), dim3(kSortThreads), 0, s, in, n_dev, n_host, shift,
+    hipLaunchKernelGGL(k_radix_upsweep<ITEMS>, dim3(groups), dim3(kSortThreads), 0, s, in, n_dev, n_host, shift,
                        mask, groups, hist);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, hist, groups, totals);
-    hipLaunchKernelGGL(k_radix_downsweep, dim3(groups), dim3(kSortThreads), 0, s, in, out, n_dev, n_host,
-                       shift, bits, groups, hist, totals);
+    hipLaunchKernelGGL(k_radix_downsweep<ITEMS>, dim3(groups), dim3(kSortThreads), 0, s, in, out, n_dev, n_host,
+                       shift, bits, groups, hist, totals, ranges);
+}
+
+hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
+                             int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
+                             uint2* ranges, hipStream_t s) {
+    if (items == 8)
+        radix_pass<8>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, s);
+    else
+        radix_pass<16>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, s);
     return hipGetLastError();
 }
 
@@ -760,14 +770,6 @@ hipError_t launch_emit(const uint64_t* depth_sorted, uint32_t n, const uint4* re
                        host_mapped_stats);
     hipLaunchKernelGGL(k_emit_pairs, dim3(groups), dim3(256), 0, s, depth_sorted, n, rec, groups, wg_scratch,
                        pair_capacity, tiles_x, pairs);
-    return hipGetLastError();
-}
-
-hipError_t launch_tile_ranges(const uint64_t* pairs, const Stats* stats, uint2* ranges, int num_tiles,
-                              hipStream_t s) {
-    hipError_t e = hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)num_tiles, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_tile_ranges, dim3(2048), dim3(256), 0, s, pairs, stats, ranges);
     return hipGetLastError();
 }
 

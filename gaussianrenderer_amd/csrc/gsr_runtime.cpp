@@ -695,10 +695,12 @@ static int sort_locked(gsr_context* c) {
     const uint32_t n = (uint32_t)c->n;
     // ---- stable depth sort of (key << 32 | index), 4 x 8 bits ----
     mark(c, GSR_STAGE_DEPTH_SORT);
-    const int gd = groups_for(c->n, gsr::kSortTile);
+    // smaller tiles for the 1M-item depth sort: ~500 workgroups instead of ~250
+    const int di = c->n < (int64_t(4) << 20) ? 8 : 16;
+    const int gd = groups_for(c->n, 256 * di);
     for (int p = 0; p < 4; p++)
-        HIP_TRY(gsr::launch_radix_pass(c->items[p & 1], c->items[(p + 1) & 1], nullptr, n, 32 + 8 * p, 8, gd,
-                                       c->hist, c->totals, c->stream));
+        HIP_TRY(gsr::launch_radix_pass(c->items[p & 1], c->items[(p + 1) & 1], nullptr, n, 32 + 8 * p, 8, gd, di,
+                                       c->hist, c->totals, nullptr, c->stream));
     // result in items[0]
     // ---- pair emission in depth order ----
     mark(c, GSR_STAGE_EMIT);
@@ -710,15 +712,16 @@ static int sort_locked(gsr_context* c) {
     const int tbits = std::max(1, ceil_log2(c->ntiles));
     const int gp = groups_for(c->p_cap, gsr::kSortTile);
     int cur = 0;
+    HIP_TRY(hipMemsetAsync(c->ranges, 0, sizeof(uint2) * (size_t)c->ntiles, c->stream));
     for (int sh = 0; sh < tbits; sh += 8) {
         const int bits = std::min(8, tbits - sh);
+        const bool last = sh + 8 >= tbits;    // final pass also writes the tile ranges
         HIP_TRY(gsr::launch_radix_pass(c->pairs[cur], c->pairs[cur ^ 1], &c->stats[0].pairs_eff, 0, 32 + sh, bits,
-                                       gp, c->hist, c->totals, c->stream));
+                                       gp, 16, c->hist, c->totals, last ? c->ranges : nullptr, c->stream));
         cur ^= 1;
     }
     c->pair_buf = cur;
     mark(c, GSR_STAGE_RANGES);
-    HIP_TRY(gsr::launch_tile_ranges(c->pairs[cur], c->stats, c->ranges, c->ntiles, c->stream));
     c->have_sort = true;
     return GSR_OK;
 }
@@ -832,6 +835,11 @@ extern "C" int gsr_read_tile_ranges(gsr_context* c, uint32_t* host, int64_t nt) 
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (nt) HIP_TRY(hipMemcpy(host, c->ranges, (size_t)nt * 8, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < nt; i++) {         // device form {~start, end}, zero = empty
+        const uint32_t x = host[2 * i], y = host[2 * i + 1];
+        host[2 * i] = y ? ~x : 0u;
+        host[2 * i + 1] = y;
+    }
     return GSR_OK;
 }
 
