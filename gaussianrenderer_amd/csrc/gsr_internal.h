@@ -55,6 +55,14 @@ hipError_t launch_emit(const uint64_t* depth_sorted, uint32_t n, const uint4* re
 // consumed: optional device counter of splat records loaded (diagnostics).
 hipError_t launch_blend(const uint64_t* pairs, const uint2* ranges, const uint4* rec, const Frame& fr,
                         float* out, unsigned long long* consumed, hipStream_t s);
+// Standalone sort ABI helpers (oneSweepSort / oneSweep3DGaussianSort).
+hipError_t launch_items_from_keys(const int* keys, uint32_t n, uint64_t* items, hipStream_t s);
+hipError_t launch_keys_from_items(const uint64_t* items, uint32_t n, int* keys, hipStream_t s);
+hipError_t launch_items_from_lwg(const gsr_lwg* rec, const uint64_t* src_perm, uint32_t n, int shift,
+                                 uint32_t mask, uint64_t* items, hipStream_t s);
+hipError_t launch_gather_lwg(const gsr_lwg* in, const uint64_t* stage1, const uint64_t* stage2, uint32_t n,
+                             gsr_lwg* out, hipStream_t s);
+
 // Device math probe for the detmath GPU parity test.
 hipError_t launch_math_probe(const float* in, int n, float* out, hipStream_t s);
 

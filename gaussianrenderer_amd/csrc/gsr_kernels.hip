@@ -703,6 +703,40 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
     }
 }
 
+// ------------------------------------------------------------------ standalone sort ABI helpers
+
+// (u32(key) << 32 | i): the reference sorts int keys as unsigned 8-bit digits
+// over all 32 bits (onesweep.cu:190-250, numPasses = 4).
+__global__ void k_items_from_keys(const int* __restrict__ keys, uint32_t n, uint64_t* __restrict__ items) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) items[i] = ((uint64_t)(uint32_t)keys[i] << 32) | i;
+}
+
+__global__ void k_keys_from_items(const uint64_t* __restrict__ items, uint32_t n, int* __restrict__ keys) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) keys[i] = (int)(uint32_t)(items[i] >> 32);
+}
+
+// Stage items for lightWeightGaussian records: (bits [shift, shift+32) of
+// radix_id << 32 | position).  src_perm (nullable) maps position -> record.
+__global__ void k_items_from_lwg(const gsr_lwg* __restrict__ rec, const uint64_t* __restrict__ src_perm,
+                                 uint32_t n, int shift, uint32_t mask, uint64_t* __restrict__ items) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = src_perm ? (uint32_t)src_perm[i] : i;
+    const uint32_t k = (uint32_t)(rec[r].radix_id >> shift) & mask;
+    items[i] = ((uint64_t)k << 32) | i;
+}
+
+__global__ void k_gather_lwg(const gsr_lwg* __restrict__ in, const uint64_t* __restrict__ stage1,
+                             const uint64_t* __restrict__ stage2, uint32_t n, gsr_lwg* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint32_t r = (uint32_t)stage2[i];
+    if (stage1) r = (uint32_t)stage1[r];
+    out[i] = in[r];
+}
+
 // ------------------------------------------------------------------ math probe
 
 __global__ void k_math_probe(const float* __restrict__ in, int n, float* __restrict__ out) {
@@ -783,6 +817,30 @@ hipError_t launch_blend(const uint64_t* pairs, const uint2* ranges, const uint4*
     else
         hipLaunchKernelGGL(k_blend<false>, dim3(nt), dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x,
                            fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
+    return hipGetLastError();
+}
+
+hipError_t launch_items_from_keys(const int* keys, uint32_t n, uint64_t* items, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_items_from_keys, dim3((n + 255) / 256), dim3(256), 0, s, keys, n, items);
+    return hipGetLastError();
+}
+
+hipError_t launch_keys_from_items(const uint64_t* items, uint32_t n, int* keys, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_keys_from_items, dim3((n + 255) / 256), dim3(256), 0, s, items, n, keys);
+    return hipGetLastError();
+}
+
+hipError_t launch_items_from_lwg(const gsr_lwg* rec, const uint64_t* src_perm, uint32_t n, int shift,
+                                 uint32_t mask, uint64_t* items, hipStream_t s) {
+    if (n)
+        hipLaunchKernelGGL(k_items_from_lwg, dim3((n + 255) / 256), dim3(256), 0, s, rec, src_perm, n, shift, mask,
+                           items);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_lwg(const gsr_lwg* in, const uint64_t* stage1, const uint64_t* stage2, uint32_t n,
+                             gsr_lwg* out, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_gather_lwg, dim3((n + 255) / 256), dim3(256), 0, s, in, stage1, stage2, n, out);
     return hipGetLastError();
 }
 

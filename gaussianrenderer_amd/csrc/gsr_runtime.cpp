@@ -970,15 +970,137 @@ extern "C" void preprocessCUDAGaussians(gsr_gaussian* d_gaussians, float* out_pi
 }
 
 // ------------------------------------------------------------------ reference sort ABI
+//
+// Both entry points take HOST arrays like the reference (they copy H2D, sort,
+// copy D2H) and report the device time of the sort passes in *kernel_ms
+// (cudaEvent bracket of render.cu:221-253 / onesweep.cu:217-240).
+
+namespace {
+
+struct SortBufs {
+    uint64_t* a = nullptr;
+    uint64_t* b = nullptr;
+    uint64_t* c = nullptr;
+    uint32_t* hist = nullptr;
+    uint32_t* totals = nullptr;
+    ~SortBufs() {
+        for (void* p : {(void*)a, (void*)b, (void*)c, (void*)hist, (void*)totals})
+            if (p) (void)hipFree(p);
+    }
+    int alloc(uint32_t n, bool third) {
+        HIP_TRY(hipMalloc(&a, sizeof(uint64_t) * std::max<size_t>(n, 1)));
+        HIP_TRY(hipMalloc(&b, sizeof(uint64_t) * std::max<size_t>(n, 1)));
+        if (third) HIP_TRY(hipMalloc(&c, sizeof(uint64_t) * std::max<size_t>(n, 1)));
+        HIP_TRY(hipMalloc(&hist, sizeof(uint32_t) * 256 * gsr::kMaxSortGroups));
+        HIP_TRY(hipMalloc(&totals, sizeof(uint32_t) * 256));
+        return GSR_OK;
+    }
+};
+
+// Stable sort of n items on bits [32, 32 + nbits); returns the buffer holding the result.
+int sort_high_bits(SortBufs& sb, uint64_t* a, uint64_t* b, uint32_t n, int nbits, uint64_t** result) {
+    const int g = groups_for(n, gsr::kSortTile);
+    uint64_t* src = a;
+    uint64_t* dst = b;
+    for (int sh = 0; sh < nbits; sh += 8) {
+        HIP_TRY(gsr::launch_radix_pass(src, dst, nullptr, n, 32 + sh, std::min(8, nbits - sh), g, 16, sb.hist,
+                                       sb.totals, nullptr, nullptr));
+        std::swap(src, dst);
+    }
+    *result = src;
+    return GSR_OK;
+}
+
+}  // namespace
 
 extern "C" void oneSweepSort(int* input, int* output, int N, int maxVal, float* kernel_ms) {
-    (void)input; (void)output; (void)N; (void)maxVal;
+    (void)maxVal;   // the reference sorts all 32 bits regardless (onesweep.cu:197-198)
     if (kernel_ms) *kernel_ms = 0.0f;
-    std::fprintf(stderr, "oneSweepSort: not implemented yet\n");
+    if (N <= 0) return;
+    if (!input || !output) {
+        std::fprintf(stderr, "oneSweepSort: null buffer\n");
+        return;
+    }
+    auto body = [&]() -> int {
+        SortBufs sb;
+        if (int rc = sb.alloc((uint32_t)N, false)) return rc;
+        int* dkeys = nullptr;
+        HIP_TRY(hipMalloc(&dkeys, sizeof(int) * (size_t)N));
+        HIP_TRY(hipMemcpy(dkeys, input, sizeof(int) * (size_t)N, hipMemcpyHostToDevice));
+        hipEvent_t e0, e1;
+        HIP_TRY(hipEventCreate(&e0));
+        HIP_TRY(hipEventCreate(&e1));
+        HIP_TRY(hipEventRecord(e0, nullptr));
+        HIP_TRY(gsr::launch_items_from_keys(dkeys, (uint32_t)N, sb.a, nullptr));
+        uint64_t* res = nullptr;
+        if (int rc = sort_high_bits(sb, sb.a, sb.b, (uint32_t)N, 32, &res)) return rc;
+        HIP_TRY(gsr::launch_keys_from_items(res, (uint32_t)N, dkeys, nullptr));
+        HIP_TRY(hipEventRecord(e1, nullptr));
+        HIP_TRY(hipEventSynchronize(e1));
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+        if (kernel_ms) *kernel_ms = ms;
+        HIP_TRY(hipMemcpy(output, dkeys, sizeof(int) * (size_t)N, hipMemcpyDeviceToHost));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipFree(dkeys);
+        return GSR_OK;
+    };
+    if (body() != GSR_OK) std::fprintf(stderr, "oneSweepSort: %s\n", g_err.c_str());
 }
 
 extern "C" void oneSweep3DGaussianSort(gsr_lwg* d_in, int N, int num_bits, float* kernel_ms) {
-    (void)d_in; (void)N; (void)num_bits;
     if (kernel_ms) *kernel_ms = 0.0f;
-    std::fprintf(stderr, "oneSweep3DGaussianSort: not implemented yet\n");
+    if (N <= 0) return;
+    if (!d_in || num_bits <= 0 || num_bits > 64) {
+        std::fprintf(stderr, "oneSweep3DGaussianSort: bad argument\n");
+        return;
+    }
+    // numPasses = (num_bits + 7) / 8 full 8-bit digits (render.cu:201): sort on
+    // the low 8*numPasses bits of radix_id, stable, values travel with keys.
+    const int nb = 8 * ((num_bits + 7) / 8);
+    auto body = [&]() -> int {
+        SortBufs sb;
+        if (int rc = sb.alloc((uint32_t)N, true)) return rc;
+        gsr_lwg *din = nullptr, *dout = nullptr;
+        HIP_TRY(hipMalloc(&din, sizeof(gsr_lwg) * (size_t)N));
+        HIP_TRY(hipMalloc(&dout, sizeof(gsr_lwg) * (size_t)N));
+        HIP_TRY(hipMemcpy(din, d_in, sizeof(gsr_lwg) * (size_t)N, hipMemcpyHostToDevice));
+        hipEvent_t e0, e1;
+        HIP_TRY(hipEventCreate(&e0));
+        HIP_TRY(hipEventCreate(&e1));
+        HIP_TRY(hipEventRecord(e0, nullptr));
+        // stage 1: low min(32, nb) bits
+        const int b1 = std::min(32, nb);
+        HIP_TRY(gsr::launch_items_from_lwg(din, nullptr, (uint32_t)N, 0, b1 == 32 ? 0xffffffffu : ((1u << b1) - 1u),
+                                           sb.a, nullptr));
+        uint64_t* r1 = nullptr;
+        if (int rc = sort_high_bits(sb, sb.a, sb.b, (uint32_t)N, b1, &r1)) return rc;
+        const uint64_t* s1 = nullptr;
+        const uint64_t* s2 = r1;
+        if (nb > 32) {
+            // stage 2: bits [32, nb), stable over the stage-1 order (LSD composition)
+            const int b2 = nb - 32;
+            uint64_t* spare = (r1 == sb.a) ? sb.b : sb.a;
+            HIP_TRY(gsr::launch_items_from_lwg(din, r1, (uint32_t)N, 32, b2 == 32 ? 0xffffffffu : ((1u << b2) - 1u),
+                                               sb.c, nullptr));
+            uint64_t* r2 = nullptr;
+            if (int rc = sort_high_bits(sb, sb.c, spare, (uint32_t)N, b2, &r2)) return rc;
+            s1 = r1;
+            s2 = r2;
+        }
+        HIP_TRY(gsr::launch_gather_lwg(din, s1, s2, (uint32_t)N, dout, nullptr));
+        HIP_TRY(hipEventRecord(e1, nullptr));
+        HIP_TRY(hipEventSynchronize(e1));
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+        if (kernel_ms) *kernel_ms = ms;
+        HIP_TRY(hipMemcpy(d_in, dout, sizeof(gsr_lwg) * (size_t)N, hipMemcpyDeviceToHost));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipFree(din);
+        (void)hipFree(dout);
+        return GSR_OK;
+    };
+    if (body() != GSR_OK) std::fprintf(stderr, "oneSweep3DGaussianSort: %s\n", g_err.c_str());
 }
