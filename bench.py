@@ -62,6 +62,36 @@ def algorithmic_blend_bytes(ntiles: int, consumed: int, W: int, H: int) -> int:
     return 8 * ntiles + 56 * consumed + 12 * W * H
 
 
+def load_pmc_traffic(config: int, kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of the same
+    workload (tools/profile.sh: separate FETCH_SIZE / WRITE_SIZE passes, KiB x 1024,
+    FETCH doubled per the gfx950 correction), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        d = json.load(open(p))
+    except (OSError, ValueError):
+        return None
+    if d.get("config") != config or kernel not in d.get("kernels", {}):
+        return None
+    k = d["kernels"][kernel]
+    return {"bytes_per_launch": int(k["fetch_bytes_corrected"] + k["write_bytes"]),
+            "source": f"profiles/pmc_latest.json ({d.get('source', '')})"}
+
+
+def dropin_rate(gsr, scene, cam, W, H, k, frames=20):
+    """frames/sec through the reference's drop-in symbol preprocessCUDAGaussians:
+    synchronous, header probe + full frame + 3*W*H float D2H into host memory
+    (PCIe-inclusive; never reported as `value`)."""
+    t = gsr.TilingInformation(50, 50, H, W)
+    gsr.preprocessCUDAGaussians(scene.ptr, scene.n, cam, t.num_tile_y, t.num_tile_x, t.width_stride,
+                                t.height_stride, W, H, k)
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        gsr.preprocessCUDAGaussians(scene.ptr, scene.n, cam, t.num_tile_y, t.num_tile_x, t.width_stride,
+                                    t.height_stride, W, H, k)
+    return frames / (time.perf_counter() - t0)
+
+
 def cpu_baseline(soa, cam, W, H, k, seconds):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle  # test infrastructure: CPU baseline leg only
@@ -218,6 +248,12 @@ def main():
     }
     if gather_ms is not None:
         result["gather_ms"] = round(gather_ms, 3)
+    traffic = load_pmc_traffic(args.config, "k_blend")
+    if traffic is not None:
+        result["roofline"]["traffic"] = traffic["bytes_per_launch"]
+        result["roofline"]["traffic_source"] = traffic["source"]
+    if world == 1:
+        result["dropin_host_fps"] = round(dropin_rate(gsr, scene, cam, W, H, args.k), 2)
     if world == 1 and not args.no_cpu_baseline:
         soa = gsr.read_ply(ply)
         result["cpu_baseline"] = cpu_baseline(soa, cam, W, H, args.k, args.cpu_seconds)

@@ -48,5 +48,26 @@ def main(d):
               f"{(f'{gbs:13.1f}' if gbs is not None else f'{chr(45):>13}')}")
 
 
+def write_json(d, out, config, source):
+    """Per-kernel HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, bytes) for bench.py."""
+    import json
+    res = {}
+    pm = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        p = os.path.join(d, f"pmc_{c}", "pmc_counter_collection.csv")
+        agg = collections.defaultdict(list)
+        for r in csv.DictReader(open(p)):
+            agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)
+        pm[c] = {k: sum(v) / len(v) for k, v in agg.items()}
+    for k in pm["FETCH_SIZE"]:
+        if k in pm["WRITE_SIZE"]:
+            res[k] = {"fetch_bytes_raw": pm["FETCH_SIZE"][k], "fetch_bytes_corrected": 2 * pm["FETCH_SIZE"][k],
+                      "write_bytes": pm["WRITE_SIZE"][k]}
+    json.dump({"config": config, "source": source, "kernels": res}, open(out, "w"), indent=1)
+
+
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof")
+    if len(sys.argv) > 2 and sys.argv[2] == "--json":
+        write_json(sys.argv[1], sys.argv[3], int(sys.argv[4]), sys.argv[5])
+    else:
+        main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof")
