@@ -248,7 +248,7 @@ def main():
     }
     if gather_ms is not None:
         result["gather_ms"] = round(gather_ms, 3)
-    traffic = load_pmc_traffic(args.config, "k_blend")
+    traffic = load_pmc_traffic(args.config, "k_blend<false>")
     if traffic is not None:
         result["roofline"]["traffic"] = traffic["bytes_per_launch"]
         result["roofline"]["traffic_source"] = traffic["source"]

@@ -17,7 +17,7 @@ import sys
 
 
 def short(name: str) -> str:
-    m = re.search(r"(k_\w+)", name)
+    m = re.search(r"(k_\w+(?:<[^>(]*>)?)", name)
     if m:
         return m.group(1)
     return name.split("(")[0][:60]
