@@ -557,7 +557,6 @@ __global__ __launch_bounds__(256) void k_emit_pairs(const uint64_t* __restrict__
 
 // ------------------------------------------------------------------ blend
 
-constexpr int kBatch = 256;
 
 // Bijective XCD-aware remap: blocks that share an XCD (b % 8) get one
 // contiguous run of tiles, so neighbouring tiles' shared splats hit one L2.
@@ -578,6 +577,36 @@ __device__ __forceinline__ float md2_cutoff(float op) {
     return (l * 1.38629436111989061f) * 1.00001f + 1e-3f;     // 2 ln2 log2(1000 op)
 }
 
+// Can any pixel of an integer rectangle reach md2 <= cut?  dx0..dy1 bound the
+// (float)pixel - (float)centre offsets of the rectangle's pixels (monotone, so
+// every pixel's dx lies in [dx0, dx1]).  Returns false only when the exact
+// minimum of the quadratic form a dx^2 + (b+c) dx dy + e dy^2 over that
+// rectangle exceeds cut by more than a bound on the float rounding of md2
+// (<= ~6 ulp of |a|dx^2 + (|b|+|c|)|dx dy| + |e|dy^2, padded 10x) — so a culled
+// splat could never have composited onto this block.  Not positive definite
+// (robustly), NaN or inf inputs: never culled.
+__device__ __forceinline__ bool block_may_reach(float a, float b, float c, float e, float dx0, float dx1,
+                                                float dy0, float dy1, float cut) {
+    if (dx0 <= 0.0f && dx1 >= 0.0f && dy0 <= 0.0f && dy1 >= 0.0f) return true;
+    const float h = 0.5f * (b + c);
+    const float det = a * e - h * h;
+    if (!(a > 0.0f && e > 0.0f && det > 1e-4f * (a * e)) || !(cut < 3.0e38f)) return true;
+    const float ih = -h / e, iv = -h / a;
+    auto q = [&](float x, float y) { return a * x * x + 2.0f * h * x * y + e * y * y; };
+    float qm = q(dx0, fminf(fmaxf(ih * dx0, dy0), dy1));
+    qm = fminf(qm, q(dx1, fminf(fmaxf(ih * dx1, dy0), dy1)));
+    qm = fminf(qm, q(fminf(fmaxf(iv * dy0, dx0), dx1), dy0));
+    qm = fminf(qm, q(fminf(fmaxf(iv * dy1, dx0), dx1), dy1));
+    const float M = fmaxf(fmaxf(fabsf(dx0), fabsf(dx1)), fmaxf(fabsf(dy0), fabsf(dy1)));
+    const float err = 4e-6f * (fabsf(a) + fabsf(b) + fabsf(c) + fabsf(e)) * M * M + 1e-3f;
+    return !(qm - err > cut);
+}
+
+// One wave64 per 8x8 pixel block, four per 16x16 tile (one tile per 256-thread
+// workgroup), and NO workgroup barrier: each wave streams its tile's splat list
+// on its own in 64-record batches (lane l holds record l of the batch), with
+// the next batch's pair indices and records prefetched into registers while the
+// current one is composited, and a private LDS slice for the broadcast reads.
 template <bool DIAG>
 __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pairs,
                                                 const uint2* __restrict__ ranges,
@@ -585,13 +614,12 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
                                                 int W, int H, int cover_w, int cover_h,
                                                 float* __restrict__ out,
                                                 unsigned long long* __restrict__ counters) {
-    __shared__ uint4 sA[kBatch], sB[kBatch], sC[kBatch];
-    __shared__ float sCut[kBatch];
+    __shared__ uint4 sA[4][64], sB[4][64], sC[4][64];
+    __shared__ float sCut[4][64];
     const int ntiles = tiles_x * tiles_y;
     const int tile = xcd_remap(blockIdx.x, ntiles);
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    // each wave owns one 8x8 pixel block of the 16x16 tile, one pixel per lane
     const int bx = tx * GSR_TILE_PX + (w & 1) * 8;
     const int by = ty * GSR_TILE_PX + (w >> 1) * 8;
     const int px = bx + (lane & 7), py = by + (lane >> 3);
@@ -602,97 +630,128 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
     float T = inside ? 1.0f : 0.0f;
     float cr = 0.0f, cg = 0.0f, cb = 0.0f;
     const uint2 rr = ranges[tile];                       // {~start, end}, zero = empty
-    const uint2 rg = make_uint2(rr.y ? ~rr.x : 0u, rr.y);
-    uint64_t d_loaded = 0, d_iter = 0, d_active = 0, d_taken = 0, d_zero_active = 0, d_skipped = 0;
-    for (uint32_t base = rg.x; base < rg.y; base += kBatch) {
-        const uint32_t cnt = min((uint32_t)kBatch, rg.y - base);
-        if (DIAG) d_loaded += cnt;
-        __syncthreads();                                   // previous batch fully consumed
-        if ((uint32_t)t < cnt) {
-            const uint32_t gi = (uint32_t)pairs[base + t];
-            const uint4* R = rec + 4 * (uint64_t)gi;
-            const uint4 b4 = R[1];
-            sA[t] = R[0];
-            sB[t] = b4;
-            sC[t] = R[2];
-            sCut[t] = md2_cutoff(__uint_as_float(b4.x));
-        }
-        __syncthreads();
-        if (__ballot(!(T < 1e-3f)) != 0ull) {
-            // wave-parallel cull: which splats of the batch touch this wave's 8x8 block
-            uint64_t hit[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t s = q * 64 + lane;
-                bool h = false;
-                if (s < cnt) {
-                    const uint4 C = sC[s];
-                    const int xmin = (int)(C.z & 0xffffu), xmax = (int)(C.z >> 16);
-                    const int ymin = (int)(C.w & 0xffffu), ymax = (int)(C.w >> 16);
-                    h = !(xmax < bx || xmin > bx + 7 || ymax < by || ymin > by + 7);
-                }
-                hit[q] = __ballot(h);
-            }
-            // splats in list order; predicated (branch-free) per-pixel body
-            bool alive = true;
-            auto run = [&](uint64_t m, int q0) {
-                while (m && alive) {
-                    const int s = q0 + __builtin_ctzll(m);
-                    m &= m - 1;
-                    const uint4 C = sC[s];
-                    const uint4 A = sA[s];
-                    const float cut = sCut[s];
-                    const int xmin = (int)(C.z & 0xffffu), xmax = (int)(C.z >> 16);
-                    const int ymin = (int)(C.w & 0xffffu), ymax = (int)(C.w >> 16);
-                    const bool live = (px >= xmin) & (px <= xmax) & (py >= ymin) & (py <= ymax) &
-                                      !(T < 1e-3f);
-                    // render.cu:329-340, same operation order
-                    const float dx = fpx - (float)(int)C.x;
-                    const float dy = fpy - (float)(int)C.y;
-                    const float md2 = dx * (__uint_as_float(A.x) * dx + __uint_as_float(A.y) * dy) +
-                                      dy * (__uint_as_float(A.z) * dx + __uint_as_float(A.w) * dy);
-                    if (DIAG) {
-                        d_iter += 1;
-                        const uint64_t act = __ballot(live);
-                        d_active += (uint64_t)__popcll(act);
-                        d_zero_active += act == 0ull;
-                    }
-                    if (__ballot(live & !(md2 > cut)) == 0ull) {   // no lane can reach alpha >= 1e-3
-                        if (DIAG) d_skipped += 1;
-                        continue;
-                    }
-                    const uint4 B = sB[s];
-                    float alpha = __uint_as_float(B.x) * gsr_expf(-0.5f * md2);
-                    alpha = fminf(alpha, 0.99f);
-                    const bool take = live & !(alpha < 1e-3f);
-                    const float wr = __uint_as_float(B.y) * alpha * T;
-                    const float wg = __uint_as_float(B.z) * alpha * T;
-                    const float wb = __uint_as_float(B.w) * alpha * T;
-                    const float Tn = T * (1.0f - alpha);
-                    cr = take ? cr + wr : cr;
-                    cg = take ? cg + wg : cg;
-                    cb = take ? cb + wb : cb;
-                    T = take ? Tn : T;
-                    if (DIAG) d_taken += (uint64_t)__popcll(__ballot(take));
-                    alive = __ballot(!(T < 1e-3f)) != 0ull;   // whole block saturated -> stop
-                }
-            };
-            run(hit[0], 0);
-            run(hit[1], 64);
-            run(hit[2], 128);
-            run(hit[3], 192);
-        }
-        if (__syncthreads_and((T < 1e-3f) ? 1 : 0)) break;
+    const uint32_t beg = rr.y ? ~rr.x : 0u, end = rr.y;
+    uint64_t d_loaded = 0, d_iter = 0, d_active = 0, d_taken = 0, d_skipped = 0;
+    uint4* wA = sA[w];
+    uint4* wB = sB[w];
+    uint4* wC = sC[w];
+    float* wCut = sCut[w];
+
+    // software pipeline: records of batch k in (ra, rb, rc); pair index of batch k+1 in nidx
+    uint4 ra = make_uint4(0, 0, 0, 0), rb = ra, rc = ra;
+    uint32_t nidx = 0;
+    if (beg + lane < end) {
+        const uint32_t gi = (uint32_t)pairs[beg + lane];
+        const uint4* R = rec + 4 * (uint64_t)gi;
+        ra = R[0];
+        rb = R[1];
+        rc = R[2];
     }
-    if (DIAG) {
-        if (t == 0 && d_loaded) atomicAdd(counters, (unsigned long long)d_loaded);
-        if (lane == 0) {
-            atomicAdd(counters + 1, (unsigned long long)d_iter);
-            atomicAdd(counters + 2, (unsigned long long)d_active);
-            atomicAdd(counters + 3, (unsigned long long)d_taken);
-            atomicAdd(counters + 4, (unsigned long long)d_zero_active);
-            atomicAdd(counters + 5, (unsigned long long)d_skipped);
+    if (beg + 64 + lane < end) nidx = (uint32_t)pairs[beg + 64 + lane];
+    bool alive = __ballot(!(T < 1e-3f)) != 0ull;
+    for (uint32_t base = beg; base < end && alive; base += 64) {
+        const uint32_t cnt = min(64u, end - base);
+        // stage the current batch in this wave's LDS slice (same-wave LDS ops are in order)
+        wA[lane] = ra;
+        wB[lane] = rb;
+        wC[lane] = rc;
+        wCut[lane] = md2_cutoff(__uint_as_float(rb.x));
+        // cull: lane = record; AABB vs block, then exact ellipse test on block n AABB
+        bool h = false;
+        if ((uint32_t)lane < cnt) {
+            const int xmin = (int)(rc.z & 0xffffu), xmax = (int)(rc.z >> 16);
+            const int ymin = (int)(rc.w & 0xffffu), ymax = (int)(rc.w >> 16);
+            h = !(xmax < bx || xmin > bx + 7 || ymax < by || ymin > by + 7);
+            if (h) {
+                const float cx = (float)(int)rc.x, cy = (float)(int)rc.y;
+                h = block_may_reach(__uint_as_float(ra.x), __uint_as_float(ra.y), __uint_as_float(ra.z),
+                                    __uint_as_float(ra.w), (float)max(bx, xmin) - cx, (float)min(bx + 7, xmax) - cx,
+                                    (float)max(by, ymin) - cy, (float)min(by + 7, ymax) - cy,
+                                    md2_cutoff(__uint_as_float(rb.x)));
+            }
         }
+        uint64_t m = __ballot(h);
+        if (DIAG) d_loaded += cnt;
+        // prefetch: records of batch k+1 (indices already in nidx), indices of batch k+2
+        if (base + 64 + lane < end) {
+            const uint4* R = rec + 4 * (uint64_t)nidx;
+            ra = R[0];
+            rb = R[1];
+            rc = R[2];
+        }
+        if (base + 128 + lane < end) nidx = (uint32_t)pairs[base + 128 + lane];
+        while (m && alive) {
+            // two splats per iteration: their md2/exp are independent (ILP);
+            // compositing stays strictly in list order, per pixel
+            const int s0 = __builtin_ctzll(m);
+            m &= m - 1;
+            const bool has1 = m != 0ull;
+            const int s1 = has1 ? __builtin_ctzll(m) : s0;
+            if (has1) m &= m - 1;
+            const uint4 C0 = wC[s0], C1 = wC[s1];
+            const uint4 A0 = wA[s0], A1 = wA[s1];
+            const float cut0 = wCut[s0], cut1 = wCut[s1];
+            const bool box0 = (px >= (int)(C0.z & 0xffffu)) & (px <= (int)(C0.z >> 16)) &
+                              (py >= (int)(C0.w & 0xffffu)) & (py <= (int)(C0.w >> 16));
+            const bool box1 = (px >= (int)(C1.z & 0xffffu)) & (px <= (int)(C1.z >> 16)) &
+                              (py >= (int)(C1.w & 0xffffu)) & (py <= (int)(C1.w >> 16)) & has1;
+            // render.cu:329-332, same operation order
+            const float dx0 = fpx - (float)(int)C0.x, dy0 = fpy - (float)(int)C0.y;
+            const float dx1 = fpx - (float)(int)C1.x, dy1 = fpy - (float)(int)C1.y;
+            const float md0 = dx0 * (__uint_as_float(A0.x) * dx0 + __uint_as_float(A0.y) * dy0) +
+                              dy0 * (__uint_as_float(A0.z) * dx0 + __uint_as_float(A0.w) * dy0);
+            const float md1 = dx1 * (__uint_as_float(A1.x) * dx1 + __uint_as_float(A1.y) * dy1) +
+                              dy1 * (__uint_as_float(A1.z) * dx1 + __uint_as_float(A1.w) * dy1);
+            const bool unsat = !(T < 1e-3f);
+            if (DIAG) {
+                d_iter += has1 ? 2 : 1;
+                d_active += (uint64_t)__popcll(__ballot(box0 & unsat)) + (uint64_t)__popcll(__ballot(box1 & unsat));
+            }
+            // no lane can reach alpha >= 1e-3 for either splat: skip both
+            if (__ballot(unsat & ((box0 & !(md0 > cut0)) | (box1 & !(md1 > cut1)))) == 0ull) {
+                if (DIAG) d_skipped += has1 ? 2 : 1;
+                continue;
+            }
+            const uint4 B0 = wB[s0], B1 = wB[s1];
+            const float e0 = gsr_expf(-0.5f * md0);
+            const float e1 = gsr_expf(-0.5f * md1);
+            {   // splat s0 (render.cu:333-340)
+                float alpha = __uint_as_float(B0.x) * e0;
+                alpha = fminf(alpha, 0.99f);
+                const bool take = box0 & unsat & !(alpha < 1e-3f);
+                const float wr = __uint_as_float(B0.y) * alpha * T;
+                const float wg = __uint_as_float(B0.z) * alpha * T;
+                const float wb = __uint_as_float(B0.w) * alpha * T;
+                const float Tn = T * (1.0f - alpha);
+                cr = take ? cr + wr : cr;
+                cg = take ? cg + wg : cg;
+                cb = take ? cb + wb : cb;
+                T = take ? Tn : T;
+                if (DIAG) d_taken += (uint64_t)__popcll(__ballot(take));
+            }
+            {   // splat s1, against the transmittance left by s0
+                float alpha = __uint_as_float(B1.x) * e1;
+                alpha = fminf(alpha, 0.99f);
+                const bool take = box1 & !(T < 1e-3f) & !(alpha < 1e-3f);
+                const float wr = __uint_as_float(B1.y) * alpha * T;
+                const float wg = __uint_as_float(B1.z) * alpha * T;
+                const float wb = __uint_as_float(B1.w) * alpha * T;
+                const float Tn = T * (1.0f - alpha);
+                cr = take ? cr + wr : cr;
+                cg = take ? cg + wg : cg;
+                cb = take ? cb + wb : cb;
+                T = take ? Tn : T;
+                if (DIAG) d_taken += (uint64_t)__popcll(__ballot(take));
+            }
+            alive = __ballot(!(T < 1e-3f)) != 0ull;   // whole block saturated -> stop
+        }
+    }
+    if (DIAG && lane == 0) {
+        if (w == 0 && d_loaded) atomicAdd(counters, (unsigned long long)d_loaded);
+        atomicAdd(counters + 1, (unsigned long long)d_iter);
+        atomicAdd(counters + 2, (unsigned long long)d_active);
+        atomicAdd(counters + 3, (unsigned long long)d_taken);
+        atomicAdd(counters + 5, (unsigned long long)d_skipped);
     }
     if (px < W && py < H) {
         const size_t o = (size_t)py * (size_t)W + (size_t)px;
