@@ -242,7 +242,7 @@ def main():
         "pairs": pairs,
         "pairs_consumed": consumed,
         "blend_counters": counters,
-        "blend_lane_efficiency": round(counters["active_lanes"] / max(1, 64 * counters["wave_splat_iters"]), 4),
+        "blend_lane_efficiency": round(counters["active_lanes"] / max(1, counters["lane_slots"]), 4),
         "image_mean": float(img.mean().item()),
         "overflow_after_timed": overflow,
     }

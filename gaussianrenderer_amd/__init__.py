@@ -252,9 +252,12 @@ class Renderer:
     def blend_counters(self) -> dict:
         v = np.zeros(8, dtype=np.int64)
         check(lib().gsr_blend_counters(self.ctx, v.ctypes.data), "gsr_blend_counters")
-        keys = ("records_loaded", "wave_splat_iters", "active_lanes", "taken_lanes", "iters_no_active",
-                "iters_skipped_cutoff")
+        keys = ("records_loaded", "wave_splat_iters", "active_lanes", "taken_lanes", "slow_path_iters",
+                "iters_skipped_cutoff", "lane_slots")
         return dict(zip(keys, (int(x) for x in v)))
+
+    def set_blend_variant(self, variant: int):
+        check(lib().gsr_set_blend_variant(self.ctx, int(variant)), "gsr_set_blend_variant")
 
     def stage_times(self):
         ms = (ctypes.c_double * NUM_STAGES)()

@@ -52,9 +52,11 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
 hipError_t launch_emit(const uint64_t* depth_sorted, uint32_t n, const uint4* rec, int groups,
                        unsigned long long* wg_scratch, Stats* stats, Stats* host_mapped_stats,
                        uint32_t pair_capacity, int tiles_x, uint64_t* pairs, hipStream_t s);
-// consumed: optional device counter of splat records loaded (diagnostics).
+// consumed: optional device counters (diagnostics).  variant: blend kernel
+// schedule (0 = default; 1/2/4 = pixel-chain kernel with that many pixels per
+// lane) — every variant produces bit-identical images.
 hipError_t launch_blend(const uint64_t* pairs, const uint2* ranges, const uint4* rec, const Frame& fr,
-                        float* out, unsigned long long* consumed, hipStream_t s);
+                        float* out, unsigned long long* consumed, int variant, hipStream_t s);
 // Standalone sort ABI helpers (oneSweepSort / oneSweep3DGaussianSort).
 hipError_t launch_items_from_keys(const int* keys, uint32_t n, uint64_t* items, hipStream_t s);
 hipError_t launch_keys_from_items(const uint64_t* items, uint32_t n, int* keys, hipStream_t s);

@@ -608,7 +608,7 @@ __device__ __forceinline__ bool block_may_reach(float a, float b, float c, float
 // the next batch's pair indices and records prefetched into registers while the
 // current one is composited, and a private LDS slice for the broadcast reads.
 template <bool DIAG>
-__global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pairs,
+__global__ __launch_bounds__(256) void k_blend_v5(const uint64_t* __restrict__ pairs,
                                                 const uint2* __restrict__ ranges,
                                                 const uint4* __restrict__ rec, int tiles_x, int tiles_y,
                                                 int W, int H, int cover_w, int cover_h,
@@ -752,6 +752,7 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
         atomicAdd(counters + 2, (unsigned long long)d_active);
         atomicAdd(counters + 3, (unsigned long long)d_taken);
         atomicAdd(counters + 5, (unsigned long long)d_skipped);
+        atomicAdd(counters + 6, (unsigned long long)(d_iter * 64));
     }
     if (px < W && py < H) {
         const size_t o = (size_t)py * (size_t)W + (size_t)px;
@@ -759,6 +760,411 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
         out[o] = inside ? cr : 0.0f;
         out[hw + o] = inside ? cg : 0.0f;
         out[2 * hw + o] = inside ? cb : 0.0f;
+    }
+}
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// gsr_expf on two lanes at once (v_pk_* for every float op that has a packed
+// form), for inputs the caller has PROVEN finite and <= 88.75: there the upper
+// clamp and the NaN select of gsr_expf are no-ops, and every remaining step is
+// the same IEEE operation in the same order, so each half is bit-identical to
+// gsr_expf of that half.
+__device__ __forceinline__ f2 gsr_expf_x2(f2 x) {
+    f2 xc;
+    xc.x = fmaxf(x.x, -104.0f);
+    xc.y = fmaxf(x.y, -104.0f);
+    const f2 t = xc * 1.44269504088896341f;
+    f2 n;
+    n.x = rintf(t.x);
+    n.y = rintf(t.y);
+    f2 r = __builtin_elementwise_fma(-n, (f2)0.693359375f, xc);
+    r = __builtin_elementwise_fma(-n, (f2)-2.12194440e-4f, r);
+    f2 p = __builtin_elementwise_fma((f2)1.9875691500e-4f, r, (f2)1.3981999507e-3f);
+    p = __builtin_elementwise_fma(p, r, (f2)8.3334519073e-3f);
+    p = __builtin_elementwise_fma(p, r, (f2)4.1665795894e-2f);
+    p = __builtin_elementwise_fma(p, r, (f2)1.6666665459e-1f);
+    p = __builtin_elementwise_fma(p, r, (f2)5.0000001201e-1f);
+    const f2 r2 = r * r;
+    const f2 y = __builtin_elementwise_fma(p, r2, r) + 1.0f;
+    f2 res;
+    res.x = __builtin_amdgcn_ldexpf(y.x, (int)n.x);
+    res.y = __builtin_amdgcn_ldexpf(y.y, (int)n.y);
+    return res;
+}
+
+// Fast-path proof for one splat on one block (exactness, not a heuristic):
+// finite conic that is robustly positive definite with |a|+|b|+|c|+|e| times
+// the squared largest block offset <= 4e7 keeps every in-box md2 finite and
+// >= -10 (float error of the 9-op form < 10), so -md2/2 lies in gsr_expf_x2's
+// proven range; finite colours make "alpha = 0 when not taken" leave the
+// accumulators bit-identical (c + (col*0)*T == c, T*(1-0) == T).
+__device__ __forceinline__ bool fast_safe(float a, float b, float c, float e, float M, float r, float g,
+                                          float bl) {
+    const float h = 0.5f * (b + c);
+    const float S = fabsf(a) + fabsf(b) + fabsf(c) + fabsf(e);
+    return a > 0.0f && e > 0.0f && (a * e - h * h) > 1e-4f * (a * e) && S * M * M <= 4e7f &&
+           isfinite(S) && isfinite(r) && isfinite(g) && isfinite(bl);
+}
+
+// One wave64 per 8x8 pixel block (four per 16x16 tile, one tile per
+// workgroup), no workgroup barrier.  Each wave streams its tile's splat list in
+// 64-record batches (records of batch k+1 and indices of batch k+2 prefetched
+// into registers).  Per batch, lane l culls record l (AABB, then the exact
+// ellipse-vs-block test) and computes its 64-bit in-AABB pixel mask; the
+// survivors are compacted, in list order, into PAIR SLOTS of the wave's LDS
+// slice so that {parameter of splat 2j, parameter of splat 2j+1} are adjacent
+// and feed v_pk_* instructions directly.  The compositing loop takes two
+// splats per iteration: md2, exp and alpha packed, then the two composites in
+// list order.  Batches holding a survivor without the fast-path proof run an
+// exact one-splat path instead (same values, full gsr_expf, plain selects).
+//
+// Pair slot dwords (h = 0 / 1 for the first / second splat of the pair):
+//   [0+h] cx  [2+h] cy  [4+h] a  [6+h] b  [8+h] c  [10+h] e  [12+h] opacity
+//   [14+2h] red  [15+2h] green  [18+h] blue
+template <bool DIAG>
+__global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pairs,
+                                                const uint2* __restrict__ ranges,
+                                                const uint4* __restrict__ rec, int tiles_x, int tiles_y,
+                                                int W, int H, int cover_w, int cover_h,
+                                                float* __restrict__ out,
+                                                unsigned long long* __restrict__ counters) {
+    constexpr int kSlot = 20;                               // dwords per pair slot
+    __shared__ float4 sP[4][32 * kSlot / 4];
+    const int ntiles = tiles_x * tiles_y;
+    const int tile = xcd_remap(blockIdx.x, ntiles);
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int bx = tx * GSR_TILE_PX + (w & 1) * 8;
+    const int by = ty * GSR_TILE_PX + (w >> 1) * 8;
+    const int px = bx + (lane & 7), py = by + (lane >> 3);
+    const bool inside = px < cover_w && py < cover_h;
+    const float fpx = (float)px, fpy = (float)py;
+    // transmittance; a pixel is saturated ("done", render.cu:328) iff T < 1e-3.
+    // Pixels outside the covered area start saturated (T = 0) and write 0.
+    float T = inside ? 1.0f : 0.0f;
+    f2 crg = (f2)0.0f;
+    float cb = 0.0f;
+    const uint2 rr = ranges[tile];                          // {~start, end}, zero = empty
+    const uint32_t beg = rr.y ? ~rr.x : 0u, end = rr.y;
+    uint64_t d_loaded = 0, d_iter = 0, d_active = 0, d_taken = 0, d_slow = 0;
+    float* wP = reinterpret_cast<float*>(sP[w]);
+    const float4* wP4 = sP[w];
+
+    uint4 ra = make_uint4(0, 0, 0, 0), rb = ra, rc = ra;
+    uint32_t nidx = 0;
+    if (beg + lane < end) {
+        const uint32_t gi = (uint32_t)pairs[beg + lane];
+        const uint4* R = rec + 4 * (uint64_t)gi;
+        ra = R[0];
+        rb = R[1];
+        rc = R[2];
+    }
+    if (beg + 64 + lane < end) nidx = (uint32_t)pairs[beg + 64 + lane];
+    bool alive = __ballot(!(T < 1e-3f)) != 0ull;
+    for (uint32_t base = beg; base < end && alive; base += 64) {
+        const uint32_t cnt = min(64u, end - base);
+        // ---- cull + lane masks + compaction (lane = record) ----
+        bool hit = false, fast = true;
+        uint32_t mlo = 0, mhi = 0;
+        if ((uint32_t)lane < cnt) {
+            const int xmin = (int)(rc.z & 0xffffu), xmax = (int)(rc.z >> 16);
+            const int ymin = (int)(rc.w & 0xffffu), ymax = (int)(rc.w >> 16);
+            hit = !(xmax < bx || xmin > bx + 7 || ymax < by || ymin > by + 7);
+            if (hit) {
+                const float cx = (float)(int)rc.x, cy = (float)(int)rc.y;
+                const float a = __uint_as_float(ra.x), b = __uint_as_float(ra.y);
+                const float c = __uint_as_float(ra.z), e = __uint_as_float(ra.w);
+                const int x0 = max(xmin - bx, 0), x1 = min(xmax - bx, 7);
+                const int y0 = max(ymin - by, 0), y1 = min(ymax - by, 7);
+                const float dx0 = (float)(bx + x0) - cx, dx1 = (float)(bx + x1) - cx;
+                const float dy0 = (float)(by + y0) - cy, dy1 = (float)(by + y1) - cy;
+                hit = block_may_reach(a, b, c, e, dx0, dx1, dy0, dy1, md2_cutoff(__uint_as_float(rb.x)));
+                const float M = fmaxf(fmaxf(fabsf(dx0), fabsf(dx1)), fmaxf(fabsf(dy0), fabsf(dy1)));
+                fast = fast_safe(a, b, c, e, M, __uint_as_float(rb.y), __uint_as_float(rb.z),
+                                 __uint_as_float(rb.w));
+                // bit (row * 8 + col) of the block: pixel inside the AABB
+                const uint32_t rep = ((0xffu >> (7 - (x1 - x0))) << x0) * 0x01010101u;
+                const uint64_t rows = (y1 == 7 ? ~0ull : ((1ull << (8 * (y1 + 1))) - 1ull)) & (~0ull << (8 * y0));
+                mlo = rep & (uint32_t)rows;
+                mhi = rep & (uint32_t)(rows >> 32);
+            }
+        }
+        const uint64_t m = __ballot(hit);
+        const bool all_fast = __ballot(hit & !fast) == 0ull;
+        if (hit) {
+            const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            float* S = wP + (k >> 1) * kSlot;
+            const int h = (int)(k & 1u);
+            S[0 + h] = (float)(int)rc.x;
+            S[2 + h] = (float)(int)rc.y;
+            S[4 + h] = __uint_as_float(ra.x);
+            S[6 + h] = __uint_as_float(ra.y);
+            S[8 + h] = __uint_as_float(ra.z);
+            S[10 + h] = __uint_as_float(ra.w);
+            S[12 + h] = __uint_as_float(rb.x);
+            S[14 + 2 * h] = __uint_as_float(rb.y);
+            S[15 + 2 * h] = __uint_as_float(rb.z);
+            S[18 + h] = __uint_as_float(rb.w);
+        }
+        const uint32_t nsurv = (uint32_t)__popcll(m);
+        if ((nsurv & 1u) && lane < 10) {
+            // odd count: zero the unused second half of the last slot (mask 0 keeps it inert)
+            static constexpr int kHalf1[10] = {1, 3, 5, 7, 9, 11, 13, 16, 17, 19};
+            wP[(nsurv >> 1) * kSlot + kHalf1[lane]] = 0.0f;
+        }
+        if (DIAG) d_loaded += cnt;
+        // ---- prefetch: records of batch k+1, indices of batch k+2 ----
+        if (base + 64 + lane < end) {
+            const uint4* R = rec + 4 * (uint64_t)nidx;
+            ra = R[0];
+            rb = R[1];
+            rc = R[2];
+        }
+        if (base + 128 + lane < end) nidx = (uint32_t)pairs[base + 128 + lane];
+
+        uint64_t mm = m;
+        if (all_fast) {
+            for (uint32_t j = 0; mm && alive; ++j) {
+                const int s0 = __builtin_ctzll(mm);
+                mm &= mm - 1;
+                const bool has1 = mm != 0ull;
+                const int s1 = has1 ? __builtin_ctzll(mm) : s0;
+                if (has1) mm &= mm - 1;
+                const uint64_t box0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mhi, s0) << 32) |
+                                      (uint32_t)__builtin_amdgcn_readlane((int)mlo, s0);
+                uint64_t box1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mhi, s1) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)mlo, s1);
+                box1 = has1 ? box1 : 0ull;
+                const float4 q0 = wP4[j * 5 + 0], q1 = wP4[j * 5 + 1], q2 = wP4[j * 5 + 2];
+                const float4 q3 = wP4[j * 5 + 3], q4 = wP4[j * 5 + 4];
+                // render.cu:329-332, same operation order, both splats at once
+                const f2 dx = (f2)fpx - (f2){q0.x, q0.y};
+                const f2 dy = (f2)fpy - (f2){q0.z, q0.w};
+                const f2 md = dx * ((f2){q1.x, q1.y} * dx + (f2){q1.z, q1.w} * dy) +
+                              dy * ((f2){q2.x, q2.y} * dx + (f2){q2.z, q2.w} * dy);
+                const f2 ee = gsr_expf_x2(-0.5f * md);
+                const f2 al = (f2){q3.x, q3.y} * ee;
+                const float al0 = fminf(al.x, 0.99f), al1 = fminf(al.y, 0.99f);
+                // render.cu:333-340: splat 2j, then splat 2j+1 against what 2j left
+                const bool in0 = __builtin_amdgcn_inverse_ballot_w64(box0);
+                const bool in1 = __builtin_amdgcn_inverse_ballot_w64(box1);
+                const bool take0 = in0 & !(T < 1e-3f) & !(al0 < 1e-3f);
+                const float a0 = take0 ? al0 : 0.0f;
+                const float T1 = T * (1.0f - a0);
+                const bool take1 = in1 & !(T1 < 1e-3f) & !(al1 < 1e-3f);
+                const float a1 = take1 ? al1 : 0.0f;
+                const float T2 = T1 * (1.0f - a1);
+                crg = crg + ((f2){q3.z, q3.w} * a0) * T;
+                crg = crg + ((f2){q4.x, q4.y} * a1) * T1;
+                const f2 wb = ((f2){q4.z, q4.w} * (f2){a0, a1}) * (f2){T, T1};
+                cb = (cb + wb.x) + wb.y;
+                if (DIAG) {
+                    d_iter += has1 ? 2 : 1;
+                    d_active += (uint64_t)__popcll(__ballot(in0 & !(T < 1e-3f))) +
+                                (uint64_t)__popcll(__ballot(in1 & !(T1 < 1e-3f)));
+                    d_taken += (uint64_t)__popcll(__ballot(take0)) + (uint64_t)__popcll(__ballot(take1));
+                }
+                T = T2;
+                alive = __ballot(!(T < 1e-3f)) != 0ull;   // whole block saturated -> stop
+            }
+        } else {
+            // exact one-splat path (render.cu:329-340 with gsr_expf and selects)
+            for (uint32_t k = 0; mm && alive; ++k) {
+                const int s = __builtin_ctzll(mm);
+                mm &= mm - 1;
+                const uint64_t box = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mhi, s) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((int)mlo, s);
+                const float* S = wP + (k >> 1) * kSlot;
+                const int h = (int)(k & 1u);
+                const float dx = fpx - S[0 + h], dy = fpy - S[2 + h];
+                const float md = dx * (S[4 + h] * dx + S[6 + h] * dy) + dy * (S[8 + h] * dx + S[10 + h] * dy);
+                const float ee = gsr_expf(-0.5f * md);
+                float alpha = S[12 + h] * ee;
+                alpha = fminf(alpha, 0.99f);
+                const bool in = __builtin_amdgcn_inverse_ballot_w64(box);
+                const bool take = in & !(T < 1e-3f) & !(alpha < 1e-3f);
+                const float wr = S[14 + 2 * h] * alpha * T;
+                const float wg = S[15 + 2 * h] * alpha * T;
+                const float wb = S[18 + h] * alpha * T;
+                const float Tn = T * (1.0f - alpha);
+                if (DIAG) {
+                    d_iter += 1;
+                    d_slow += 1;
+                    d_active += (uint64_t)__popcll(__ballot(in & !(T < 1e-3f)));
+                    d_taken += (uint64_t)__popcll(__ballot(take));
+                }
+                crg.x = take ? crg.x + wr : crg.x;
+                crg.y = take ? crg.y + wg : crg.y;
+                cb = take ? cb + wb : cb;
+                T = take ? Tn : T;
+                alive = __ballot(!(T < 1e-3f)) != 0ull;
+            }
+        }
+    }
+    if (DIAG && lane == 0) {
+        if (w == 0 && d_loaded) atomicAdd(counters, (unsigned long long)d_loaded);
+        atomicAdd(counters + 1, (unsigned long long)d_iter);
+        atomicAdd(counters + 2, (unsigned long long)d_active);
+        atomicAdd(counters + 3, (unsigned long long)d_taken);
+        atomicAdd(counters + 4, (unsigned long long)d_slow);
+        atomicAdd(counters + 6, (unsigned long long)(d_iter * 64));
+    }
+    if (px < W && py < H) {
+        const size_t o = (size_t)py * (size_t)W + (size_t)px;
+        const size_t hw = (size_t)W * (size_t)H;
+        out[o] = inside ? crg.x : 0.0f;
+        out[hw + o] = inside ? crg.y : 0.0f;
+        out[2 * hw + o] = inside ? cb : 0.0f;
+    }
+}
+
+// Pixel-chain blend: each lane owns PPL pixels of one column (rows y0 + R*j),
+// so one broadcast splat read feeds PPL independent md2/exp/composite chains.
+// Block = BW x (R*PPL) pixels per wave; PPL 1: 8x8 (4 waves per 16x16 tile),
+// PPL 2: 8x16 (2 waves), PPL 4: 16x16 (1 wave).  One splat per iteration; the
+// exact ellipse-vs-block cull of the batch is the only skip.
+template <bool DIAG, int PPL>
+__global__ __launch_bounds__(256) void k_blend_px(const uint64_t* __restrict__ pairs,
+                                                   const uint2* __restrict__ ranges,
+                                                   const uint4* __restrict__ rec, int tiles_x, int tiles_y,
+                                                   int W, int H, int cover_w, int cover_h,
+                                                   float* __restrict__ out,
+                                                   unsigned long long* __restrict__ counters) {
+    constexpr int BW = PPL == 4 ? 16 : 8;          // block width
+    constexpr int R = 64 / BW;                     // rows per pixel pass
+    constexpr int BH = R * PPL;                    // block height
+    constexpr int WPT = (GSR_TILE_PX / BW) * (GSR_TILE_PX / BH);   // waves per tile
+    constexpr int TPB = 256 / (64 * WPT);          // tiles per 256-thread workgroup
+    __shared__ uint4 sA[4][64], sB[4][64], sC[4][64];
+    const int ntiles = tiles_x * tiles_y;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int tslot = blockIdx.x * TPB + w / WPT;
+    if (tslot >= ntiles) return;                   // whole wave exits (no barrier in this kernel)
+    const int tile = xcd_remap(tslot, ntiles);
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
+    const int wt = w % WPT;                        // wave within its tile
+    const int bx = tx * GSR_TILE_PX + (wt % (GSR_TILE_PX / BW)) * BW;
+    const int by = ty * GSR_TILE_PX + (wt / (GSR_TILE_PX / BW)) * BH;
+    const int px = bx + (lane % BW), py0 = by + lane / BW;
+    const float fpx = (float)px;
+    float T[PPL], cr[PPL], cg[PPL], cb[PPL];
+    bool inside[PPL];
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+        inside[j] = px < cover_w && py0 + R * j < cover_h;
+        T[j] = inside[j] ? 1.0f : 0.0f;
+        cr[j] = cg[j] = cb[j] = 0.0f;
+    }
+    const uint2 rr = ranges[tile];
+    const uint32_t beg = rr.y ? ~rr.x : 0u, end = rr.y;
+    uint64_t d_loaded = 0, d_iter = 0, d_active = 0, d_taken = 0;
+    uint4* wA = sA[w];
+    uint4* wB = sB[w];
+    uint4* wC = sC[w];
+
+    uint4 ra = make_uint4(0, 0, 0, 0), rb = ra, rc = ra;
+    uint32_t nidx = 0;
+    if (beg + lane < end) {
+        const uint32_t gi = (uint32_t)pairs[beg + lane];
+        const uint4* Rp = rec + 4 * (uint64_t)gi;
+        ra = Rp[0];
+        rb = Rp[1];
+        rc = Rp[2];
+    }
+    if (beg + 64 + lane < end) nidx = (uint32_t)pairs[beg + 64 + lane];
+    auto unsat_any = [&]() {
+        bool u = false;
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) u |= !(T[j] < 1e-3f);
+        return __ballot(u) != 0ull;
+    };
+    bool alive = unsat_any();
+    for (uint32_t base = beg; base < end && alive; base += 64) {
+        const uint32_t cnt = min(64u, end - base);
+        wA[lane] = ra;
+        wB[lane] = rb;
+        wC[lane] = rc;
+        bool h = false;
+        if ((uint32_t)lane < cnt) {
+            const int xmin = (int)(rc.z & 0xffffu), xmax = (int)(rc.z >> 16);
+            const int ymin = (int)(rc.w & 0xffffu), ymax = (int)(rc.w >> 16);
+            h = !(xmax < bx || xmin > bx + BW - 1 || ymax < by || ymin > by + BH - 1);
+            if (h) {
+                const float cx = (float)(int)rc.x, cy = (float)(int)rc.y;
+                h = block_may_reach(__uint_as_float(ra.x), __uint_as_float(ra.y), __uint_as_float(ra.z),
+                                    __uint_as_float(ra.w), (float)max(bx, xmin) - cx,
+                                    (float)min(bx + BW - 1, xmax) - cx, (float)max(by, ymin) - cy,
+                                    (float)min(by + BH - 1, ymax) - cy, md2_cutoff(__uint_as_float(rb.x)));
+            }
+        }
+        uint64_t m = __ballot(h);
+        if (DIAG) d_loaded += cnt;
+        if (base + 64 + lane < end) {
+            const uint4* Rp = rec + 4 * (uint64_t)nidx;
+            ra = Rp[0];
+            rb = Rp[1];
+            rc = Rp[2];
+        }
+        if (base + 128 + lane < end) nidx = (uint32_t)pairs[base + 128 + lane];
+        while (m && alive) {
+            const int s = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint4 C = wC[s], A = wA[s], B = wB[s];
+            const int xmin = (int)(C.z & 0xffffu), xmax = (int)(C.z >> 16);
+            const int ymin = (int)(C.w & 0xffffu), ymax = (int)(C.w >> 16);
+            const bool xin = (px >= xmin) & (px <= xmax);
+            const float dx = fpx - (float)(int)C.x;
+            const float cy = (float)(int)C.y;
+            const float a = __uint_as_float(A.x), b = __uint_as_float(A.y);
+            const float c = __uint_as_float(A.z), e = __uint_as_float(A.w);
+            const float ax = a * dx, cx = c * dx;
+            if (DIAG) d_iter += 1;
+#pragma unroll
+            for (int j = 0; j < PPL; ++j) {
+                const int py = py0 + R * j;
+                const float dy = (float)py - cy;
+                // render.cu:329-340, same operation order
+                const float md = dx * (ax + b * dy) + dy * (cx + e * dy);
+                const float ee = gsr_expf(-0.5f * md);
+                float alpha = __uint_as_float(B.x) * ee;
+                alpha = fminf(alpha, 0.99f);
+                const bool box = xin & (py >= ymin) & (py <= ymax);
+                const bool take = box & !(T[j] < 1e-3f) & !(alpha < 1e-3f);
+                const float wr = __uint_as_float(B.y) * alpha * T[j];
+                const float wg = __uint_as_float(B.z) * alpha * T[j];
+                const float wb = __uint_as_float(B.w) * alpha * T[j];
+                const float Tn = T[j] * (1.0f - alpha);
+                if (DIAG) {
+                    d_active += (uint64_t)__popcll(__ballot(box & !(T[j] < 1e-3f)));
+                    d_taken += (uint64_t)__popcll(__ballot(take));
+                }
+                cr[j] = take ? cr[j] + wr : cr[j];
+                cg[j] = take ? cg[j] + wg : cg[j];
+                cb[j] = take ? cb[j] + wb : cb[j];
+                T[j] = take ? Tn : T[j];
+            }
+            alive = unsat_any();
+        }
+    }
+    if (DIAG && lane == 0) {
+        if (wt == 0 && d_loaded) atomicAdd(counters, (unsigned long long)d_loaded);
+        atomicAdd(counters + 1, (unsigned long long)d_iter);
+        atomicAdd(counters + 2, (unsigned long long)d_active);
+        atomicAdd(counters + 3, (unsigned long long)d_taken);
+        atomicAdd(counters + 6, (unsigned long long)(d_iter * 64 * PPL));
+    }
+    const size_t hw = (size_t)W * (size_t)H;
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+        const int py = py0 + R * j;
+        if (px < W && py < H) {
+            const size_t o = (size_t)py * (size_t)W + (size_t)px;
+            out[o] = inside[j] ? cr[j] : 0.0f;
+            out[hw + o] = inside[j] ? cg[j] : 0.0f;
+            out[2 * hw + o] = inside[j] ? cb[j] : 0.0f;
+        }
     }
 }
 
@@ -866,10 +1272,38 @@ hipError_t launch_emit(const uint64_t* depth_sorted, uint32_t n, const uint4* re
     return hipGetLastError();
 }
 
+template <int PPL>
+static void blend_px(const uint64_t* pairs, const uint2* ranges, const uint4* rec, const Frame& fr, float* out,
+                     unsigned long long* consumed, hipStream_t s) {
+    constexpr int TPB = PPL;   // tiles per 256-thread workgroup (waves per tile = 4 / PPL)
+    const int nt = fr.tiles_x * fr.tiles_y;
+    const dim3 grid((nt + TPB - 1) / TPB);
+    if (consumed)
+        hipLaunchKernelGGL((k_blend_px<true, PPL>), grid, dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x,
+                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
+    else
+        hipLaunchKernelGGL((k_blend_px<false, PPL>), grid, dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x,
+                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
+}
+
 hipError_t launch_blend(const uint64_t* pairs, const uint2* ranges, const uint4* rec, const Frame& fr,
-                        float* out, unsigned long long* consumed, hipStream_t s) {
+                        float* out, unsigned long long* consumed, int variant, hipStream_t s) {
     const int nt = fr.tiles_x * fr.tiles_y;
     if (nt <= 0) return hipSuccess;
+    switch (variant) {
+    case 1: blend_px<1>(pairs, ranges, rec, fr, out, consumed, s); return hipGetLastError();
+    case 2: blend_px<2>(pairs, ranges, rec, fr, out, consumed, s); return hipGetLastError();
+    case 4: blend_px<4>(pairs, ranges, rec, fr, out, consumed, s); return hipGetLastError();
+    case 5:
+        if (consumed)
+            hipLaunchKernelGGL(k_blend_v5<true>, dim3(nt), dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x,
+                               fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
+        else
+            hipLaunchKernelGGL(k_blend_v5<false>, dim3(nt), dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x,
+                               fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
+        return hipGetLastError();
+    default: break;
+    }
     if (consumed)
         hipLaunchKernelGGL(k_blend<true>, dim3(nt), dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x, fr.tiles_y,
                            fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);

@@ -459,6 +459,7 @@ struct gsr_context {
     float* soa_tmp = nullptr;
     unsigned long long* consumed = nullptr;   // diagnostics: records loaded by the blend
     bool diagnostics = false;
+    int blend_variant = 0;
     // frame state
     Frame fr{};
     int64_t n = 0;
@@ -737,7 +738,7 @@ static int blend_locked(gsr_context* c, float* d_out) {
         HIP_TRY(hipMemsetAsync(c->consumed, 0, 8 * sizeof(unsigned long long), c->stream));
     }
     HIP_TRY(gsr::launch_blend(c->pairs[c->pair_buf], c->ranges, c->rec, c->fr, d_out,
-                              c->diagnostics ? c->consumed : nullptr, c->stream));
+                              c->diagnostics ? c->consumed : nullptr, c->blend_variant, c->stream));
     mark(c, GSR_NUM_STAGES);
     if (c->timing) c->ev_frames.push_back(c->cur);
     c->cur = FrameEvents{};
@@ -879,6 +880,15 @@ extern "C" int gsr_set_diagnostics(gsr_context* c, int on) {
     if (!c) return set_err(GSR_E_ARG, "null context");
     std::lock_guard<std::mutex> lk(c->mu);
     c->diagnostics = on != 0;
+    return GSR_OK;
+}
+
+extern "C" int gsr_set_blend_variant(gsr_context* c, int variant) {
+    if (!c) return set_err(GSR_E_ARG, "null context");
+    if (variant != 0 && variant != 1 && variant != 2 && variant != 4 && variant != 5)
+        return set_err(GSR_E_ARG, "gsr_set_blend_variant: variant must be 0, 1, 2, 4 or 5");
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->blend_variant = variant;
     return GSR_OK;
 }
 

@@ -157,10 +157,18 @@ int gsr_set_diagnostics(gsr_context* ctx, int on);
 int64_t gsr_blend_records_loaded(gsr_context* ctx);
 /* All blend counters of the last diagnostics frame (8 values): {records
  * loaded (Pc), wave-splat iterations, active lanes (in AABB and not
- * saturated), lanes that composited, iterations with no active lane,
- * iterations skipped by the per-splat md2 cutoff, 0, 0};
- * lane efficiency = active / (64 * iterations). */
+ * saturated), lanes that composited, iterations on the exact one-splat
+ * path (default schedule; batches without the fast-path proof),
+ * iterations skipped by the per-splat md2 cutoff (variant 5), pixel-lane slots
+ * (64 x pixels per lane x iterations), 0};
+ * lane efficiency = active / slots. */
 int gsr_blend_counters(gsr_context* ctx, int64_t* out8);
+/* Blend schedule (tuning knob, default 0): 0 = 8x8 block per wave, survivors
+ * compacted into pair slots, two splats per iteration with packed math;
+ * 1, 2, 4 = pixel-chain kernel with that many pixels per lane (8x8, 8x16,
+ * 16x16 blocks); 5 = previous 8x8 two-splat kernel.  All produce
+ * bit-identical images. */
+int gsr_set_blend_variant(gsr_context* ctx, int variant);
 
 /* ---------------------------------------------------------------- scenes */
 

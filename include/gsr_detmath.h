@@ -102,9 +102,16 @@ GSR_HD float gsr_expf(float x) {
     const float r2 = r * r;
     const float y = __builtin_fmaf(p, r2, r) + 1.0f;
     const int ni = (int)n;                                /* n in [-150, 128] */
+#if defined(__HIP_DEVICE_COMPILE__)
+    /* v_ldexp_f32: one correctly rounded y * 2^ni — the same value as the two
+     * multiplies below (y * 2^e1 is exact and normal, so the second product
+     * is the only rounding); gfx950 keeps f32 denormals. */
+    const float res = __builtin_amdgcn_ldexpf(y, ni);
+#else
     const int e1 = ni / 2;
     const int e2 = ni - e1;
     const float res = (y * gsr_pow2i(e1)) * gsr_pow2i(e2);
+#endif
     return (x != x) ? x + x : res;                        /* NaN */
 }
 

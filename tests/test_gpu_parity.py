@@ -151,6 +151,26 @@ def test_image_config1_parity(gpu, orc, torch, c1, ci):
     assert_image_parity(got, want)
 
 
+@pytest.mark.parametrize("variant", [1, 2, 4])
+@pytest.mark.parametrize("ci", [0, 2])
+def test_blend_variants_parity(gpu, orc, torch, c1, variant, ci):
+    """Every blend schedule (gsr_set_blend_variant) is bit-exact vs the oracle,
+    including partial coverage and sizes that are not multiples of the blocks."""
+    path, soa = c1
+    scene = gpu.Scene.from_soa(soa)
+    for W, H, tiling in ((640, 480, None), (37, 23, None), (640, 480, (7, 3, 92, 160))):
+        cam = cam_for(gpu, W, H, **CAMS[ci])
+        r = gpu.Renderer()
+        r.set_blend_variant(variant)
+        t = None
+        if tiling is not None:
+            t = gpu.TilingInformation(1, 1, H, W)
+            t.num_tile_x, t.num_tile_y, t.width_stride, t.height_stride = tiling
+        got, _ = render_gpu(gpu, torch, scene, cam, W, H, tiling=t, renderer=r)
+        want = orc.render(soa, cam, W, H, 3.0, tiling=tiling)
+        assert_image_parity(got, want)
+
+
 def test_dropin_scene_block_reference_tiling(gpu, orc, torch, c1):
     """loadGaussianCudaFromPly + preprocessCUDAGaussians (the viewer's calls),
     reference 50x50 tiling (cull_sort_test.cpp:44-45)."""
