@@ -259,6 +259,17 @@ class Renderer:
     def set_blend_variant(self, variant: int):
         check(lib().gsr_set_blend_variant(self.ctx, int(variant)), "gsr_set_blend_variant")
 
+    def set_tuning(self, knob: int, value: int):
+        """gsr_set_tuning: 0 blend schedule, 1 tile-sort items/thread, 2 depth-sort items/thread."""
+        check(lib().gsr_set_tuning(self.ctx, int(knob), int(value)), "gsr_set_tuning")
+
+    def blend_stamps(self, n_groups: int) -> np.ndarray:
+        """{start, end} s_memrealtime stamps (100 MHz) per blend workgroup of the
+        last diagnostics frame rendered with schedule 2."""
+        out = np.zeros(2 * n_groups, dtype=np.uint64)
+        check(lib().gsr_blend_stamps(self.ctx, out.ctypes.data, out.size), "gsr_blend_stamps")
+        return out.reshape(n_groups, 2)
+
     def stage_times(self):
         ms = (ctypes.c_double * NUM_STAGES)()
         frames = c_int64()

@@ -101,6 +101,8 @@ SIGNATURES = [
     ("gsr_blend_records_loaded", c_int64, [c_void_p]),
     ("gsr_blend_counters", c_int, [c_void_p, c_void_p]),
     ("gsr_set_blend_variant", c_int, [c_void_p, c_int]),
+    ("gsr_blend_stamps", c_int, [c_void_p, c_void_p, c_int64]),
+    ("gsr_set_tuning", c_int, [c_void_p, c_int, c_int]),
     ("gsr_scene_upload", c_void_p, [c_void_p, c_int64]),
     ("gsr_scene_free", None, [c_void_p]),
     ("gsr_scene_download", c_int, [c_void_p, c_void_p, c_int64]),

@@ -27,7 +27,7 @@ struct Frame {
 // Radix-sort geometry.
 constexpr int kSortThreads = 256;
 constexpr int kSortTile = kSortThreads * 16;           // largest tile (items = 16 per thread)
-constexpr int kMaxSortGroups = 1024;                    // fixed grid upper bound
+constexpr int kMaxSortGroups = 8192;                    // grid upper bound (hist: 256 x this)
 
 // Device-side frame statistics block (device memory).
 struct Stats {
@@ -40,7 +40,7 @@ struct Stats {
 hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, int64_t stride,
                              hipStream_t s);
 hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
-                             uint4* rec, uint64_t* items, hipStream_t s);
+                             uint4* rec, uint64_t* items, uint64_t* rect, hipStream_t s);
 // One stable LSD pass over u64 items on bits [shift, shift + bits) (bits <= 8).
 // n = n_dev ? *n_dev : n_host.  hist: 256 * groups u32, totals: 256 u32.
 // ranges (nullable, final tile-sort pass): per-tile {~start, end} of key (item >> 32),
@@ -49,14 +49,22 @@ hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, con
 hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
                              int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
                              uint2* ranges, hipStream_t s);
-hipError_t launch_emit(const uint64_t* depth_sorted, uint32_t n, const uint4* rec, int groups,
+// Pair emission in depth order: tile counts (gathering each Gaussian's rect
+// once into srect), scan, then keys (uint16_t if key16 else uint32_t) + values.
+hipError_t launch_emit(const uint64_t* depth_sorted, uint32_t n, const uint64_t* rect, int groups,
                        unsigned long long* wg_scratch, Stats* stats, Stats* host_mapped_stats,
-                       uint32_t pair_capacity, int tiles_x, uint64_t* pairs, hipStream_t s);
-// consumed: optional device counters (diagnostics).  variant: blend kernel
-// schedule (0 = default; 1/2/4 = pixel-chain kernel with that many pixels per
-// lane) — every variant produces bit-identical images.
-hipError_t launch_blend(const uint64_t* pairs, const uint2* ranges, const uint4* rec, const Frame& fr,
-                        float* out, unsigned long long* consumed, int variant, hipStream_t s);
+                       uint32_t pair_capacity, int tiles_x, uint64_t* srect, void* keys, bool key16,
+                       uint32_t* vals, hipStream_t s);
+// One stable key-value LSD pass of the tile sort; keys_out == nullptr marks the
+// final pass (values only, tile ranges recorded).
+hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* keys_out, uint32_t* vals_out,
+                          bool key16, const uint32_t* n_dev, int shift, int bits, int groups, int items,
+                          uint32_t* hist, uint32_t* totals, uint2* ranges, hipStream_t s);
+// consumed: optional device counters (diagnostics).  variant 1 = persistent
+// per-wave block queue (queue: 8 device uints; resident_groups: grid size).
+hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
+                        float* out, unsigned long long* consumed, int variant, unsigned int* queue,
+                        int resident_groups, hipStream_t s);
 // Standalone sort ABI helpers (oneSweepSort / oneSweep3DGaussianSort).
 hipError_t launch_items_from_keys(const int* keys, uint32_t n, uint64_t* items, hipStream_t s);
 hipError_t launch_keys_from_items(const uint64_t* items, uint32_t n, int* keys, hipStream_t s);

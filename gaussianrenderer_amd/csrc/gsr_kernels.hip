@@ -3,23 +3,28 @@
 // Pipeline per frame (all stream-ordered, no host round trip):
 //   k_preprocess      one thread per Gaussian, SoA coalesced loads: cull + SH
 //                     colour + view/clip + 2D covariance + extent + AABB, writes a
-//                     64-B splat record and the (depth_key << 32 | index) item
-//                     [render.cu:472-786]
+//                     64-B splat record, the (depth_key << 32 | index) item and
+//                     a compact 8-B tile rectangle [render.cu:472-786]
 //   radix passes      stable LSD sort of the N items by depth key (4 x 8 bits)
-//   k_emit_*          scan of per-Gaussian tile counts in depth order, then one
-//                     (tile << 32 | index) pair per covered 16x16 tile
-//                     [render.cu:811-857, 788-809]
-//   radix passes      stable LSD sort of the pairs by tile id (2 x <= 8 bits)
-//                     (the last tile pass also records each tile's [start, end))
-//   k_blend           one workgroup per 16x16 tile, one pixel per lane, 8x8 pixel
-//                     block per wave64; LDS-staged batches of 256 splat records;
-//                     exact per-pixel early termination [render.cu:266-367]
+//   k_emit_*          tile counts in depth order (the rect gathered once), scan,
+//                     then one (tile key, index) pair per covered 16x16 tile as
+//                     separate key / value arrays [render.cu:811-857, 788-809]
+//   k_kv_* passes     stable key-value LSD sort of the pairs by tile (2 x <= 8
+//                     bits; the last pass writes values only and records each
+//                     tile's [start, end))
+//   k_blend           one workgroup per 16x16 tile, one wave64 per 8x8 block,
+//                     one pixel per lane; 64-record batches culled against the
+//                     block, survivors compacted into LDS pair slots, two
+//                     splats per iteration with packed math; exact per-pixel
+//                     early termination [render.cu:266-367]
 //
 // Every float expression restates render.cu / math.cu in the same operation
 // order; the file is compiled with -ffp-contract=off so no FMA is formed
 // implicitly, and the transcendental functions come from gsr_detmath.h, so the
 // results are bit-identical to the CPU oracle (oracle/gsr_oracle.c).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 #include "gsr_detmath.h"
 #include "gsr.h"
@@ -139,9 +144,19 @@ __device__ __forceinline__ uint4 dead_record_d() {
     return make_uint4(0u, 0u, 0u, 0xffffffffu);
 }
 
+// Compact tile rectangle of one Gaussian for the emission: tx0 | tx1 << 16 |
+// ty0 << 32 | ty1 << 48; tile count (tx1 - tx0 + 1) * (ty1 - ty0 + 1), which
+// is 0 for the dead value below (tx0 = ty0 = 1, tx1 = ty1 = 0).
+constexpr uint64_t kDeadRect = 0x0000000100000001ull;
+__device__ __forceinline__ uint32_t rect_count(uint64_t r) {
+    const int tx0 = (int)(r & 0xffffu), tx1 = (int)((r >> 16) & 0xffffu);
+    const int ty0 = (int)((r >> 32) & 0xffffu), ty1 = (int)(r >> 48);
+    return (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1));
+}
+
 __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ arr, int64_t stride,
                                                     int64_t n, Frame fr, uint4* __restrict__ rec,
-                                                    uint64_t* __restrict__ items) {
+                                                    uint64_t* __restrict__ items, uint64_t* __restrict__ rect) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const float gx = arr[GSR_A_X * stride + i];
@@ -156,6 +171,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     mv4(fr.V, old_xyz, tmp_xyz);
     if (!isfinite(tmp_xyz[0]) || !isfinite(tmp_xyz[1]) || !isfinite(tmp_xyz[2])) {
         R[3] = dead_record_d();
+        rect[i] = kDeadRect;
         return;
     }
     mv4(fr.P, tmp_xyz, new_xyz);
@@ -165,6 +181,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     if (!isfinite(new_xyz[0]) || !isfinite(new_xyz[1]) || !isfinite(new_xyz[2]) ||
         tmp_xyz[2] >= -fr.znear || new_xyz[2] < -1.0f || new_xyz[2] > 1.0f) {
         R[3] = dead_record_d();
+        rect[i] = kDeadRect;
         return;
     }
 
@@ -212,6 +229,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     const float det = S2[0] * S2[3] - S2[1] * S2[2];
     if (!isfinite(det) || det < 1e-8f) {                        // render.cu:690
         R[3] = dead_record_d();
+        rect[i] = kDeadRect;
         return;
     }
     const float invDet = 1.0f / det;
@@ -240,6 +258,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     float ymin = new_xyz[1] - ey, ymax = new_xyz[1] + ey;
     if (xmax < -0.99f || xmin > 0.99f || ymax < -0.99f || ymin > 0.99f) {   // render.cu:737
         R[3] = dead_record_d();
+        rect[i] = kDeadRect;
         return;
     }
     xmin = fmaxf(xmin, -1.0f);
@@ -300,6 +319,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     R[2] = make_uint4((uint32_t)px_x, (uint32_t)px_y, (uint32_t)xmin_px | ((uint32_t)xmax_px << 16),
                       (uint32_t)ymin_px | ((uint32_t)ymax_px << 16));
     R[3] = make_uint4((uint32_t)tx0 | ((uint32_t)tx1 << 16), (uint32_t)ty0 | ((uint32_t)ty1 << 16), count, key);
+    rect[i] = (uint64_t)((uint32_t)tx0 | ((uint32_t)tx1 << 16)) | ((uint64_t)((uint32_t)ty0 | ((uint32_t)ty1 << 16)) << 32);
     items[i] = ((uint64_t)key << 32) | (uint64_t)(uint32_t)i;
 }
 
@@ -466,18 +486,175 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     }
 }
 
+// Key-value variant for the tile sort: keys of type K (uint16_t when the frame
+// has <= 65536 tiles, else uint32_t) and uint32_t values in separate arrays,
+// so the upsweep reads only the keys and the final pass writes only the values
+// (plus the tile ranges).  Same reduce-then-scan structure and ranking.
+template <typename K, int ITEMS>
+__global__ __launch_bounds__(kSortThreads) void k_kv_upsweep(const K* __restrict__ keys,
+                                                             const uint32_t* __restrict__ n_dev, int shift,
+                                                             uint32_t mask, int groups,
+                                                             uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[4][256];
+    const uint32_t t = threadIdx.x;
+    const uint32_t w = t >> 6;
+#pragma unroll
+    for (int k = 0; k < 4; k++) h[k][t] = 0;
+    __syncthreads();
+    const uint64_t n = (uint64_t)*n_dev;
+    uint64_t b, e;
+    chunk_range(n, groups, blockIdx.x, kSortThreads * ITEMS, b, e);
+    uint64_t i = b + t;
+    for (; i + 3 * kSortThreads < e; i += 4 * kSortThreads) {
+        const uint32_t k0 = keys[i], k1 = keys[i + kSortThreads], k2 = keys[i + 2 * kSortThreads],
+                       k3 = keys[i + 3 * kSortThreads];
+        atomicAdd(&h[w][(k0 >> shift) & mask], 1u);
+        atomicAdd(&h[w][(k1 >> shift) & mask], 1u);
+        atomicAdd(&h[w][(k2 >> shift) & mask], 1u);
+        atomicAdd(&h[w][(k3 >> shift) & mask], 1u);
+    }
+    for (; i < e; i += kSortThreads) atomicAdd(&h[w][((uint32_t)keys[i] >> shift) & mask], 1u);
+    __syncthreads();
+    hist[t * (uint32_t)groups + blockIdx.x] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
+}
+
+// keys_out == nullptr: final pass — write values only and record each tile's
+// global [start, end) as {~start, end} (atomicMax; a zeroed array = empty).
+template <typename K, int ITEMS>
+__global__ __launch_bounds__(kSortThreads) void k_kv_downsweep(
+    const K* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, K* __restrict__ keys_out,
+    uint32_t* __restrict__ vals_out, const uint32_t* __restrict__ n_dev, int shift, int bits, int groups,
+    const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals, uint2* __restrict__ ranges) {
+    constexpr int kTile = kSortThreads * ITEMS;
+    __shared__ K s_keys[kTile];
+    __shared__ uint32_t s_vals[kTile];
+    __shared__ uint32_t s_wc[4][256];
+    __shared__ uint32_t s_gbase[256];
+    __shared__ uint32_t s_lbase[256];
+    __shared__ uint32_t s_scr[4];
+    const uint32_t t = threadIdx.x;
+    const uint32_t lane = lane_id();
+    const uint32_t w = t >> 6;
+    const uint32_t mask = (1u << bits) - 1u;
+    const uint64_t n = (uint64_t)*n_dev;
+    uint64_t b, e;
+    chunk_range(n, groups, blockIdx.x, kTile, b, e);
+    if (b >= e) return;
+    {
+        uint32_t tot;
+        const uint32_t dig_excl = block_exclusive_scan<uint32_t>(totals[t], s_scr, tot);
+        s_gbase[t] = dig_excl + hist[t * (uint32_t)groups + blockIdx.x];
+    }
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+    for (uint64_t tb = b; tb < e; tb += kTile) {
+        const uint32_t tn = (uint32_t)min((uint64_t)kTile, e - tb);
+#pragma unroll
+        for (int k = 0; k < 4; k++) s_wc[k][t] = 0;
+        __syncthreads();
+        uint32_t kk[ITEMS], vv[ITEMS], rk[ITEMS];
+        const uint32_t wbase = w * 64 * ITEMS;
+#pragma unroll
+        for (int k = 0; k < ITEMS; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            kk[k] = (el < tn) ? (uint32_t)keys_in[tb + el] : 0u;
+            vv[k] = (el < tn) ? vals_in[tb + el] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < ITEMS; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            const bool valid = el < tn;
+            const uint32_t d = (kk[k] >> shift) & mask;
+            uint64_t peers = __ballot(valid);
+            for (int bit = 0; bit < bits; bit++) {
+                const bool on = (d >> bit) & 1u;
+                const uint64_t bm = __ballot(on);
+                peers &= on ? bm : ~bm;
+            }
+            uint32_t r = 0;
+            if (valid) {
+                const uint32_t before = s_wc[w][d];
+                r = before + (uint32_t)__popcll(peers & lt_mask);
+                if ((uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
+                    s_wc[w][d] = before + (uint32_t)__popcll(peers);
+            }
+            rk[k] = r;
+        }
+        __syncthreads();
+        uint32_t tcount;
+        {
+            const uint32_t c0 = s_wc[0][t], c1 = s_wc[1][t], c2 = s_wc[2][t], c3 = s_wc[3][t];
+            s_wc[0][t] = 0;
+            s_wc[1][t] = c0;
+            s_wc[2][t] = c0 + c1;
+            s_wc[3][t] = c0 + c1 + c2;
+            tcount = c0 + c1 + c2 + c3;
+            uint32_t tot;
+            s_lbase[t] = block_exclusive_scan<uint32_t>(tcount, s_scr, tot);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < ITEMS; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            if (el < tn) {
+                const uint32_t d = (kk[k] >> shift) & mask;
+                const uint32_t q = s_lbase[d] + s_wc[w][d] + rk[k];
+                s_keys[q] = (K)kk[k];
+                s_vals[q] = vv[k];
+            }
+        }
+        __syncthreads();
+        for (uint32_t q = t; q < tn; q += kSortThreads) {
+            const uint32_t key = s_keys[q];
+            const uint32_t d = (key >> shift) & mask;
+            const uint32_t dst = s_gbase[d] + (q - s_lbase[d]);
+            vals_out[dst] = s_vals[q];
+            if (keys_out) {
+                keys_out[dst] = (K)key;
+            } else {
+                if (q == 0 || (uint32_t)s_keys[q - 1] != key) atomicMax(&ranges[key].x, ~dst);
+                if (q == tn - 1 || (uint32_t)s_keys[q + 1] != key) atomicMax(&ranges[key].y, dst + 1);
+            }
+        }
+        __syncthreads();
+        s_gbase[t] += tcount;
+    }
+}
+
 // ------------------------------------------------------------------ emission
 
+// Tile counts in depth order.  The one random access of the emission — the
+// compact rect of Gaussian sorted[j] — happens here, once; the rects are
+// written back in depth order (srect) so k_emit_pairs reads them coalesced.
+// Each thread issues all four of its index loads, then all four rect gathers,
+// so the dependent gathers overlap instead of running back to back.
 __global__ __launch_bounds__(256) void k_emit_count(const uint64_t* __restrict__ sorted, uint32_t n,
-                                                     const uint4* __restrict__ rec, int groups,
-                                                     unsigned long long* __restrict__ wg_sum) {
+                                                     const uint64_t* __restrict__ rect, int groups,
+                                                     unsigned long long* __restrict__ wg_sum,
+                                                     uint64_t* __restrict__ srect) {
     __shared__ unsigned long long scr[4];
     uint64_t b, e;
-    chunk_range(n, groups, blockIdx.x, 256, b, e);
+    chunk_range(n, groups, blockIdx.x, 1024, b, e);
     unsigned long long s = 0;
-    for (uint64_t j = b + threadIdx.x; j < e; j += 256) {
-        const uint32_t i = (uint32_t)sorted[j];
-        s += rec[4 * (uint64_t)i + 3].z;
+    for (uint64_t c0 = b; c0 < e; c0 += 1024) {
+        uint32_t gi[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t j = c0 + threadIdx.x + 256 * k;
+            gi[k] = j < e ? (uint32_t)sorted[j] : 0u;
+        }
+        uint64_t r[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t j = c0 + threadIdx.x + 256 * k;
+            r[k] = j < e ? rect[gi[k]] : kDeadRect;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t j = c0 + threadIdx.x + 256 * k;
+            if (j < e) srect[j] = r[k];
+            s += rect_count(r[k]);
+        }
     }
     unsigned long long tot;
     block_exclusive_scan<unsigned long long>(s, scr, tot);
@@ -522,36 +699,83 @@ __global__ __launch_bounds__(256) void k_emit_scan(unsigned long long* __restric
     }
 }
 
+// One (tile key, Gaussian index) pair per covered tile, in depth order, as
+// separate key (K = uint16_t or uint32_t) and value (uint32_t) arrays for the
+// key-value tile sort [render.cu:788-809].  Each wave owns 256 consecutive
+// Gaussians of the workgroup's 1024 and writes their pairs cooperatively:
+// per round of 64 Gaussians, lane l of a 64-pair step finds its Gaussian by a
+// binary search over the round's inclusive count prefix, so every store
+// instruction writes 64 consecutive pairs.
+template <typename K>
 __global__ __launch_bounds__(256) void k_emit_pairs(const uint64_t* __restrict__ sorted, uint32_t n,
-                                                     const uint4* __restrict__ rec, int groups,
+                                                     const uint64_t* __restrict__ srect, int groups,
                                                      const unsigned long long* __restrict__ wg_base,
-                                                     uint32_t cap, int tiles_x,
-                                                     uint64_t* __restrict__ pairs) {
+                                                     uint32_t cap, int tiles_x, K* __restrict__ keys,
+                                                     uint32_t* __restrict__ vals) {
     __shared__ unsigned long long scr[4];
+    __shared__ uint32_t s_incl[4][64], s_idx[4][64];
+    __shared__ uint64_t s_rect[4][64];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     uint64_t b, e;
-    chunk_range(n, groups, blockIdx.x, 256, b, e);
+    chunk_range(n, groups, blockIdx.x, 1024, b, e);
     unsigned long long run = wg_base[blockIdx.x];
-    for (uint64_t rb = b; rb < e; rb += 256) {
-        const uint64_t j = rb + threadIdx.x;
-        uint32_t cnt = 0, i = 0;
-        uint4 D = make_uint4(0, 0, 0, 0);
-        if (j < e) {
-            i = (uint32_t)sorted[j];
-            D = rec[4 * (uint64_t)i + 3];
-            cnt = D.z;
+    for (uint64_t c0 = b; c0 < e; c0 += 1024) {
+        // this wave's 256 Gaussians: [c0 + 256 w, +256), four rounds of 64
+        uint32_t cnt[4], gi[4];
+        uint64_t r[4];
+        uint32_t wtot = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t j = c0 + 256 * w + 64 * k + lane;
+            gi[k] = j < e ? (uint32_t)sorted[j] : 0u;
+            r[k] = j < e ? srect[j] : kDeadRect;
         }
-        unsigned long long tot;
-        unsigned long long pos = run + block_exclusive_scan<unsigned long long>(cnt, scr, tot);
-        if (cnt) {
-            const uint32_t tx0 = D.x & 0xffffu, tx1 = D.x >> 16;
-            const uint32_t ty0 = D.y & 0xffffu, ty1 = D.y >> 16;
-            for (uint32_t ty = ty0; ty <= ty1; ty++)
-                for (uint32_t tx = tx0; tx <= tx1; tx++) {
-                    if (pos < cap) pairs[pos] = ((uint64_t)(ty * (uint32_t)tiles_x + tx) << 32) | i;
-                    pos++;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            cnt[k] = rect_count(r[k]);
+            wtot += cnt[k];
+        }
+        // wave totals -> exclusive base of this wave inside the 1024-chunk
+        unsigned long long chunk_tot;
+        const unsigned long long wsum = (unsigned long long)__reduce_add_sync(~0ull, wtot);
+        const unsigned long long wbase = block_exclusive_scan<unsigned long long>(lane == 0 ? wsum : 0ull, scr,
+                                                                                  chunk_tot);
+        unsigned long long pos = run + (unsigned long long)__shfl(wbase, 0, 64);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            // inclusive prefix of the round's counts
+            uint32_t incl = cnt[k];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (lane >= (uint32_t)o) incl += y;
+            }
+            const uint32_t rtot = __shfl(incl, 63, 64);
+            s_incl[w][lane] = incl;
+            s_idx[w][lane] = gi[k];
+            s_rect[w][lane] = r[k];
+            for (uint32_t q = lane; q < rtot; q += 64) {
+                // Gaussian l: the first lane whose inclusive prefix exceeds q
+                uint32_t l = 0;
+#pragma unroll
+                for (uint32_t st = 32; st >= 1; st >>= 1)
+                    if (s_incl[w][l + st - 1] <= q) l += st;
+                const uint64_t rr = s_rect[w][l];
+                const uint32_t before = s_incl[w][l] - rect_count(rr);   // exclusive prefix of Gaussian l
+                const uint32_t k2 = q - before;
+                const uint32_t tx0 = (uint32_t)(rr & 0xffffu), tx1 = (uint32_t)((rr >> 16) & 0xffffu);
+                const uint32_t ty0 = (uint32_t)((rr >> 32) & 0xffffu);
+                const uint32_t wdt = tx1 - tx0 + 1u;
+                const uint32_t dy = k2 / wdt, dx = k2 - dy * wdt;
+                const unsigned long long p = pos + q;
+                if (p < cap) {
+                    keys[p] = (K)((ty0 + dy) * (uint32_t)tiles_x + tx0 + dx);
+                    vals[p] = s_idx[w][l];
                 }
+            }
+            pos += rtot;
         }
-        run += tot;
+        run += chunk_tot;
     }
 }
 
@@ -600,167 +824,6 @@ __device__ __forceinline__ bool block_may_reach(float a, float b, float c, float
     const float M = fmaxf(fmaxf(fabsf(dx0), fabsf(dx1)), fmaxf(fabsf(dy0), fabsf(dy1)));
     const float err = 4e-6f * (fabsf(a) + fabsf(b) + fabsf(c) + fabsf(e)) * M * M + 1e-3f;
     return !(qm - err > cut);
-}
-
-// One wave64 per 8x8 pixel block, four per 16x16 tile (one tile per 256-thread
-// workgroup), and NO workgroup barrier: each wave streams its tile's splat list
-// on its own in 64-record batches (lane l holds record l of the batch), with
-// the next batch's pair indices and records prefetched into registers while the
-// current one is composited, and a private LDS slice for the broadcast reads.
-template <bool DIAG>
-__global__ __launch_bounds__(256) void k_blend_v5(const uint64_t* __restrict__ pairs,
-                                                const uint2* __restrict__ ranges,
-                                                const uint4* __restrict__ rec, int tiles_x, int tiles_y,
-                                                int W, int H, int cover_w, int cover_h,
-                                                float* __restrict__ out,
-                                                unsigned long long* __restrict__ counters) {
-    __shared__ uint4 sA[4][64], sB[4][64], sC[4][64];
-    __shared__ float sCut[4][64];
-    const int ntiles = tiles_x * tiles_y;
-    const int tile = xcd_remap(blockIdx.x, ntiles);
-    const int tx = tile % tiles_x, ty = tile / tiles_x;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int bx = tx * GSR_TILE_PX + (w & 1) * 8;
-    const int by = ty * GSR_TILE_PX + (w >> 1) * 8;
-    const int px = bx + (lane & 7), py = by + (lane >> 3);
-    const bool inside = px < cover_w && py < cover_h;
-    const float fpx = (float)px, fpy = (float)py;
-    // transmittance; a pixel is saturated ("done", render.cu:328) iff T < 1e-3.
-    // Pixels outside the covered area start saturated (T = 0) and write 0.
-    float T = inside ? 1.0f : 0.0f;
-    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
-    const uint2 rr = ranges[tile];                       // {~start, end}, zero = empty
-    const uint32_t beg = rr.y ? ~rr.x : 0u, end = rr.y;
-    uint64_t d_loaded = 0, d_iter = 0, d_active = 0, d_taken = 0, d_skipped = 0;
-    uint4* wA = sA[w];
-    uint4* wB = sB[w];
-    uint4* wC = sC[w];
-    float* wCut = sCut[w];
-
-    // software pipeline: records of batch k in (ra, rb, rc); pair index of batch k+1 in nidx
-    uint4 ra = make_uint4(0, 0, 0, 0), rb = ra, rc = ra;
-    uint32_t nidx = 0;
-    if (beg + lane < end) {
-        const uint32_t gi = (uint32_t)pairs[beg + lane];
-        const uint4* R = rec + 4 * (uint64_t)gi;
-        ra = R[0];
-        rb = R[1];
-        rc = R[2];
-    }
-    if (beg + 64 + lane < end) nidx = (uint32_t)pairs[beg + 64 + lane];
-    bool alive = __ballot(!(T < 1e-3f)) != 0ull;
-    for (uint32_t base = beg; base < end && alive; base += 64) {
-        const uint32_t cnt = min(64u, end - base);
-        // stage the current batch in this wave's LDS slice (same-wave LDS ops are in order)
-        wA[lane] = ra;
-        wB[lane] = rb;
-        wC[lane] = rc;
-        wCut[lane] = md2_cutoff(__uint_as_float(rb.x));
-        // cull: lane = record; AABB vs block, then exact ellipse test on block n AABB
-        bool h = false;
-        if ((uint32_t)lane < cnt) {
-            const int xmin = (int)(rc.z & 0xffffu), xmax = (int)(rc.z >> 16);
-            const int ymin = (int)(rc.w & 0xffffu), ymax = (int)(rc.w >> 16);
-            h = !(xmax < bx || xmin > bx + 7 || ymax < by || ymin > by + 7);
-            if (h) {
-                const float cx = (float)(int)rc.x, cy = (float)(int)rc.y;
-                h = block_may_reach(__uint_as_float(ra.x), __uint_as_float(ra.y), __uint_as_float(ra.z),
-                                    __uint_as_float(ra.w), (float)max(bx, xmin) - cx, (float)min(bx + 7, xmax) - cx,
-                                    (float)max(by, ymin) - cy, (float)min(by + 7, ymax) - cy,
-                                    md2_cutoff(__uint_as_float(rb.x)));
-            }
-        }
-        uint64_t m = __ballot(h);
-        if (DIAG) d_loaded += cnt;
-        // prefetch: records of batch k+1 (indices already in nidx), indices of batch k+2
-        if (base + 64 + lane < end) {
-            const uint4* R = rec + 4 * (uint64_t)nidx;
-            ra = R[0];
-            rb = R[1];
-            rc = R[2];
-        }
-        if (base + 128 + lane < end) nidx = (uint32_t)pairs[base + 128 + lane];
-        while (m && alive) {
-            // two splats per iteration: their md2/exp are independent (ILP);
-            // compositing stays strictly in list order, per pixel
-            const int s0 = __builtin_ctzll(m);
-            m &= m - 1;
-            const bool has1 = m != 0ull;
-            const int s1 = has1 ? __builtin_ctzll(m) : s0;
-            if (has1) m &= m - 1;
-            const uint4 C0 = wC[s0], C1 = wC[s1];
-            const uint4 A0 = wA[s0], A1 = wA[s1];
-            const float cut0 = wCut[s0], cut1 = wCut[s1];
-            const bool box0 = (px >= (int)(C0.z & 0xffffu)) & (px <= (int)(C0.z >> 16)) &
-                              (py >= (int)(C0.w & 0xffffu)) & (py <= (int)(C0.w >> 16));
-            const bool box1 = (px >= (int)(C1.z & 0xffffu)) & (px <= (int)(C1.z >> 16)) &
-                              (py >= (int)(C1.w & 0xffffu)) & (py <= (int)(C1.w >> 16)) & has1;
-            // render.cu:329-332, same operation order
-            const float dx0 = fpx - (float)(int)C0.x, dy0 = fpy - (float)(int)C0.y;
-            const float dx1 = fpx - (float)(int)C1.x, dy1 = fpy - (float)(int)C1.y;
-            const float md0 = dx0 * (__uint_as_float(A0.x) * dx0 + __uint_as_float(A0.y) * dy0) +
-                              dy0 * (__uint_as_float(A0.z) * dx0 + __uint_as_float(A0.w) * dy0);
-            const float md1 = dx1 * (__uint_as_float(A1.x) * dx1 + __uint_as_float(A1.y) * dy1) +
-                              dy1 * (__uint_as_float(A1.z) * dx1 + __uint_as_float(A1.w) * dy1);
-            const bool unsat = !(T < 1e-3f);
-            if (DIAG) {
-                d_iter += has1 ? 2 : 1;
-                d_active += (uint64_t)__popcll(__ballot(box0 & unsat)) + (uint64_t)__popcll(__ballot(box1 & unsat));
-            }
-            // no lane can reach alpha >= 1e-3 for either splat: skip both
-            if (__ballot(unsat & ((box0 & !(md0 > cut0)) | (box1 & !(md1 > cut1)))) == 0ull) {
-                if (DIAG) d_skipped += has1 ? 2 : 1;
-                continue;
-            }
-            const uint4 B0 = wB[s0], B1 = wB[s1];
-            const float e0 = gsr_expf(-0.5f * md0);
-            const float e1 = gsr_expf(-0.5f * md1);
-            {   // splat s0 (render.cu:333-340)
-                float alpha = __uint_as_float(B0.x) * e0;
-                alpha = fminf(alpha, 0.99f);
-                const bool take = box0 & unsat & !(alpha < 1e-3f);
-                const float wr = __uint_as_float(B0.y) * alpha * T;
-                const float wg = __uint_as_float(B0.z) * alpha * T;
-                const float wb = __uint_as_float(B0.w) * alpha * T;
-                const float Tn = T * (1.0f - alpha);
-                cr = take ? cr + wr : cr;
-                cg = take ? cg + wg : cg;
-                cb = take ? cb + wb : cb;
-                T = take ? Tn : T;
-                if (DIAG) d_taken += (uint64_t)__popcll(__ballot(take));
-            }
-            {   // splat s1, against the transmittance left by s0
-                float alpha = __uint_as_float(B1.x) * e1;
-                alpha = fminf(alpha, 0.99f);
-                const bool take = box1 & !(T < 1e-3f) & !(alpha < 1e-3f);
-                const float wr = __uint_as_float(B1.y) * alpha * T;
-                const float wg = __uint_as_float(B1.z) * alpha * T;
-                const float wb = __uint_as_float(B1.w) * alpha * T;
-                const float Tn = T * (1.0f - alpha);
-                cr = take ? cr + wr : cr;
-                cg = take ? cg + wg : cg;
-                cb = take ? cb + wb : cb;
-                T = take ? Tn : T;
-                if (DIAG) d_taken += (uint64_t)__popcll(__ballot(take));
-            }
-            alive = __ballot(!(T < 1e-3f)) != 0ull;   // whole block saturated -> stop
-        }
-    }
-    if (DIAG && lane == 0) {
-        if (w == 0 && d_loaded) atomicAdd(counters, (unsigned long long)d_loaded);
-        atomicAdd(counters + 1, (unsigned long long)d_iter);
-        atomicAdd(counters + 2, (unsigned long long)d_active);
-        atomicAdd(counters + 3, (unsigned long long)d_taken);
-        atomicAdd(counters + 5, (unsigned long long)d_skipped);
-        atomicAdd(counters + 6, (unsigned long long)(d_iter * 64));
-    }
-    if (px < W && py < H) {
-        const size_t o = (size_t)py * (size_t)W + (size_t)px;
-        const size_t hw = (size_t)W * (size_t)H;
-        out[o] = inside ? cr : 0.0f;
-        out[hw + o] = inside ? cg : 0.0f;
-        out[2 * hw + o] = inside ? cb : 0.0f;
-    }
 }
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -822,21 +885,18 @@ __device__ __forceinline__ bool fast_safe(float a, float b, float c, float e, fl
 // Pair slot dwords (h = 0 / 1 for the first / second splat of the pair):
 //   [0+h] cx  [2+h] cy  [4+h] a  [6+h] b  [8+h] c  [10+h] e  [12+h] opacity
 //   [14+2h] red  [15+2h] green  [18+h] blue
+struct BlendDiag {
+    uint64_t loaded = 0, iter = 0, active = 0, taken = 0, slow = 0;
+};
+
+// One 8x8 pixel block (bx, by) blended by one wave over the tile list
+// idx[beg, end), using the wave's private LDS slice wP (32 pair slots).
 template <bool DIAG>
-__global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pairs,
-                                                const uint2* __restrict__ ranges,
-                                                const uint4* __restrict__ rec, int tiles_x, int tiles_y,
-                                                int W, int H, int cover_w, int cover_h,
-                                                float* __restrict__ out,
-                                                unsigned long long* __restrict__ counters) {
+__device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, const uint4* __restrict__ rec,
+                                            uint32_t beg, uint32_t end, int bx, int by, int lane, int W, int H,
+                                            int cover_w, int cover_h, float* __restrict__ out, float* wP,
+                                            BlendDiag& dg) {
     constexpr int kSlot = 20;                               // dwords per pair slot
-    __shared__ float4 sP[4][32 * kSlot / 4];
-    const int ntiles = tiles_x * tiles_y;
-    const int tile = xcd_remap(blockIdx.x, ntiles);
-    const int tx = tile % tiles_x, ty = tile / tiles_x;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int bx = tx * GSR_TILE_PX + (w & 1) * 8;
-    const int by = ty * GSR_TILE_PX + (w >> 1) * 8;
     const int px = bx + (lane & 7), py = by + (lane >> 3);
     const bool inside = px < cover_w && py < cover_h;
     const float fpx = (float)px, fpy = (float)py;
@@ -845,22 +905,17 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
     float T = inside ? 1.0f : 0.0f;
     f2 crg = (f2)0.0f;
     float cb = 0.0f;
-    const uint2 rr = ranges[tile];                          // {~start, end}, zero = empty
-    const uint32_t beg = rr.y ? ~rr.x : 0u, end = rr.y;
-    uint64_t d_loaded = 0, d_iter = 0, d_active = 0, d_taken = 0, d_slow = 0;
-    float* wP = reinterpret_cast<float*>(sP[w]);
-    const float4* wP4 = sP[w];
+    const float4* wP4 = reinterpret_cast<const float4*>(wP);
 
     uint4 ra = make_uint4(0, 0, 0, 0), rb = ra, rc = ra;
     uint32_t nidx = 0;
     if (beg + lane < end) {
-        const uint32_t gi = (uint32_t)pairs[beg + lane];
-        const uint4* R = rec + 4 * (uint64_t)gi;
+        const uint4* R = rec + 4 * (uint64_t)idx[beg + lane];
         ra = R[0];
         rb = R[1];
         rc = R[2];
     }
-    if (beg + 64 + lane < end) nidx = (uint32_t)pairs[beg + 64 + lane];
+    if (beg + 64 + lane < end) nidx = idx[beg + 64 + lane];
     bool alive = __ballot(!(T < 1e-3f)) != 0ull;
     for (uint32_t base = beg; base < end && alive; base += 64) {
         const uint32_t cnt = min(64u, end - base);
@@ -914,7 +969,7 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
             static constexpr int kHalf1[10] = {1, 3, 5, 7, 9, 11, 13, 16, 17, 19};
             wP[(nsurv >> 1) * kSlot + kHalf1[lane]] = 0.0f;
         }
-        if (DIAG) d_loaded += cnt;
+        if (DIAG) dg.loaded += cnt;
         // ---- prefetch: records of batch k+1, indices of batch k+2 ----
         if (base + 64 + lane < end) {
             const uint4* R = rec + 4 * (uint64_t)nidx;
@@ -922,7 +977,7 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
             rb = R[1];
             rc = R[2];
         }
-        if (base + 128 + lane < end) nidx = (uint32_t)pairs[base + 128 + lane];
+        if (base + 128 + lane < end) nidx = idx[base + 128 + lane];
 
         uint64_t mm = m;
         if (all_fast) {
@@ -961,10 +1016,10 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
                 const f2 wb = ((f2){q4.z, q4.w} * (f2){a0, a1}) * (f2){T, T1};
                 cb = (cb + wb.x) + wb.y;
                 if (DIAG) {
-                    d_iter += has1 ? 2 : 1;
-                    d_active += (uint64_t)__popcll(__ballot(in0 & !(T < 1e-3f))) +
+                    dg.iter += has1 ? 2 : 1;
+                    dg.active += (uint64_t)__popcll(__ballot(in0 & !(T < 1e-3f))) +
                                 (uint64_t)__popcll(__ballot(in1 & !(T1 < 1e-3f)));
-                    d_taken += (uint64_t)__popcll(__ballot(take0)) + (uint64_t)__popcll(__ballot(take1));
+                    dg.taken += (uint64_t)__popcll(__ballot(take0)) + (uint64_t)__popcll(__ballot(take1));
                 }
                 T = T2;
                 alive = __ballot(!(T < 1e-3f)) != 0ull;   // whole block saturated -> stop
@@ -990,10 +1045,10 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
                 const float wb = S[18 + h] * alpha * T;
                 const float Tn = T * (1.0f - alpha);
                 if (DIAG) {
-                    d_iter += 1;
-                    d_slow += 1;
-                    d_active += (uint64_t)__popcll(__ballot(in & !(T < 1e-3f)));
-                    d_taken += (uint64_t)__popcll(__ballot(take));
+                    dg.iter += 1;
+                    dg.slow += 1;
+                    dg.active += (uint64_t)__popcll(__ballot(in & !(T < 1e-3f)));
+                    dg.taken += (uint64_t)__popcll(__ballot(take));
                 }
                 crg.x = take ? crg.x + wr : crg.x;
                 crg.y = take ? crg.y + wg : crg.y;
@@ -1002,14 +1057,6 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
                 alive = __ballot(!(T < 1e-3f)) != 0ull;
             }
         }
-    }
-    if (DIAG && lane == 0) {
-        if (w == 0 && d_loaded) atomicAdd(counters, (unsigned long long)d_loaded);
-        atomicAdd(counters + 1, (unsigned long long)d_iter);
-        atomicAdd(counters + 2, (unsigned long long)d_active);
-        atomicAdd(counters + 3, (unsigned long long)d_taken);
-        atomicAdd(counters + 4, (unsigned long long)d_slow);
-        atomicAdd(counters + 6, (unsigned long long)(d_iter * 64));
     }
     if (px < W && py < H) {
         const size_t o = (size_t)py * (size_t)W + (size_t)px;
@@ -1020,151 +1067,67 @@ __global__ __launch_bounds__(256) void k_blend(const uint64_t* __restrict__ pair
     }
 }
 
-// Pixel-chain blend: each lane owns PPL pixels of one column (rows y0 + R*j),
-// so one broadcast splat read feeds PPL independent md2/exp/composite chains.
-// Block = BW x (R*PPL) pixels per wave; PPL 1: 8x8 (4 waves per 16x16 tile),
-// PPL 2: 8x16 (2 waves), PPL 4: 16x16 (1 wave).  One splat per iteration; the
-// exact ellipse-vs-block cull of the batch is the only skip.
-template <bool DIAG, int PPL>
-__global__ __launch_bounds__(256) void k_blend_px(const uint64_t* __restrict__ pairs,
-                                                   const uint2* __restrict__ ranges,
-                                                   const uint4* __restrict__ rec, int tiles_x, int tiles_y,
-                                                   int W, int H, int cover_w, int cover_h,
-                                                   float* __restrict__ out,
-                                                   unsigned long long* __restrict__ counters) {
-    constexpr int BW = PPL == 4 ? 16 : 8;          // block width
-    constexpr int R = 64 / BW;                     // rows per pixel pass
-    constexpr int BH = R * PPL;                    // block height
-    constexpr int WPT = (GSR_TILE_PX / BW) * (GSR_TILE_PX / BH);   // waves per tile
-    constexpr int TPB = 256 / (64 * WPT);          // tiles per 256-thread workgroup
-    __shared__ uint4 sA[4][64], sB[4][64], sC[4][64];
+// STAMPS: timing diagnostics only (no counters): per workgroup, its launch
+// order slot gets {start, end} of the s_memrealtime clock (100 MHz) in
+// counters[2 * blockIdx.x ...] (end = max over the four waves).
+template <bool DIAG, bool STAMPS = false>
+__global__ __launch_bounds__(256) void k_blend(const uint32_t* __restrict__ idx,
+                                                const uint2* __restrict__ ranges,
+                                                const uint4* __restrict__ rec, int tiles_x, int tiles_y,
+                                                int W, int H, int cover_w, int cover_h,
+                                                float* __restrict__ out,
+                                                unsigned long long* __restrict__ counters) {
+    __shared__ float4 sP[4][32 * 20 / 4];
     const int ntiles = tiles_x * tiles_y;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int tslot = blockIdx.x * TPB + w / WPT;
-    if (tslot >= ntiles) return;                   // whole wave exits (no barrier in this kernel)
-    const int tile = xcd_remap(tslot, ntiles);
+    const int tile = xcd_remap(blockIdx.x, ntiles);
     const int tx = tile % tiles_x, ty = tile / tiles_x;
-    const int wt = w % WPT;                        // wave within its tile
-    const int bx = tx * GSR_TILE_PX + (wt % (GSR_TILE_PX / BW)) * BW;
-    const int by = ty * GSR_TILE_PX + (wt / (GSR_TILE_PX / BW)) * BH;
-    const int px = bx + (lane % BW), py0 = by + lane / BW;
-    const float fpx = (float)px;
-    float T[PPL], cr[PPL], cg[PPL], cb[PPL];
-    bool inside[PPL];
-#pragma unroll
-    for (int j = 0; j < PPL; ++j) {
-        inside[j] = px < cover_w && py0 + R * j < cover_h;
-        T[j] = inside[j] ? 1.0f : 0.0f;
-        cr[j] = cg[j] = cb[j] = 0.0f;
-    }
-    const uint2 rr = ranges[tile];
-    const uint32_t beg = rr.y ? ~rr.x : 0u, end = rr.y;
-    uint64_t d_loaded = 0, d_iter = 0, d_active = 0, d_taken = 0;
-    uint4* wA = sA[w];
-    uint4* wB = sB[w];
-    uint4* wC = sC[w];
-
-    uint4 ra = make_uint4(0, 0, 0, 0), rb = ra, rc = ra;
-    uint32_t nidx = 0;
-    if (beg + lane < end) {
-        const uint32_t gi = (uint32_t)pairs[beg + lane];
-        const uint4* Rp = rec + 4 * (uint64_t)gi;
-        ra = Rp[0];
-        rb = Rp[1];
-        rc = Rp[2];
-    }
-    if (beg + 64 + lane < end) nidx = (uint32_t)pairs[beg + 64 + lane];
-    auto unsat_any = [&]() {
-        bool u = false;
-#pragma unroll
-        for (int j = 0; j < PPL; ++j) u |= !(T[j] < 1e-3f);
-        return __ballot(u) != 0ull;
-    };
-    bool alive = unsat_any();
-    for (uint32_t base = beg; base < end && alive; base += 64) {
-        const uint32_t cnt = min(64u, end - base);
-        wA[lane] = ra;
-        wB[lane] = rb;
-        wC[lane] = rc;
-        bool h = false;
-        if ((uint32_t)lane < cnt) {
-            const int xmin = (int)(rc.z & 0xffffu), xmax = (int)(rc.z >> 16);
-            const int ymin = (int)(rc.w & 0xffffu), ymax = (int)(rc.w >> 16);
-            h = !(xmax < bx || xmin > bx + BW - 1 || ymax < by || ymin > by + BH - 1);
-            if (h) {
-                const float cx = (float)(int)rc.x, cy = (float)(int)rc.y;
-                h = block_may_reach(__uint_as_float(ra.x), __uint_as_float(ra.y), __uint_as_float(ra.z),
-                                    __uint_as_float(ra.w), (float)max(bx, xmin) - cx,
-                                    (float)min(bx + BW - 1, xmax) - cx, (float)max(by, ymin) - cy,
-                                    (float)min(by + BH - 1, ymax) - cy, md2_cutoff(__uint_as_float(rb.x)));
-            }
-        }
-        uint64_t m = __ballot(h);
-        if (DIAG) d_loaded += cnt;
-        if (base + 64 + lane < end) {
-            const uint4* Rp = rec + 4 * (uint64_t)nidx;
-            ra = Rp[0];
-            rb = Rp[1];
-            rc = Rp[2];
-        }
-        if (base + 128 + lane < end) nidx = (uint32_t)pairs[base + 128 + lane];
-        while (m && alive) {
-            const int s = __builtin_ctzll(m);
-            m &= m - 1;
-            const uint4 C = wC[s], A = wA[s], B = wB[s];
-            const int xmin = (int)(C.z & 0xffffu), xmax = (int)(C.z >> 16);
-            const int ymin = (int)(C.w & 0xffffu), ymax = (int)(C.w >> 16);
-            const bool xin = (px >= xmin) & (px <= xmax);
-            const float dx = fpx - (float)(int)C.x;
-            const float cy = (float)(int)C.y;
-            const float a = __uint_as_float(A.x), b = __uint_as_float(A.y);
-            const float c = __uint_as_float(A.z), e = __uint_as_float(A.w);
-            const float ax = a * dx, cx = c * dx;
-            if (DIAG) d_iter += 1;
-#pragma unroll
-            for (int j = 0; j < PPL; ++j) {
-                const int py = py0 + R * j;
-                const float dy = (float)py - cy;
-                // render.cu:329-340, same operation order
-                const float md = dx * (ax + b * dy) + dy * (cx + e * dy);
-                const float ee = gsr_expf(-0.5f * md);
-                float alpha = __uint_as_float(B.x) * ee;
-                alpha = fminf(alpha, 0.99f);
-                const bool box = xin & (py >= ymin) & (py <= ymax);
-                const bool take = box & !(T[j] < 1e-3f) & !(alpha < 1e-3f);
-                const float wr = __uint_as_float(B.y) * alpha * T[j];
-                const float wg = __uint_as_float(B.z) * alpha * T[j];
-                const float wb = __uint_as_float(B.w) * alpha * T[j];
-                const float Tn = T[j] * (1.0f - alpha);
-                if (DIAG) {
-                    d_active += (uint64_t)__popcll(__ballot(box & !(T[j] < 1e-3f)));
-                    d_taken += (uint64_t)__popcll(__ballot(take));
-                }
-                cr[j] = take ? cr[j] + wr : cr[j];
-                cg[j] = take ? cg[j] + wg : cg[j];
-                cb[j] = take ? cb[j] + wb : cb[j];
-                T[j] = take ? Tn : T[j];
-            }
-            alive = unsat_any();
-        }
-    }
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (STAMPS && t == 0) counters[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    const uint2 rr = ranges[tile];                          // {~start, end}, zero = empty
+    BlendDiag dg;
+    blend_block<DIAG>(idx, rec, rr.y ? ~rr.x : 0u, rr.y, tx * GSR_TILE_PX + (w & 1) * 8,
+                      ty * GSR_TILE_PX + (w >> 1) * 8, lane, W, H, cover_w, cover_h, out,
+                      reinterpret_cast<float*>(sP[w]), dg);
+    if (STAMPS && lane == 0) atomicMax(counters + 2 * blockIdx.x + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     if (DIAG && lane == 0) {
-        if (wt == 0 && d_loaded) atomicAdd(counters, (unsigned long long)d_loaded);
-        atomicAdd(counters + 1, (unsigned long long)d_iter);
-        atomicAdd(counters + 2, (unsigned long long)d_active);
-        atomicAdd(counters + 3, (unsigned long long)d_taken);
-        atomicAdd(counters + 6, (unsigned long long)(d_iter * 64 * PPL));
+        if (w == 0 && dg.loaded) atomicAdd(counters, (unsigned long long)dg.loaded);
+        atomicAdd(counters + 1, (unsigned long long)dg.iter);
+        atomicAdd(counters + 2, (unsigned long long)dg.active);
+        atomicAdd(counters + 3, (unsigned long long)dg.taken);
+        atomicAdd(counters + 4, (unsigned long long)dg.slow);
+        atomicAdd(counters + 6, (unsigned long long)(dg.iter * 64));
     }
-    const size_t hw = (size_t)W * (size_t)H;
-#pragma unroll
-    for (int j = 0; j < PPL; ++j) {
-        const int py = py0 + R * j;
-        if (px < W && py < H) {
-            const size_t o = (size_t)py * (size_t)W + (size_t)px;
-            out[o] = inside[j] ? cr[j] : 0.0f;
-            out[hw + o] = inside[j] ? cg[j] : 0.0f;
-            out[2 * hw + o] = inside[j] ? cb[j] : 0.0f;
-        }
+}
+
+// One-wave workgroups: workgroup g blends one 8x8 block, so a finished block
+// frees its wave slot at once (no waiting for the tile's other three waves).
+// Blocks are tile-major; the XCD-aware remap keeps a tile's four blocks (and
+// neighbouring tiles) on one XCD, i.e. one L2.
+template <bool DIAG>
+__global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx,
+                                                 const uint2* __restrict__ ranges,
+                                                 const uint4* __restrict__ rec, int tiles_x, int tiles_y,
+                                                 int W, int H, int cover_w, int cover_h,
+                                                 float* __restrict__ out,
+                                                 unsigned long long* __restrict__ counters) {
+    __shared__ float4 sP[32 * 20 / 4];
+    const int ntiles = tiles_x * tiles_y;
+    const int b = xcd_remap(blockIdx.x, ntiles * 4);
+    const int tile = b >> 2, sub = b & 3;
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
+    const int lane = threadIdx.x;
+    const uint2 rr = ranges[tile];
+    BlendDiag dg;
+    blend_block<DIAG>(idx, rec, rr.y ? ~rr.x : 0u, rr.y, tx * GSR_TILE_PX + (sub & 1) * 8,
+                      ty * GSR_TILE_PX + (sub >> 1) * 8, lane, W, H, cover_w, cover_h, out,
+                      reinterpret_cast<float*>(sP), dg);
+    if (DIAG && lane == 0) {
+        if (sub == 0 && dg.loaded) atomicAdd(counters, (unsigned long long)dg.loaded);
+        atomicAdd(counters + 1, (unsigned long long)dg.iter);
+        atomicAdd(counters + 2, (unsigned long long)dg.active);
+        atomicAdd(counters + 3, (unsigned long long)dg.taken);
+        atomicAdd(counters + 4, (unsigned long long)dg.slow);
+        atomicAdd(counters + 6, (unsigned long long)(dg.iter * 64));
     }
 }
 
@@ -1233,10 +1196,10 @@ hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, 
 }
 
 hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
-                             uint4* rec, uint64_t* items, hipStream_t s) {
+                             uint4* rec, uint64_t* items, uint64_t* rect, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_preprocess, dim3(grid_for(n, 256)), dim3(256), 0, s, arrays, stride, n, fr, rec,
-                       items);
+                       items, rect);
     return hipGetLastError();
 }
 
@@ -1261,55 +1224,77 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
     return hipGetLastError();
 }
 
-hipError_t launch_emit(const uint64_t* depth_sorted, uint32_t n, const uint4* rec, int groups,
+hipError_t launch_emit(const uint64_t* depth_sorted, uint32_t n, const uint64_t* rect, int groups,
                        unsigned long long* wg_scratch, Stats* stats, Stats* host_mapped_stats,
-                       uint32_t pair_capacity, int tiles_x, uint64_t* pairs, hipStream_t s) {
-    hipLaunchKernelGGL(k_emit_count, dim3(groups), dim3(256), 0, s, depth_sorted, n, rec, groups, wg_scratch);
+                       uint32_t pair_capacity, int tiles_x, uint64_t* srect, void* keys, bool key16,
+                       uint32_t* vals, hipStream_t s) {
+    hipLaunchKernelGGL(k_emit_count, dim3(groups), dim3(256), 0, s, depth_sorted, n, rect, groups, wg_scratch,
+                       srect);
     hipLaunchKernelGGL(k_emit_scan, dim3(1), dim3(256), 0, s, wg_scratch, groups, pair_capacity, stats,
                        host_mapped_stats);
-    hipLaunchKernelGGL(k_emit_pairs, dim3(groups), dim3(256), 0, s, depth_sorted, n, rec, groups, wg_scratch,
-                       pair_capacity, tiles_x, pairs);
+    if (key16)
+        hipLaunchKernelGGL(k_emit_pairs<uint16_t>, dim3(groups), dim3(256), 0, s, depth_sorted, n, srect, groups,
+                           wg_scratch, pair_capacity, tiles_x, static_cast<uint16_t*>(keys), vals);
+    else
+        hipLaunchKernelGGL(k_emit_pairs<uint32_t>, dim3(groups), dim3(256), 0, s, depth_sorted, n, srect, groups,
+                           wg_scratch, pair_capacity, tiles_x, static_cast<uint32_t*>(keys), vals);
     return hipGetLastError();
 }
 
-template <int PPL>
-static void blend_px(const uint64_t* pairs, const uint2* ranges, const uint4* rec, const Frame& fr, float* out,
-                     unsigned long long* consumed, hipStream_t s) {
-    constexpr int TPB = PPL;   // tiles per 256-thread workgroup (waves per tile = 4 / PPL)
-    const int nt = fr.tiles_x * fr.tiles_y;
-    const dim3 grid((nt + TPB - 1) / TPB);
-    if (consumed)
-        hipLaunchKernelGGL((k_blend_px<true, PPL>), grid, dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x,
-                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
-    else
-        hipLaunchKernelGGL((k_blend_px<false, PPL>), grid, dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x,
-                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
+template <typename K, int ITEMS>
+static void kv_pass(const K* kin, const uint32_t* vin, K* kout, uint32_t* vout, const uint32_t* n_dev, int shift,
+                    int bits, int groups, uint32_t* hist, uint32_t* totals, uint2* ranges, hipStream_t s) {
+    const uint32_t mask = (1u << bits) - 1u;
+    hipLaunchKernelGGL((k_kv_upsweep<K, ITEMS>), dim3(groups), dim3(kSortThreads), 0, s, kin, n_dev, shift, mask,
+                       groups, hist);
+    hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, hist, groups, totals);
+    hipLaunchKernelGGL((k_kv_downsweep<K, ITEMS>), dim3(groups), dim3(kSortThreads), 0, s, kin, vin, kout, vout,
+                       n_dev, shift, bits, groups, hist, totals, ranges);
 }
 
-hipError_t launch_blend(const uint64_t* pairs, const uint2* ranges, const uint4* rec, const Frame& fr,
-                        float* out, unsigned long long* consumed, int variant, hipStream_t s) {
+hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* keys_out, uint32_t* vals_out,
+                          bool key16, const uint32_t* n_dev, int shift, int bits, int groups, int items,
+                          uint32_t* hist, uint32_t* totals, uint2* ranges, hipStream_t s) {
+    using u16 = uint16_t;
+    using u32 = uint32_t;
+    const auto* k16 = static_cast<const u16*>(keys_in);
+    const auto* k32 = static_cast<const u32*>(keys_in);
+    auto* o16 = static_cast<u16*>(keys_out);
+    auto* o32 = static_cast<u32*>(keys_out);
+    if (key16 && items == 8)
+        kv_pass<u16, 8>(k16, vals_in, o16, vals_out, n_dev, shift, bits, groups, hist, totals, ranges, s);
+    else if (key16)
+        kv_pass<u16, 16>(k16, vals_in, o16, vals_out, n_dev, shift, bits, groups, hist, totals, ranges, s);
+    else if (items == 8)
+        kv_pass<u32, 8>(k32, vals_in, o32, vals_out, n_dev, shift, bits, groups, hist, totals, ranges, s);
+    else
+        kv_pass<u32, 16>(k32, vals_in, o32, vals_out, n_dev, shift, bits, groups, hist, totals, ranges, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
+                        float* out, unsigned long long* consumed, int variant, unsigned int* queue,
+                        int resident_groups, hipStream_t s) {
     const int nt = fr.tiles_x * fr.tiles_y;
     if (nt <= 0) return hipSuccess;
-    switch (variant) {
-    case 1: blend_px<1>(pairs, ranges, rec, fr, out, consumed, s); return hipGetLastError();
-    case 2: blend_px<2>(pairs, ranges, rec, fr, out, consumed, s); return hipGetLastError();
-    case 4: blend_px<4>(pairs, ranges, rec, fr, out, consumed, s); return hipGetLastError();
-    case 5:
+    if (variant == 1) {
         if (consumed)
-            hipLaunchKernelGGL(k_blend_v5<true>, dim3(nt), dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x,
+            hipLaunchKernelGGL(k_blend_w<true>, dim3(4 * nt), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,
                                fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
         else
-            hipLaunchKernelGGL(k_blend_v5<false>, dim3(nt), dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x,
+            hipLaunchKernelGGL(k_blend_w<false>, dim3(4 * nt), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,
                                fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
         return hipGetLastError();
-    default: break;
     }
-    if (consumed)
-        hipLaunchKernelGGL(k_blend<true>, dim3(nt), dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x, fr.tiles_y,
+    if (variant == 2 && consumed)   // timestamps into consumed[2 * nt] (diagnostics)
+        hipLaunchKernelGGL((k_blend<false, true>), dim3(nt), dim3(256), 0, s, idx, ranges, rec, fr.tiles_x,
+                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
+    else if (consumed)
+        hipLaunchKernelGGL(k_blend<true>, dim3(nt), dim3(256), 0, s, idx, ranges, rec, fr.tiles_x, fr.tiles_y,
                            fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
     else
-        hipLaunchKernelGGL(k_blend<false>, dim3(nt), dim3(256), 0, s, pairs, ranges, rec, fr.tiles_x,
-                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
+        hipLaunchKernelGGL(k_blend<false>, dim3(nt), dim3(256), 0, s, idx, ranges, rec, fr.tiles_x, fr.tiles_y,
+                           fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
     return hipGetLastError();
 }
 

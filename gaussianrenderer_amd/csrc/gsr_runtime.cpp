@@ -448,7 +448,9 @@ struct gsr_context {
     int64_t n_cap = 0, p_cap = 0, t_cap = 0, soa_cap = 0;
     uint4* rec = nullptr;
     uint64_t* items[2] = {nullptr, nullptr};
+    // pair buffers: p_cap u64 each, used as {keys: p_cap x 4 B, values: p_cap x 4 B}
     uint64_t* pairs[2] = {nullptr, nullptr};
+    uint64_t* rect = nullptr;        // per-Gaussian tile rectangle (preprocess output)
     uint32_t* hist = nullptr;
     uint32_t* totals = nullptr;
     unsigned long long* wg = nullptr;
@@ -457,9 +459,17 @@ struct gsr_context {
     Stats* hstats_dev = nullptr;
     uint2* ranges = nullptr;
     float* soa_tmp = nullptr;
-    unsigned long long* consumed = nullptr;   // diagnostics: records loaded by the blend
+    unsigned long long* consumed = nullptr;   // diagnostics: blend counters (or stamps)
+    int64_t consumed_cap = 0;
     bool diagnostics = false;
     int blend_variant = 0;
+    int tile_items = 16;             // tile sort: items per thread (8 | 16)
+    int depth_items = 0;             // depth sort: items per thread (0 = by size | 8 | 16)
+    int tile_groups = 1024;          // tile sort: workgroup cap (measured best: 2 tiles of items per group)
+    int tile_split_even = 1;         // tile sort: digits split evenly over the passes
+    int depth_groups = 0;            // depth sort: workgroup cap (0 = default)
+    unsigned int* queue = nullptr;   // blend block queue (variant 1), 8 counters
+    int resident_groups = 2048;      // workgroups of 256 that fit on the device at once
     // frame state
     Frame fr{};
     int64_t n = 0;
@@ -501,6 +511,13 @@ int ensure_static(gsr_context* c) {
     if (int rc = realloc_dev(&c->totals, 256)) return rc;
     if (int rc = realloc_dev(&c->wg, (size_t)gsr::kMaxSortGroups)) return rc;
     if (int rc = realloc_dev(&c->stats, 2)) return rc;
+    if (int rc = realloc_dev(&c->queue, 8)) return rc;
+    {
+        int dev = 0, cus = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        c->resident_groups = std::max(8, cus * 8);      // 8 workgroups of 4 waves per CU (VGPR-limited)
+    }
     HIP_TRY(hipMemset(c->stats, 0, 2 * sizeof(Stats)));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->hstats), sizeof(Stats), hipHostMallocMapped));
     std::memset(c->hstats, 0, sizeof(Stats));
@@ -516,6 +533,7 @@ int ensure_n(gsr_context* c, int64_t n) {
     if (int rc = realloc_dev(&c->rec, 4 * (size_t)cap)) return rc;
     if (int rc = realloc_dev(&c->items[0], (size_t)cap)) return rc;
     if (int rc = realloc_dev(&c->items[1], (size_t)cap)) return rc;
+    if (int rc = realloc_dev(&c->rect, (size_t)cap)) return rc;
     c->n_cap = cap;
     if (c->p_cap < 4 * cap) {
         const int64_t pc = std::min<int64_t>(std::max<int64_t>(4 * cap, 1 << 20), 0xffffffffLL);
@@ -635,8 +653,8 @@ extern "C" gsr_context* gsr_create(void) { return new gsr_context(); }
 extern "C" void gsr_destroy(gsr_context* c) {
     if (!c) return;
     (void)hipDeviceSynchronize();
-    for (auto* p : {(void*)c->rec, (void*)c->items[0], (void*)c->items[1], (void*)c->pairs[0],
-                    (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats,
+    for (auto* p : {(void*)c->rec, (void*)c->items[0], (void*)c->items[1], (void*)c->rect, (void*)c->pairs[0],
+                    (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->queue,
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
@@ -685,10 +703,15 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     } else {
         arrays = reinterpret_cast<const float*>(static_cast<const char*>(scene) + GSR_SCENE_HEADER_BYTES);
     }
-    HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[0], c->stream));
+    HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[0], c->rect, c->stream));
     c->have_pre = true;
     c->have_sort = false;
     return rc_over;
+}
+
+static void* pair_keys(gsr_context* c, int b) { return c->pairs[b]; }
+static uint32_t* pair_vals(gsr_context* c, int b) {
+    return reinterpret_cast<uint32_t*>(c->pairs[b]) + c->p_cap;
 }
 
 static int sort_locked(gsr_context* c) {
@@ -697,28 +720,36 @@ static int sort_locked(gsr_context* c) {
     // ---- stable depth sort of (key << 32 | index), 4 x 8 bits ----
     mark(c, GSR_STAGE_DEPTH_SORT);
     // smaller tiles for the 1M-item depth sort: ~500 workgroups instead of ~250
-    const int di = c->n < (int64_t(4) << 20) ? 8 : 16;
-    const int gd = groups_for(c->n, 256 * di);
+    const int di = c->depth_items ? c->depth_items : (c->n < (int64_t(4) << 20) ? 8 : 16);
+    int gd = groups_for(c->n, 256 * di);
+    if (c->depth_groups) gd = std::min(gd, c->depth_groups);
     for (int p = 0; p < 4; p++)
         HIP_TRY(gsr::launch_radix_pass(c->items[p & 1], c->items[(p + 1) & 1], nullptr, n, 32 + 8 * p, 8, gd, di,
                                        c->hist, c->totals, nullptr, c->stream));
     // result in items[0]
-    // ---- pair emission in depth order ----
+    // ---- pair emission in depth order (srect staged in the free items[1]) ----
     mark(c, GSR_STAGE_EMIT);
     const int ge = groups_for(c->n, 1024);
-    HIP_TRY(gsr::launch_emit(c->items[0], n, c->rec, ge, c->wg, c->stats, c->hstats_dev, (uint32_t)c->p_cap,
-                             c->fr.tiles_x, c->pairs[0], c->stream));
-    // ---- stable tile sort of the pairs ----
+    const bool key16 = c->ntiles <= 65536;
+    HIP_TRY(gsr::launch_emit(c->items[0], n, c->rect, ge, c->wg, c->stats, c->hstats_dev, (uint32_t)c->p_cap,
+                             c->fr.tiles_x, c->items[1], pair_keys(c, 0), key16, pair_vals(c, 0), c->stream));
+    // ---- stable key-value tile sort ----
     mark(c, GSR_STAGE_TILE_SORT);
     const int tbits = std::max(1, ceil_log2(c->ntiles));
-    const int gp = groups_for(c->p_cap, gsr::kSortTile);
+    int gp = groups_for(c->p_cap, 256 * c->tile_items);
+    if (c->tile_groups) gp = std::min(gp, c->tile_groups);
     int cur = 0;
     HIP_TRY(hipMemsetAsync(c->ranges, 0, sizeof(uint2) * (size_t)c->ntiles, c->stream));
-    for (int sh = 0; sh < tbits; sh += 8) {
-        const int bits = std::min(8, tbits - sh);
-        const bool last = sh + 8 >= tbits;    // final pass also writes the tile ranges
-        HIP_TRY(gsr::launch_radix_pass(c->pairs[cur], c->pairs[cur ^ 1], &c->stats[0].pairs_eff, 0, 32 + sh, bits,
-                                       gp, 16, c->hist, c->totals, last ? c->ranges : nullptr, c->stream));
+    // digits split evenly over the passes (13 bits: 7 + 6, not 8 + 5): longer
+    // digit runs per sorted tile of items, so the scattered stores coalesce better
+    const int tpasses = (tbits + 7) / 8;
+    const int tdig = c->tile_split_even ? (tbits + tpasses - 1) / tpasses : 8;
+    for (int sh = 0; sh < tbits; sh += tdig) {
+        const int bits = std::min(tdig, tbits - sh);
+        const bool last = sh + tdig >= tbits;    // final pass: values only + tile ranges
+        HIP_TRY(gsr::launch_kv_pass(pair_keys(c, cur), pair_vals(c, cur), last ? nullptr : pair_keys(c, cur ^ 1),
+                                    pair_vals(c, cur ^ 1), key16, &c->stats[0].pairs_eff, sh, bits, gp,
+                                    c->tile_items, c->hist, c->totals, last ? c->ranges : nullptr, c->stream));
         cur ^= 1;
     }
     c->pair_buf = cur;
@@ -732,13 +763,17 @@ static int blend_locked(gsr_context* c, float* d_out) {
     if (!d_out) return set_err(GSR_E_ARG, "null output");
     mark(c, GSR_STAGE_BLEND);
     if (c->diagnostics) {
-        if (!c->consumed) {
-            if (int rc = realloc_dev(&c->consumed, 8)) return rc;
+        // counters (8) or, for the timestamp schedule, 2 stamps per tile
+        const int64_t need = c->blend_variant == 2 ? std::max<int64_t>(8, 2 * (int64_t)c->ntiles) : 8;
+        if (c->consumed_cap < need) {
+            if (int rc = realloc_dev(&c->consumed, (size_t)need)) return rc;
+            c->consumed_cap = need;
         }
-        HIP_TRY(hipMemsetAsync(c->consumed, 0, 8 * sizeof(unsigned long long), c->stream));
+        HIP_TRY(hipMemsetAsync(c->consumed, 0, (size_t)need * sizeof(unsigned long long), c->stream));
     }
-    HIP_TRY(gsr::launch_blend(c->pairs[c->pair_buf], c->ranges, c->rec, c->fr, d_out,
-                              c->diagnostics ? c->consumed : nullptr, c->blend_variant, c->stream));
+    HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
+                              c->diagnostics ? c->consumed : nullptr, c->blend_variant, c->queue,
+                              c->resident_groups, c->stream));
     mark(c, GSR_NUM_STAGES);
     if (c->timing) c->ev_frames.push_back(c->cur);
     c->cur = FrameEvents{};
@@ -820,7 +855,18 @@ extern "C" int64_t gsr_read_pairs(gsr_context* c, uint64_t* host, int64_t cap) {
     Stats s{};
     HIP_TRY(hipMemcpy(&s, c->stats, sizeof s, hipMemcpyDeviceToHost));
     const int64_t m = std::min<int64_t>(cap, s.pairs_eff);
-    if (m) HIP_TRY(hipMemcpy(host, c->pairs[c->pair_buf], (size_t)m * 8, hipMemcpyDeviceToHost));
+    if (!m) return 0;
+    // the sorted pairs live as values + tile ranges; rebuild (tile << 32 | index)
+    std::vector<uint32_t> vals((size_t)m);
+    std::vector<uint2> rg((size_t)c->ntiles);
+    HIP_TRY(hipMemcpy(vals.data(), pair_vals(c, c->pair_buf), (size_t)m * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(rg.data(), c->ranges, sizeof(uint2) * rg.size(), hipMemcpyDeviceToHost));
+    for (int64_t j = 0; j < m; j++) host[j] = ~0ull;
+    for (int t = 0; t < c->ntiles; t++) {
+        if (!rg[t].y) continue;
+        for (int64_t j = ~rg[t].x; j < (int64_t)rg[t].y && j < m; j++)
+            host[j] = ((uint64_t)(uint32_t)t << 32) | vals[(size_t)j];
+    }
     return m;
 }
 
@@ -883,12 +929,51 @@ extern "C" int gsr_set_diagnostics(gsr_context* c, int on) {
     return GSR_OK;
 }
 
+extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
+    if (!c) return set_err(GSR_E_ARG, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    switch (knob) {
+    case GSR_TUNE_BLEND_SCHEDULE:
+        if (value < 0 || value > 2) return set_err(GSR_E_ARG, "gsr_set_tuning: blend schedule must be 0, 1 or 2");
+        c->blend_variant = value;
+        return GSR_OK;
+    case GSR_TUNE_TILE_SORT_ITEMS:
+        if (value != 8 && value != 16) return set_err(GSR_E_ARG, "gsr_set_tuning: tile-sort items must be 8 or 16");
+        c->tile_items = value;
+        return GSR_OK;
+    case GSR_TUNE_DEPTH_SORT_ITEMS:
+        if (value != 0 && value != 8 && value != 16)
+            return set_err(GSR_E_ARG, "gsr_set_tuning: depth-sort items must be 0, 8 or 16");
+        c->depth_items = value;
+        return GSR_OK;
+    case GSR_TUNE_TILE_SORT_SPLIT:
+        c->tile_split_even = value != 0;
+        return GSR_OK;
+    case GSR_TUNE_TILE_SORT_GROUPS:
+    case GSR_TUNE_DEPTH_SORT_GROUPS:
+        if (value < 0 || value > gsr::kMaxSortGroups) return set_err(GSR_E_ARG, "gsr_set_tuning: bad group cap");
+        (knob == GSR_TUNE_TILE_SORT_GROUPS ? c->tile_groups : c->depth_groups) = value;
+        return GSR_OK;
+    default:
+        return set_err(GSR_E_ARG, "gsr_set_tuning: unknown knob");
+    }
+}
+
 extern "C" int gsr_set_blend_variant(gsr_context* c, int variant) {
     if (!c) return set_err(GSR_E_ARG, "null context");
-    if (variant != 0 && variant != 1 && variant != 2 && variant != 4 && variant != 5)
-        return set_err(GSR_E_ARG, "gsr_set_blend_variant: variant must be 0, 1, 2, 4 or 5");
+    if (variant < 0 || variant > 2)
+        return set_err(GSR_E_ARG, "gsr_set_blend_variant: variant must be 0, 1 or 2");
     std::lock_guard<std::mutex> lk(c->mu);
     c->blend_variant = variant;
+    return GSR_OK;
+}
+
+extern "C" int gsr_blend_stamps(gsr_context* c, uint64_t* out, int64_t n) {
+    if (!c || !out || !c->consumed || n < 0 || n > c->consumed_cap)
+        return set_err(GSR_E_ARG, "gsr_blend_stamps: bad argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (n) HIP_TRY(hipMemcpy(out, c->consumed, (size_t)n * 8, hipMemcpyDeviceToHost));
     return GSR_OK;
 }
 

@@ -163,12 +163,26 @@ int64_t gsr_blend_records_loaded(gsr_context* ctx);
  * (64 x pixels per lane x iterations), 0};
  * lane efficiency = active / slots. */
 int gsr_blend_counters(gsr_context* ctx, int64_t* out8);
-/* Blend schedule (tuning knob, default 0): 0 = 8x8 block per wave, survivors
- * compacted into pair slots, two splats per iteration with packed math;
- * 1, 2, 4 = pixel-chain kernel with that many pixels per lane (8x8, 8x16,
- * 16x16 blocks); 5 = previous 8x8 two-splat kernel.  All produce
- * bit-identical images. */
+/* Blend schedule (tuning knob for A/B experiments, tools/ab_blend.py): only
+ * 0 = one workgroup per 16x16 tile, 8x8 block per wave, survivors compacted
+ * into LDS pair slots, two splats per iteration (default); 1 = persistent
+ * per-wave block queue (experiment); 2 = schedule 0 with timestamps (see
+ * gsr_blend_stamps).  Every schedule produces bit-identical images. */
 int gsr_set_blend_variant(gsr_context* ctx, int variant);
+/* Tuning knobs for A/B experiments (all settings give bit-identical output). */
+enum {
+    GSR_TUNE_BLEND_SCHEDULE = 0,     /* as gsr_set_blend_variant */
+    GSR_TUNE_TILE_SORT_ITEMS = 1,    /* tile sort items per thread: 8 | 16 (default 16) */
+    GSR_TUNE_DEPTH_SORT_ITEMS = 2,   /* depth sort items per thread: 0 = by size | 8 | 16 */
+    GSR_TUNE_TILE_SORT_GROUPS = 3,   /* tile sort workgroup cap (default 1024; 0 = one per tile of items) */
+    GSR_TUNE_DEPTH_SORT_GROUPS = 4,  /* depth sort workgroup cap (0 = one per tile of items) */
+    GSR_TUNE_TILE_SORT_SPLIT = 5     /* tile sort digits: 1 = split evenly (default), 0 = 8 bits first */
+};
+int gsr_set_tuning(gsr_context* ctx, int knob, int value);
+/* Schedule 2 = schedule 0 with per-workgroup timestamps instead of counters:
+ * with diagnostics on, the last frame's blend stores {start, end} of the
+ * 100 MHz s_memrealtime clock per workgroup (launch order); read n values. */
+int gsr_blend_stamps(gsr_context* ctx, uint64_t* out, int64_t n);
 
 /* ---------------------------------------------------------------- scenes */
 
