@@ -40,6 +40,7 @@ CONFIGS = {
     3: (5_000_000, 1600, 1063, 3),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+BLEND_KERNEL = "k_blend_w<false>"   # default blend schedule (one 64-thread workgroup per 8x8 block)
 
 
 def parse():
@@ -58,8 +59,40 @@ def parse():
 
 
 def algorithmic_blend_bytes(ntiles: int, consumed: int, W: int, H: int) -> int:
-    """SURVEY.md 8d blend row: T*8 (tile ranges) + Pc*(8 pair + 48 record) + 12*W*H (image)."""
-    return 8 * ntiles + 56 * consumed + 12 * W * H
+    """SURVEY.md 8d blend row for this design: T*8 (tile ranges) + Pc*(4 index + 48 record)
+    + 12*W*H (planar fp32 image)."""
+    return 8 * ntiles + 52 * consumed + 12 * W * H
+
+
+def algorithmic_stage_bytes(n: int, m: int, pairs: int, ntiles: int, consumed: int, W: int, H: int,
+                            depth_passes: int = 4, tile_passes: int = 2) -> dict:
+    """Minimal bytes each stage of this design must move (per-stage table):
+    preprocess N*152 read (38 fp32 SoA arrays) + M*64 records + N*16 (item + tile rect);
+    depth sort passes*N*24 (upsweep read 8, downsweep read 8 + write 8);
+    emit N*40 (sorted items twice, rect gather, srect write/read) + P*6 (u16 key + u32 value);
+    tile sort P*14 per non-final pass, P*12 for the final one (keys 2 up, 6 read, 6|4 write) + T*8;
+    blend as algorithmic_blend_bytes."""
+    return {"preprocess": 152 * n + 64 * m + 16 * n,
+            "depth_sort": depth_passes * 24 * n,
+            "emit": 40 * n + 6 * pairs,
+            "tile_sort": 14 * pairs * (tile_passes - 1) + 12 * pairs + 8 * ntiles,
+            "blend": algorithmic_blend_bytes(ntiles, consumed, W, H)}
+
+
+VALU_PEAK_PER_SIMD_CYCLE = 0.5   # wave64 non-packed VALU issue: one per 2 cycles per SIMD (32 lanes)
+N_SIMDS = 256 * 4
+CLOCK_HZ = 2.4e9
+
+
+def load_pmc_counter(config: int, kernel: str, counter: str):
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        d = json.load(open(p))
+    except (OSError, ValueError):
+        return None
+    if d.get("config") != config:
+        return None
+    return d.get("kernels", {}).get(kernel, {}).get(counter)
 
 
 def load_pmc_traffic(config: int, kernel: str):
@@ -74,6 +107,8 @@ def load_pmc_traffic(config: int, kernel: str):
     if d.get("config") != config or kernel not in d.get("kernels", {}):
         return None
     k = d["kernels"][kernel]
+    if "fetch_bytes_corrected" not in k:
+        return None
     return {"bytes_per_launch": int(k["fetch_bytes_corrected"] + k["write_bytes"]),
             "source": f"profiles/pmc_latest.json ({d.get('source', '')})"}
 
@@ -173,6 +208,8 @@ def main():
     consumed = counters["records_loaded"]
     r.set_diagnostics(False)
     tiles_x, tiles_y = r.tile_grid()
+    # visible Gaussians M (depth key != 0xFFFFFFFF after the depth sort), untimed
+    visible = int(((r.read_depth_order(n) >> 32) != 0xFFFFFFFF).sum())
 
     # timed region: K frames, HIP events around every blend launch
     r.set_timing(1)
@@ -234,7 +271,7 @@ def main():
                                + (f"one orbit camera per GPU, RCCL gather to rank 0 ({args.gather})" if world > 1
                                   else "camera (0,0,4) fovY 50"),
                    "gaussians": n, "width": W, "height": H, "parallelism": f"frames{world}"},
-        "roofline": {"bound": "hbm", "kernel": "k_blend", "achieved": round(achieved, 2),
+        "roofline": {"bound": "hbm", "kernel": BLEND_KERNEL, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None, "avg_launch_ms": round(blend_avg_ms, 4),
                      "algorithmic_bytes": bytes_blend},
@@ -248,7 +285,19 @@ def main():
     }
     if gather_ms is not None:
         result["gather_ms"] = round(gather_ms, 3)
-    traffic = load_pmc_traffic(args.config, "k_blend<false>")
+    sb = algorithmic_stage_bytes(n, visible, pairs, ntiles, consumed, W, H)
+    result["stages_gbs"] = {k: round(sb[k] / (stages[k] * 1e-3) / 1e9, 1) for k in sb if stages.get(k)}
+    result["stages_gbs"]["blend"] = round(achieved, 1)     # timed frames, not the diagnostics frame
+    result["stages_algorithmic_bytes"] = sb
+    valu = load_pmc_counter(args.config, BLEND_KERNEL, "SQ_INSTS_VALU")
+    if valu:
+        rate = valu / (N_SIMDS * blend_avg_ms * 1e-3 * CLOCK_HZ)
+        result["roofline_valu"] = {"bound": "valu", "kernel": BLEND_KERNEL, "achieved": round(rate, 4),
+                                   "peak": VALU_PEAK_PER_SIMD_CYCLE, "unit": "wave64 VALU instr / SIMD / cycle @2.4GHz",
+                                   "frac": round(rate / VALU_PEAK_PER_SIMD_CYCLE, 4),
+                                   "instr_per_launch": valu,
+                                   "source": "SQ_INSTS_VALU from profiles/pmc_latest.json (packed ops count 2)"}
+    traffic = load_pmc_traffic(args.config, BLEND_KERNEL)
     if traffic is not None:
         result["roofline"]["traffic"] = traffic["bytes_per_launch"]
         result["roofline"]["traffic_source"] = traffic["source"]

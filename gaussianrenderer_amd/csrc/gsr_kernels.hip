@@ -1277,7 +1277,7 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
                         int resident_groups, hipStream_t s) {
     const int nt = fr.tiles_x * fr.tiles_y;
     if (nt <= 0) return hipSuccess;
-    if (variant == 1) {
+    if (variant == 0) {   // default: one wave per workgroup, one 8x8 block each
         if (consumed)
             hipLaunchKernelGGL(k_blend_w<true>, dim3(4 * nt), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,
                                fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);

@@ -163,11 +163,12 @@ int64_t gsr_blend_records_loaded(gsr_context* ctx);
  * (64 x pixels per lane x iterations), 0};
  * lane efficiency = active / slots. */
 int gsr_blend_counters(gsr_context* ctx, int64_t* out8);
-/* Blend schedule (tuning knob for A/B experiments, tools/ab_blend.py): only
- * 0 = one workgroup per 16x16 tile, 8x8 block per wave, survivors compacted
- * into LDS pair slots, two splats per iteration (default); 1 = persistent
- * per-wave block queue (experiment); 2 = schedule 0 with timestamps (see
- * gsr_blend_stamps).  Every schedule produces bit-identical images. */
+/* Blend schedule (tuning knob for A/B experiments, tools/ab_blend.py):
+ * 0 = one 64-thread workgroup per 8x8 pixel block (default); 1 = one
+ * 256-thread workgroup per 16x16 tile (four blocks); 2 = schedule 1 with
+ * per-workgroup timestamps (see gsr_blend_stamps).  Every schedule culls each
+ * 64-record batch against its block, compacts the survivors into LDS pair
+ * slots and composites two splats per iteration; all are bit-identical. */
 int gsr_set_blend_variant(gsr_context* ctx, int variant);
 /* Tuning knobs for A/B experiments (all settings give bit-identical output). */
 enum {

@@ -152,8 +152,8 @@ def test_image_config1_parity(gpu, orc, torch, c1, ci):
 
 
 @pytest.mark.parametrize("ci", [0, 2])
-def test_blend_queue_variant_parity(gpu, orc, torch, c1, ci):
-    """The one-wave-per-workgroup blend (variant 1) is bit-exact vs the oracle,
+def test_blend_tile_schedule_parity(gpu, orc, torch, c1, ci):
+    """The tile-per-workgroup blend (schedule 1) is bit-exact vs the oracle,
     including tiny frames, partial coverage and
     sizes that are not multiples of the 8x8 blocks."""
     path, soa = c1

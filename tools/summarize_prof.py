@@ -63,6 +63,19 @@ def write_json(d, out, config, source):
         if k in pm["WRITE_SIZE"]:
             res[k] = {"fetch_bytes_raw": pm["FETCH_SIZE"][k], "fetch_bytes_corrected": 2 * pm["FETCH_SIZE"][k],
                       "write_bytes": pm["WRITE_SIZE"][k]}
+    # any other counter passes present (SQ_*): per-kernel mean per launch, latest process only
+    import glob
+    for f in glob.glob(os.path.join(d, "pmc_*", "pmc_counter_collection.csv")):
+        rows = list(csv.DictReader(open(f)))
+        if not rows:
+            continue
+        last = max(int(r["Process_Id"]) for r in rows)
+        agg = collections.defaultdict(list)
+        for r in rows:
+            if int(r["Process_Id"]) == last and not r["Counter_Name"].endswith("_SIZE"):
+                agg[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
+        for (k, c), v in agg.items():
+            res.setdefault(k, {})[c] = sum(v) / len(v)
     json.dump({"config": config, "source": source, "kernels": res}, open(out, "w"), indent=1)
 
 
