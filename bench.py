@@ -296,7 +296,10 @@ def main():
                                    "peak": VALU_PEAK_PER_SIMD_CYCLE, "unit": "wave64 VALU instr / SIMD / cycle @2.4GHz",
                                    "frac": round(rate / VALU_PEAK_PER_SIMD_CYCLE, 4),
                                    "instr_per_launch": valu,
-                                   "source": "SQ_INSTS_VALU from profiles/pmc_latest.json (packed ops count 2)"}
+                                   "measured_issue_peak": {"v_fma_f32": 0.348, "v_pk_fma_f32": 0.212,
+                                                           "source": "profiles/r01_valu_rate.txt"},
+                                   "source": "SQ_INSTS_VALU per launch from profiles/pmc_latest.json (one count "
+                                             "per instruction, packed or not) / live blend time"}
     traffic = load_pmc_traffic(args.config, BLEND_KERNEL)
     if traffic is not None:
         result["roofline"]["traffic"] = traffic["bytes_per_launch"]
