@@ -26,7 +26,11 @@ $(OBJDIR)/gsr_runtime.o: $(SRCDIR)/gsr_runtime.cpp $(HDRS)
 	mkdir -p $(OBJDIR)
 	$(HIPCC) $(HOSTFLAGS) -x c++ -D__HIP_PLATFORM_AMD__ -c $< -o $@
 
-$(LIB): $(OBJDIR)/gsr_kernels.o $(OBJDIR)/gsr_runtime.o
+$(OBJDIR)/gsr_ply.o: $(SRCDIR)/gsr_ply.cpp $(HDRS)
+	mkdir -p $(OBJDIR)
+	$(HIPCC) $(HOSTFLAGS) -x c++ -D__HIP_PLATFORM_AMD__ -c $< -o $@
+
+$(LIB): $(OBJDIR)/gsr_kernels.o $(OBJDIR)/gsr_runtime.o $(OBJDIR)/gsr_ply.o
 	mkdir -p $(dir $(LIB))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libgsr.so
 

@@ -38,7 +38,9 @@ CONFIGS = {
     1: (10_000, 640, 480, 1),
     2: (1_000_000, 1920, 1080, 2),
     3: (5_000_000, 1600, 1063, 3),
+    5: (2_000_000, 1920, 1080, 5),     # 4D (Spacetime-Gaussian style), 120 timesteps
 }
+TIMESTEPS_4D = 120
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 BLEND_KERNEL = "k_blend_w<false>"   # default blend schedule (one 64-thread workgroup per 8x8 block)
 
@@ -127,13 +129,16 @@ def dropin_rate(gsr, scene, cam, W, H, k, frames=20):
     return frames / (time.perf_counter() - t0)
 
 
-def cpu_baseline(soa, cam, W, H, k, seconds):
+def cpu_baseline(soa, cam, W, H, k, seconds, four_d=False):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle  # test infrastructure: CPU baseline leg only
     threads = min(16, os.cpu_count() or 1)
     frames, t0 = 0, time.perf_counter()
     while True:
-        _oracle.render(soa, cam, W, H, k, threads=threads)
+        if four_d:   # temporal state of the frame, then the 3D render (no cull)
+            _oracle.render(_oracle.temporal(soa, frame_time(frames)), cam, W, H, k, threads=threads)
+        else:
+            _oracle.render(soa, cam, W, H, k, threads=threads)
         frames += 1
         el = time.perf_counter() - t0
         if el >= seconds or frames >= 50:
@@ -141,6 +146,11 @@ def cpu_baseline(soa, cam, W, H, k, seconds):
     return {"value": frames / el, "unit": "frames/sec", "cores": threads, "kind": "port",
             "sample": f"{frames} full frame(s) of the same workload by the C oracle (oracle/gsr_oracle.c, "
                       f"OpenMP {threads} threads), {el:.1f} s"}
+
+
+def frame_time(i: int) -> float:
+    """Config 5: frame i renders timestep i mod 120 of [0, 1]."""
+    return (i % TIMESTEPS_4D) / (TIMESTEPS_4D - 1)
 
 
 def main():
@@ -159,10 +169,11 @@ def main():
     n, W, H, seed = CONFIGS[args.config]
     scene_dir = args.scene_dir or os.path.join(tempfile.gettempdir(), "gsr_bench")
     os.makedirs(scene_dir, exist_ok=True)
-    ply = os.path.join(scene_dir, f"config{args.config}_n{n}_s{seed}.ply")
+    four_d = args.config == 5
+    ply = os.path.join(scene_dir, f"config{args.config}_n{n}_s{seed}{'_4d' if four_d else ''}.ply")
     if local_rank == 0 and not os.path.exists(ply):
         tmp = ply + f".tmp{os.getpid()}"
-        gsr.write_synthetic_ply(tmp, n, seed)
+        (gsr.write_synthetic_ply4d if four_d else gsr.write_synthetic_ply)(tmp, n, seed)
         os.replace(tmp, ply)
     if dist:
         dist.barrier()
@@ -182,7 +193,8 @@ def main():
         if pending[b] is not None:
             pending[b].wait()                   # stream-wait: gather of this buffer done
             pending[b] = None
-        r.render(scene, cam, W, H, outs[b].data_ptr(), k=args.k, stream=stream)
+        r.render(scene, cam, W, H, outs[b].data_ptr(), k=args.k, stream=stream,
+                 time=frame_time(i) if four_d else None)
         if dist and args.gather == "step":
             pending[b] = dist.gather(outs[b], recv[b] if recv else None, dst=0, async_op=True)
 
@@ -200,7 +212,8 @@ def main():
     # untimed diagnostic frame: per-stage breakdown, P, Pc and blend counters
     r.set_timing(2)
     r.set_diagnostics(True)
-    r.render(scene, cam, W, H, outs[0].data_ptr(), k=args.k, stream=stream)
+    r.render(scene, cam, W, H, outs[0].data_ptr(), k=args.k, stream=stream,
+             time=frame_time(TIMESTEPS_4D // 2) if four_d else None)
     r.sync()
     stages, _ = r.stage_times()
     pairs = r.pair_count()
@@ -255,7 +268,8 @@ def main():
     img = outs[0].view(3, H, W)
     result = {
         "metric": "frames/sec at 1920x1080, 1M Gaussians (config %d)" % args.config if args.config == 2
-        else f"frames/sec (config {args.config})",
+        else (f"frames/sec at 1920x1080, 2M 4D Gaussians, {TIMESTEPS_4D} timesteps (config 5)" if four_d
+              else f"frames/sec (config {args.config})"),
         "value": round(value, 3),
         "unit": "frames/sec",
         "n_gpus": world,
@@ -267,7 +281,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded 3DGS .ply, SURVEY.md 8d)",
-        "config": {"workload": f"config{args.config}: {n} Gaussians, {W}x{H}, k={args.k}, "
+        "config": {"workload": f"config{args.config}: {n} {'4D ' if four_d else ''}Gaussians, {W}x{H}, k={args.k}, "
+                               + (f"frame i at t = (i mod {TIMESTEPS_4D})/{TIMESTEPS_4D - 1} with temporal cull, "
+                                  if four_d else "")
                                + (f"one orbit camera per GPU, RCCL gather to rank 0 ({args.gather})" if world > 1
                                   else "camera (0,0,4) fovY 50"),
                    "gaussians": n, "width": W, "height": H, "parallelism": f"frames{world}"},
@@ -307,8 +323,8 @@ def main():
     if world == 1:
         result["dropin_host_fps"] = round(dropin_rate(gsr, scene, cam, W, H, args.k), 2)
     if world == 1 and not args.no_cpu_baseline:
-        soa = gsr.read_ply(ply)
-        result["cpu_baseline"] = cpu_baseline(soa, cam, W, H, args.k, args.cpu_seconds)
+        soa = gsr.read_ply(ply, four_d=four_d)
+        result["cpu_baseline"] = cpu_baseline(soa, cam, W, H, args.k, args.cpu_seconds, four_d=four_d)
     print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -19,7 +19,8 @@ from ctypes import byref, c_float, c_int, c_int64
 import numpy as np
 
 from . import _native
-from ._native import (Camera, GsrError, LAYOUT_AOS, LAYOUT_SCENE_BLOCK, NUM_STAGES, SCENE_NARRAYS,
+from ._native import (Camera, GsrError, LAYOUT_AOS, LAYOUT_SCENE_BLOCK, LAYOUT_SCENE_BLOCK_4D, NUM_STAGES,
+                      PLY_TYPED, SCENE4D_NARRAYS, SCENE_NARRAYS,
                       SPLAT_RECORD_BYTES, STAGES, TILE_PX, check, lib)
 
 __all__ = [
@@ -80,13 +81,20 @@ def camera_intrinsics(cam: Camera):
     return fx.value, fy.value
 
 
-def read_ply(path: str) -> np.ndarray:
-    """Host PLY parse with the reference loader's semantics -> (38, n) float32 SoA."""
+def read_ply(path: str, typed: bool = False, four_d: bool | None = False) -> np.ndarray:
+    """Host PLY parse -> (38, n) float32 SoA (reference loader semantics), or the
+    hardened typed reader (typed=True: declared types, ascii, big-endian).
+    four_d=True returns the (49, n) 4D arrays; four_d=None picks by the file."""
     L = lib()
     n = c_int64(-1)
-    check(L.gsr_ply_read_host(path.encode(), None, 0, byref(n)), "gsr_ply_read_host")
-    soa = np.zeros((SCENE_NARRAYS, n.value), dtype=np.float32)
-    check(L.gsr_ply_read_host(path.encode(), soa.ctypes.data, n.value, byref(n)), "gsr_ply_read_host")
+    is4d = c_int(0)
+    flags = PLY_TYPED if typed else 0
+    check(L.gsr_ply_read_host_ex(path.encode(), None, SCENE_NARRAYS, 0, byref(n), flags, byref(is4d)),
+          "gsr_ply_read_host")
+    na = SCENE4D_NARRAYS if (four_d or (four_d is None and is4d.value)) else SCENE_NARRAYS
+    soa = np.zeros((na, n.value), dtype=np.float32)
+    check(L.gsr_ply_read_host_ex(path.encode(), soa.ctypes.data, na, n.value, byref(n), flags, None),
+          "gsr_ply_read_host")
     return soa
 
 
@@ -95,30 +103,48 @@ def write_synthetic_ply(path: str, n: int, seed: int) -> None:
     check(lib().gsr_synth_write_ply(path.encode(), int(n), int(seed)), "gsr_synth_write_ply")
 
 
+def write_synthetic_ply4d(path: str, n: int, seed: int) -> None:
+    """Seeded synthetic 4D (Spacetime-Gaussian style, 73-property) PLY for config 5."""
+    check(lib().gsr_synth_write_ply4d(path.encode(), int(n), int(seed)), "gsr_synth_write_ply4d")
+
+
 class Scene:
     """A device scene block (one hipMalloc: header + SoA arrays)."""
 
-    def __init__(self, ptr: int, n: int, owned: bool = True):
-        self.ptr, self.n, self.owned = ptr, n, owned
+    def __init__(self, ptr: int, n: int, owned: bool = True, narrays: int = SCENE_NARRAYS):
+        self.ptr, self.n, self.owned, self.narrays = ptr, n, owned, narrays
+
+    @property
+    def is_4d(self) -> bool:
+        return self.narrays == SCENE4D_NARRAYS
+
+    @property
+    def layout(self) -> int:
+        return LAYOUT_SCENE_BLOCK_4D if self.is_4d else LAYOUT_SCENE_BLOCK
 
     @classmethod
     def from_soa(cls, soa: np.ndarray) -> "Scene":
         soa = np.ascontiguousarray(soa, dtype=np.float32)
-        assert soa.shape[0] == SCENE_NARRAYS
-        ptr = lib().gsr_scene_upload(soa.ctypes.data, soa.shape[1])
+        assert soa.shape[0] in (SCENE_NARRAYS, SCENE4D_NARRAYS)
+        ptr = lib().gsr_scene_upload_ex(soa.ctypes.data, soa.shape[0], soa.shape[1])
         if not ptr:
             raise GsrError(-2, "gsr_scene_upload")
-        return cls(ptr, soa.shape[1])
+        return cls(ptr, soa.shape[1], narrays=soa.shape[0])
 
     @classmethod
-    def from_ply(cls, path: str) -> "Scene":
-        ptr, n = loadGaussianCudaFromPly(path)
+    def from_ply(cls, path: str, typed: bool = False, allow_4d: bool = True) -> "Scene":
+        """Device scene from a .ply (the reference loader unless typed=True); a file
+        with the 4D properties loads as a 4D scene when allow_4d."""
+        n = c_int(0)
+        na = c_int(SCENE_NARRAYS)
+        ptr = lib().gsr_load_ply_device_ex(path.encode(), byref(n), PLY_TYPED if typed else 0,
+                                           byref(na) if allow_4d else None)
         if not ptr:
-            raise GsrError(-3, f"loadGaussianCudaFromPly({path})")
-        return cls(ptr, n)
+            raise GsrError(-3, f"loadGaussianCudaFromPly({path}): {lib().gsr_last_error().decode()}")
+        return cls(ptr, n.value, narrays=na.value if allow_4d else SCENE_NARRAYS)
 
     def download(self) -> np.ndarray:
-        soa = np.zeros((SCENE_NARRAYS, self.n), dtype=np.float32)
+        soa = np.zeros((self.narrays, self.n), dtype=np.float32)
         check(lib().gsr_scene_download(self.ptr, soa.ctypes.data, self.n), "gsr_scene_download")
         return soa
 
@@ -172,13 +198,19 @@ class Renderer:
         check(lib().gsr_reserve(self.ctx, n, pairs), "gsr_reserve")
 
     def render(self, scene, cam: Camera, W: int, H: int, out_ptr: int, k: float = 3.0, tiling=None,
-               stream: int = 0, layout: int = LAYOUT_SCENE_BLOCK, n: int | None = None) -> int:
+               stream: int = 0, layout: int = LAYOUT_SCENE_BLOCK, n: int | None = None,
+               time: float | None = None) -> int:
         """Enqueue one frame into the device buffer out_ptr (3*W*H float32).
+        4D scenes render at `time` (or the last gsr_set_time value).
 
         Returns GSR_OK, or GSR_E_OVERFLOW when an earlier frame overflowed the
         pair buffer (it has been grown; that frame must be re-rendered)."""
         ptr = scene.ptr if isinstance(scene, Scene) else int(scene)
         n = scene.n if n is None else n
+        if isinstance(scene, Scene) and scene.is_4d and layout == LAYOUT_SCENE_BLOCK:
+            layout = LAYOUT_SCENE_BLOCK_4D
+        if time is not None:
+            self.set_time(time)
         t = tiling or TilingInformation(1, 1, H, W)
         rc = lib().gsr_render(self.ctx, ptr, layout, n, byref(cam), W, H, t.num_tile_x, t.num_tile_y,
                               t.width_stride, t.height_stride, k, out_ptr, stream or None)
@@ -186,10 +218,17 @@ class Renderer:
             raise GsrError(rc, "gsr_render")
         return rc
 
+    def set_time(self, t: float):
+        check(lib().gsr_set_time(self.ctx, float(t)), "gsr_set_time")
+
     def preprocess(self, scene, cam: Camera, W: int, H: int, k: float = 3.0, tiling=None, stream: int = 0,
-                   layout: int = LAYOUT_SCENE_BLOCK, n: int | None = None):
+                   layout: int = LAYOUT_SCENE_BLOCK, n: int | None = None, time: float | None = None):
         ptr = scene.ptr if isinstance(scene, Scene) else int(scene)
         n = scene.n if n is None else n
+        if isinstance(scene, Scene) and scene.is_4d and layout == LAYOUT_SCENE_BLOCK:
+            layout = LAYOUT_SCENE_BLOCK_4D
+        if time is not None:
+            self.set_time(time)
         t = tiling or TilingInformation(1, 1, H, W)
         rc = lib().gsr_preprocess(self.ctx, ptr, layout, n, byref(cam), W, H, t.num_tile_x, t.num_tile_y,
                                   t.width_stride, t.height_stride, k, stream or None)

@@ -27,12 +27,15 @@ GSR_E_OVERFLOW = -5
 
 LAYOUT_SCENE_BLOCK = 0
 LAYOUT_AOS = 1
+LAYOUT_SCENE_BLOCK_4D = 2
+PLY_TYPED = 1
 
 STAGES = ("preprocess", "depth_sort", "emit", "tile_sort", "ranges", "blend")
 NUM_STAGES = len(STAGES)
 TILE_PX = 16
 SPLAT_RECORD_BYTES = 64
 SCENE_NARRAYS = 38
+SCENE4D_NARRAYS = 49
 
 
 class Camera(ctypes.Structure):
@@ -77,6 +80,7 @@ SIGNATURES = [
     ("preprocessCUDAGaussians", None,
      [c_void_p, POINTER(c_float), c_int, Camera, c_int, c_int, c_int, c_int, c_int, c_int, c_float]),
     ("gsr_load_ply_device", c_void_p, [c_char_p, POINTER(c_int)]),
+    ("gsr_load_ply_device_ex", c_void_p, [c_char_p, POINTER(c_int), c_int, POINTER(c_int)]),
     ("oneSweep3DGaussianSort", None, [POINTER(Lwg), c_int, c_int, POINTER(c_float)]),
     ("oneSweepSort", None, [POINTER(c_int), POINTER(c_int), c_int, c_int, POINTER(c_float)]),
     ("gsr_create", c_void_p, []),
@@ -104,10 +108,14 @@ SIGNATURES = [
     ("gsr_blend_stamps", c_int, [c_void_p, c_void_p, c_int64]),
     ("gsr_set_tuning", c_int, [c_void_p, c_int, c_int]),
     ("gsr_scene_upload", c_void_p, [c_void_p, c_int64]),
+    ("gsr_scene_upload_ex", c_void_p, [c_void_p, c_int, c_int64]),
+    ("gsr_set_time", c_int, [c_void_p, c_float]),
     ("gsr_scene_free", None, [c_void_p]),
     ("gsr_scene_download", c_int, [c_void_p, c_void_p, c_int64]),
     ("gsr_ply_read_host", c_int, [c_char_p, c_void_p, c_int64, POINTER(c_int64)]),
+    ("gsr_ply_read_host_ex", c_int, [c_char_p, c_void_p, c_int, c_int64, POINTER(c_int64), c_int, POINTER(c_int)]),
     ("gsr_synth_write_ply", c_int, [c_char_p, c_int64, c_uint64]),
+    ("gsr_synth_write_ply4d", c_int, [c_char_p, c_int64, c_uint64]),
     ("gsr_camera_default", None, [POINTER(Camera)]),
     ("gsr_camera_update", None, [POINTER(Camera)]),
     ("gsr_camera_update_frustum", None, [POINTER(Camera)]),

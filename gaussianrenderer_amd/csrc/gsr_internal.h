@@ -9,6 +9,10 @@
 
 namespace gsr {
 
+// Set the thread's last error (gsr_last_error) and return `code`.
+int set_error(int code, const char* fmt, ...);
+
+
 // Per-frame constants, passed by value to the kernels.
 struct Frame {
     float V[16];        // view matrix (camera.cpp:53, row-major)
@@ -40,7 +44,7 @@ struct Stats {
 hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, int64_t stride,
                              hipStream_t s);
 hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
-                             uint4* rec, uint64_t* items, uint64_t* rect, hipStream_t s);
+                             uint4* rec, uint64_t* items, uint64_t* rect, bool four_d, float t, hipStream_t s);
 // One stable LSD pass over u64 items on bits [shift, shift + bits) (bits <= 8).
 // n = n_dev ? *n_dev : n_host.  hist: 256 * groups u32, totals: 256 u32.
 // ranges (nullable, final tile-sort pass): per-tile {~start, end} of key (item >> 32),

@@ -154,14 +154,31 @@ __device__ __forceinline__ uint32_t rect_count(uint64_t r) {
     return (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1));
 }
 
+// Temporal state of a 4D (Spacetime-Gaussian style) Gaussian at time t, in
+// this exact operation order (the oracle restates it, oracle/gsr_oracle.c):
+// dt = t - c; x_t = ((x + m0 dt) + m3 dt^2) + m6 dt^3 (dt^2 = dt dt, dt^3 =
+// dt^2 dt; y, z with m1/m4/m7, m2/m5/m8); temporal factor exp(-(dt/s)^2).
+template <bool T4D>
 __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ arr, int64_t stride,
                                                     int64_t n, Frame fr, uint4* __restrict__ rec,
-                                                    uint64_t* __restrict__ items, uint64_t* __restrict__ rect) {
+                                                    uint64_t* __restrict__ items, uint64_t* __restrict__ rect,
+                                                    float tnow) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const float gx = arr[GSR_A_X * stride + i];
-    const float gy = arr[GSR_A_Y * stride + i];
-    const float gz = arr[GSR_A_Z * stride + i];
+    float gx = arr[GSR_A_X * stride + i];
+    float gy = arr[GSR_A_Y * stride + i];
+    float gz = arr[GSR_A_Z * stride + i];
+    float tfac = 1.0f;
+    if (T4D) {
+        const float dt = tnow - arr[GSR_A_TCENTER * stride + i];
+        const float dt2 = dt * dt, dt3 = dt2 * dt;
+        const float* m = arr + GSR_A_MOTION0 * stride + i;
+        gx = ((gx + m[0] * dt) + m[3 * stride] * dt2) + m[6 * stride] * dt3;
+        gy = ((gy + m[1 * stride] * dt) + m[4 * stride] * dt2) + m[7 * stride] * dt3;
+        gz = ((gz + m[2 * stride] * dt) + m[5 * stride] * dt2) + m[8 * stride] * dt3;
+        const float u = dt / arr[GSR_A_TSCALE * stride + i];
+        tfac = gsr_expf(-(u * u));
+    }
     uint4* R = rec + 4 * i;
     items[i] = ((uint64_t)0xffffffffu << 32) | (uint64_t)(uint32_t)i;
 
@@ -235,6 +252,18 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     const float invDet = 1.0f / det;
     const float ic0 = S2[3] * invDet, ic1 = -S2[1] * invDet;
     const float ic2 = -S2[2] * invDet, ic3 = S2[0] * invDet;
+    if (T4D) {
+        // temporal cull (exact): opacity below 0.9e-3 with a robustly positive
+        // definite conic keeps md2 >= -0.05 at every pixel of the AABB, so alpha
+        // = min(op exp(-md2/2), 0.99) < 1e-3 everywhere and the splat never composites
+        const float opt = arr[GSR_A_OPACITY * stride + i] * tfac;
+        const float hh = 0.5f * (ic1 + ic2);
+        if (opt < 0.9e-3f && ic0 > 0.0f && ic3 > 0.0f && (ic0 * ic3 - hh * hh) > 1e-4f * (ic0 * ic3)) {
+            R[3] = dead_record_d();
+            rect[i] = kDeadRect;
+            return;
+        }
+    }
 
     // ---- extent (render.cu:704-764) ----
     const float sxy = 0.5f * (S2[1] + S2[2]);
@@ -311,7 +340,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
         cc += 0.5f;
         col[ch] = fminf(fmaxf(cc, 0.0f), 1.0f);
     }
-    const float opacity = arr[GSR_A_OPACITY * stride + i];
+    const float opacity = T4D ? arr[GSR_A_OPACITY * stride + i] * tfac : arr[GSR_A_OPACITY * stride + i];
 
     R[0] = make_uint4(__float_as_uint(ic0), __float_as_uint(ic1), __float_as_uint(ic2), __float_as_uint(ic3));
     R[1] = make_uint4(__float_as_uint(opacity), __float_as_uint(col[0]), __float_as_uint(col[1]),
@@ -1196,10 +1225,14 @@ hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, 
 }
 
 hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
-                             uint4* rec, uint64_t* items, uint64_t* rect, hipStream_t s) {
+                             uint4* rec, uint64_t* items, uint64_t* rect, bool four_d, float t, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_preprocess, dim3(grid_for(n, 256)), dim3(256), 0, s, arrays, stride, n, fr, rec,
-                       items, rect);
+    if (four_d)
+        hipLaunchKernelGGL(k_preprocess<true>, dim3(grid_for(n, 256)), dim3(256), 0, s, arrays, stride, n, fr, rec,
+                           items, rect, t);
+    else
+        hipLaunchKernelGGL(k_preprocess<false>, dim3(grid_for(n, 256)), dim3(256), 0, s, arrays, stride, n, fr,
+                           rec, items, rect, t);
     return hipGetLastError();
 }
 

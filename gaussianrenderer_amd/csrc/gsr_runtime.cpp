@@ -30,7 +30,8 @@ using gsr::Stats;
 
 static thread_local std::string g_err;
 
-static int set_err(int code, const char* fmt, ...) {
+namespace gsr {
+int set_error(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -39,6 +40,9 @@ static int set_err(int code, const char* fmt, ...) {
     g_err = buf;
     return code;
 }
+}  // namespace gsr
+
+#define set_err gsr::set_error
 
 #define HIP_TRY(expr)                                                                        \
     do {                                                                                     \
@@ -197,181 +201,18 @@ extern "C" void gsr_camera_intrinsics(const gsr_camera* cam, float* fx, float* f
     *fx = *fy / cam->aspectRatio;
 }
 
-// ------------------------------------------------------------------ PLY (misc.cu:13-134)
-
-namespace {
-
-enum Slot { S_X, S_Y, S_Z, S_NORMAL, S_DC, S_REST, S_OPACITY, S_SCALE, S_ROT, S_SKIP };
-struct Prop {
-    Slot type;
-    int index;
-};
-
-struct PlyHeader {
-    std::string format;
-    int64_t n = -1;
-    std::vector<Prop> props;
-    std::streampos data_begin;
-};
-
-int parse_header(std::ifstream& file, PlyHeader& h) {
-    std::string line;
-    std::string prefix = "format ";
-    while (std::getline(file, line)) {
-        if (line.substr(0, prefix.size()) == prefix) {
-            h.format = line.substr(prefix.size());
-            break;
-        }
-    }
-    prefix = "element vertex ";
-    bool found = false;
-    while (std::getline(file, line)) {
-        if (line.substr(0, prefix.size()) == prefix) {
-            found = true;
-            break;
-        }
-    }
-    if (!found) return set_err(GSR_E_FORMAT, "PLY: no 'element vertex' line");
-    try {
-        h.n = std::stoll(line.substr(prefix.size()));
-    } catch (...) {
-        return set_err(GSR_E_FORMAT, "PLY: bad vertex count '%s'", line.c_str());
-    }
-    if (h.n < 0 || h.n > INT32_MAX) return set_err(GSR_E_FORMAT, "PLY: vertex count out of range");
-    prefix = "property ";
-    while (std::getline(file, line)) {
-        if (line == "end_header") break;
-        if (line.substr(0, prefix.size()) != prefix) continue;
-        std::istringstream iss(line.substr(prefix.size()));
-        std::string type, name;
-        iss >> type >> name;
-        Prop p{S_SKIP, 0};
-        if (name == "x") p = {S_X, 0};
-        else if (name == "y") p = {S_Y, 0};
-        else if (name == "z") p = {S_Z, 0};
-        else if (name == "nxx") p = {S_NORMAL, 0};   // sic, misc.cu:68
-        else if (name == "ny") p = {S_NORMAL, 1};
-        else if (name == "nz") p = {S_NORMAL, 2};
-        else if (name == "f_dc_0") p = {S_DC, 0};
-        else if (name == "f_dc_1") p = {S_DC, 1};
-        else if (name == "f_dc_2") p = {S_DC, 2};
-        else if (name.rfind("f_rest_", 0) == 0) {
-            int idx = std::atoi(name.c_str() + 7);
-            if (idx < 24) p = {S_REST, idx};        // misc.cu:76
-        } else if (name == "opacity") p = {S_OPACITY, 0};
-        else if (name.rfind("scale_", 0) == 0) {
-            int idx = std::atoi(name.c_str() + 6);
-            if (idx >= 0 && idx < 3) p = {S_SCALE, idx};
-        } else if (name.rfind("rot_", 0) == 0) {
-            int idx = std::atoi(name.c_str() + 4);
-            if (idx >= 0 && idx < 4) p = {S_ROT, idx};
-        }
-        h.props.push_back(p);
-    }
-    if (h.format != "binary_little_endian 1.0")
-        return set_err(GSR_E_FORMAT, "Unsupported PLY format: %s", h.format.c_str());
-    h.data_begin = file.tellg();
-    return GSR_OK;
-}
-
-// storeGaussianFromProperty (gaussians.cpp:17-30) into SoA arrays.
-inline void store(const Prop& p, float* soa, int64_t n, int64_t i, float v) {
-    switch (p.type) {
-    case S_X: soa[GSR_A_X * n + i] = v; break;
-    case S_Y: soa[GSR_A_Y * n + i] = v; break;
-    case S_Z: soa[GSR_A_Z * n + i] = v; break;
-    case S_DC: soa[(GSR_A_SH0 + p.index) * n + i] = v; break;
-    case S_REST: soa[(GSR_A_SH0 + 3 + p.index) * n + i] = v; break;
-    case S_OPACITY: soa[GSR_A_OPACITY * n + i] = 1.0f / (1.0f + std::exp(-v)); break;   // sigmoid<float>
-    case S_SCALE: soa[(GSR_A_SCALE0 + p.index) * n + i] = (float)::exp((double)v); break; // ::exp(double)
-    case S_ROT: soa[(GSR_A_ROT0 + p.index) * n + i] = v; break;
-    default: break;   // normals and skipped properties are not used by the render path
-    }
-}
-
-}  // namespace
-
-extern "C" int gsr_ply_read_host(const char* path, float* soa, int64_t capacity, int64_t* n_out) {
-    if (!path || !n_out) return set_err(GSR_E_ARG, "gsr_ply_read_host: null argument");
-    std::ifstream file(path, std::ios::binary);
-    if (!file.is_open()) return set_err(GSR_E_IO, "Failed to open file: %s", path);
-    PlyHeader h;
-    int rc = parse_header(file, h);
-    if (h.n >= 0) *n_out = h.n;
-    if (rc) return rc;
-    if (!soa || capacity < h.n) return GSR_OK;
-    const int64_t n = h.n;
-    std::fill(soa, soa + (size_t)GSR_SCENE_NARRAYS * (size_t)n, 0.0f);   // Gaussian g{} (misc.cu:97)
-    const size_t np = h.props.size();
-    std::vector<float> buf;
-    const int64_t chunk = 65536;
-    for (int64_t i0 = 0; i0 < n; i0 += chunk) {
-        const int64_t m = std::min(chunk, n - i0);
-        buf.resize((size_t)m * np);
-        if (np && !file.read(reinterpret_cast<char*>(buf.data()), (std::streamsize)(buf.size() * sizeof(float))))
-            return set_err(GSR_E_IO, "PLY: truncated data in %s", path);
-        for (int64_t r = 0; r < m; r++)
-            for (size_t p = 0; p < np; p++) store(h.props[p], soa, n, i0 + r, buf[(size_t)r * np + p]);
-    }
-    return GSR_OK;
-}
-
-// ------------------------------------------------------------------ synthetic scenes
-
-extern "C" int gsr_synth_write_ply(const char* path, int64_t n, uint64_t seed) {
-    if (!path || n < 0 || n > INT32_MAX) return set_err(GSR_E_ARG, "gsr_synth_write_ply: bad argument");
-    std::ofstream f(path, std::ios::binary);
-    if (!f) return set_err(GSR_E_IO, "cannot write %s", path);
-    f << "ply\nformat binary_little_endian 1.0\nelement vertex " << n << "\n";
-    const char* base[] = {"x", "y", "z", "nx", "ny", "nz", "f_dc_0", "f_dc_1", "f_dc_2"};
-    for (const char* b : base) f << "property float " << b << "\n";
-    for (int r = 0; r < 45; r++) f << "property float f_rest_" << r << "\n";
-    f << "property float opacity\n";
-    for (int r = 0; r < 3; r++) f << "property float scale_" << r << "\n";
-    for (int r = 0; r < 4; r++) f << "property float rot_" << r << "\n";
-    f << "end_header\n";
-    std::mt19937_64 rng(seed);
-    std::uniform_real_distribution<float> ux(-3.0f, 3.0f), uy(-1.7f, 1.7f), uz(-1.0f, 1.0f);
-    std::normal_distribution<float> ndc(0.0f, 0.6f), nrest(0.0f, 0.15f), nrot(0.0f, 1.0f);
-    std::uniform_real_distribution<float> uop(-1.0f, 3.0f), usc(-5.65f, -4.07f);
-    std::vector<float> row(62);
-    std::vector<float> block;
-    block.reserve(62 * 4096);
-    for (int64_t i = 0; i < n; i++) {
-        int k = 0;
-        row[k++] = ux(rng);
-        row[k++] = uy(rng);
-        row[k++] = uz(rng);
-        row[k++] = 0.0f;
-        row[k++] = 0.0f;
-        row[k++] = 0.0f;
-        for (int c = 0; c < 3; c++) row[k++] = ndc(rng);
-        for (int c = 0; c < 45; c++) row[k++] = nrest(rng);
-        row[k++] = uop(rng);
-        for (int c = 0; c < 3; c++) row[k++] = usc(rng);
-        for (int c = 0; c < 4; c++) row[k++] = nrot(rng);
-        block.insert(block.end(), row.begin(), row.end());
-        if (block.size() >= 62 * 4096) {
-            f.write(reinterpret_cast<const char*>(block.data()), (std::streamsize)(block.size() * sizeof(float)));
-            block.clear();
-        }
-    }
-    f.write(reinterpret_cast<const char*>(block.data()), (std::streamsize)(block.size() * sizeof(float)));
-    if (!f) return set_err(GSR_E_IO, "write failed: %s", path);
-    return GSR_OK;
-}
-
 // ------------------------------------------------------------------ device scene blocks
 
 static int64_t scene_stride(int64_t n) { return (n + 63) / 64 * 64; }
 
-extern "C" void* gsr_scene_upload(const float* host_soa, int64_t n) {
-    if (n < 0 || n > INT32_MAX || (n > 0 && !host_soa)) {
+extern "C" void* gsr_scene_upload_ex(const float* host_soa, int narrays, int64_t n) {
+    if (n < 0 || n > INT32_MAX || (n > 0 && !host_soa) ||
+        (narrays != GSR_SCENE_NARRAYS && narrays != GSR_SCENE4D_NARRAYS)) {
         set_err(GSR_E_ARG, "gsr_scene_upload: bad argument");
         return nullptr;
     }
     const int64_t stride = scene_stride(n);
-    const size_t bytes = GSR_SCENE_HEADER_BYTES + sizeof(float) * (size_t)GSR_SCENE_NARRAYS * (size_t)stride;
+    const size_t bytes = GSR_SCENE_HEADER_BYTES + sizeof(float) * (size_t)narrays * (size_t)stride;
     void* d = nullptr;
     hipError_t e = hipMalloc(&d, bytes);
     if (e != hipSuccess) {
@@ -385,11 +226,12 @@ extern "C" void* gsr_scene_upload(const float* host_soa, int64_t n) {
     h.magic[3] = GSR_SCENE_MAGIC3;
     h.count = (uint64_t)n;
     h.stride = (uint64_t)stride;
+    h.narrays = (uint64_t)narrays;
     e = hipMemcpy(d, &h, sizeof h, hipMemcpyHostToDevice);
     float* arr = reinterpret_cast<float*>(static_cast<char*>(d) + GSR_SCENE_HEADER_BYTES);
     if (e == hipSuccess && n > 0)
         e = hipMemcpy2D(arr, sizeof(float) * (size_t)stride, host_soa, sizeof(float) * (size_t)n,
-                        sizeof(float) * (size_t)n, GSR_SCENE_NARRAYS, hipMemcpyHostToDevice);
+                        sizeof(float) * (size_t)n, (size_t)narrays, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         set_err(GSR_E_HIP, "scene upload failed: %s", hipGetErrorString(e));
         (void)hipFree(d);
@@ -398,37 +240,51 @@ extern "C" void* gsr_scene_upload(const float* host_soa, int64_t n) {
     return d;
 }
 
+extern "C" void* gsr_scene_upload(const float* host_soa, int64_t n) {
+    return gsr_scene_upload_ex(host_soa, GSR_SCENE_NARRAYS, n);
+}
+
 extern "C" void gsr_scene_free(void* d) {
     if (d) (void)hipFree(d);
 }
 
 extern "C" int gsr_scene_download(const void* d, float* host_soa, int64_t n) {
     if (!d || !host_soa || n < 0) return set_err(GSR_E_ARG, "gsr_scene_download: bad argument");
+    gsr_scene_header h{};
+    HIP_TRY(hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost));
+    const int narrays = h.narrays == GSR_SCENE4D_NARRAYS ? GSR_SCENE4D_NARRAYS : GSR_SCENE_NARRAYS;
     const int64_t stride = scene_stride(n);
     const float* arr = reinterpret_cast<const float*>(static_cast<const char*>(d) + GSR_SCENE_HEADER_BYTES);
     if (n == 0) return GSR_OK;
     HIP_TRY(hipMemcpy2D(host_soa, sizeof(float) * (size_t)n, arr, sizeof(float) * (size_t)stride,
-                        sizeof(float) * (size_t)n, GSR_SCENE_NARRAYS, hipMemcpyDeviceToHost));
+                        sizeof(float) * (size_t)n, (size_t)narrays, hipMemcpyDeviceToHost));
     return GSR_OK;
 }
 
-extern "C" gsr_gaussian* gsr_load_ply_device(const char* filename, int* out_n) {
+extern "C" gsr_gaussian* gsr_load_ply_device_ex(const char* filename, int* out_n, int flags, int* out_narrays) {
     int64_t n = -1;
-    int rc = gsr_ply_read_host(filename, nullptr, 0, &n);
+    int is4d = 0;
+    int rc = gsr_ply_read_host_ex(filename, nullptr, GSR_SCENE_NARRAYS, 0, &n, flags, &is4d);
     if (n >= 0 && out_n) *out_n = (int)n;   // misc.cu:38 sets the count before reading data
     if (rc) {
         std::fprintf(stderr, "%s\n", g_err.c_str());
         return nullptr;
     }
-    std::vector<float> soa((size_t)GSR_SCENE_NARRAYS * (size_t)n);
-    rc = gsr_ply_read_host(filename, soa.data(), n, &n);
+    const int narrays = (is4d && out_narrays) ? GSR_SCENE4D_NARRAYS : GSR_SCENE_NARRAYS;
+    std::vector<float> soa((size_t)narrays * (size_t)n);
+    rc = gsr_ply_read_host_ex(filename, soa.data(), narrays, n, &n, flags, nullptr);
     if (rc) {
         std::fprintf(stderr, "%s\n", g_err.c_str());
         return nullptr;
     }
-    void* d = gsr_scene_upload(soa.data(), n);
+    void* d = gsr_scene_upload_ex(soa.data(), narrays, n);
     if (!d) std::fprintf(stderr, "CUDA memory allocation failed: %s\n", g_err.c_str());
+    if (out_narrays) *out_narrays = narrays;
     return static_cast<gsr_gaussian*>(d);
+}
+
+extern "C" gsr_gaussian* gsr_load_ply_device(const char* filename, int* out_n) {
+    return gsr_load_ply_device_ex(filename, out_n, 0, nullptr);
 }
 
 gsr_gaussian* loadGaussianCudaFromPly(const std::string& filename, int* out_numGaussians) {
@@ -463,6 +319,7 @@ struct gsr_context {
     int64_t consumed_cap = 0;
     bool diagnostics = false;
     int blend_variant = 0;
+    float time = 0.0f;               // frame time for 4D scene blocks
     int tile_items = 16;             // tile sort: items per thread (8 | 16)
     int depth_items = 0;             // depth sort: items per thread (0 = by size | 8 | 16)
     int tile_groups = 1024;          // tile sort: workgroup cap (measured best: 2 tiles of items per group)
@@ -678,7 +535,7 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
                              int W, int H, int nx, int ny, int ws, int hs, float k, void* stream) {
     if (n < 0 || n > INT32_MAX) return set_err(GSR_E_ARG, "Gaussian count %lld out of range", (long long)n);
     if (n > 0 && !scene) return set_err(GSR_E_ARG, "null scene");
-    if (layout != GSR_LAYOUT_SCENE_BLOCK && layout != GSR_LAYOUT_AOS)
+    if (layout != GSR_LAYOUT_SCENE_BLOCK && layout != GSR_LAYOUT_AOS && layout != GSR_LAYOUT_SCENE_BLOCK_4D)
         return set_err(GSR_E_ARG, "unknown scene layout %d", layout);
     if (int rc = fill_frame(c, cam, W, H, nx, ny, ws, hs, k)) return rc;
     if (int rc = ensure_static(c)) return rc;
@@ -703,7 +560,8 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     } else {
         arrays = reinterpret_cast<const float*>(static_cast<const char*>(scene) + GSR_SCENE_HEADER_BYTES);
     }
-    HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[0], c->rect, c->stream));
+    HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[0], c->rect,
+                                   layout == GSR_LAYOUT_SCENE_BLOCK_4D, c->time, c->stream));
     c->have_pre = true;
     c->have_sort = false;
     return rc_over;
@@ -929,6 +787,13 @@ extern "C" int gsr_set_diagnostics(gsr_context* c, int on) {
     return GSR_OK;
 }
 
+extern "C" int gsr_set_time(gsr_context* c, float t) {
+    if (!c) return set_err(GSR_E_ARG, "null context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->time = t;
+    return GSR_OK;
+}
+
 extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     if (!c) return set_err(GSR_E_ARG, "null context");
     std::lock_guard<std::mutex> lk(c->mu);
@@ -1041,7 +906,9 @@ extern "C" void preprocessCUDAGaussians(gsr_gaussian* d_gaussians, float* out_pi
         }
         if (h.magic[0] == GSR_SCENE_MAGIC0 && h.magic[1] == GSR_SCENE_MAGIC1 && h.magic[2] == GSR_SCENE_MAGIC2 &&
             h.magic[3] == GSR_SCENE_MAGIC3) {
-            layout = GSR_LAYOUT_SCENE_BLOCK;
+            // 4D blocks render at the drop-in context's time (gsr_set_time on it is not
+            // reachable through this ABI, so t = 0: the sequence's first frame)
+            layout = h.narrays == GSR_SCENE4D_NARRAYS ? GSR_LAYOUT_SCENE_BLOCK_4D : GSR_LAYOUT_SCENE_BLOCK;
             if ((int64_t)h.count != num_gaussians) {
                 set_err(GSR_E_ARG, "num_gaussians %d != scene block count %llu", num_gaussians,
                         (unsigned long long)h.count);

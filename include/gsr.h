@@ -48,7 +48,15 @@ enum {
 /* Scene layout accepted by the render entry points. */
 enum {
     GSR_LAYOUT_SCENE_BLOCK = 0,   /* our SoA block (gsr_scene_header + arrays) */
-    GSR_LAYOUT_AOS = 1            /* reference Gaussian[] (240 B records) */
+    GSR_LAYOUT_AOS = 1,           /* reference Gaussian[] (240 B records) */
+    GSR_LAYOUT_SCENE_BLOCK_4D = 2 /* 4D SoA block (GSR_SCENE4D_NARRAYS), rendered at gsr_set_time() */
+};
+
+/* PLY loading flags (gsr_ply_read_host_ex / gsr_load_ply_device_ex). */
+enum {
+    GSR_PLY_TYPED = 1   /* hardened reader: declared property types, ascii and big-endian
+                           formats, other elements skipped, "nx" accepted.
+                           Off = the reference's reader exactly (every property a 4-B float). */
 };
 
 /* Stage indices for gsr_stage_times(). */
@@ -84,6 +92,10 @@ void preprocessCUDAGaussians(gsr_gaussian* d_gaussians, float* out_pixels, int n
  * returns a device scene block (free with hipFree or gsr_scene_free), or
  * NULL on failure; *out_numGaussians is set once the header is parsed. */
 gsr_gaussian* gsr_load_ply_device(const char* filename, int* out_numGaussians);
+/* Same with loader flags (GSR_PLY_TYPED).  If out_narrays is non-NULL, a file
+ * carrying the 4D properties (trbf_center, trbf_scale, motion_0..8) loads as a
+ * 4D scene block and *out_narrays = GSR_SCENE4D_NARRAYS (else 38). */
+gsr_gaussian* gsr_load_ply_device_ex(const char* filename, int* out_numGaussians, int flags, int* out_narrays);
 
 /* render.cu:194-264: stable sort of N host-side lightWeightGaussian records
  * by the low num_bits bits of radix_id, in place; *kernel_ms = device time. */
@@ -119,6 +131,14 @@ int gsr_preprocess(gsr_context* ctx, const void* d_scene, int layout, int64_t n,
                    int width_stride, int height_stride, float k, void* stream);
 int gsr_sort(gsr_context* ctx, void* stream);
 int gsr_blend(gsr_context* ctx, float* d_out, void* stream);
+
+/* Frame time t for GSR_LAYOUT_SCENE_BLOCK_4D scenes (config 5):
+ * dt = t - trbf_center; position = xyz + m0..2*dt + m3..5*dt^2 + m6..8*dt^3;
+ * opacity = sigmoid(opacity) * exp(-(dt / trbf_scale)^2).  Gaussians whose
+ * temporal opacity is below 0.9e-3 (and whose 2D conic is robustly positive
+ * definite) are culled in preprocess: they could never reach alpha >= 1e-3,
+ * so the image equals the uncut render. */
+int gsr_set_time(gsr_context* ctx, float t);
 
 /* Wait for all work of the context; returns GSR_E_OVERFLOW if the last frame
  * overflowed (and grows the buffer). */
@@ -190,8 +210,11 @@ int gsr_blend_stamps(gsr_context* ctx, uint64_t* out, int64_t n);
 /* Upload a host SoA scene (GSR_SCENE_NARRAYS arrays of n floats, contiguous,
  * already activated as by the loader) into a new device scene block. */
 void* gsr_scene_upload(const float* host_soa, int64_t n);
+/* narrays = GSR_SCENE_NARRAYS (3D) or GSR_SCENE4D_NARRAYS (4D). */
+void* gsr_scene_upload_ex(const float* host_soa, int narrays, int64_t n);
 void gsr_scene_free(void* d_scene);
 /* Copy a device scene block back into host SoA form (38 * n floats). */
+/* Copies every array of the block (38, or 49 for a 4D block) into host_soa. */
 int gsr_scene_download(const void* d_scene, float* host_soa, int64_t n);
 
 /* ---------------------------------------------------------------- host helpers */
@@ -200,11 +223,19 @@ int gsr_scene_download(const void* d_scene, float* host_soa, int64_t n);
  * storeGaussianFromProperty gaussians.cpp:17-30), host side only.  Call with
  * host_soa == NULL to get the count; then with a buffer of 38*n floats. */
 int gsr_ply_read_host(const char* path, float* host_soa, int64_t capacity, int64_t* n_out);
+/* Same with flags (GSR_PLY_TYPED) and narrays = 38 or 49 (4D arrays filled
+ * when present; defaults trbf_center 0, trbf_scale 1, motion 0); *is_4d (if
+ * non-NULL) reports whether the file has the 4D properties. */
+int gsr_ply_read_host_ex(const char* path, float* host_soa, int narrays, int64_t capacity, int64_t* n_out,
+                         int flags, int* is_4d);
 
 /* Seeded synthetic scene: writes a standard 62-property
  * binary_little_endian 3DGS .ply, or fills raw (pre-activation) property
  * values.  Same generator, same values, for a given (n, seed). */
 int gsr_synth_write_ply(const char* path, int64_t n, uint64_t seed);
+/* Config 5 4D synthetic scene: the 62 properties plus trbf_center U(0,1),
+ * trbf_scale U(-3.5,-2) (log), motion_0..8 N(0, .5 | .2 | .1). */
+int gsr_synth_write_ply4d(const char* path, int64_t n, uint64_t seed);
 
 /* Camera (camera.cpp): Camera() ctor 8-13, updateCameraMatrices 36-57,
  * updateFrustumPlanes 59-121, zoom 123-128, orbit 130-158. */

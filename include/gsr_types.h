@@ -88,19 +88,26 @@ typedef struct gsr_lwg {
  *   7..10  rot_0..3 (w, x, y, z), raw    (gaussians.cpp:27)
  *   11..37 sh[0..26]: f_dc_0..2 then f_rest_0..23 (gaussians.cpp:23-24,
  *          misc.cu:74-77; f_rest_24..44 are dropped as in the reference)
+ * 4D scene blocks (GSR_SCENE4D_NARRAYS, config 5 — Spacetime-Gaussian style,
+ * DESIGN.md) append:
+ *   38     trbf_center (temporal centre, raw)
+ *   39     trbf_scale = (float)exp((double)v) (temporal scale)
+ *   40..48 motion_0..8: linear xyz, quadratic xyz, cubic xyz (raw)
  */
 #define GSR_SCENE_MAGIC0 0x7fc0a5e1u   /* NaN bit patterns: never a sane AoS x,y,z */
 #define GSR_SCENE_MAGIC1 0x7fc05352u
 #define GSR_SCENE_MAGIC2 0x7fc03347u
 #define GSR_SCENE_MAGIC3 0x7fc00001u
 #define GSR_SCENE_NARRAYS 38
+#define GSR_SCENE4D_NARRAYS 49
 #define GSR_SCENE_HEADER_BYTES 256
 
 typedef struct gsr_scene_header {
     uint32_t magic[4];
     uint64_t count;        /* number of Gaussians */
     uint64_t stride;       /* elements per array (count rounded up to 64) */
-    uint64_t reserved[28];
+    uint64_t narrays;      /* GSR_SCENE_NARRAYS or GSR_SCENE4D_NARRAYS */
+    uint64_t reserved[27];
 } gsr_scene_header;
 
 /* Index of each attribute array inside a scene block. */
@@ -109,7 +116,10 @@ enum {
     GSR_A_OPACITY = 3,
     GSR_A_SCALE0 = 4,
     GSR_A_ROT0 = 7,
-    GSR_A_SH0 = 11
+    GSR_A_SH0 = 11,
+    GSR_A_TCENTER = 38,
+    GSR_A_TSCALE = 39,
+    GSR_A_MOTION0 = 40
 };
 
 #ifdef __cplusplus

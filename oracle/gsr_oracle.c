@@ -42,10 +42,10 @@ static int read_line(FILE* f, char** buf, size_t* cap) {
 static int starts_with(const char* s, const char* p) { return strncmp(s, p, strlen(p)) == 0; }
 
 /* Slot kinds of gaussians.hpp:10 (SlotType). */
-enum { S_X, S_Y, S_Z, S_NORMAL, S_DC, S_REST, S_OPACITY, S_SCALE, S_ROT, S_SKIP };
+enum { S_X, S_Y, S_Z, S_NORMAL, S_DC, S_REST, S_OPACITY, S_SCALE, S_ROT, S_TCENTER, S_TSCALE, S_MOTION, S_SKIP };
 
 /* misc.cu:13-134 + gaussians.cpp:17-30 (storeGaussianFromProperty). */
-int orc_ply_read(const char* path, float* soa, int64_t capacity, int64_t* n_out) {
+int orc_ply_read_ex(const char* path, float* soa, int narrays, int64_t capacity, int64_t* n_out) {
     FILE* f = fopen(path, "rb");
     if (!f) return -3;
     char* line = NULL;
@@ -93,6 +93,10 @@ int orc_ply_read(const char* path, float* soa, int64_t capacity, int64_t* n_out)
         } else if (!strcmp(name, "opacity")) kind = S_OPACITY;
         else if (starts_with(name, "scale_")) { idx = atoi(name + 6); kind = (idx >= 0 && idx < 3) ? S_SCALE : S_SKIP; }
         else if (starts_with(name, "rot_")) { idx = atoi(name + 4); kind = (idx >= 0 && idx < 4) ? S_ROT : S_SKIP; }
+        /* config 5 (own spec): Spacetime-Gaussian temporal properties */
+        else if (!strcmp(name, "trbf_center")) kind = S_TCENTER;
+        else if (!strcmp(name, "trbf_scale")) kind = S_TSCALE;
+        else if (starts_with(name, "motion_")) { idx = atoi(name + 7); kind = (idx >= 0 && idx < 9) ? S_MOTION : S_SKIP; }
         if (nprops < 1024) { kinds[nprops] = kind; idxs[nprops] = idx; }
         nprops++;
     }
@@ -101,7 +105,9 @@ int orc_ply_read(const char* path, float* soa, int64_t capacity, int64_t* n_out)
     if (!soa || capacity < nv) { fclose(f); return 0; }
 
     const int64_t n = nv;
-    memset(soa, 0, sizeof(float) * (size_t)GSR_SCENE_NARRAYS * (size_t)n);   /* Gaussian g{} */
+    memset(soa, 0, sizeof(float) * (size_t)narrays * (size_t)n);   /* Gaussian g{} */
+    if (narrays > GSR_A_TSCALE)   /* 4D defaults: a static Gaussian (temporal scale 1) */
+        for (int64_t i = 0; i < n; i++) soa[GSR_A_TSCALE * n + i] = 1.0f;
     float* row = (float*)malloc(sizeof(float) * (size_t)(nprops > 0 ? nprops : 1));
     int rc = 0;
     for (int64_t i = 0; i < n && rc == 0; i++) {
@@ -119,6 +125,9 @@ int orc_ply_read(const char* path, float* soa, int64_t capacity, int64_t* n_out)
             /* exp(value) resolves to ::exp(double) (gaussians.cpp:26) */
             case S_SCALE: soa[(GSR_A_SCALE0 + idxs[p]) * n + i] = (float)exp((double)v); break;
             case S_ROT: soa[(GSR_A_ROT0 + idxs[p]) * n + i] = v; break;
+            case S_TCENTER: if (narrays > GSR_A_TCENTER) soa[GSR_A_TCENTER * n + i] = v; break;
+            case S_TSCALE: if (narrays > GSR_A_TSCALE) soa[GSR_A_TSCALE * n + i] = (float)exp((double)v); break;
+            case S_MOTION: if (narrays > GSR_A_MOTION0 + idxs[p]) soa[(GSR_A_MOTION0 + idxs[p]) * n + i] = v; break;
             default: break;   /* normals are not used by the render path */
             }
         }
@@ -126,6 +135,36 @@ int orc_ply_read(const char* path, float* soa, int64_t capacity, int64_t* n_out)
     free(row);
     fclose(f);
     return rc;
+}
+
+int orc_ply_read(const char* path, float* soa, int64_t capacity, int64_t* n_out) {
+    return orc_ply_read_ex(path, soa, GSR_SCENE_NARRAYS, capacity, n_out);
+}
+
+/*
+ * Config 5 (own spec; Spacetime-Gaussian style): the 3D arrays of a
+ * 4D scene at time t, with NO temporal cull — every Gaussian keeps its slot,
+ * its position moved by the cubic motion and its opacity scaled by the
+ * temporal RBF:
+ *   dt = t - trbf_center; dt2 = dt*dt; dt3 = dt2*dt
+ *   x_t = ((x + m0*dt) + m3*dt2) + m6*dt3      (y: m1 m4 m7, z: m2 m5 m8)
+ *   u = dt / trbf_scale; opacity_t = opacity * exp(-(u*u))
+ * out38 gets all 38 arrays of the time-t 3D scene (n elements each).
+ */
+void orc_temporal(const float* soa49, int64_t n, float t, float* out38) {
+    memcpy(out38, soa49, sizeof(float) * (size_t)GSR_SCENE_NARRAYS * (size_t)n);
+    for (int64_t i = 0; i < n; i++) {
+        const float dt = t - soa49[GSR_A_TCENTER * n + i];
+        const float dt2 = dt * dt, dt3 = dt2 * dt;
+        for (int a = 0; a < 3; a++) {
+            const float m1 = soa49[(GSR_A_MOTION0 + a) * n + i];
+            const float m2 = soa49[(GSR_A_MOTION0 + 3 + a) * n + i];
+            const float m3 = soa49[(GSR_A_MOTION0 + 6 + a) * n + i];
+            out38[(GSR_A_X + a) * n + i] = ((soa49[(GSR_A_X + a) * n + i] + m1 * dt) + m2 * dt2) + m3 * dt3;
+        }
+        const float u = dt / soa49[GSR_A_TSCALE * n + i];
+        out38[GSR_A_OPACITY * n + i] = soa49[GSR_A_OPACITY * n + i] * orc_expf(-(u * u));
+    }
 }
 
 /* ------------------------------------------------------------ math.cu */

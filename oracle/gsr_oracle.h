@@ -40,6 +40,10 @@ typedef struct orc_splat {
 
 /* misc.cu:13-134 restated: returns 0 ok, <0 error.  soa may be NULL to get n. */
 int orc_ply_read(const char* path, float* soa, int64_t capacity, int64_t* n_out);
+/* narrays 38 (3D) or 49 (4D arrays: trbf_center, exp(trbf_scale), motion_0..8). */
+int orc_ply_read_ex(const char* path, float* soa, int narrays, int64_t capacity, int64_t* n_out);
+/* Config 5: the 38 arrays of a 4D scene at time t, no temporal cull. */
+void orc_temporal(const float* soa49, int64_t n, float t, float* out38);
 
 /* render.cu:620-621 fx, fy. */
 void orc_intrinsics(const gsr_camera* cam, float* fx, float* fy);

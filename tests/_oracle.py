@@ -33,6 +33,10 @@ def lib():
         cam = POINTER(Camera)
         L.orc_ply_read.argtypes = [ctypes.c_char_p, c_void_p, c_int64, POINTER(c_int64)]
         L.orc_ply_read.restype = c_int
+        L.orc_ply_read_ex.argtypes = [ctypes.c_char_p, c_void_p, c_int, c_int64, POINTER(c_int64)]
+        L.orc_ply_read_ex.restype = c_int
+        L.orc_temporal.argtypes = [c_void_p, c_int64, c_float, c_void_p]
+        L.orc_temporal.restype = None
         L.orc_intrinsics.argtypes = [cam, POINTER(c_float), POINTER(c_float)]
         L.orc_preprocess.argtypes = [c_void_p, c_int64, cam, c_int, c_int, c_float, c_void_p]
         L.orc_preprocess.restype = c_int
@@ -65,6 +69,28 @@ def ply_read(path: str) -> np.ndarray:
     if rc:
         raise IOError(f"orc_ply_read({path}) = {rc}")
     return soa
+
+
+def ply_read4d(path: str) -> np.ndarray:
+    """(49, n) arrays of a 4D (config 5) .ply through the oracle's reader."""
+    n = c_int64(-1)
+    rc = lib().orc_ply_read_ex(path.encode(), None, 49, 0, ctypes.byref(n))
+    if rc:
+        raise IOError(f"orc_ply_read_ex({path}) = {rc}")
+    soa = np.zeros((49, n.value), dtype=np.float32)
+    rc = lib().orc_ply_read_ex(path.encode(), soa.ctypes.data, 49, n.value, ctypes.byref(n))
+    if rc:
+        raise IOError(f"orc_ply_read_ex({path}) = {rc}")
+    return soa
+
+
+def temporal(soa49: np.ndarray, t: float) -> np.ndarray:
+    """Config 5: the (38, n) 3D scene at time t (no temporal cull)."""
+    soa49 = np.ascontiguousarray(soa49, dtype=np.float32)
+    n = soa49.shape[1]
+    out = np.zeros((38, n), dtype=np.float32)
+    lib().orc_temporal(soa49.ctypes.data, n, float(t), out.ctypes.data)
+    return out
 
 
 def preprocess(soa: np.ndarray, cam, W: int, H: int, k: float) -> np.ndarray:

@@ -1,0 +1,156 @@
+"""Loader hardening and the config-5 4D loader.
+
+Reference mode must stay the reference's reader exactly (every property read
+as a 4-byte float, binary_little_endian only); the typed reader must decode
+ascii / big-endian / float64 / extra-element files to exactly the arrays the
+reference reader gives for the plain float32 file of the same values.  The 4D
+properties (trbf_center, trbf_scale, motion_0..8) must load identically through
+the product and through the oracle's own reader."""
+import numpy as np
+import pytest
+
+from gaussianrenderer_amd import _native
+
+BASE = ["x", "y", "z", "nx", "ny", "nz", "f_dc_0", "f_dc_1", "f_dc_2"] + [f"f_rest_{r}" for r in range(45)] + \
+       ["opacity", "scale_0", "scale_1", "scale_2", "rot_0", "rot_1", "rot_2", "rot_3"]
+
+
+def raw_values(n, seed=7):
+    rng = np.random.default_rng(seed)
+    v = rng.standard_normal((n, len(BASE))).astype(np.float32)
+    v[:, 54] = rng.uniform(-1, 3, n)          # opacity logit
+    v[:, 55:58] = rng.uniform(-5.6, -4.1, (n, 3))
+    return v
+
+
+def header(n, fmt, props, pre="", post=""):
+    h = f"ply\nformat {fmt} 1.0\n{pre}element vertex {n}\n"
+    h += "".join(f"property {t} {name}\n" for t, name in props)
+    return (h + post + "end_header\n").encode()
+
+
+def write_float_le(path, v, names=BASE):
+    path.write_bytes(header(len(v), "binary_little_endian", [("float", s) for s in names]) + v.tobytes())
+
+
+@pytest.fixture(scope="module")
+def ref_file(tmp_path_factory):
+    v = raw_values(777)
+    p = tmp_path_factory.mktemp("ply") / "ref.ply"
+    write_float_le(p, v)
+    return p, v
+
+
+def test_reference_mode_unchanged_on_float_file(gsr, ref_file):
+    p, v = ref_file
+    a = gsr.read_ply(str(p))
+    b = gsr.read_ply(str(p), typed=True)
+    assert a.shape == (38, 777)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("variant", ["ascii", "big", "double", "mixed_ints", "extra_elements", "nx"])
+def test_typed_reader_formats(gsr, ref_file, tmp_path, variant):
+    p, v = ref_file
+    want = gsr.read_ply(str(p))
+    n = len(v)
+    q = tmp_path / f"{variant}.ply"
+    if variant == "ascii":
+        body = "".join(" ".join(f"{x:.9g}" for x in row) + "\n" for row in v).encode()
+        q.write_bytes(header(n, "ascii", [("float", s) for s in BASE]) + body)
+    elif variant == "big":
+        q.write_bytes(header(n, "binary_big_endian", [("float32", s) for s in BASE]) + v.astype(">f4").tobytes())
+    elif variant == "double":
+        q.write_bytes(header(n, "binary_little_endian", [("double", s) for s in BASE]) + v.astype("<f8").tobytes())
+    elif variant == "mixed_ints":
+        # normals as int16 and an extra uchar property: unused by the render path
+        dt = [(s, "<i2") if s in ("nx", "ny", "nz") else (s, "<f4") for s in BASE] + [("flag", "u1")]
+        rec = np.zeros(n, dtype=dt)
+        for j, s in enumerate(BASE):
+            rec[s] = v[:, j] if s not in ("nx", "ny", "nz") else 3
+        props = [("short" if s in ("nx", "ny", "nz") else "float", s) for s in BASE] + [("uchar", "flag")]
+        q.write_bytes(header(n, "binary_little_endian", props) + rec.tobytes())
+    elif variant == "extra_elements":
+        # an element before the vertices and a face list after them
+        pre = "element camera 1\nproperty float fx\nproperty double fy\n"
+        post = "element face 2\nproperty list uchar int vertex_indices\n"
+        cam = np.array([1.5], "<f4").tobytes() + np.array([2.5], "<f8").tobytes()
+        faces = bytes([3]) + np.arange(3, dtype="<i4").tobytes() + bytes([4]) + np.arange(4, dtype="<i4").tobytes()
+        q.write_bytes(header(n, "binary_little_endian", [("float", s) for s in BASE], pre, post) + cam +
+                      v.tobytes() + faces)
+    else:   # "nx" spelled normally (the reference reads only "nxx"): normals are unused, arrays equal
+        q.write_bytes(header(n, "binary_little_endian", [("float", s) for s in BASE]) + v.tobytes())
+    got = gsr.read_ply(str(q), typed=True)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_reference_mode_reads_every_property_as_float(gsr, ref_file, tmp_path):
+    """misc.cu:103: the reference reads each declared property as 4 bytes whatever
+    its type, so a float64 file reads as its data block reinterpreted as float32."""
+    p, v = ref_file
+    n = len(v)
+    data = v.astype("<f8").tobytes()
+    dbl = tmp_path / "double.ply"
+    dbl.write_bytes(header(n, "binary_little_endian", [("double", s) for s in BASE]) + data)
+    as_float = tmp_path / "as_float.ply"
+    as_float.write_bytes(header(n, "binary_little_endian", [("float", s) for s in BASE]) + data[: n * 62 * 4])
+    a = gsr.read_ply(str(dbl))
+    b = gsr.read_ply(str(as_float))
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_reference_mode_rejects_ascii_typed_mode_errors(gsr, ref_file, tmp_path):
+    p, v = ref_file
+    q = tmp_path / "a.ply"
+    q.write_bytes(header(2, "ascii", [("float", "x")]) + b"1\n2\n")
+    with pytest.raises(_native.GsrError) as e:
+        gsr.read_ply(str(q))
+    assert e.value.code == _native.GSR_E_FORMAT
+    assert gsr.read_ply(str(q), typed=True)[0].tolist() == [1.0, 2.0]
+    t = tmp_path / "trunc.ply"
+    t.write_bytes(p.read_bytes()[:-100])
+    for typed in (False, True):
+        with pytest.raises(_native.GsrError) as e:
+            gsr.read_ply(str(t), typed=typed)
+        assert e.value.code == _native.GSR_E_IO
+    bad = tmp_path / "bad.ply"
+    bad.write_bytes(b"ply\nformat binary_little_endian 1.0\nelement vertex 1\nproperty quad x\nend_header\n")
+    with pytest.raises(_native.GsrError):
+        gsr.read_ply(str(bad), typed=True)
+
+
+def test_4d_loader_matches_oracle(gsr, orc, tmp_path):
+    p = tmp_path / "s4d.ply"
+    gsr.write_synthetic_ply4d(str(p), 3000, 5)
+    got = gsr.read_ply(str(p), four_d=True)
+    want = orc.ply_read4d(str(p))
+    assert got.shape == (49, 3000)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    # typed reader agrees; a 3D read of a 4D file is its first 38 arrays
+    assert np.array_equal(gsr.read_ply(str(p), typed=True, four_d=True).view(np.uint32), got.view(np.uint32))
+    assert np.array_equal(gsr.read_ply(str(p)).view(np.uint32), got[:38].view(np.uint32))
+    assert gsr.read_ply(str(p), four_d=None).shape[0] == 49
+    # temporal scale is exp()'d, centres in [0, 1], motion present
+    assert (got[39] > 0).all() and (got[38] >= 0).all() and (got[38] <= 1).all()
+    assert np.abs(got[40:49]).sum() > 0
+
+
+def test_4d_defaults_for_3d_file(gsr, ref_file):
+    p, v = ref_file
+    a = gsr.read_ply(str(p), four_d=True)
+    assert np.array_equal(a[:38].view(np.uint32), gsr.read_ply(str(p)).view(np.uint32))
+    assert (a[38] == 0).all() and (a[39] == 1).all() and (a[40:] == 0).all()
+
+
+def test_oracle_temporal_identities(gsr, orc, tmp_path):
+    p = tmp_path / "s4d.ply"
+    gsr.write_synthetic_ply4d(str(p), 500, 9)
+    s = orc.ply_read4d(str(p))
+    # at t = trbf_center of every Gaussian: positions and opacity unchanged
+    s2 = s.copy()
+    s2[38] = 0.25
+    out = orc.temporal(s2, 0.25)
+    assert np.array_equal(out[[0, 1, 2, 3]], s2[[0, 1, 2, 3]])
+    assert np.array_equal(out[4:38], s2[4:38])
+    far = orc.temporal(s, 50.0)
+    assert (far[3] < 1e-6).all()          # far from every centre: opacity ~0
