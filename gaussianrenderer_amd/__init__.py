@@ -302,6 +302,13 @@ class Renderer:
         """gsr_set_tuning: 0 blend schedule, 1 tile-sort items/thread, 2 depth-sort items/thread."""
         check(lib().gsr_set_tuning(self.ctx, int(knob), int(value)), "gsr_set_tuning")
 
+    def depth_passes(self) -> int:
+        """Depth-sort digit passes the last frame ran (trailing identities are skipped)."""
+        rc = lib().gsr_depth_passes(self.ctx)
+        if rc < 0:
+            raise GsrError(rc, "gsr_depth_passes")
+        return rc
+
     def blend_stamps(self, n_groups: int) -> np.ndarray:
         """{start, end} s_memrealtime stamps (100 MHz) per blend workgroup of the
         last diagnostics frame rendered with schedule 2."""

@@ -50,15 +50,18 @@ hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, con
 // ranges (nullable, final tile-sort pass): per-tile {~start, end} of key (item >> 32),
 // zeroed beforehand.
 // items: 8 or 16 per thread (tile = 256 * items); groups from sort_groups().
+// dstats (nullable): depth-sort pass plan, zeroed per frame; pass 0 fills it,
+// passes >= 1 skip themselves when they would be identities (gsr_kernels.hip).
 hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
                              int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
-                             uint2* ranges, hipStream_t s);
+                             uint2* ranges, hipStream_t s, uint32_t* dstats = nullptr, int pass = 0);
 // Pair emission in depth order: tile counts (gathering each Gaussian's rect
-// once into srect), scan, then keys (uint16_t if key16 else uint32_t) + values.
-hipError_t launch_emit(const uint64_t* depth_sorted, uint32_t n, const uint64_t* rect, int groups,
-                       unsigned long long* wg_scratch, Stats* stats, Stats* host_mapped_stats,
-                       uint32_t pair_capacity, int tiles_x, uint64_t* srect, void* keys, bool key16,
-                       uint32_t* vals, hipStream_t s);
+// once into srect, and zeroing the tile ranges), scan, then keys (uint16_t if
+// key16 else uint32_t) + values.
+hipError_t launch_emit(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,
+                       const uint64_t* rect, int groups, unsigned long long* wg_scratch, Stats* stats,
+                       Stats* host_mapped_stats, uint32_t pair_capacity, int tiles_x, int tiles_y, void* keys,
+                       bool key16, uint32_t* vals, uint2* ranges, hipStream_t s);
 // One stable key-value LSD pass of the tile sort; keys_out == nullptr marks the
 // final pass (values only, tile ranges recorded).
 hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* keys_out, uint32_t* vals_out,

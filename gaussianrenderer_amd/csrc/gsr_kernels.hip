@@ -67,6 +67,18 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
     return pre + x - v;
 }
 
+// Wave64-wide max / or (every lane gets the result).
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
+    return v;
+}
+
 // [begin, end) of workgroup g when n items are split over `groups` workgroups in
 // chunks that are multiples of `gran`.
 __device__ __forceinline__ void chunk_range(uint64_t n, int groups, int g, uint64_t gran,
@@ -360,20 +372,56 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
 // wave64 ballot matching (the AMD stand-in for __match_any), scatters into LDS
 // in digit order and writes runs out coalesced.
 
+// Depth-sort pass plan.  dstats (zeroed per frame, filled by pass 0's upsweep
+// over every key except 0xFFFFFFFF, which culled records carry): [0] max of ~key
+// (= ~min key), [1] max key, [2] bit p set if some key has its low 8p bits all
+// ones, [3] nonzero if any such key exists.  Pass p >= 1 is an identity (and is
+// skipped) when every key shares the digits at and above p and no key has
+// all-ones low 8p bits: the 0xFFFFFFFF keys then already trail in index order,
+// exactly where the full sort puts them.  Skippable(p) implies skippable(p+1).
+__device__ __forceinline__ bool depth_pass_skipped(const uint32_t* __restrict__ dstats, int pass) {
+    if (!dstats || pass == 0) return false;
+    if (dstats[3] == 0u) return true;
+    const uint32_t kmin = ~dstats[0], kmax = dstats[1];
+    return (kmin >> (8 * pass)) == (kmax >> (8 * pass)) && !((dstats[2] >> pass) & 1u);
+}
+
+__device__ __forceinline__ int depth_passes_run(const uint32_t* __restrict__ dstats) {
+    int p = 1;
+    while (p < 4 && !depth_pass_skipped(dstats, p)) ++p;
+    return p;
+}
+
 template <int ITEMS>
 __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* __restrict__ in,
                                                                 const uint32_t* __restrict__ n_dev,
                                                                 uint32_t n_host, int shift, uint32_t mask,
-                                                                int groups, uint32_t* __restrict__ hist) {
+                                                                int groups, uint32_t* __restrict__ hist,
+                                                                uint32_t* __restrict__ dstats, int pass) {
     __shared__ uint32_t h[4][256];
+    __shared__ uint32_t s_st[4];
+    if (depth_pass_skipped(dstats, pass)) return;
     const uint32_t t = threadIdx.x;
     const uint32_t w = t >> 6;
+    const bool plan = dstats && pass == 0;
+    uint32_t inv_min = 0, kmax = 0, lowones = 0, any = 0;
+    if (plan && t < 4) s_st[t] = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) h[k][t] = 0;
     __syncthreads();
     const uint64_t n = n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, kSortThreads * ITEMS, b, e);
+    auto note = [&](uint64_t v) {
+        const uint32_t k = (uint32_t)(v >> 32);
+        if (k != 0xffffffffu) {
+            inv_min = max(inv_min, ~k);
+            kmax = max(kmax, k);
+            any = 1u;
+            lowones |= ((k & 0xffu) == 0xffu ? 2u : 0u) | ((k & 0xffffu) == 0xffffu ? 4u : 0u) |
+                       ((k & 0xffffffu) == 0xffffffu ? 8u : 0u);
+        }
+    };
     uint64_t i = b + t;
     for (; i + 3 * kSortThreads < e; i += 4 * kSortThreads) {
         const uint64_t v0 = in[i], v1 = in[i + kSortThreads], v2 = in[i + 2 * kSortThreads],
@@ -382,16 +430,69 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
         atomicAdd(&h[w][(uint32_t)(v1 >> shift) & mask], 1u);
         atomicAdd(&h[w][(uint32_t)(v2 >> shift) & mask], 1u);
         atomicAdd(&h[w][(uint32_t)(v3 >> shift) & mask], 1u);
+        if (plan) {
+            note(v0);
+            note(v1);
+            note(v2);
+            note(v3);
+        }
     }
-    for (; i < e; i += kSortThreads) atomicAdd(&h[w][(uint32_t)(in[i] >> shift) & mask], 1u);
+    for (; i < e; i += kSortThreads) {
+        const uint64_t v = in[i];
+        atomicAdd(&h[w][(uint32_t)(v >> shift) & mask], 1u);
+        if (plan) note(v);
+    }
+    if (plan) {   // wave reductions first: one LDS atomic per wave and word
+        inv_min = wave_max_u32(inv_min);
+        kmax = wave_max_u32(kmax);
+        lowones = wave_or_u32(lowones);
+        any = wave_or_u32(any);
+        if ((t & 63u) == 0) {
+            atomicMax(&s_st[0], inv_min);
+            atomicMax(&s_st[1], kmax);
+            atomicOr(&s_st[2], lowones);
+            atomicOr(&s_st[3], any);
+        }
+    }
     __syncthreads();
     hist[t * (uint32_t)groups + blockIdx.x] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
+    // per-workgroup plan words after the 4 final ones; pass 0's scan kernel
+    // reduces them (plain stores: ~500 device atomics on 4 addresses serialise)
+    if (plan && t < 4) dstats[4 + 4 * blockIdx.x + t] = s_st[t];
 }
 
 // One workgroup per digit: exclusive scan of hist[d][0..groups) in place.
 __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist, int groups,
-                                                     uint32_t* __restrict__ totals) {
+                                                     uint32_t* __restrict__ totals,
+                                                     const uint32_t* __restrict__ dstats, int pass) {
     __shared__ uint32_t scratch[4];
+    if (dstats && pass == 0 && blockIdx.x == 0) {
+        // reduce the upsweep's per-workgroup plan words into dstats[0..3]
+        __shared__ uint32_t r[4];
+        if (threadIdx.x < 4) r[threadIdx.x] = 0;
+        __syncthreads();
+        uint32_t a = 0, b = 0, c = 0, d = 0;
+        for (int g = threadIdx.x; g < groups; g += 256) {
+            const uint32_t* q = dstats + 4 + 4 * g;
+            a = max(a, q[0]);
+            b = max(b, q[1]);
+            c |= q[2];
+            d |= q[3];
+        }
+        a = wave_max_u32(a);
+        b = wave_max_u32(b);
+        c = wave_or_u32(c);
+        d = wave_or_u32(d);
+        if ((threadIdx.x & 63u) == 0) {
+            atomicMax(&r[0], a);
+            atomicMax(&r[1], b);
+            atomicOr(&r[2], c);
+            atomicOr(&r[3], d);
+        }
+        __syncthreads();
+        if (threadIdx.x < 4) const_cast<uint32_t*>(dstats)[threadIdx.x] = r[threadIdx.x];
+    }
+    if (depth_pass_skipped(dstats, pass)) return;
     uint32_t* row = hist + (size_t)blockIdx.x * groups;
     const int per = (groups + 255) / 256;
     const int b = threadIdx.x * per;
@@ -413,9 +514,11 @@ template <int ITEMS>
 __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const uint64_t* __restrict__ in, uint64_t* __restrict__ out, const uint32_t* __restrict__ n_dev,
     uint32_t n_host, int shift, int bits, int groups, const uint32_t* __restrict__ hist,
-    const uint32_t* __restrict__ totals, uint2* __restrict__ ranges) {
+    const uint32_t* __restrict__ totals, uint2* __restrict__ ranges, const uint32_t* __restrict__ dstats,
+    int pass) {
     constexpr int kTile = kSortThreads * ITEMS;
     __shared__ uint64_t s_items[kTile];
+    if (depth_pass_skipped(dstats, pass)) return;
     __shared__ uint32_t s_wc[4][256];           // per-wave digit counters, then wave bases
     __shared__ uint32_t s_gbase[256];           // running global offset per digit
     __shared__ uint32_t s_lbase[256];           // tile-local exclusive base per digit
@@ -657,11 +760,24 @@ __global__ __launch_bounds__(kSortThreads) void k_kv_downsweep(
 // written back in depth order (srect) so k_emit_pairs reads them coalesced.
 // Each thread issues all four of its index loads, then all four rect gathers,
 // so the dependent gathers overlap instead of running back to back.
-__global__ __launch_bounds__(256) void k_emit_count(const uint64_t* __restrict__ sorted, uint32_t n,
+// The depth sort ends in items[passes run & 1] (trailing identity passes are
+// skipped on the device); the other buffer is free for srect.
+__device__ __forceinline__ const uint64_t* depth_sorted(const uint64_t* items0, const uint64_t* items1,
+                                                        const uint32_t* dstats) {
+    return (depth_passes_run(dstats) & 1) ? items1 : items0;
+}
+
+__global__ __launch_bounds__(256) void k_emit_count(const uint64_t* __restrict__ items0,
+                                                     const uint64_t* __restrict__ items1,
+                                                     const uint32_t* __restrict__ dstats, uint32_t n,
                                                      const uint64_t* __restrict__ rect, int groups,
                                                      unsigned long long* __restrict__ wg_sum,
-                                                     uint64_t* __restrict__ srect) {
+                                                     uint2* __restrict__ ranges, int ntiles) {
     __shared__ unsigned long long scr[4];
+    // zero the tile ranges for the tile sort's final pass (a slice per workgroup)
+    for (int q = blockIdx.x * 256 + threadIdx.x; q < ntiles; q += groups * 256) ranges[q] = make_uint2(0u, 0u);
+    const uint64_t* sorted = depth_sorted(items0, items1, dstats);
+    uint64_t* srect = const_cast<uint64_t*>(sorted == items0 ? items1 : items0);
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, 1024, b, e);
     unsigned long long s = 0;
@@ -690,6 +806,9 @@ __global__ __launch_bounds__(256) void k_emit_count(const uint64_t* __restrict__
     if (threadIdx.x == 0) wg_sum[blockIdx.x] = tot;
 }
 
+// Exclusive scan of the per-workgroup pair counts + the frame's pair stats.
+// (Folding it into k_emit_count's last-arriving workgroup was measured slower:
+// the agent-scope fences before each arrival ticket write back the L2 on gfx950.)
 __global__ __launch_bounds__(256) void k_emit_scan(unsigned long long* __restrict__ wg, int groups,
                                                     uint32_t cap, Stats* __restrict__ st,
                                                     Stats* host_st) {
@@ -736,14 +855,17 @@ __global__ __launch_bounds__(256) void k_emit_scan(unsigned long long* __restric
 // binary search over the round's inclusive count prefix, so every store
 // instruction writes 64 consecutive pairs.
 template <typename K>
-__global__ __launch_bounds__(256) void k_emit_pairs(const uint64_t* __restrict__ sorted, uint32_t n,
-                                                     const uint64_t* __restrict__ srect, int groups,
+__global__ __launch_bounds__(256) void k_emit_pairs(const uint64_t* __restrict__ items0,
+                                                     const uint64_t* __restrict__ items1,
+                                                     const uint32_t* __restrict__ dstats, uint32_t n, int groups,
                                                      const unsigned long long* __restrict__ wg_base,
                                                      uint32_t cap, int tiles_x, K* __restrict__ keys,
                                                      uint32_t* __restrict__ vals) {
     __shared__ unsigned long long scr[4];
     __shared__ uint32_t s_incl[4][64], s_idx[4][64];
     __shared__ uint64_t s_rect[4][64];
+    const uint64_t* sorted = depth_sorted(items0, items1, dstats);
+    const uint64_t* srect = sorted == items0 ? items1 : items0;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, 1024, b, e);
@@ -1238,38 +1360,40 @@ hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, con
 
 template <int ITEMS>
 static void radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host, int shift,
-                       int bits, int groups, uint32_t* hist, uint32_t* totals, uint2* ranges, hipStream_t s) {
+                       int bits, int groups, uint32_t* hist, uint32_t* totals, uint2* ranges, uint32_t* dstats,
+                       int pass, hipStream_t s) {
     const uint32_t mask = (1u << bits) - 1u;
     hipLaunchKernelGGL(k_radix_upsweep<ITEMS>, dim3(groups), dim3(kSortThreads), 0, s, in, n_dev, n_host, shift,
-                       mask, groups, hist);
-    hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, hist, groups, totals);
+                       mask, groups, hist, dstats, pass);
+    hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, hist, groups, totals,
+                       static_cast<const uint32_t*>(dstats), pass);
     hipLaunchKernelGGL(k_radix_downsweep<ITEMS>, dim3(groups), dim3(kSortThreads), 0, s, in, out, n_dev, n_host,
-                       shift, bits, groups, hist, totals, ranges);
+                       shift, bits, groups, hist, totals, ranges, static_cast<const uint32_t*>(dstats), pass);
 }
 
 hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
                              int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
-                             uint2* ranges, hipStream_t s) {
+                             uint2* ranges, hipStream_t s, uint32_t* dstats, int pass) {
     if (items == 8)
-        radix_pass<8>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, s);
+        radix_pass<8>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, s);
     else
-        radix_pass<16>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, s);
+        radix_pass<16>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, s);
     return hipGetLastError();
 }
 
-hipError_t launch_emit(const uint64_t* depth_sorted, uint32_t n, const uint64_t* rect, int groups,
-                       unsigned long long* wg_scratch, Stats* stats, Stats* host_mapped_stats,
-                       uint32_t pair_capacity, int tiles_x, uint64_t* srect, void* keys, bool key16,
-                       uint32_t* vals, hipStream_t s) {
-    hipLaunchKernelGGL(k_emit_count, dim3(groups), dim3(256), 0, s, depth_sorted, n, rect, groups, wg_scratch,
-                       srect);
+hipError_t launch_emit(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,
+                       const uint64_t* rect, int groups, unsigned long long* wg_scratch, Stats* stats,
+                       Stats* host_mapped_stats, uint32_t pair_capacity, int tiles_x, int tiles_y, void* keys,
+                       bool key16, uint32_t* vals, uint2* ranges, hipStream_t s) {
+    hipLaunchKernelGGL(k_emit_count, dim3(groups), dim3(256), 0, s, items0, items1, dstats, n, rect, groups,
+                       wg_scratch, ranges, tiles_x * tiles_y);
     hipLaunchKernelGGL(k_emit_scan, dim3(1), dim3(256), 0, s, wg_scratch, groups, pair_capacity, stats,
                        host_mapped_stats);
     if (key16)
-        hipLaunchKernelGGL(k_emit_pairs<uint16_t>, dim3(groups), dim3(256), 0, s, depth_sorted, n, srect, groups,
+        hipLaunchKernelGGL(k_emit_pairs<uint16_t>, dim3(groups), dim3(256), 0, s, items0, items1, dstats, n, groups,
                            wg_scratch, pair_capacity, tiles_x, static_cast<uint16_t*>(keys), vals);
     else
-        hipLaunchKernelGGL(k_emit_pairs<uint32_t>, dim3(groups), dim3(256), 0, s, depth_sorted, n, srect, groups,
+        hipLaunchKernelGGL(k_emit_pairs<uint32_t>, dim3(groups), dim3(256), 0, s, items0, items1, dstats, n, groups,
                            wg_scratch, pair_capacity, tiles_x, static_cast<uint32_t*>(keys), vals);
     return hipGetLastError();
 }
@@ -1280,7 +1404,8 @@ static void kv_pass(const K* kin, const uint32_t* vin, K* kout, uint32_t* vout, 
     const uint32_t mask = (1u << bits) - 1u;
     hipLaunchKernelGGL((k_kv_upsweep<K, ITEMS>), dim3(groups), dim3(kSortThreads), 0, s, kin, n_dev, shift, mask,
                        groups, hist);
-    hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, hist, groups, totals);
+    hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, hist, groups, totals,
+                       static_cast<const uint32_t*>(nullptr), 0);
     hipLaunchKernelGGL((k_kv_downsweep<K, ITEMS>), dim3(groups), dim3(kSortThreads), 0, s, kin, vin, kout, vout,
                        n_dev, shift, bits, groups, hist, totals, ranges);
 }

@@ -324,8 +324,10 @@ struct gsr_context {
     int depth_items = 0;             // depth sort: items per thread (0 = by size | 8 | 16)
     int tile_groups = 1024;          // tile sort: workgroup cap (measured best: 2 tiles of items per group)
     int tile_split_even = 1;         // tile sort: digits split evenly over the passes
+    int depth_skip = 1;              // depth sort: skip trailing identity passes (device-side plan)
+    uint32_t* dstats = nullptr;      // depth-sort pass plan: 4 final words + 4 per upsweep workgroup
     int depth_groups = 0;            // depth sort: workgroup cap (0 = default)
-    unsigned int* queue = nullptr;   // blend block queue (variant 1), 8 counters
+    unsigned int* queue = nullptr;   // spare device counters (blend experiments)
     int resident_groups = 2048;      // workgroups of 256 that fit on the device at once
     // frame state
     Frame fr{};
@@ -369,6 +371,7 @@ int ensure_static(gsr_context* c) {
     if (int rc = realloc_dev(&c->wg, (size_t)gsr::kMaxSortGroups)) return rc;
     if (int rc = realloc_dev(&c->stats, 2)) return rc;
     if (int rc = realloc_dev(&c->queue, 8)) return rc;
+    if (int rc = realloc_dev(&c->dstats, 4 + 4 * (size_t)gsr::kMaxSortGroups)) return rc;
     {
         int dev = 0, cus = 0;
         HIP_TRY(hipGetDevice(&dev));
@@ -511,7 +514,7 @@ extern "C" void gsr_destroy(gsr_context* c) {
     if (!c) return;
     (void)hipDeviceSynchronize();
     for (auto* p : {(void*)c->rec, (void*)c->items[0], (void*)c->items[1], (void*)c->rect, (void*)c->pairs[0],
-                    (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->queue,
+                    (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->queue, (void*)c->dstats,
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
@@ -583,21 +586,22 @@ static int sort_locked(gsr_context* c) {
     if (c->depth_groups) gd = std::min(gd, c->depth_groups);
     for (int p = 0; p < 4; p++)
         HIP_TRY(gsr::launch_radix_pass(c->items[p & 1], c->items[(p + 1) & 1], nullptr, n, 32 + 8 * p, 8, gd, di,
-                                       c->hist, c->totals, nullptr, c->stream));
-    // result in items[0]
-    // ---- pair emission in depth order (srect staged in the free items[1]) ----
+                                       c->hist, c->totals, nullptr, c->stream, c->depth_skip ? c->dstats : nullptr,
+                                       p));
+    // result in items[passes run & 1] (device-side plan; emission picks it)
+    // ---- pair emission in depth order (srect staged in the free items buffer) ----
     mark(c, GSR_STAGE_EMIT);
     const int ge = groups_for(c->n, 1024);
     const bool key16 = c->ntiles <= 65536;
-    HIP_TRY(gsr::launch_emit(c->items[0], n, c->rect, ge, c->wg, c->stats, c->hstats_dev, (uint32_t)c->p_cap,
-                             c->fr.tiles_x, c->items[1], pair_keys(c, 0), key16, pair_vals(c, 0), c->stream));
+    HIP_TRY(gsr::launch_emit(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n, c->rect, ge, c->wg,
+                             c->stats, c->hstats_dev, (uint32_t)c->p_cap, c->fr.tiles_x, c->fr.tiles_y,
+                             pair_keys(c, 0), key16, pair_vals(c, 0), c->ranges, c->stream));
     // ---- stable key-value tile sort ----
     mark(c, GSR_STAGE_TILE_SORT);
     const int tbits = std::max(1, ceil_log2(c->ntiles));
     int gp = groups_for(c->p_cap, 256 * c->tile_items);
     if (c->tile_groups) gp = std::min(gp, c->tile_groups);
     int cur = 0;
-    HIP_TRY(hipMemsetAsync(c->ranges, 0, sizeof(uint2) * (size_t)c->ntiles, c->stream));
     // digits split evenly over the passes (13 bits: 7 + 6, not 8 + 5): longer
     // digit runs per sorted tile of items, so the scattered stores coalesce better
     const int tpasses = (tbits + 7) / 8;
@@ -698,11 +702,36 @@ extern "C" int gsr_read_splats(gsr_context* c, void* host, int64_t n) {
     return GSR_OK;
 }
 
+static int depth_passes_locked(gsr_context* c, int* passes) {
+    *passes = 4;
+    if (!c->depth_skip) return GSR_OK;
+    uint32_t st[4];   // same plan as the kernels (gsr_kernels.hip depth_pass_skipped)
+    HIP_TRY(hipMemcpy(st, c->dstats, sizeof st, hipMemcpyDeviceToHost));
+    int p = 1;
+    for (; p < 4; ++p) {
+        const bool skip = st[3] == 0u || ((~st[0] >> (8 * p)) == (st[1] >> (8 * p)) && !((st[2] >> p) & 1u));
+        if (skip) break;
+    }
+    *passes = p;
+    return GSR_OK;
+}
+
+extern "C" int gsr_depth_passes(gsr_context* c) {
+    if (!c || !c->have_sort) return set_err(GSR_E_ARG, "gsr_depth_passes: no sorted frame");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    int p = 4;
+    if (int rc = depth_passes_locked(c, &p)) return rc;
+    return p;
+}
+
 extern "C" int gsr_read_depth_order(gsr_context* c, uint64_t* host, int64_t n) {
     if (!c || !host || n < 0 || n > c->n || !c->have_sort) return set_err(GSR_E_ARG, "gsr_read_depth_order: bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (n) HIP_TRY(hipMemcpy(host, c->items[0], (size_t)n * 8, hipMemcpyDeviceToHost));
+    int p = 4;
+    if (int rc = depth_passes_locked(c, &p)) return rc;
+    if (n) HIP_TRY(hipMemcpy(host, c->items[p & 1], (size_t)n * 8, hipMemcpyDeviceToHost));
     return GSR_OK;
 }
 
@@ -810,6 +839,9 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         if (value != 0 && value != 8 && value != 16)
             return set_err(GSR_E_ARG, "gsr_set_tuning: depth-sort items must be 0, 8 or 16");
         c->depth_items = value;
+        return GSR_OK;
+    case GSR_TUNE_DEPTH_SORT_SKIP:
+        c->depth_skip = value != 0;
         return GSR_OK;
     case GSR_TUNE_TILE_SORT_SPLIT:
         c->tile_split_even = value != 0;

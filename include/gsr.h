@@ -197,9 +197,13 @@ enum {
     GSR_TUNE_DEPTH_SORT_ITEMS = 2,   /* depth sort items per thread: 0 = by size | 8 | 16 */
     GSR_TUNE_TILE_SORT_GROUPS = 3,   /* tile sort workgroup cap (default 1024; 0 = one per tile of items) */
     GSR_TUNE_DEPTH_SORT_GROUPS = 4,  /* depth sort workgroup cap (0 = one per tile of items) */
-    GSR_TUNE_TILE_SORT_SPLIT = 5     /* tile sort digits: 1 = split evenly (default), 0 = 8 bits first */
+    GSR_TUNE_TILE_SORT_SPLIT = 5,    /* tile sort digits: 1 = split evenly (default), 0 = 8 bits first */
+    GSR_TUNE_DEPTH_SORT_SKIP = 6     /* depth sort: 1 = skip trailing identity passes (default), 0 = run all 4 */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
+/* Depth-sort digit passes the last sorted frame ran (1..4; trailing identity
+ * passes are skipped on the device), or a negative error code. */
+int gsr_depth_passes(gsr_context* ctx);
 /* Schedule 2 = schedule 0 with per-workgroup timestamps instead of counters:
  * with diagnostics on, the last frame's blend stores {start, end} of the
  * 100 MHz s_memrealtime clock per workgroup (launch order); read n values. */

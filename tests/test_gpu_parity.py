@@ -171,6 +171,35 @@ def test_blend_tile_schedule_parity(gpu, orc, torch, c1, ci):
         assert_image_parity(got, want)
 
 
+@pytest.mark.parametrize("pos,look", [((0, 0, 4), (0, 0, 0)), ((0, 0, 17.3), (0, 0, 0)), ((0, 0, 4), (0, 0, 9))])
+def test_depth_pass_plan_exact(gpu, orc, torch, c1, pos, look):
+    """Trailing depth-sort passes are skipped on the device when they would be
+    identities (camera at 4: keys < 2^24; at 17.3: keys straddle 2^24, no skip;
+    looking away: everything culled).  The depth order must equal the full
+    stable sort by (key, index) either way, and so must the image."""
+    path, soa = c1
+    W, H = 640, 480
+    cam = cam_for(gpu, W, H, pos=pos, look=look)
+    scene = gpu.Scene.from_soa(soa)
+    want = orc.preprocess(soa, cam, W, H, 3.0)
+    orders = []
+    for skip in (1, 0):
+        r = gpu.Renderer()
+        r.set_tuning(6, skip)
+        got, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
+        assert_image_parity(got, orc.render(soa, cam, W, H, 3.0))
+        orders.append(r.read_depth_order(soa.shape[1]))
+        keys = want["depth_key"][want["status"] == 2].astype(np.int64)
+        if not skip:
+            assert r.depth_passes() == 4
+        elif keys.size == 0:
+            assert r.depth_passes() == 1
+        else:
+            assert r.depth_passes() == (3 if keys.max() < (1 << 24) else 4)
+    assert np.array_equal(orders[0], orc.expected_depth_order(want))
+    assert np.array_equal(orders[0], orders[1])
+
+
 def test_dropin_scene_block_reference_tiling(gpu, orc, torch, c1):
     """loadGaussianCudaFromPly + preprocessCUDAGaussians (the viewer's calls),
     reference 50x50 tiling (cull_sort_test.cpp:44-45)."""
