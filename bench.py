@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-oracle sample length")
     ap.add_argument("--scene-dir", default=None)
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="N>1: nccl (= RCCL over xGMI, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--gather", choices=("step", "end", "none"), default="step",
                     help="N>1: RCCL gather of finished frames to rank 0 every step (overlapped) or once at the end")
     return ap.parse_args()
@@ -159,11 +161,15 @@ def main():
     from gaussianrenderer_amd import multi
     info = multi.rank_info()
     rank, world, local_rank = info.rank, info.world, info.local_rank
-    torch.cuda.set_device(local_rank)
+    device = local_rank % max(1, torch.cuda.device_count())   # == local_rank on a full node
+    torch.cuda.set_device(device)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
     import gaussianrenderer_amd as gsr
 
     n, W, H, seed = CONFIGS[args.config]
@@ -183,8 +189,9 @@ def main():
     r = gsr.Renderer()
     nbuf = 2 if (dist and args.gather == "step") else 1
     outs = [torch.empty(3 * W * H, dtype=torch.float32, device="cuda") for _ in range(nbuf)]
-    recv = ([[torch.empty_like(outs[0]) for _ in range(world)] for _ in range(nbuf)]
-            if (dist and rank == 0 and args.gather == "step") else None)
+    gloo = dist is not None and args.dist_backend == "gloo"
+    recv = ([[torch.empty_like(outs[0], device="cpu" if gloo else outs[0].device) for _ in range(world)]
+             for _ in range(nbuf)] if (dist and rank == 0 and args.gather == "step") else None)
     stream = torch.cuda.current_stream().cuda_stream
     pending = [None] * nbuf
 
@@ -196,7 +203,9 @@ def main():
         r.render(scene, cam, W, H, outs[b].data_ptr(), k=args.k, stream=stream,
                  time=frame_time(i) if four_d else None)
         if dist and args.gather == "step":
-            pending[b] = dist.gather(outs[b], recv[b] if recv else None, dst=0, async_op=True)
+            # gloo rehearsal: host copies, synchronous; nccl (RCCL): device buffers, overlapped
+            src = outs[b].cpu() if gloo else outs[b]
+            pending[b] = dist.gather(src, recv[b] if recv else None, dst=0, async_op=not gloo)
 
     # warmup (+ grow the pair buffer to the high-water mark)
     for i in range(max(1, args.warmup)):
@@ -245,12 +254,12 @@ def main():
     r.set_timing(0)
     overflow = r.sync()
 
-    max_elapsed = multi.max_over_ranks(dist, elapsed, "cuda")
+    max_elapsed = multi.max_over_ranks(dist, elapsed, "cpu" if gloo else "cuda")
     gather_ms = None
     if dist and args.gather == "end":
         torch.cuda.synchronize()
         g0 = time.perf_counter()
-        multi.gather_frames(dist, outs[0])
+        multi.gather_frames(dist, outs[0].cpu() if gloo else outs[0])
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) * 1e3
 
@@ -284,7 +293,8 @@ def main():
         "config": {"workload": f"config{args.config}: {n} {'4D ' if four_d else ''}Gaussians, {W}x{H}, k={args.k}, "
                                + (f"frame i at t = (i mod {TIMESTEPS_4D})/{TIMESTEPS_4D - 1} with temporal cull, "
                                   if four_d else "")
-                               + (f"one orbit camera per GPU, RCCL gather to rank 0 ({args.gather})" if world > 1
+                               + (f"one orbit camera per GPU, {'RCCL' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'} "
+                                  f"gather to rank 0 ({args.gather})" if world > 1
                                   else "camera (0,0,4) fovY 50"),
                    "gaussians": n, "width": W, "height": H, "parallelism": f"frames{world}"},
         "roofline": {"bound": "hbm", "kernel": BLEND_KERNEL, "achieved": round(achieved, 2),
