@@ -19,8 +19,9 @@ from ctypes import byref, c_float, c_int, c_int64
 import numpy as np
 
 from . import _native
-from ._native import (Camera, GsrError, LAYOUT_AOS, LAYOUT_SCENE_BLOCK, LAYOUT_SCENE_BLOCK_4D, NUM_STAGES,
-                      PLY_TYPED, SCENE4D_NARRAYS, SCENE_NARRAYS,
+from ._native import (Camera, GsrError, LAYOUT_AOS, LAYOUT_SCENE_BLOCK, LAYOUT_SCENE_BLOCK_4D,
+                      LAYOUT_SCENE_BLOCK_SH3, NUM_STAGES, PLY_SH3, PLY_TYPED, SCENE4D_NARRAYS, SCENE_NARRAYS,
+                      SCENE_SH3_NARRAYS,
                       SPLAT_RECORD_BYTES, STAGES, TILE_PX, check, lib)
 
 __all__ = [
@@ -81,17 +82,20 @@ def camera_intrinsics(cam: Camera):
     return fx.value, fy.value
 
 
-def read_ply(path: str, typed: bool = False, four_d: bool | None = False) -> np.ndarray:
+def read_ply(path: str, typed: bool = False, four_d: bool | None = False, sh3: bool = False) -> np.ndarray:
     """Host PLY parse -> (38, n) float32 SoA (reference loader semantics), or the
     hardened typed reader (typed=True: declared types, ascii, big-endian).
-    four_d=True returns the (49, n) 4D arrays; four_d=None picks by the file."""
+    four_d=True returns the (49, n) 4D arrays; four_d=None picks by the file;
+    sh3=True the (59, n) "Inria-correct" degree-3 SH arrays."""
     L = lib()
     n = c_int64(-1)
     is4d = c_int(0)
-    flags = PLY_TYPED if typed else 0
-    check(L.gsr_ply_read_host_ex(path.encode(), None, SCENE_NARRAYS, 0, byref(n), flags, byref(is4d)),
-          "gsr_ply_read_host")
+    flags = (PLY_TYPED if typed else 0) | (PLY_SH3 if sh3 else 0)
+    check(L.gsr_ply_read_host_ex(path.encode(), None, SCENE_SH3_NARRAYS if sh3 else SCENE_NARRAYS, 0, byref(n),
+                                 flags, byref(is4d)), "gsr_ply_read_host")
     na = SCENE4D_NARRAYS if (four_d or (four_d is None and is4d.value)) else SCENE_NARRAYS
+    if sh3:
+        na = SCENE_SH3_NARRAYS
     soa = np.zeros((na, n.value), dtype=np.float32)
     check(L.gsr_ply_read_host_ex(path.encode(), soa.ctypes.data, na, n.value, byref(n), flags, None),
           "gsr_ply_read_host")
@@ -119,29 +123,36 @@ class Scene:
         return self.narrays == SCENE4D_NARRAYS
 
     @property
+    def is_sh3(self) -> bool:
+        return self.narrays == SCENE_SH3_NARRAYS
+
+    @property
     def layout(self) -> int:
-        return LAYOUT_SCENE_BLOCK_4D if self.is_4d else LAYOUT_SCENE_BLOCK
+        return (LAYOUT_SCENE_BLOCK_4D if self.is_4d else LAYOUT_SCENE_BLOCK_SH3 if self.is_sh3
+                else LAYOUT_SCENE_BLOCK)
 
     @classmethod
     def from_soa(cls, soa: np.ndarray) -> "Scene":
         soa = np.ascontiguousarray(soa, dtype=np.float32)
-        assert soa.shape[0] in (SCENE_NARRAYS, SCENE4D_NARRAYS)
+        assert soa.shape[0] in (SCENE_NARRAYS, SCENE4D_NARRAYS, SCENE_SH3_NARRAYS)
         ptr = lib().gsr_scene_upload_ex(soa.ctypes.data, soa.shape[0], soa.shape[1])
         if not ptr:
             raise GsrError(-2, "gsr_scene_upload")
         return cls(ptr, soa.shape[1], narrays=soa.shape[0])
 
     @classmethod
-    def from_ply(cls, path: str, typed: bool = False, allow_4d: bool = True) -> "Scene":
+    def from_ply(cls, path: str, typed: bool = False, allow_4d: bool = True, sh3: bool = False) -> "Scene":
         """Device scene from a .ply (the reference loader unless typed=True); a file
-        with the 4D properties loads as a 4D scene when allow_4d."""
+        with the 4D properties loads as a 4D scene when allow_4d; sh3=True gives
+        the "Inria-correct" degree-3 SH scene."""
         n = c_int(0)
         na = c_int(SCENE_NARRAYS)
-        ptr = lib().gsr_load_ply_device_ex(path.encode(), byref(n), PLY_TYPED if typed else 0,
-                                           byref(na) if allow_4d else None)
+        flags = (PLY_TYPED if typed else 0) | (PLY_SH3 if sh3 else 0)
+        ptr = lib().gsr_load_ply_device_ex(path.encode(), byref(n), flags,
+                                           byref(na) if (allow_4d or sh3) else None)
         if not ptr:
             raise GsrError(-3, f"loadGaussianCudaFromPly({path}): {lib().gsr_last_error().decode()}")
-        return cls(ptr, n.value, narrays=na.value if allow_4d else SCENE_NARRAYS)
+        return cls(ptr, n.value, narrays=na.value if (allow_4d or sh3) else SCENE_NARRAYS)
 
     def download(self) -> np.ndarray:
         soa = np.zeros((self.narrays, self.n), dtype=np.float32)
@@ -207,8 +218,8 @@ class Renderer:
         pair buffer (it has been grown; that frame must be re-rendered)."""
         ptr = scene.ptr if isinstance(scene, Scene) else int(scene)
         n = scene.n if n is None else n
-        if isinstance(scene, Scene) and scene.is_4d and layout == LAYOUT_SCENE_BLOCK:
-            layout = LAYOUT_SCENE_BLOCK_4D
+        if isinstance(scene, Scene) and layout == LAYOUT_SCENE_BLOCK:
+            layout = scene.layout
         if time is not None:
             self.set_time(time)
         t = tiling or TilingInformation(1, 1, H, W)
@@ -225,8 +236,8 @@ class Renderer:
                    layout: int = LAYOUT_SCENE_BLOCK, n: int | None = None, time: float | None = None):
         ptr = scene.ptr if isinstance(scene, Scene) else int(scene)
         n = scene.n if n is None else n
-        if isinstance(scene, Scene) and scene.is_4d and layout == LAYOUT_SCENE_BLOCK:
-            layout = LAYOUT_SCENE_BLOCK_4D
+        if isinstance(scene, Scene) and layout == LAYOUT_SCENE_BLOCK:
+            layout = scene.layout
         if time is not None:
             self.set_time(time)
         t = tiling or TilingInformation(1, 1, H, W)

@@ -28,7 +28,9 @@ GSR_E_OVERFLOW = -5
 LAYOUT_SCENE_BLOCK = 0
 LAYOUT_AOS = 1
 LAYOUT_SCENE_BLOCK_4D = 2
+LAYOUT_SCENE_BLOCK_SH3 = 3
 PLY_TYPED = 1
+PLY_SH3 = 2
 
 STAGES = ("preprocess", "depth_sort", "emit", "tile_sort", "ranges", "blend")
 NUM_STAGES = len(STAGES)
@@ -36,6 +38,7 @@ TILE_PX = 16
 SPLAT_RECORD_BYTES = 64
 SCENE_NARRAYS = 38
 SCENE4D_NARRAYS = 49
+SCENE_SH3_NARRAYS = 59
 
 
 class Camera(ctypes.Structure):

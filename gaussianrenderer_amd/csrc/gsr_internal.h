@@ -44,7 +44,8 @@ struct Stats {
 hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, int64_t stride,
                              hipStream_t s);
 hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
-                             uint4* rec, uint64_t* items, uint64_t* rect, bool four_d, float t, hipStream_t s);
+                             uint4* rec, uint64_t* items, uint64_t* rect, bool four_d, bool sh3, float t,
+                             hipStream_t s);
 // One stable LSD pass over u64 items on bits [shift, shift + bits) (bits <= 8).
 // n = n_dev ? *n_dev : n_host.  hist: 256 * groups u32, totals: 256 u32.
 // ranges (nullable, final tile-sort pass): per-tile {~start, end} of key (item >> 32),

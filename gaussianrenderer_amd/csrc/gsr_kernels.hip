@@ -170,7 +170,7 @@ __device__ __forceinline__ uint32_t rect_count(uint64_t r) {
 // this exact operation order (the oracle restates it, oracle/gsr_oracle.c):
 // dt = t - c; x_t = ((x + m0 dt) + m3 dt^2) + m6 dt^3 (dt^2 = dt dt, dt^3 =
 // dt^2 dt; y, z with m1/m4/m7, m2/m5/m8); temporal factor exp(-(dt/s)^2).
-template <bool T4D>
+template <bool T4D, bool SH3>
 __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ arr, int64_t stride,
                                                     int64_t n, Frame fr, uint4* __restrict__ rec,
                                                     uint64_t* __restrict__ items, uint64_t* __restrict__ rect,
@@ -337,20 +337,43 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     const float C2_0 = 1.0925484305920792f, C2_1 = -1.0925484305920792f, C2_2 = 0.31539156525252005f,
                 C2_3 = -1.0925484305920792f, C2_4 = 0.5462742152960396f;
     float col[3];
+    if (!SH3) {
 #pragma unroll
-    for (int ch = 0; ch < 3; ch++) {
-        const float* sh = arr + (GSR_A_SH0 + ch) * stride + i;   // sh[ch], sh[3+ch], ...
-        float cc = sh[0] * kShC0;
-        cc += kShC1 * z * sh[6 * stride];
-        cc -= kShC1 * y * sh[3 * stride];
-        cc -= kShC1 * x * sh[9 * stride];
-        cc += C2_0 * xy * sh[12 * stride];
-        cc += C2_1 * yz * sh[15 * stride];
-        cc += C2_2 * (2.0f * zz - xx - yy) * sh[18 * stride];
-        cc += C2_3 * xz * sh[21 * stride];
-        cc += C2_4 * (xx - yy) * sh[24 * stride];
-        cc += 0.5f;
-        col[ch] = fminf(fmaxf(cc, 0.0f), 1.0f);
+        for (int ch = 0; ch < 3; ch++) {
+            const float* sh = arr + (GSR_A_SH0 + ch) * stride + i;   // sh[ch], sh[3+ch], ...
+            float cc = sh[0] * kShC0;
+            cc += kShC1 * z * sh[6 * stride];
+            cc -= kShC1 * y * sh[3 * stride];
+            cc -= kShC1 * x * sh[9 * stride];
+            cc += C2_0 * xy * sh[12 * stride];
+            cc += C2_1 * yz * sh[15 * stride];
+            cc += C2_2 * (2.0f * zz - xx - yy) * sh[18 * stride];
+            cc += C2_3 * xz * sh[21 * stride];
+            cc += C2_4 * (xx - yy) * sh[24 * stride];
+            cc += 0.5f;
+            col[ch] = fminf(fmaxf(cc, 0.0f), 1.0f);
+        }
+    } else {
+        // "Inria-correct" mode: degree-3 SH as the 3DGS training code evaluates it
+        // (left-to-right, bands 0..3), + 0.5, clamped at 0 only
+        const float C3_0 = -0.5900435899266435f, C3_1 = 2.890611442640554f, C3_2 = -0.4570457994644658f,
+                    C3_3 = 0.3731763325901154f, C3_4 = -0.4570457994644658f, C3_5 = 1.445305721320277f,
+                    C3_6 = -0.5900435899266435f;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) {
+            const float* sh = arr + (GSR_A_SH0 + ch) * stride + i;   // coefficient k at sh[3k * stride]
+            auto S = [&](int k) { return sh[3 * k * stride]; };
+            float r = kShC0 * S(0);
+            r = r - kShC1 * y * S(1) + kShC1 * z * S(2) - kShC1 * x * S(3);
+            r = r + C2_0 * xy * S(4) + C2_1 * yz * S(5) + C2_2 * (2.0f * zz - xx - yy) * S(6) +
+                C2_3 * xz * S(7) + C2_4 * (xx - yy) * S(8);
+            r = r + C3_0 * y * (3.0f * xx - yy) * S(9) + C3_1 * xy * z * S(10) +
+                C3_2 * y * (4.0f * zz - xx - yy) * S(11) + C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * S(12) +
+                C3_4 * x * (4.0f * zz - xx - yy) * S(13) + C3_5 * z * (xx - yy) * S(14) +
+                C3_6 * x * (xx - 3.0f * yy) * S(15);
+            r += 0.5f;
+            col[ch] = fmaxf(r, 0.0f);
+        }
     }
     const float opacity = T4D ? arr[GSR_A_OPACITY * stride + i] * tfac : arr[GSR_A_OPACITY * stride + i];
 
@@ -1347,14 +1370,17 @@ hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, 
 }
 
 hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
-                             uint4* rec, uint64_t* items, uint64_t* rect, bool four_d, float t, hipStream_t s) {
+                             uint4* rec, uint64_t* items, uint64_t* rect, bool four_d, bool sh3, float t,
+                             hipStream_t s) {
     if (n <= 0) return hipSuccess;
+    const dim3 g(grid_for(n, 256));
     if (four_d)
-        hipLaunchKernelGGL(k_preprocess<true>, dim3(grid_for(n, 256)), dim3(256), 0, s, arrays, stride, n, fr, rec,
-                           items, rect, t);
+        hipLaunchKernelGGL((k_preprocess<true, false>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect, t);
+    else if (sh3)
+        hipLaunchKernelGGL((k_preprocess<false, true>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect, t);
     else
-        hipLaunchKernelGGL(k_preprocess<false>, dim3(grid_for(n, 256)), dim3(256), 0, s, arrays, stride, n, fr,
-                           rec, items, rect, t);
+        hipLaunchKernelGGL((k_preprocess<false, false>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect,
+                           t);
     return hipGetLastError();
 }
 

@@ -15,7 +15,8 @@
 //     vertex element skipped properly (list properties included), "nx" or "nxx".
 // Both map the same names to the same arrays and apply the same activations,
 // plus the Spacetime-Gaussian 4D properties (trbf_center, trbf_scale,
-// motion_0..8) into arrays 38..48 when the caller asks for 49 arrays.
+// motion_0..8) into arrays 38..48 when the caller asks for 49 arrays, and
+// (GSR_PLY_SH3, 59 arrays) all 45 f_rest mapped channel-major -> sh[3k + c].
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -82,7 +83,7 @@ int type_size(Type t) {
 
 // Name -> (slot, index); the reference's map (misc.cu:60-90) plus "nx" in typed
 // mode and the 4D names.
-Prop slot_for(const std::string& name, bool typed) {
+Prop slot_for(const std::string& name, bool typed, bool sh3) {
     Prop p;
     if (name == "x") p.slot = S_X;
     else if (name == "y") p.slot = S_Y;
@@ -95,7 +96,7 @@ Prop slot_for(const std::string& name, bool typed) {
     else if (name == "f_dc_2") p.slot = S_DC, p.index = 2;
     else if (name.rfind("f_rest_", 0) == 0) {
         const int idx = std::atoi(name.c_str() + 7);
-        if (idx >= 0 && idx < 24) p.slot = S_REST, p.index = idx;   // misc.cu:76
+        if (idx >= 0 && idx < (sh3 ? 45 : 24)) p.slot = S_REST, p.index = idx;   // misc.cu:76 (24)
     } else if (name == "opacity") p.slot = S_OPACITY;
     else if (name.rfind("scale_", 0) == 0) {
         const int idx = std::atoi(name.c_str() + 6);
@@ -116,7 +117,7 @@ bool starts(const std::string& s, const char* pre) { return s.compare(0, std::st
 
 // misc.cu:21-58 as written: first "format ", first "element vertex ", then every
 // "property" line until end_header.
-int parse_header_reference(std::ifstream& file, PlyHeader& h) {
+int parse_header_reference(std::ifstream& file, PlyHeader& h, bool sh3) {
     std::string line;
     while (std::getline(file, line))
         if (starts(line, "format ")) {
@@ -142,14 +143,14 @@ int parse_header_reference(std::ifstream& file, PlyHeader& h) {
         std::istringstream iss(line.substr(9));
         std::string type, name;
         iss >> type >> name;
-        h.props.push_back(slot_for(name, false));     // type ignored: read as float (misc.cu:103)
+        h.props.push_back(slot_for(name, false, sh3));   // type ignored: read as float (misc.cu:103)
     }
     if (h.format != "binary_little_endian 1.0")
         return set_error(GSR_E_FORMAT, "Unsupported PLY format: %s", h.format.c_str());
     return GSR_OK;
 }
 
-int parse_header_typed(std::ifstream& file, PlyHeader& h) {
+int parse_header_typed(std::ifstream& file, PlyHeader& h, bool sh3) {
     std::string line;
     if (!std::getline(file, line) || line.compare(0, 3, "ply") != 0) return set_error(GSR_E_FORMAT, "PLY: missing magic");
     bool done = false;
@@ -185,7 +186,7 @@ int parse_header_typed(std::ifstream& file, PlyHeader& h) {
                 iss >> name;
                 p.type = parse_type(t1);
                 if (p.type == T_BAD) return set_error(GSR_E_FORMAT, "PLY: bad property type '%s'", t1.c_str());
-                const Prop s = slot_for(name, true);
+                const Prop s = slot_for(name, true, sh3);
                 p.slot = s.slot;
                 p.index = s.index;
             }
@@ -217,13 +218,20 @@ inline void store(const Prop& p, float* soa, int narrays, int64_t n, int64_t i, 
     case S_Y: soa[GSR_A_Y * n + i] = v; break;
     case S_Z: soa[GSR_A_Z * n + i] = v; break;
     case S_DC: soa[(GSR_A_SH0 + p.index) * n + i] = v; break;
-    case S_REST: soa[(GSR_A_SH0 + 3 + p.index) * n + i] = v; break;
+    case S_REST:
+        if (narrays == GSR_SCENE_SH3_NARRAYS)   // channel-major f_rest -> coefficient-major sh[3k + c]
+            soa[(GSR_A_SH0 + 3 * (1 + p.index % 15) + p.index / 15) * n + i] = v;
+        else
+            soa[(GSR_A_SH0 + 3 + p.index) * n + i] = v;
+        break;
     case S_OPACITY: soa[GSR_A_OPACITY * n + i] = 1.0f / (1.0f + std::exp(-v)); break;   // sigmoid<float>
     case S_SCALE: soa[(GSR_A_SCALE0 + p.index) * n + i] = (float)::exp((double)v); break; // ::exp(double)
     case S_ROT: soa[(GSR_A_ROT0 + p.index) * n + i] = v; break;
-    case S_TCENTER: if (narrays > GSR_A_TCENTER) soa[GSR_A_TCENTER * n + i] = v; break;
-    case S_TSCALE: if (narrays > GSR_A_TSCALE) soa[GSR_A_TSCALE * n + i] = (float)::exp((double)v); break;
-    case S_MOTION: if (narrays > GSR_A_MOTION0 + p.index) soa[(GSR_A_MOTION0 + p.index) * n + i] = v; break;
+    case S_TCENTER: if (narrays == GSR_SCENE4D_NARRAYS) soa[GSR_A_TCENTER * n + i] = v; break;
+    case S_TSCALE:
+        if (narrays == GSR_SCENE4D_NARRAYS) soa[GSR_A_TSCALE * n + i] = (float)::exp((double)v);
+        break;
+    case S_MOTION: if (narrays == GSR_SCENE4D_NARRAYS) soa[(GSR_A_MOTION0 + p.index) * n + i] = v; break;
     default: break;   // normals and skipped properties are not used by the render path
     }
 }
@@ -358,20 +366,21 @@ int read_typed(std::ifstream& file, const PlyHeader& h, float* soa, int narrays,
 extern "C" int gsr_ply_read_host_ex(const char* path, float* soa, int narrays, int64_t capacity, int64_t* n_out,
                                     int flags, int* is_4d) {
     if (!path || !n_out) return set_error(GSR_E_ARG, "gsr_ply_read_host: null argument");
-    if (narrays != GSR_SCENE_NARRAYS && narrays != GSR_SCENE4D_NARRAYS)
-        return set_error(GSR_E_ARG, "gsr_ply_read_host: narrays must be %d or %d", GSR_SCENE_NARRAYS,
-                         GSR_SCENE4D_NARRAYS);
+    const bool sh3 = (flags & GSR_PLY_SH3) != 0;
+    if (sh3 ? narrays != GSR_SCENE_SH3_NARRAYS : (narrays != GSR_SCENE_NARRAYS && narrays != GSR_SCENE4D_NARRAYS))
+        return set_error(GSR_E_ARG, "gsr_ply_read_host: narrays must be %d or %d (%d with GSR_PLY_SH3)",
+                         GSR_SCENE_NARRAYS, GSR_SCENE4D_NARRAYS, GSR_SCENE_SH3_NARRAYS);
     std::ifstream file(path, std::ios::binary);
     if (!file.is_open()) return set_error(GSR_E_IO, "Failed to open file: %s", path);
     PlyHeader h;
     const bool typed = (flags & GSR_PLY_TYPED) != 0;
-    int rc = typed ? parse_header_typed(file, h) : parse_header_reference(file, h);
+    int rc = typed ? parse_header_typed(file, h, sh3) : parse_header_reference(file, h, sh3);
     if (h.n >= 0) *n_out = h.n;
     if (rc) return rc;
     if (is_4d) *is_4d = has_4d(typed ? h.elements[h.vertex_element].props : h.props) ? 1 : 0;
     if (!soa || capacity < h.n) return GSR_OK;
     std::fill(soa, soa + (size_t)narrays * (size_t)h.n, 0.0f);   // Gaussian g{} (misc.cu:97)
-    if (narrays > GSR_A_TSCALE)   // 4D defaults: static Gaussian (centre 0, scale 1, no motion)
+    if (narrays == GSR_SCENE4D_NARRAYS)   // 4D defaults: static Gaussian (centre 0, scale 1, no motion)
         std::fill(soa + (size_t)GSR_A_TSCALE * (size_t)h.n, soa + (size_t)(GSR_A_TSCALE + 1) * (size_t)h.n, 1.0f);
     return typed ? read_typed(file, h, soa, narrays, path) : read_reference(file, h, soa, narrays, path);
 }

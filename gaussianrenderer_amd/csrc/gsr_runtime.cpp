@@ -207,7 +207,7 @@ static int64_t scene_stride(int64_t n) { return (n + 63) / 64 * 64; }
 
 extern "C" void* gsr_scene_upload_ex(const float* host_soa, int narrays, int64_t n) {
     if (n < 0 || n > INT32_MAX || (n > 0 && !host_soa) ||
-        (narrays != GSR_SCENE_NARRAYS && narrays != GSR_SCENE4D_NARRAYS)) {
+        (narrays != GSR_SCENE_NARRAYS && narrays != GSR_SCENE4D_NARRAYS && narrays != GSR_SCENE_SH3_NARRAYS)) {
         set_err(GSR_E_ARG, "gsr_scene_upload: bad argument");
         return nullptr;
     }
@@ -252,7 +252,8 @@ extern "C" int gsr_scene_download(const void* d, float* host_soa, int64_t n) {
     if (!d || !host_soa || n < 0) return set_err(GSR_E_ARG, "gsr_scene_download: bad argument");
     gsr_scene_header h{};
     HIP_TRY(hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost));
-    const int narrays = h.narrays == GSR_SCENE4D_NARRAYS ? GSR_SCENE4D_NARRAYS : GSR_SCENE_NARRAYS;
+    const int narrays = (h.narrays == GSR_SCENE4D_NARRAYS || h.narrays == GSR_SCENE_SH3_NARRAYS)
+                            ? (int)h.narrays : GSR_SCENE_NARRAYS;
     const int64_t stride = scene_stride(n);
     const float* arr = reinterpret_cast<const float*>(static_cast<const char*>(d) + GSR_SCENE_HEADER_BYTES);
     if (n == 0) return GSR_OK;
@@ -264,13 +265,16 @@ extern "C" int gsr_scene_download(const void* d, float* host_soa, int64_t n) {
 extern "C" gsr_gaussian* gsr_load_ply_device_ex(const char* filename, int* out_n, int flags, int* out_narrays) {
     int64_t n = -1;
     int is4d = 0;
-    int rc = gsr_ply_read_host_ex(filename, nullptr, GSR_SCENE_NARRAYS, 0, &n, flags, &is4d);
+    int rc = gsr_ply_read_host_ex(filename, nullptr,
+                                  (flags & GSR_PLY_SH3) ? GSR_SCENE_SH3_NARRAYS : GSR_SCENE_NARRAYS, 0, &n, flags,
+                                  &is4d);
     if (n >= 0 && out_n) *out_n = (int)n;   // misc.cu:38 sets the count before reading data
     if (rc) {
         std::fprintf(stderr, "%s\n", g_err.c_str());
         return nullptr;
     }
-    const int narrays = (is4d && out_narrays) ? GSR_SCENE4D_NARRAYS : GSR_SCENE_NARRAYS;
+    int narrays = (is4d && out_narrays) ? GSR_SCENE4D_NARRAYS : GSR_SCENE_NARRAYS;
+    if (flags & GSR_PLY_SH3) narrays = GSR_SCENE_SH3_NARRAYS;   // 3D only (4D properties ignored)
     std::vector<float> soa((size_t)narrays * (size_t)n);
     rc = gsr_ply_read_host_ex(filename, soa.data(), narrays, n, &n, flags, nullptr);
     if (rc) {
@@ -538,7 +542,8 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
                              int W, int H, int nx, int ny, int ws, int hs, float k, void* stream) {
     if (n < 0 || n > INT32_MAX) return set_err(GSR_E_ARG, "Gaussian count %lld out of range", (long long)n);
     if (n > 0 && !scene) return set_err(GSR_E_ARG, "null scene");
-    if (layout != GSR_LAYOUT_SCENE_BLOCK && layout != GSR_LAYOUT_AOS && layout != GSR_LAYOUT_SCENE_BLOCK_4D)
+    if (layout != GSR_LAYOUT_SCENE_BLOCK && layout != GSR_LAYOUT_AOS && layout != GSR_LAYOUT_SCENE_BLOCK_4D &&
+        layout != GSR_LAYOUT_SCENE_BLOCK_SH3)
         return set_err(GSR_E_ARG, "unknown scene layout %d", layout);
     if (int rc = fill_frame(c, cam, W, H, nx, ny, ws, hs, k)) return rc;
     if (int rc = ensure_static(c)) return rc;
@@ -564,7 +569,8 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
         arrays = reinterpret_cast<const float*>(static_cast<const char*>(scene) + GSR_SCENE_HEADER_BYTES);
     }
     HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[0], c->rect,
-                                   layout == GSR_LAYOUT_SCENE_BLOCK_4D, c->time, c->stream));
+                                   layout == GSR_LAYOUT_SCENE_BLOCK_4D, layout == GSR_LAYOUT_SCENE_BLOCK_SH3, c->time,
+                                   c->stream));
     c->have_pre = true;
     c->have_sort = false;
     return rc_over;
@@ -940,7 +946,9 @@ extern "C" void preprocessCUDAGaussians(gsr_gaussian* d_gaussians, float* out_pi
             h.magic[3] == GSR_SCENE_MAGIC3) {
             // 4D blocks render at the drop-in context's time (gsr_set_time on it is not
             // reachable through this ABI, so t = 0: the sequence's first frame)
-            layout = h.narrays == GSR_SCENE4D_NARRAYS ? GSR_LAYOUT_SCENE_BLOCK_4D : GSR_LAYOUT_SCENE_BLOCK;
+            layout = h.narrays == GSR_SCENE4D_NARRAYS    ? GSR_LAYOUT_SCENE_BLOCK_4D
+                     : h.narrays == GSR_SCENE_SH3_NARRAYS ? GSR_LAYOUT_SCENE_BLOCK_SH3
+                                                         : GSR_LAYOUT_SCENE_BLOCK;
             if ((int64_t)h.count != num_gaussians) {
                 set_err(GSR_E_ARG, "num_gaussians %d != scene block count %llu", num_gaussians,
                         (unsigned long long)h.count);

@@ -49,14 +49,17 @@ enum {
 enum {
     GSR_LAYOUT_SCENE_BLOCK = 0,   /* our SoA block (gsr_scene_header + arrays) */
     GSR_LAYOUT_AOS = 1,           /* reference Gaussian[] (240 B records) */
-    GSR_LAYOUT_SCENE_BLOCK_4D = 2 /* 4D SoA block (GSR_SCENE4D_NARRAYS), rendered at gsr_set_time() */
+    GSR_LAYOUT_SCENE_BLOCK_4D = 2, /* 4D SoA block (GSR_SCENE4D_NARRAYS), rendered at gsr_set_time() */
+    GSR_LAYOUT_SCENE_BLOCK_SH3 = 3 /* SH-3 block (GSR_SCENE_SH3_NARRAYS): degree-3 colour, clamped at 0 */
 };
 
 /* PLY loading flags (gsr_ply_read_host_ex / gsr_load_ply_device_ex). */
 enum {
-    GSR_PLY_TYPED = 1   /* hardened reader: declared property types, ascii and big-endian
+    GSR_PLY_TYPED = 1,  /* hardened reader: declared property types, ascii and big-endian
                            formats, other elements skipped, "nx" accepted.
                            Off = the reference's reader exactly (every property a 4-B float). */
+    GSR_PLY_SH3 = 2     /* "Inria-correct" SH: all 45 f_rest, channel-major, into a 59-array
+                           block rendered with degree-3 SH (off = the reference's 24 f_rest) */
 };
 
 /* Stage indices for gsr_stage_times(). */
@@ -92,9 +95,10 @@ void preprocessCUDAGaussians(gsr_gaussian* d_gaussians, float* out_pixels, int n
  * returns a device scene block (free with hipFree or gsr_scene_free), or
  * NULL on failure; *out_numGaussians is set once the header is parsed. */
 gsr_gaussian* gsr_load_ply_device(const char* filename, int* out_numGaussians);
-/* Same with loader flags (GSR_PLY_TYPED).  If out_narrays is non-NULL, a file
- * carrying the 4D properties (trbf_center, trbf_scale, motion_0..8) loads as a
- * 4D scene block and *out_narrays = GSR_SCENE4D_NARRAYS (else 38). */
+/* Same with loader flags (GSR_PLY_TYPED | GSR_PLY_SH3).  If out_narrays is
+ * non-NULL, a file carrying the 4D properties (trbf_center, trbf_scale,
+ * motion_0..8) loads as a 4D scene block (*out_narrays = 49); GSR_PLY_SH3
+ * gives an SH-3 block (59); else 38. */
 gsr_gaussian* gsr_load_ply_device_ex(const char* filename, int* out_numGaussians, int flags, int* out_narrays);
 
 /* render.cu:194-264: stable sort of N host-side lightWeightGaussian records
@@ -214,11 +218,11 @@ int gsr_blend_stamps(gsr_context* ctx, uint64_t* out, int64_t n);
 /* Upload a host SoA scene (GSR_SCENE_NARRAYS arrays of n floats, contiguous,
  * already activated as by the loader) into a new device scene block. */
 void* gsr_scene_upload(const float* host_soa, int64_t n);
-/* narrays = GSR_SCENE_NARRAYS (3D) or GSR_SCENE4D_NARRAYS (4D). */
+/* narrays = GSR_SCENE_NARRAYS (3D), GSR_SCENE4D_NARRAYS (4D) or GSR_SCENE_SH3_NARRAYS. */
 void* gsr_scene_upload_ex(const float* host_soa, int narrays, int64_t n);
 void gsr_scene_free(void* d_scene);
 /* Copy a device scene block back into host SoA form (38 * n floats). */
-/* Copies every array of the block (38, or 49 for a 4D block) into host_soa. */
+/* Copies every array of the block (38, 49 for 4D, 59 for SH-3) into host_soa. */
 int gsr_scene_download(const void* d_scene, float* host_soa, int64_t n);
 
 /* ---------------------------------------------------------------- host helpers */
@@ -227,9 +231,10 @@ int gsr_scene_download(const void* d_scene, float* host_soa, int64_t n);
  * storeGaussianFromProperty gaussians.cpp:17-30), host side only.  Call with
  * host_soa == NULL to get the count; then with a buffer of 38*n floats. */
 int gsr_ply_read_host(const char* path, float* host_soa, int64_t capacity, int64_t* n_out);
-/* Same with flags (GSR_PLY_TYPED) and narrays = 38 or 49 (4D arrays filled
- * when present; defaults trbf_center 0, trbf_scale 1, motion 0); *is_4d (if
- * non-NULL) reports whether the file has the 4D properties. */
+/* Same with flags (GSR_PLY_TYPED, GSR_PLY_SH3) and narrays = 38, 49 (4D arrays
+ * filled when present; defaults trbf_center 0, trbf_scale 1, motion 0) or 59
+ * (with GSR_PLY_SH3); *is_4d (if non-NULL) reports whether the file has the 4D
+ * properties. */
 int gsr_ply_read_host_ex(const char* path, float* host_soa, int narrays, int64_t capacity, int64_t* n_out,
                          int flags, int* is_4d);
 

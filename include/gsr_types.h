@@ -93,6 +93,10 @@ typedef struct gsr_lwg {
  *   38     trbf_center (temporal centre, raw)
  *   39     trbf_scale = (float)exp((double)v) (temporal scale)
  *   40..48 motion_0..8: linear xyz, quadratic xyz, cubic xyz (raw)
+ * SH-3 blocks (GSR_SCENE_SH3_NARRAYS, opt-in "Inria-correct" mode)
+ * replace 11..37 with 11..58 = sh[3k + c] for the 16 coefficients k of
+ * degree <= 3: k = 0 from f_dc_c, k >= 1 from f_rest_{15c + k - 1} (the
+ * channel-major layout of 3DGS training output).
  */
 #define GSR_SCENE_MAGIC0 0x7fc0a5e1u   /* NaN bit patterns: never a sane AoS x,y,z */
 #define GSR_SCENE_MAGIC1 0x7fc05352u
@@ -100,6 +104,7 @@ typedef struct gsr_lwg {
 #define GSR_SCENE_MAGIC3 0x7fc00001u
 #define GSR_SCENE_NARRAYS 38
 #define GSR_SCENE4D_NARRAYS 49
+#define GSR_SCENE_SH3_NARRAYS 59      /* 3D block with full degree-3 SH (opt-in, GSR_PLY_SH3) */
 #define GSR_SCENE_HEADER_BYTES 256
 
 typedef struct gsr_scene_header {

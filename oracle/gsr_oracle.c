@@ -89,7 +89,7 @@ int orc_ply_read_ex(const char* path, float* soa, int narrays, int64_t capacity,
         else if (!strcmp(name, "f_dc_2")) { kind = S_DC; idx = 2; }
         else if (starts_with(name, "f_rest_")) {
             int r = atoi(name + 7);
-            if (r < 24) { kind = S_REST; idx = r; }                    /* misc.cu:76 */
+            if (r < (narrays == GSR_SCENE_SH3_NARRAYS ? 45 : 24)) { kind = S_REST; idx = r; }   /* misc.cu:76 */
         } else if (!strcmp(name, "opacity")) kind = S_OPACITY;
         else if (starts_with(name, "scale_")) { idx = atoi(name + 6); kind = (idx >= 0 && idx < 3) ? S_SCALE : S_SKIP; }
         else if (starts_with(name, "rot_")) { idx = atoi(name + 4); kind = (idx >= 0 && idx < 4) ? S_ROT : S_SKIP; }
@@ -106,7 +106,7 @@ int orc_ply_read_ex(const char* path, float* soa, int narrays, int64_t capacity,
 
     const int64_t n = nv;
     memset(soa, 0, sizeof(float) * (size_t)narrays * (size_t)n);   /* Gaussian g{} */
-    if (narrays > GSR_A_TSCALE)   /* 4D defaults: a static Gaussian (temporal scale 1) */
+    if (narrays == GSR_SCENE4D_NARRAYS)   /* 4D defaults: a static Gaussian (temporal scale 1) */
         for (int64_t i = 0; i < n; i++) soa[GSR_A_TSCALE * n + i] = 1.0f;
     float* row = (float*)malloc(sizeof(float) * (size_t)(nprops > 0 ? nprops : 1));
     int rc = 0;
@@ -119,15 +119,20 @@ int orc_ply_read_ex(const char* path, float* soa, int narrays, int64_t capacity,
             case S_Y: soa[GSR_A_Y * n + i] = v; break;
             case S_Z: soa[GSR_A_Z * n + i] = v; break;
             case S_DC: soa[(GSR_A_SH0 + idxs[p]) * n + i] = v; break;
-            case S_REST: soa[(GSR_A_SH0 + 3 + idxs[p]) * n + i] = v; break;
+            case S_REST:
+                if (narrays == GSR_SCENE_SH3_NARRAYS)   /* SH-3 mode: f_rest channel-major (15 per channel) */
+                    soa[(GSR_A_SH0 + 3 * (1 + idxs[p] % 15) + idxs[p] / 15) * n + i] = v;
+                else
+                    soa[(GSR_A_SH0 + 3 + idxs[p]) * n + i] = v;
+                break;
             /* sigmoid<float>: 1.0f / (1.0f + std::exp(-x)) (gaussians.cpp:12-15) */
             case S_OPACITY: soa[GSR_A_OPACITY * n + i] = 1.0f / (1.0f + expf(-v)); break;
             /* exp(value) resolves to ::exp(double) (gaussians.cpp:26) */
             case S_SCALE: soa[(GSR_A_SCALE0 + idxs[p]) * n + i] = (float)exp((double)v); break;
             case S_ROT: soa[(GSR_A_ROT0 + idxs[p]) * n + i] = v; break;
-            case S_TCENTER: if (narrays > GSR_A_TCENTER) soa[GSR_A_TCENTER * n + i] = v; break;
-            case S_TSCALE: if (narrays > GSR_A_TSCALE) soa[GSR_A_TSCALE * n + i] = (float)exp((double)v); break;
-            case S_MOTION: if (narrays > GSR_A_MOTION0 + idxs[p]) soa[(GSR_A_MOTION0 + idxs[p]) * n + i] = v; break;
+            case S_TCENTER: if (narrays == GSR_SCENE4D_NARRAYS) soa[GSR_A_TCENTER * n + i] = v; break;
+            case S_TSCALE: if (narrays == GSR_SCENE4D_NARRAYS) soa[GSR_A_TSCALE * n + i] = (float)exp((double)v); break;
+            case S_MOTION: if (narrays == GSR_SCENE4D_NARRAYS) soa[(GSR_A_MOTION0 + idxs[p]) * n + i] = v; break;
             default: break;   /* normals are not used by the render path */
             }
         }
@@ -263,6 +268,33 @@ static const float SH_C1 = 0.4886025119029199f;
 static const float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
                                -1.0925484305920792f, 0.5462742152960396f};
 
+/* SH-3 ("Inria-correct") mode: the soa holds 59 arrays, sh[3k + c] for k < 16,
+ * and the colour is the degree-3 evaluation of the 3DGS training code
+ * (bands 0..3 left to right, + 0.5, clamped at 0 only). */
+static int g_sh3 = 0;
+void orc_set_sh3(int on) { g_sh3 = on != 0; }
+
+static void color_sh3(const float* soa, int64_t n, int64_t i, const float dir[3], float color[3]) {
+    static const float C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                                0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
+                                -0.5900435899266435f};
+    const float x = dir[0], y = dir[1], z = dir[2];
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    for (int c = 0; c < 3; c++) {
+        float S[16];
+        for (int k = 0; k < 16; k++) S[k] = soa[(GSR_A_SH0 + 3 * k + c) * n + i];
+        float r = SH_C0 * S[0];
+        r = r - SH_C1 * y * S[1] + SH_C1 * z * S[2] - SH_C1 * x * S[3];
+        r = r + SH_C2[0] * xy * S[4] + SH_C2[1] * yz * S[5] + SH_C2[2] * (2.0f * zz - xx - yy) * S[6] +
+            SH_C2[3] * xz * S[7] + SH_C2[4] * (xx - yy) * S[8];
+        r = r + C3[0] * y * (3.0f * xx - yy) * S[9] + C3[1] * xy * z * S[10] + C3[2] * y * (4.0f * zz - xx - yy) * S[11] +
+            C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * S[12] + C3[4] * x * (4.0f * zz - xx - yy) * S[13] +
+            C3[5] * z * (xx - yy) * S[14] + C3[6] * x * (xx - 3.0f * yy) * S[15];
+        r += 0.5f;
+        color[c] = fmaxf(r, 0.0f);
+    }
+}
+
 void orc_intrinsics(const gsr_camera* cam, float* fx, float* fy) {
     /* fy = 1.0f / tanf(fovY * 0.5f * (CUDART_PI_F / 180.0f)) (render.cu:620);
        tanf taken correctly rounded via double. */
@@ -292,6 +324,10 @@ int orc_preprocess(const float* soa, int64_t n, const gsr_camera* cam, int W, in
         float dir[3] = {gx - cam->position[0], gy - cam->position[1], gz - cam->position[2]};
         o_normalize(dir);
         float color[3];
+        if (g_sh3) {
+            color_sh3(soa, n, i, dir, color);
+            for (int c = 0; c < 3; c++) s->color[c] = color[c];
+        } else {
         for (int c = 0; c < 3; c++) color[c] = sh[c] * SH_C0;
         {
             const float x = dir[0], y = dir[1], z = dir[2];
@@ -315,6 +351,7 @@ int orc_preprocess(const float* soa, int64_t n, const gsr_camera* cam, int W, in
             color[c] = fminf(fmaxf(color[c], 0.0f), 1.0f);
             s->color[c] = color[c];
         }
+        }   /* reference SH (bands 0..2) */
         float old_xyz[4] = {gx, gy, gz, 1.0f};
         float tmp_xyz[4], new_xyz[4];
         o_matvec4(V, old_xyz, tmp_xyz);

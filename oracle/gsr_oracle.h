@@ -42,6 +42,9 @@ typedef struct orc_splat {
 int orc_ply_read(const char* path, float* soa, int64_t capacity, int64_t* n_out);
 /* narrays 38 (3D) or 49 (4D arrays: trbf_center, exp(trbf_scale), motion_0..8). */
 int orc_ply_read_ex(const char* path, float* soa, int narrays, int64_t capacity, int64_t* n_out);
+/* SH-3 ("Inria-correct") mode for orc_preprocess / orc_render: soa then has
+ * GSR_SCENE_SH3_NARRAYS arrays (process-wide switch; tests reset it). */
+void orc_set_sh3(int on);
 /* Config 5: the 38 arrays of a 4D scene at time t, no temporal cull. */
 void orc_temporal(const float* soa49, int64_t n, float t, float* out38);
 

@@ -37,6 +37,8 @@ def lib():
         L.orc_ply_read_ex.restype = c_int
         L.orc_temporal.argtypes = [c_void_p, c_int64, c_float, c_void_p]
         L.orc_temporal.restype = None
+        L.orc_set_sh3.argtypes = [c_int]
+        L.orc_set_sh3.restype = None
         L.orc_intrinsics.argtypes = [cam, POINTER(c_float), POINTER(c_float)]
         L.orc_preprocess.argtypes = [c_void_p, c_int64, cam, c_int, c_int, c_float, c_void_p]
         L.orc_preprocess.restype = c_int
@@ -69,6 +71,29 @@ def ply_read(path: str) -> np.ndarray:
     if rc:
         raise IOError(f"orc_ply_read({path}) = {rc}")
     return soa
+
+
+def ply_read_sh3(path: str) -> np.ndarray:
+    """(59, n) SH-3 ("Inria-correct") arrays through the oracle's reader."""
+    n = c_int64(-1)
+    rc = lib().orc_ply_read_ex(path.encode(), None, 59, 0, ctypes.byref(n))
+    if rc:
+        raise IOError(f"orc_ply_read_ex({path}) = {rc}")
+    soa = np.zeros((59, n.value), dtype=np.float32)
+    rc = lib().orc_ply_read_ex(path.encode(), soa.ctypes.data, 59, n.value, ctypes.byref(n))
+    if rc:
+        raise IOError(f"orc_ply_read_ex({path}) = {rc}")
+    return soa
+
+
+class sh3_mode:
+    """Context manager: the oracle evaluates degree-3 SH on 59-array scenes."""
+
+    def __enter__(self):
+        lib().orc_set_sh3(1)
+
+    def __exit__(self, *exc):
+        lib().orc_set_sh3(0)
 
 
 def ply_read4d(path: str) -> np.ndarray:

@@ -200,6 +200,33 @@ def test_depth_pass_plan_exact(gpu, orc, torch, c1, pos, look):
     assert np.array_equal(orders[0], orders[1])
 
 
+@pytest.mark.parametrize("ci", [0, 1, 3])
+def test_sh3_mode_parity(gpu, orc, torch, c1, ci):
+    """Opt-in "Inria-correct" SH-3 scenes (degree-3 colour, channel-major f_rest)
+    against the oracle's independent restatement, bit-exact; the colours differ
+    from the reference-mode render of the same file (sanity)."""
+    path, soa = c1
+    W, H = 640, 480
+    cam = cam_for(gpu, W, H, **CAMS[ci])
+    scene = gpu.Scene.from_ply(path, sh3=True)
+    assert scene.is_sh3
+    got, r = render_gpu(gpu, torch, scene, cam, W, H)
+    soa3 = orc.ply_read_sh3(path)
+    with orc.sh3_mode():
+        want = orc.render(soa3, cam, W, H, 3.0)
+        want_spl = orc.preprocess(soa3, cam, W, H, 3.0)
+    assert_image_parity(got, want)
+    vis = want_spl["status"] == 2
+    g = r.read_splats(soa.shape[1])[vis]
+    assert np.array_equal(g["color"].view(np.uint32), want_spl["color"][vis].view(np.uint32))
+    assert not np.array_equal(got, orc.render(soa, cam, W, H, 3.0))
+    # the drop-in recognises an SH-3 block from its header
+    t = gpu.TilingInformation(50, 50, H, W)
+    host = gpu.preprocessCUDAGaussians(scene.ptr, scene.n, cam, t.num_tile_y, t.num_tile_x, t.width_stride,
+                                       t.height_stride, W, H, 3.0)
+    assert np.array_equal(host.view(np.uint32), want.view(np.uint32))
+
+
 def test_dropin_scene_block_reference_tiling(gpu, orc, torch, c1):
     """loadGaussianCudaFromPly + preprocessCUDAGaussians (the viewer's calls),
     reference 50x50 tiling (cull_sort_test.cpp:44-45)."""

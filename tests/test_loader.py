@@ -154,3 +154,23 @@ def test_oracle_temporal_identities(gsr, orc, tmp_path):
     assert np.array_equal(out[4:38], s2[4:38])
     far = orc.temporal(s, 50.0)
     assert (far[3] < 1e-6).all()          # far from every centre: opacity ~0
+
+
+def test_sh3_loader_mapping(gsr, orc, tmp_path):
+    """GSR_PLY_SH3: all 45 f_rest, channel-major (f_rest_{15c + k - 1} is channel c of
+    coefficient k), into sh[3k + c] of a 59-array block; the oracle's own reader agrees."""
+    p = tmp_path / "s.ply"
+    gsr.write_synthetic_ply(str(p), 1500, 11)
+    a = gsr.read_ply(str(p), sh3=True)
+    assert a.shape == (59, 1500)
+    assert np.array_equal(a.view(np.uint32), orc.ply_read_sh3(str(p)).view(np.uint32))
+    assert np.array_equal(gsr.read_ply(str(p), sh3=True, typed=True).view(np.uint32), a.view(np.uint32))
+    ref = gsr.read_ply(str(p))
+    assert np.array_equal(a[:14].view(np.uint32), ref[:14].view(np.uint32))   # base + f_dc unchanged
+    # raw f_rest values straight from the file body
+    body = p.read_bytes()
+    raw = np.frombuffer(body[body.index(b"end_header\n") + 11:], dtype="<f4").reshape(1500, 62)
+    f_rest = raw[:, 9:54]
+    for k in range(1, 16):
+        for c in range(3):
+            assert np.array_equal(a[11 + 3 * k + c], f_rest[:, 15 * c + k - 1])
