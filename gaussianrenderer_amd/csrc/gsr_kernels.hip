@@ -989,7 +989,10 @@ __device__ __forceinline__ bool block_may_reach(float a, float b, float c, float
     const float h = 0.5f * (b + c);
     const float det = a * e - h * h;
     if (!(a > 0.0f && e > 0.0f && det > 1e-4f * (a * e)) || !(cut < 3.0e38f)) return true;
-    const float ih = -h / e, iv = -h / a;
+    // minimiser along each edge; v_rcp_f32 (~1 ulp) moves it by ~1e-7 relative,
+    // which changes the edge minimum only at second order (e * delta^2), far
+    // inside the err margin below
+    const float ih = -h * __builtin_amdgcn_rcpf(e), iv = -h * __builtin_amdgcn_rcpf(a);
     auto q = [&](float x, float y) { return a * x * x + 2.0f * h * x * y + e * y * y; };
     float qm = q(dx0, fminf(fmaxf(ih * dx0, dy0), dy1));
     qm = fminf(qm, q(dx1, fminf(fmaxf(ih * dx1, dy0), dy1)));
@@ -1003,14 +1006,15 @@ __device__ __forceinline__ bool block_may_reach(float a, float b, float c, float
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 // gsr_expf on two lanes at once (v_pk_* for every float op that has a packed
-// form), for inputs the caller has PROVEN finite and <= 88.75: there the upper
-// clamp and the NaN select of gsr_expf are no-ops, and every remaining step is
-// the same IEEE operation in the same order, so each half is bit-identical to
-// gsr_expf of that half.
-__device__ __forceinline__ f2 gsr_expf_x2(f2 x) {
-    f2 xc;
-    xc.x = fmaxf(x.x, -104.0f);
-    xc.y = fmaxf(x.y, -104.0f);
+// form), for inputs the caller has PROVEN finite and in [-2e7, 88.75]: there the
+// clamps and the NaN select of gsr_expf do not change the result, and every
+// remaining step is the same IEEE operation in the same order, so each half is
+// bit-identical to gsr_expf of that half.
+__device__ __forceinline__ f2 gsr_expf_x2(f2 xc) {
+    // No clamp: the fast-path proof bounds every in-box input to [-2e7, 5], where
+    // n = rint(x log2e) >= -2.9e7 keeps the Cody-Waite remainder accurate (one
+    // fma rounding on ~6e3) and ldexp(y, n) rounds to +0 for every x < -104 —
+    // gsr_expf's clamped result.  Out-of-box lanes are discarded by the caller.
     const f2 t = xc * 1.44269504088896341f;
     f2 n;
     n.x = rintf(t.x);
