@@ -180,9 +180,15 @@ def loadGaussianCudaFromPly(path: str):
 
 def preprocessCUDAGaussians(d_gaussians: int, num_gaussians: int, cam: Camera, num_tile_y: int, num_tile_x: int,
                             width_stride: int, height_stride: int, tile_W: int, tile_H: int,
-                            k: float) -> np.ndarray:
-    """render.cu:871-1157 through the drop-in C symbol; returns the host image (3, H, W)."""
-    out = np.zeros((3, tile_H, tile_W), dtype=np.float32)
+                            k: float, out: np.ndarray = None) -> np.ndarray:
+    """render.cu:871-1157 through the drop-in C symbol; returns the host image (3, H, W).
+
+    `out`: optional persistent C-contiguous float32 (3, H, W) host image to render
+    into (the reference viewer's loop reuses one host buffer the same way)."""
+    if out is None:
+        out = np.zeros((3, tile_H, tile_W), dtype=np.float32)
+    elif out.dtype != np.float32 or out.shape != (3, tile_H, tile_W) or not out.flags.c_contiguous:
+        raise ValueError(f"out must be C-contiguous float32 (3, {tile_H}, {tile_W})")
     lib().preprocessCUDAGaussians(d_gaussians, out.ctypes.data_as(ctypes.POINTER(c_float)), num_gaussians, cam,
                                   num_tile_y, num_tile_x, width_stride, height_stride, tile_W, tile_H, k)
     return out
@@ -290,8 +296,9 @@ class Renderer:
         check(lib().gsr_read_tile_ranges(self.ctx, out.ctypes.data, tx * ty), "gsr_read_tile_ranges")
         return out
 
-    def set_timing(self, mode: int):
-        check(lib().gsr_set_timing(self.ctx, mode), "gsr_set_timing")
+    def set_timing(self, mode: int, stride: int = 1):
+        """0 off, 1 blend events, 2 every stage; events on every `stride`-th frame."""
+        check(lib().gsr_set_timing_stride(self.ctx, mode, stride), "gsr_set_timing")
 
     def set_diagnostics(self, on: bool):
         check(lib().gsr_set_diagnostics(self.ctx, int(on)), "gsr_set_diagnostics")

@@ -110,6 +110,7 @@ SIGNATURES = [
     ("gsr_set_blend_variant", c_int, [c_void_p, c_int]),
     ("gsr_blend_stamps", c_int, [c_void_p, c_void_p, c_int64]),
     ("gsr_set_tuning", c_int, [c_void_p, c_int, c_int]),
+    ("gsr_set_timing_stride", c_int, [c_void_p, c_int, c_int]),
     ("gsr_depth_passes", c_int, [c_void_p]),
     ("gsr_scene_upload", c_void_p, [c_void_p, c_int64]),
     ("gsr_scene_upload_ex", c_void_p, [c_void_p, c_int, c_int64]),

@@ -344,6 +344,9 @@ struct gsr_context {
     bool pending = false;
     // timing
     int timing = 0;
+    int timing_stride = 1;           // record the timing events on every k-th frame only
+    int64_t timing_count = 0;        // frames seen since timing was enabled
+    bool timing_now = false;         // this frame records events
     std::vector<hipEvent_t> ev_pool;
     std::vector<FrameEvents> ev_frames;
     FrameEvents cur{};
@@ -448,7 +451,7 @@ hipEvent_t get_event(gsr_context* c) {
 
 // Record the boundary event that opens stage `stage` (stage == GSR_NUM_STAGES closes the frame).
 void mark(gsr_context* c, int stage) {
-    if (!c->timing) return;
+    if (!c->timing || !c->timing_now) return;
     const bool want = (c->timing == 2) || stage == GSR_STAGE_BLEND || stage == GSR_NUM_STAGES;
     if (!want) return;
     hipEvent_t e = get_event(c);
@@ -472,6 +475,10 @@ int check_overflow(gsr_context* c, bool blocking) {
     s.pairs_eff = hv->pairs_eff;
     s.overflow = hv->overflow;
     if (!s.overflow) return GSR_OK;
+    // frames queued after the event may still be running: drain them so the
+    // grown capacity covers their totals too (ensure_pairs syncs again; cheap)
+    HIP_TRY(hipDeviceSynchronize());
+    if (hv->pairs_total > s.pairs_total) s.pairs_total = hv->pairs_total;
     const int64_t want = (int64_t)(s.pairs_total + s.pairs_total / 4 + 4096);
     if (int rc = ensure_pairs(c, want)) return rc;
     HIP_TRY(hipMemset(c->stats + 1, 0, sizeof(Stats)));
@@ -557,6 +564,7 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     if (c->timing) {
         c->cur = FrameEvents{};
         c->cur.mode = c->timing;
+        c->timing_now = (c->timing_count++ % c->timing_stride) == 0;
     }
     mark(c, GSR_STAGE_PREPROCESS);
     const float* arrays = nullptr;
@@ -643,10 +651,16 @@ static int blend_locked(gsr_context* c, float* d_out) {
                               c->diagnostics ? c->consumed : nullptr, c->blend_variant, c->queue,
                               c->resident_groups, c->stream));
     mark(c, GSR_NUM_STAGES);
-    if (c->timing) c->ev_frames.push_back(c->cur);
+    if (c->timing && c->timing_now) c->ev_frames.push_back(c->cur);
     c->cur = FrameEvents{};
-    HIP_TRY(hipEventRecord(c->done_ev, c->stream));
-    c->pending = true;
+    // At most one completion event in flight: while the last one is unread, later
+    // frames skip the record (~3 us each). The overflow stats are sticky, so reading
+    // them when that older frame completes still sees every overflow so far, and
+    // gsr_sync drains the stream before it reads them.
+    if (!c->pending) {
+        HIP_TRY(hipEventRecord(c->done_ev, c->stream));
+        c->pending = true;
+    }
     return GSR_OK;
 }
 
@@ -786,9 +800,15 @@ extern "C" int gsr_read_tile_ranges(gsr_context* c, uint32_t* host, int64_t nt) 
 // ------------------------------------------------------------------ timing
 
 extern "C" int gsr_set_timing(gsr_context* c, int mode) {
-    if (!c || mode < 0 || mode > 2) return set_err(GSR_E_ARG, "gsr_set_timing: bad argument");
+    return gsr_set_timing_stride(c, mode, 1);
+}
+
+extern "C" int gsr_set_timing_stride(gsr_context* c, int mode, int stride) {
+    if (!c || mode < 0 || mode > 2 || stride < 1) return set_err(GSR_E_ARG, "gsr_set_timing: bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
     c->timing = mode;
+    c->timing_stride = stride;
+    c->timing_count = 0;
     return GSR_OK;
 }
 

@@ -170,6 +170,9 @@ int gsr_read_tile_ranges(gsr_context* ctx, uint32_t* host_ranges, int64_t num_ti
 /* ---- per-stage device timing with hipEvents on the render stream ----
  * mode 0 = off, 1 = blend only (two events per frame), 2 = every stage. */
 int gsr_set_timing(gsr_context* ctx, int mode);
+/* Same, recording the events on every `stride`-th frame only (frames 0, k, 2k, …
+ * after the call); gsr_stage_times then averages over the recorded frames. */
+int gsr_set_timing_stride(gsr_context* ctx, int mode, int stride);
 /* Sums of per-stage device milliseconds and the number of frames timed since
  * the last call (synchronises, then resets). */
 int gsr_stage_times(gsr_context* ctx, double* ms_out /* GSR_NUM_STAGES */, int64_t* frames);
