@@ -30,9 +30,13 @@ $(OBJDIR)/gsr_ply.o: $(SRCDIR)/gsr_ply.cpp $(HDRS)
 	mkdir -p $(OBJDIR)
 	$(HIPCC) $(HOSTFLAGS) -x c++ -D__HIP_PLATFORM_AMD__ -c $< -o $@
 
-$(LIB): $(OBJDIR)/gsr_kernels.o $(OBJDIR)/gsr_runtime.o $(OBJDIR)/gsr_ply.o
+$(OBJDIR)/gsr_gl.o: $(SRCDIR)/gsr_gl.cpp $(HDRS) include/gsr_gl.h
+	mkdir -p $(OBJDIR)
+	$(HIPCC) $(HOSTFLAGS) -x c++ -D__HIP_PLATFORM_AMD__ -c $< -o $@
+
+$(LIB): $(OBJDIR)/gsr_kernels.o $(OBJDIR)/gsr_runtime.o $(OBJDIR)/gsr_ply.o $(OBJDIR)/gsr_gl.o
 	mkdir -p $(dir $(LIB))
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libgsr.so
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -ldl -Wl,-soname,libgsr.so
 
 oracle:
 	$(MAKE) -C oracle

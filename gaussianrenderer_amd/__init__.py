@@ -4,6 +4,8 @@ Host-side mirror of the reference's interface (wwangg22/GaussianRenderer):
 
 * :func:`loadGaussianCudaFromPly`  — misc.cu:13-134 (device scene block)
 * :func:`preprocessCUDAGaussians`  — render.cu:871-1157 (whole frame, host image)
+* :func:`preprocessCUDAGaussiansGL` — Canvas::render (canvas.cpp:337-351) into the
+  viewer's colour SSBO, no host round trip (include/gsr_gl.h; :class:`DisplayTarget`)
 * :class:`TilingInformation`       — utils/gaussians.hpp:38-60
 * :func:`make_camera` / :func:`orbit` — scene/camera.cpp
 
@@ -14,7 +16,7 @@ there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
-from ctypes import byref, c_float, c_int, c_int64
+from ctypes import byref, c_float, c_int, c_int64, c_void_p
 
 import numpy as np
 
@@ -27,7 +29,7 @@ from ._native import (Camera, GsrError, LAYOUT_AOS, LAYOUT_SCENE_BLOCK, LAYOUT_S
 __all__ = [
     "Camera", "GsrError", "Renderer", "Scene", "TilingInformation", "make_camera", "orbit",
     "loadGaussianCudaFromPly", "preprocessCUDAGaussians", "read_ply", "write_synthetic_ply",
-    "SPLAT_DTYPE", "STAGES", "TILE_PX", "lib",
+    "SPLAT_DTYPE", "STAGES", "TILE_PX", "lib", "DisplayTarget", "display_gl_current", "preprocessCUDAGaussiansGL",
 ]
 
 # gsr_read_splats record (include/gsr.h).
@@ -194,6 +196,52 @@ def preprocessCUDAGaussians(d_gaussians: int, num_gaussians: int, cam: Camera, n
     return out
 
 
+def display_gl_current() -> bool:
+    """True if a GL context (GLX or EGL) is current on this thread."""
+    return bool(lib().gsr_display_gl_current())
+
+
+class DisplayTarget:
+    """Where a frame is displayed (include/gsr_gl.h): the viewer's colour SSBO
+    registered with HIP (`from_gl`), or device memory such as an imported
+    Vulkan buffer (`from_device`).  The render writes it in place."""
+
+    def __init__(self, ptr: int):
+        self.ptr = ptr
+
+    @classmethod
+    def from_gl(cls, gl_buffer: int) -> "DisplayTarget":
+        p = c_void_p()
+        check(lib().gsr_display_register_gl(int(gl_buffer), byref(p)), "gsr_display_register_gl")
+        return cls(p.value)
+
+    @classmethod
+    def from_device(cls, d_ptr: int, nbytes: int) -> "DisplayTarget":
+        p = c_void_p()
+        check(lib().gsr_display_wrap_device(d_ptr, int(nbytes), byref(p)), "gsr_display_wrap_device")
+        return cls(p.value)
+
+    def free(self):
+        if self.ptr:
+            p, self.ptr = self.ptr, 0
+            check(lib().gsr_display_free(p), "gsr_display_free")
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def preprocessCUDAGaussiansGL(d_gaussians: int, gl_buffer: int, num_gaussians: int, cam: Camera, num_tile_y: int,
+                              num_tile_x: int, width_stride: int, height_stride: int, tile_W: int, tile_H: int,
+                              k: float) -> None:
+    """Canvas::render (canvas.cpp:337-342) into the colour SSBO, no host round trip
+    (include/gsr_gl.h).  Needs the viewer's GL context current on this thread."""
+    lib().preprocessCUDAGaussiansGL(d_gaussians, int(gl_buffer), num_gaussians, cam, num_tile_y, num_tile_x,
+                                    width_stride, height_stride, tile_W, tile_H, k)
+
+
 class Renderer:
     """Persistent render context (stream-ordered, device-resident)."""
 
@@ -233,6 +281,24 @@ class Renderer:
                               t.width_stride, t.height_stride, k, out_ptr, stream or None)
         if rc not in (_native.GSR_OK, _native.GSR_E_OVERFLOW):
             raise GsrError(rc, "gsr_render")
+        return rc
+
+    def render_display(self, target: "DisplayTarget", scene, cam: Camera, W: int, H: int, k: float = 3.0,
+                       tiling=None, stream: int = 0, layout: int = LAYOUT_SCENE_BLOCK, n: int | None = None,
+                       time: float | None = None) -> int:
+        """Enqueue one frame straight into a display target (include/gsr_gl.h):
+        map, check it holds 3*W*H floats, render, unmap.  Same returns as render()."""
+        ptr = scene.ptr if isinstance(scene, Scene) else int(scene)
+        n = scene.n if n is None else n
+        if isinstance(scene, Scene) and layout == LAYOUT_SCENE_BLOCK:
+            layout = scene.layout
+        if time is not None:
+            self.set_time(time)
+        t = tiling or TilingInformation(1, 1, H, W)
+        rc = lib().gsr_render_display(self.ctx, target.ptr, ptr, layout, n, byref(cam), W, H, t.num_tile_x,
+                                      t.num_tile_y, t.width_stride, t.height_stride, k, stream or None)
+        if rc not in (_native.GSR_OK, _native.GSR_E_OVERFLOW):
+            raise GsrError(rc, "gsr_render_display")
         return rc
 
     def set_time(self, t: float):

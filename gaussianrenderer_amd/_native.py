@@ -24,6 +24,7 @@ GSR_E_HIP = -2
 GSR_E_IO = -3
 GSR_E_FORMAT = -4
 GSR_E_OVERFLOW = -5
+GSR_E_DISPLAY = -6
 
 LAYOUT_SCENE_BLOCK = 0
 LAYOUT_AOS = 1
@@ -78,7 +79,7 @@ class Lwg(ctypes.Structure):
 
 assert ctypes.sizeof(Lwg) == 16
 
-# (name, restype, argtypes) for every symbol of include/gsr.h.
+# (name, restype, argtypes) for every symbol of include/gsr.h and include/gsr_gl.h.
 SIGNATURES = [
     ("preprocessCUDAGaussians", None,
      [c_void_p, POINTER(c_float), c_int, Camera, c_int, c_int, c_int, c_int, c_int, c_int, c_float]),
@@ -86,6 +87,15 @@ SIGNATURES = [
     ("gsr_load_ply_device_ex", c_void_p, [c_char_p, POINTER(c_int), c_int, POINTER(c_int)]),
     ("oneSweep3DGaussianSort", None, [POINTER(Lwg), c_int, c_int, POINTER(c_float)]),
     ("oneSweepSort", None, [POINTER(c_int), POINTER(c_int), c_int, c_int, POINTER(c_float)]),
+    # include/gsr_gl.h: display interop (SSBO written in place, no host round trip)
+    ("preprocessCUDAGaussiansGL", None,
+     [c_void_p, ctypes.c_uint, c_int, Camera, c_int, c_int, c_int, c_int, c_int, c_int, c_float]),
+    ("gsr_display_register_gl", c_int, [ctypes.c_uint, POINTER(c_void_p)]),
+    ("gsr_display_wrap_device", c_int, [c_void_p, ctypes.c_size_t, POINTER(c_void_p)]),
+    ("gsr_display_free", c_int, [c_void_p]),
+    ("gsr_display_gl_current", c_int, []),
+    ("gsr_render_display", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, POINTER(Camera), c_int, c_int,
+                                   c_int, c_int, c_int, c_int, c_float, c_void_p]),
     ("gsr_create", c_void_p, []),
     ("gsr_destroy", None, [c_void_p]),
     ("gsr_reserve", c_int, [c_void_p, c_int64, c_int64]),

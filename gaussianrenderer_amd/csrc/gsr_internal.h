@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "gsr_types.h"
 
 namespace gsr {
@@ -83,5 +85,13 @@ hipError_t launch_gather_lwg(const gsr_lwg* in, const uint64_t* stage1, const ui
 
 // Device math probe for the detmath GPU parity test.
 hipError_t launch_math_probe(const float* in, int n, float* out, hipStream_t s);
+
+// Drop-in frame into a device image on the drop-in context (gsr_runtime.cpp);
+// callers hold dropin_mutex().  `what` names the failing step for the message.
+int dropin_render_device(gsr_gaussian* d_gaussians, int num_gaussians, const gsr_camera& cam, int num_tile_y,
+                         int num_tile_x, int width_stride, int height_stride, int W, int H, float k,
+                         float* d_out, const char** what);
+std::mutex& dropin_mutex();
+const char* last_error();
 
 }  // namespace gsr

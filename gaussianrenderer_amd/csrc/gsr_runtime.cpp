@@ -936,10 +936,53 @@ extern "C" int gsr_math_probe(const float* host_in, int n, float* host_out) {
 static std::mutex g_dropin_mu;
 static gsr_context* g_dropin = nullptr;
 
+// Whole drop-in frame into a DEVICE image (3*W*H floats) on the drop-in
+// context, synchronous like the reference call: scene-layout detection from the
+// block header, and up to two re-renders after a pair-buffer overflow.  Shared by
+// preprocessCUDAGaussians (host image) and preprocessCUDAGaussiansGL (the
+// viewer's SSBO, gsr_gl.cpp).  Returns a GSR_* code; `what` names the failing step.
+int gsr::dropin_render_device(gsr_gaussian* d_gaussians, int num_gaussians, const gsr_camera& cam,
+                              int num_tile_y, int num_tile_x, int width_stride, int height_stride, int W,
+                              int H, float k, float* d_out, const char** what) {
+    *what = "render";
+    if (!g_dropin) g_dropin = gsr_create();
+    gsr_context* c = g_dropin;
+    // Layout detection: our scene block starts with a NaN-pattern magic.
+    int layout = GSR_LAYOUT_AOS;
+    if (num_gaussians > 0 && d_gaussians) {
+        gsr_scene_header h{};
+        *what = "scene";
+        HIP_TRY(hipMemcpy(&h, d_gaussians, sizeof h, hipMemcpyDeviceToHost));
+        if (h.magic[0] == GSR_SCENE_MAGIC0 && h.magic[1] == GSR_SCENE_MAGIC1 && h.magic[2] == GSR_SCENE_MAGIC2 &&
+            h.magic[3] == GSR_SCENE_MAGIC3) {
+            // 4D blocks render at the drop-in context's time (gsr_set_time on it is not
+            // reachable through this ABI, so t = 0: the sequence's first frame)
+            layout = h.narrays == GSR_SCENE4D_NARRAYS    ? GSR_LAYOUT_SCENE_BLOCK_4D
+                     : h.narrays == GSR_SCENE_SH3_NARRAYS ? GSR_LAYOUT_SCENE_BLOCK_SH3
+                                                         : GSR_LAYOUT_SCENE_BLOCK;
+            if ((int64_t)h.count != num_gaussians)
+                return set_err(GSR_E_ARG, "num_gaussians %d != scene block count %llu", num_gaussians,
+                               (unsigned long long)h.count);
+        }
+    }
+    for (int attempt = 0; attempt < 3; attempt++) {
+        *what = "render";
+        int rc = gsr_render(c, d_gaussians, layout, num_gaussians, &cam, W, H, num_tile_x, num_tile_y,
+                            width_stride, height_stride, k, d_out, nullptr);
+        if (rc != GSR_OK && rc != GSR_E_OVERFLOW) return rc;
+        *what = "sync";
+        rc = gsr_sync(c);
+        if (rc != GSR_E_OVERFLOW) return rc;
+    }
+    // each overflow grows the buffer to 1.25x the frame's pair count, so a repeat
+    // means the scene or camera changed under us: report it, never a partial image
+    return set_err(GSR_E_OVERFLOW, "pair buffer still overflowing after 3 renders");
+}
+
 extern "C" void preprocessCUDAGaussians(gsr_gaussian* d_gaussians, float* out_pixels, int num_gaussians,
                                         gsr_camera cam, int num_tile_y, int num_tile_x, int width_stride,
                                         int height_stride, int tile_W, int tile_H, float k) {
-    std::lock_guard<std::mutex> lk(g_dropin_mu);
+    std::lock_guard<std::mutex> lk(gsr::dropin_mutex());
     auto fail = [](const char* what) { std::fprintf(stderr, "preprocessCUDAGaussians: %s: %s\n", what, g_err.c_str()); };
     if (!out_pixels || tile_W <= 0 || tile_H <= 0) {
         set_err(GSR_E_ARG, "bad output buffer or size");
@@ -953,43 +996,20 @@ extern "C" void preprocessCUDAGaussians(gsr_gaussian* d_gaussians, float* out_pi
         if (realloc_dev(&c->out_tmp, npx)) { fail("alloc"); return; }
         c->out_cap = (int64_t)npx;
     }
-    // Layout detection: our scene block starts with a NaN-pattern magic.
-    int layout = GSR_LAYOUT_AOS;
-    if (num_gaussians > 0 && d_gaussians) {
-        gsr_scene_header h{};
-        if (hipMemcpy(&h, d_gaussians, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) {
-            set_err(GSR_E_HIP, "cannot read scene header");
-            fail("scene");
-            return;
-        }
-        if (h.magic[0] == GSR_SCENE_MAGIC0 && h.magic[1] == GSR_SCENE_MAGIC1 && h.magic[2] == GSR_SCENE_MAGIC2 &&
-            h.magic[3] == GSR_SCENE_MAGIC3) {
-            // 4D blocks render at the drop-in context's time (gsr_set_time on it is not
-            // reachable through this ABI, so t = 0: the sequence's first frame)
-            layout = h.narrays == GSR_SCENE4D_NARRAYS    ? GSR_LAYOUT_SCENE_BLOCK_4D
-                     : h.narrays == GSR_SCENE_SH3_NARRAYS ? GSR_LAYOUT_SCENE_BLOCK_SH3
-                                                         : GSR_LAYOUT_SCENE_BLOCK;
-            if ((int64_t)h.count != num_gaussians) {
-                set_err(GSR_E_ARG, "num_gaussians %d != scene block count %llu", num_gaussians,
-                        (unsigned long long)h.count);
-                fail("scene");
-                return;
-            }
-        }
-    }
-    for (int attempt = 0; attempt < 3; attempt++) {
-        int rc = gsr_render(c, d_gaussians, layout, num_gaussians, &cam, tile_W, tile_H, num_tile_x, num_tile_y,
-                            width_stride, height_stride, k, c->out_tmp, nullptr);
-        if (rc != GSR_OK && rc != GSR_E_OVERFLOW) { fail("render"); return; }
-        rc = gsr_sync(c);
-        if (rc == GSR_OK) break;
-        if (rc != GSR_E_OVERFLOW) { fail("sync"); return; }
+    const char* what = "render";
+    if (gsr::dropin_render_device(d_gaussians, num_gaussians, cam, num_tile_y, num_tile_x, width_stride,
+                                  height_stride, tile_W, tile_H, k, c->out_tmp, &what) != GSR_OK) {
+        fail(what);
+        return;
     }
     if (hipMemcpy(out_pixels, c->out_tmp, npx * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) {
         set_err(GSR_E_HIP, "image readback failed");
         fail("readback");
     }
 }
+
+std::mutex& gsr::dropin_mutex() { return g_dropin_mu; }
+const char* gsr::last_error() { return g_err.c_str(); }
 
 // ------------------------------------------------------------------ reference sort ABI
 //

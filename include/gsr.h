@@ -42,7 +42,8 @@ enum {
     GSR_E_HIP = -2,        /* HIP runtime error (no device, OOM, launch failure) */
     GSR_E_IO = -3,         /* file missing / unreadable / truncated */
     GSR_E_FORMAT = -4,     /* unsupported PLY format */
-    GSR_E_OVERFLOW = -5    /* pair buffer overflowed in the previous frame (grown; re-render) */
+    GSR_E_OVERFLOW = -5,   /* pair buffer overflowed in the previous frame (grown; re-render) */
+    GSR_E_DISPLAY = -6     /* display interop: no current GL context / GL registration failed (gsr_gl.h) */
 };
 
 /* Scene layout accepted by the render entry points. */

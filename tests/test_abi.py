@@ -10,7 +10,9 @@ import pytest
 
 from conftest import ROOT
 
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("gsr.h", "gsr_types.h")]
+# every public header except gsr_detmath.h (header-only inline math, nothing exported)
+HEADERS = [os.path.join(ROOT, "include", h) for h in sorted(os.listdir(os.path.join(ROOT, "include")))
+           if h.endswith(".h") and h != "gsr_detmath.h"]
 
 
 def declared_functions():
