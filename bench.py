@@ -42,6 +42,7 @@ CONFIGS = {
 }
 TIMESTEPS_4D = 120
 TIMING_STRIDE = 8
+STAGE_FRAMES = 10     # untimed frames averaged for stages_ms
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 BLEND_KERNEL = "k_blend_w<false>"   # default blend schedule (one 64-thread workgroup per 8x8 block)
 
@@ -219,13 +220,16 @@ def main():
             pending[b] = None
     torch.cuda.synchronize()
 
-    # untimed frames: the per-stage breakdown from a plain frame (events between
-    # stages), then P, Pc and the blend counters from the instrumented blend kernel
+    # untimed frames: the per-stage breakdown averaged over STAGE_FRAMES plain
+    # frames (events between stages), then P, Pc and the blend counters from the
+    # instrumented blend kernel
     t_mid = frame_time(TIMESTEPS_4D // 2) if four_d else None
     r.set_timing(2)
-    r.render(scene, cam, W, H, outs[0].data_ptr(), k=args.k, stream=stream, time=t_mid)
+    for _ in range(STAGE_FRAMES):
+        r.render(scene, cam, W, H, outs[0].data_ptr(), k=args.k, stream=stream, time=t_mid)
     r.sync()
-    stages, _ = r.stage_times()
+    stage_sums, stage_frames = r.stage_times()
+    stages = {k: v / max(1, stage_frames) for k, v in stage_sums.items()}
     r.set_timing(0)
     r.set_diagnostics(True)
     r.render(scene, cam, W, H, outs[0].data_ptr(), k=args.k, stream=stream, time=t_mid)

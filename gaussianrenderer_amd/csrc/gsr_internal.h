@@ -75,6 +75,19 @@ hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* ke
 hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
                         float* out, unsigned long long* consumed, int variant, unsigned int* queue,
                         int resident_groups, hipStream_t s);
+// Tile binning (row pass + column pass, tile grids <= 256 x 256): replaces
+// launch_emit + the key-value tile sort.  hist: 512 x groups; row_items /
+// row_pairs: 256 each; cbins: 256 x bin_col_chunks_max(); rows_buf: pair
+// capacity 8-B row items; vals/ranges as the tile sort's final pass.
+hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,
+                           const uint64_t* rect, int groups, uint32_t* hist, uint32_t* row_items,
+                           unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
+                           int items, hipStream_t s);
+hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, const unsigned long long* row_pairs,
+                           uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
+                           uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,
+                           hipStream_t s);
+uint32_t bin_col_chunks_max(uint32_t pair_capacity, int tiles_y);
 // Standalone sort ABI helpers (oneSweepSort / oneSweep3DGaussianSort).
 hipError_t launch_items_from_keys(const int* keys, uint32_t n, uint64_t* items, hipStream_t s);
 hipError_t launch_keys_from_items(const uint64_t* items, uint32_t n, int* keys, hipStream_t s);

@@ -953,6 +953,505 @@ __global__ __launch_bounds__(256) void k_emit_pairs(const uint64_t* __restrict__
     }
 }
 
+// ------------------------------------------------------------------ tile binning
+//
+// For tile grids up to 256 x 256, two stable counting passes replace "emit every
+// (tile, Gaussian) pair in depth order, then LSD-sort the pairs by tile":
+//   row pass     each depth-ordered Gaussian expands into one item per covered
+//                tile ROW (index | tx0 << 32 | tx1 << 48), binned stably by row:
+//                ~2.4 items per Gaussian instead of ~5.6 pairs
+//   column pass  each row's items expand into one value per covered tile COLUMN,
+//                binned stably by column inside the row: the final tile-major,
+//                depth-ordered Gaussian indices; the tile ranges come straight
+//                from the column scan and no tile key is ever stored
+// Each pass is count (per-chunk histograms) -> scan -> scatter.  The scatters
+// rank one tile of generated items at a time in LDS (wave ballots on the digit
+// bits) and write them digit run by digit run, so the stores coalesce.  Every
+// source is processed in order and chunks are scanned in order: the result is
+// the same stable order as the pair sort [render.cu:788-857].
+
+constexpr uint32_t kRowSources = 1024;              // Gaussians per row-pass sub-chunk
+constexpr uint32_t kColChunk = 2048;                // row items per column-pass chunk (inside one row)
+
+__device__ __forceinline__ uint32_t rect_rows(uint64_t r) {
+    return rect_count(r) ? (uint32_t)((r >> 48) - ((r >> 32) & 0xffffu) + 1u) : 0u;
+}
+__device__ __forceinline__ uint32_t rect_cols(uint64_t r) {
+    return rect_count(r) ? (uint32_t)(((r >> 16) & 0xffffu) - (r & 0xffffu) + 1u) : 0u;
+}
+
+// Stable rank of one tile of up to 256*ITEMS items with 8-bit digits.  Item k
+// of thread t is tile element w*64*ITEMS + k*64 + lane (each wave's items are
+// contiguous).  On return pos[k] is the item's slot in the digit-sorted tile,
+// s_lbase[d] the first slot of digit d; returns the tile's count of digit t.
+template <int ITEMS>
+__device__ __forceinline__ uint32_t bin_rank_tile(const uint32_t (&dig)[ITEMS], uint32_t tn,
+                                                  uint32_t (&pos)[ITEMS], uint32_t (*s_wc)[256],
+                                                  uint32_t* s_lbase, uint32_t* s_scr) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int k = 0; k < 4; k++) s_wc[k][t] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < ITEMS; k++) {
+        const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
+        const bool valid = el < tn;
+        const uint32_t d = dig[k];
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; bit++) {
+            const bool on = (d >> bit) & 1u;
+            const uint64_t bm = __ballot(on);
+            peers &= on ? bm : ~bm;
+        }
+        uint32_t r = 0;
+        if (valid) {
+            const uint32_t before = s_wc[w][d];
+            r = before + (uint32_t)__popcll(peers & lt_mask);
+            if ((uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane) s_wc[w][d] = before + (uint32_t)__popcll(peers);
+        }
+        pos[k] = r;
+    }
+    __syncthreads();
+    uint32_t tcount;
+    {
+        const uint32_t c0 = s_wc[0][t], c1 = s_wc[1][t], c2 = s_wc[2][t], c3 = s_wc[3][t];
+        s_wc[0][t] = 0;
+        s_wc[1][t] = c0;
+        s_wc[2][t] = c0 + c1;
+        s_wc[3][t] = c0 + c1 + c2;
+        tcount = c0 + c1 + c2 + c3;
+        uint32_t tot;
+        s_lbase[t] = block_exclusive_scan<uint32_t>(tcount, s_scr, tot);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < ITEMS; k++) {
+        const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
+        if (el < tn) pos[k] += s_lbase[dig[k]] + s_wc[w][dig[k]];
+    }
+    return tcount;
+}
+
+// Inclusive prefix (in source order) of per-source counts held in LDS s_cnt[m]
+// (m <= 256 * PER): thread t owns sources PER*t .. PER*t + PER-1.  Writes
+// s_pref and returns the total.  Two barriers.
+template <int PER>
+__device__ __forceinline__ uint32_t bin_source_prefix(const uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_scr) {
+    const uint32_t t = threadIdx.x;
+    uint32_t v[PER], loc = 0;
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        v[i] = s_cnt[PER * t + i];
+        loc += v[i];
+    }
+    uint32_t tot;
+    uint32_t run = block_exclusive_scan<uint32_t>(loc, s_scr, tot);
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        run += v[i];
+        s_pref[PER * t + i] = run;
+    }
+    __syncthreads();
+    return tot;
+}
+
+// First source l in [0, M) whose inclusive prefix exceeds q (q < total).
+template <uint32_t M>
+__device__ __forceinline__ uint32_t bin_find_source(const uint32_t* s_pref, uint32_t q) {
+    uint32_t l = 0;
+#pragma unroll
+    for (uint32_t st = M / 2; st >= 1; st >>= 1)
+        if (s_pref[l + st - 1] <= q) l += st;
+    return l;
+}
+
+// Frame pair statistics (st[0]) + the sticky copy (st[1], and the host-mapped
+// mirror) the non-blocking overflow check reads.
+__device__ __forceinline__ void publish_pair_stats(unsigned long long total, uint32_t cap, Stats* st,
+                                                   Stats* host_st) {
+    Stats s;
+    s.pairs_total = total;
+    s.pairs_eff = (uint32_t)(total < cap ? total : cap);
+    s.overflow = total > cap ? 1u : 0u;
+    st[0] = s;
+    Stats k = st[1];
+    if (s.pairs_total > k.pairs_total) k.pairs_total = s.pairs_total;
+    k.pairs_eff = s.pairs_eff;
+    k.overflow |= s.overflow;
+    st[1] = k;
+    if (host_st) {
+        host_st->pairs_total = k.pairs_total;
+        host_st->pairs_eff = k.pairs_eff;
+        host_st->overflow = k.overflow;
+        __threadfence_system();
+    }
+}
+
+// Row pass, count: per workgroup (1024-Gaussian sub-chunks in depth order) the
+// number of row items and of pairs per tile row; hist[row][g] and
+// hist[256 + row][g].  Gathers each Gaussian's rect once and stores it in depth
+// order (srect, the free depth-sort buffer) for the scatter.
+__global__ __launch_bounds__(256) void k_bin_rows_count(const uint64_t* __restrict__ items0,
+                                                         const uint64_t* __restrict__ items1,
+                                                         const uint32_t* __restrict__ dstats, uint32_t n,
+                                                         const uint64_t* __restrict__ rect, int groups,
+                                                         uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h_items[4][256], h_pairs[4][256];
+    const uint32_t t = threadIdx.x, w = t >> 6;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        h_items[k][t] = 0;
+        h_pairs[k][t] = 0;
+    }
+    __syncthreads();
+    const uint64_t* sorted = depth_sorted(items0, items1, dstats);
+    uint64_t* srect = const_cast<uint64_t*>(sorted == items0 ? items1 : items0);
+    uint64_t b, e;
+    chunk_range(n, groups, blockIdx.x, kRowSources, b, e);
+    for (uint64_t c0 = b; c0 < e; c0 += 1024) {
+        uint32_t gi[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t j = c0 + t + 256 * k;
+            gi[k] = j < e ? (uint32_t)sorted[j] : 0u;
+        }
+        uint64_t r[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t j = c0 + t + 256 * k;
+            r[k] = j < e ? rect[gi[k]] : kDeadRect;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t j = c0 + t + 256 * k;
+            if (j < e) srect[j] = r[k];
+            const uint32_t rows = rect_rows(r[k]);
+            if (rows) {
+                const uint32_t ty0 = (uint32_t)((r[k] >> 32) & 0xffffu), cols = rect_cols(r[k]);
+                for (uint32_t q = 0; q < rows; q++) {
+                    atomicAdd(&h_items[w][ty0 + q], 1u);
+                    atomicAdd(&h_pairs[w][ty0 + q], cols);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    hist[t * (uint32_t)groups + blockIdx.x] = h_items[0][t] + h_items[1][t] + h_items[2][t] + h_items[3][t];
+    hist[(256 + t) * (uint32_t)groups + blockIdx.x] = h_pairs[0][t] + h_pairs[1][t] + h_pairs[2][t] + h_pairs[3][t];
+}
+
+// Row pass, scan: one workgroup per row.  Exclusive scan of the row's item
+// counts over the workgroups (in place) and the row's totals.
+__global__ __launch_bounds__(256) void k_bin_rows_scan(uint32_t* __restrict__ hist, int groups,
+                                                        uint32_t* __restrict__ row_items,
+                                                        unsigned long long* __restrict__ row_pairs) {
+    __shared__ uint32_t scr[4];
+    __shared__ unsigned long long scr64[4];
+    const uint32_t r = blockIdx.x, t = threadIdx.x;
+    uint32_t* hi = hist + (size_t)r * (uint32_t)groups;
+    const uint32_t* hp = hist + (size_t)(256 + r) * (uint32_t)groups;
+    const int per = (groups + 255) / 256;
+    const int b = (int)t * per;
+    uint32_t local = 0;
+    unsigned long long lp = 0;
+    for (int k = 0; k < per; k++)
+        if (b + k < groups) {
+            local += hi[b + k];
+            lp += hp[b + k];
+        }
+    uint32_t tot;
+    uint32_t run = block_exclusive_scan<uint32_t>(local, scr, tot);
+    unsigned long long ptot;
+    block_exclusive_scan<unsigned long long>(lp, scr64, ptot);
+    for (int k = 0; k < per; k++)
+        if (b + k < groups) {
+            const uint32_t v = hi[b + k];
+            hi[b + k] = run;
+            run += v;
+        }
+    if (t == 0) {
+        row_items[r] = tot;
+        row_pairs[r] = ptot;
+    }
+}
+
+// Row pass, scatter: the workgroup's Gaussians, 1024 at a time, expand into
+// their row items; tiles of 256*ITEMS items are ranked by row and written in
+// row runs to rows_out (positions >= cap are dropped; the frame then overflows
+// and the column pass emits nothing).  The sorted tile holds only each item's
+// source slot: the payload (index | tx0 << 32 | tx1 << 48) is rebuilt at the write.
+template <int ITEMS>
+__global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __restrict__ items0,
+                                                           const uint64_t* __restrict__ items1,
+                                                           const uint32_t* __restrict__ dstats, uint32_t n,
+                                                           int groups, const uint32_t* __restrict__ hist,
+                                                           const uint32_t* __restrict__ row_items,
+                                                           const unsigned long long* __restrict__ row_pairs,
+                                                           uint32_t cap, uint64_t* __restrict__ rows_out) {
+    constexpr uint32_t kTile = 256u * ITEMS;
+    __shared__ uint32_t s_cnt[kRowSources], s_pref[kRowSources], s_idx[kRowSources];
+    __shared__ uint64_t s_rect[kRowSources];
+    __shared__ uint16_t s_l[kTile];
+    __shared__ uint8_t s_dig[kTile];
+    __shared__ uint32_t s_wc[4][256], s_gbase[256], s_lbase[256], s_scr[4];
+    __shared__ unsigned long long s_scr64[4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    uint64_t b, e;
+    chunk_range(n, groups, blockIdx.x, kRowSources, b, e);
+    {
+        uint32_t tot;
+        s_gbase[t] = block_exclusive_scan<uint32_t>(row_items[t], s_scr, tot) + hist[t * (uint32_t)groups + blockIdx.x];
+        unsigned long long ptot;
+        block_exclusive_scan<unsigned long long>(row_pairs[t], s_scr64, ptot);
+        if (ptot > cap || b >= e) return;   // uniform: overflow frames stop here
+    }
+    const uint64_t* sorted = depth_sorted(items0, items1, dstats);
+    const uint64_t* srect = sorted == items0 ? items1 : items0;
+    for (uint64_t c0 = b; c0 < e; c0 += kRowSources) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t j = c0 + t + 256 * k;
+            const uint64_t r = j < e ? srect[j] : kDeadRect;
+            s_idx[t + 256 * k] = j < e ? (uint32_t)sorted[j] : 0u;
+            s_rect[t + 256 * k] = r;
+            s_cnt[t + 256 * k] = rect_rows(r);
+        }
+        __syncthreads();
+        const uint32_t total = bin_source_prefix<4>(s_cnt, s_pref, s_scr);
+        for (uint32_t tb = 0; tb < total; tb += kTile) {
+            const uint32_t tn = min(kTile, total - tb);
+            // branch-free generation: lanes past the tile's end repeat its last
+            // item (ranked as invalid), so the ITEMS independent searches overlap
+            uint32_t dig[ITEMS], pos[ITEMS], src[ITEMS];
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++)
+                src[k] = bin_find_source<kRowSources>(s_pref, tb + min(w * 64 * ITEMS + k * 64 + lane, tn - 1));
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++) {
+                const uint32_t q = tb + min(w * 64 * ITEMS + k * 64 + lane, tn - 1);
+                const uint32_t l = src[k];
+                dig[k] = (uint32_t)((s_rect[l] >> 32) & 0xffffu) + (q - (s_pref[l] - s_cnt[l]));
+            }
+            const uint32_t tcount = bin_rank_tile<ITEMS>(dig, tn, pos, s_wc, s_lbase, s_scr);
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++) {
+                const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
+                if (el < tn) {
+                    s_dig[pos[k]] = (uint8_t)dig[k];
+                    s_l[pos[k]] = (uint16_t)src[k];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++) {
+                const uint32_t q = t + 256 * k;
+                const uint32_t qc = min(q, tn - 1);
+                const uint32_t d = s_dig[qc], l = s_l[qc];
+                const uint32_t dst = s_gbase[d] + (qc - s_lbase[d]);
+                const uint64_t r = s_rect[l];
+                if (q < tn && dst < cap)
+                    rows_out[dst] = (uint64_t)s_idx[l] | ((r & 0xffffu) << 32) | (((r >> 16) & 0xffffu) << 48);
+            }
+            __syncthreads();
+            s_gbase[t] += tcount;
+        }
+    }
+}
+
+// Row geometry of the column pass, rebuilt by each workgroup from the row
+// totals: item base and count per row, first chunk per row (chunks of
+// kColChunk items never cross a row), chunk total, pair base per row, P.
+struct ColPlan {
+    uint32_t rbase[256], rcnt[256], chbase[257];
+    unsigned long long pbase[256];
+};
+
+__device__ __forceinline__ unsigned long long col_plan(const uint32_t* __restrict__ row_items,
+                                                       const unsigned long long* __restrict__ row_pairs,
+                                                       ColPlan& pl, uint32_t* s_scr,
+                                                       unsigned long long* s_scr64) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t cnt = row_items[t];
+    uint32_t tot;
+    pl.rbase[t] = block_exclusive_scan<uint32_t>(cnt, s_scr, tot);
+    pl.rcnt[t] = cnt;
+    pl.chbase[t] = block_exclusive_scan<uint32_t>((cnt + kColChunk - 1) / kColChunk, s_scr, tot);
+    if (t == 255) pl.chbase[256] = tot;
+    unsigned long long ptot;
+    pl.pbase[t] = block_exclusive_scan<unsigned long long>(row_pairs[t], s_scr64, ptot);
+    __syncthreads();
+    return ptot;
+}
+
+// Row of chunk c: the last row whose first chunk is <= c (empty rows own none).
+__device__ __forceinline__ uint32_t col_chunk_row(const ColPlan& pl, uint32_t c) {
+    uint32_t l = 0;
+#pragma unroll
+    for (uint32_t st = 128; st >= 1; st >>= 1)
+        if (pl.chbase[l + st] <= c) l += st;
+    return l;
+}
+
+// Column pass, count: per chunk, pairs per tile column -> cbins[chunk][col].
+__global__ __launch_bounds__(256) void k_bin_cols_count(const uint64_t* __restrict__ rows_in,
+                                                         const uint32_t* __restrict__ row_items,
+                                                         const unsigned long long* __restrict__ row_pairs,
+                                                         uint32_t cap, uint32_t* __restrict__ cbins) {
+    __shared__ ColPlan pl;
+    __shared__ uint32_t h[4][256], s_scr[4];
+    __shared__ unsigned long long s_scr64[4];
+    const uint32_t t = threadIdx.x, w = t >> 6;
+    if (col_plan(row_items, row_pairs, pl, s_scr, s_scr64) > cap) return;
+    const uint32_t nch = pl.chbase[256];
+    for (uint32_t c = blockIdx.x; c < nch; c += gridDim.x) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) h[k][t] = 0;
+        __syncthreads();
+        const uint32_t r = col_chunk_row(pl, c);
+        const uint32_t ib = pl.rbase[r] + (c - pl.chbase[r]) * kColChunk;
+        const uint32_t ie = min(ib + kColChunk, pl.rbase[r] + pl.rcnt[r]);
+        for (uint32_t i = ib + t; i < ie; i += 256) {
+            const uint64_t it = rows_in[i];
+            const uint32_t tx0 = (uint32_t)((it >> 32) & 0xffffu), tx1 = (uint32_t)(it >> 48);
+            for (uint32_t x = tx0; x <= tx1; x++) atomicAdd(&h[w][x], 1u);
+        }
+        __syncthreads();
+        cbins[(size_t)c * 256 + t] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
+        __syncthreads();
+    }
+}
+
+// Column pass, scan: one workgroup per row.  Exclusive scan of each column's
+// chunk counts over the row's chunks (in place), then the row's tiles: start =
+// row pair base + exclusive scan over columns; ranges = {~start, end} (zero =
+// empty).  Overflowed frames (P > cap) get empty ranges.  Workgroup 0 publishes
+// the frame's pair statistics.
+__global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restrict__ row_items,
+                                                        const unsigned long long* __restrict__ row_pairs,
+                                                        uint32_t cap, int tiles_x, uint32_t* __restrict__ cbins,
+                                                        uint2* __restrict__ ranges, Stats* __restrict__ st,
+                                                        Stats* host_st) {
+    __shared__ ColPlan pl;
+    __shared__ uint32_t s_scr[4];
+    __shared__ unsigned long long s_scr64[4];
+    const uint32_t t = threadIdx.x, r = blockIdx.x;
+    const unsigned long long P = col_plan(row_items, row_pairs, pl, s_scr, s_scr64);
+    if (r == 0 && t == 0) publish_pair_stats(P, cap, st, host_st);
+    uint32_t run = 0;
+    if (P <= cap) {
+        for (uint32_t c = pl.chbase[r]; c < pl.chbase[r + 1]; c++) {
+            const uint32_t v = cbins[(size_t)c * 256 + t];
+            cbins[(size_t)c * 256 + t] = run;
+            run += v;
+        }
+    }
+    uint32_t tot;
+    const uint32_t excl = block_exclusive_scan<uint32_t>(run, s_scr, tot);
+    if (t < (uint32_t)tiles_x) {
+        const uint32_t start = (uint32_t)pl.pbase[r] + excl;
+        ranges[r * (uint32_t)tiles_x + t] = run ? make_uint2(~start, start + run) : make_uint2(0u, 0u);
+    }
+}
+
+// Column pass, scatter: per chunk, its row items expand into one value per
+// covered column; tiles of 256*ITEMS values are ranked by column and written in
+// column runs at tile start + chunk offset.
+template <int ITEMS>
+__global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __restrict__ rows_in,
+                                                           const uint32_t* __restrict__ row_items,
+                                                           const unsigned long long* __restrict__ row_pairs,
+                                                           uint32_t cap, int tiles_x,
+                                                           const uint32_t* __restrict__ cbins,
+                                                           const uint2* __restrict__ ranges,
+                                                           uint32_t* __restrict__ vals) {
+    constexpr uint32_t kTile = 256u * ITEMS;
+    __shared__ ColPlan pl;
+    __shared__ uint32_t s_pref[kColChunk], s_idx[kColChunk];
+    __shared__ uint16_t s_cnt[kColChunk];
+    __shared__ uint8_t s_tx0[kColChunk];
+    __shared__ uint16_t s_l[kTile];
+    __shared__ uint8_t s_dig[kTile];
+    __shared__ uint32_t s_wc[4][256], s_gbase[256], s_lbase[256], s_scr[4];
+    __shared__ unsigned long long s_scr64[4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    if (col_plan(row_items, row_pairs, pl, s_scr, s_scr64) > cap) return;
+    const uint32_t nch = pl.chbase[256];
+    for (uint32_t c = blockIdx.x; c < nch; c += gridDim.x) {
+        const uint32_t r = col_chunk_row(pl, c);
+        const uint32_t ib = pl.rbase[r] + (c - pl.chbase[r]) * kColChunk;
+        const uint32_t m = min(kColChunk, pl.rbase[r] + pl.rcnt[r] - ib);
+        s_gbase[t] = t < (uint32_t)tiles_x ? ~ranges[r * (uint32_t)tiles_x + t].x + cbins[(size_t)c * 256 + t] : 0u;
+        uint32_t cnt[kColChunk / 256];
+#pragma unroll
+        for (int k = 0; k < (int)(kColChunk / 256); k++) {
+            const uint32_t j = t + 256 * k;
+            const uint64_t it = j < m ? rows_in[ib + j] : 0ull;
+            const uint32_t tx0 = (uint32_t)((it >> 32) & 0xffffu);
+            cnt[k] = j < m ? (uint32_t)(it >> 48) - tx0 + 1u : 0u;
+            s_idx[j] = (uint32_t)it;
+            s_tx0[j] = (uint8_t)tx0;
+            s_cnt[j] = (uint16_t)cnt[k];
+        }
+        __syncthreads();
+        uint32_t total;
+        {
+            // inclusive prefix in source order: thread t owns sources 8t .. 8t+7
+            constexpr int PER = kColChunk / 256;
+            uint32_t v[PER], loc = 0;
+#pragma unroll
+            for (int i = 0; i < PER; i++) {
+                v[i] = s_cnt[PER * t + i];
+                loc += v[i];
+            }
+            uint32_t run = block_exclusive_scan<uint32_t>(loc, s_scr, total);
+#pragma unroll
+            for (int i = 0; i < PER; i++) {
+                run += v[i];
+                s_pref[PER * t + i] = run;
+            }
+            __syncthreads();
+        }
+        for (uint32_t tb = 0; tb < total; tb += kTile) {
+            const uint32_t tn = min(kTile, total - tb);
+            // branch-free generation (see the row pass)
+            uint32_t dig[ITEMS], pos[ITEMS], src[ITEMS];
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++)
+                src[k] = bin_find_source<kColChunk>(s_pref, tb + min(w * 64 * ITEMS + k * 64 + lane, tn - 1));
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++) {
+                const uint32_t q = tb + min(w * 64 * ITEMS + k * 64 + lane, tn - 1);
+                const uint32_t l = src[k];
+                dig[k] = (uint32_t)s_tx0[l] + (q - (s_pref[l] - (uint32_t)s_cnt[l]));
+            }
+            const uint32_t tcount = bin_rank_tile<ITEMS>(dig, tn, pos, s_wc, s_lbase, s_scr);
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++) {
+                const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
+                if (el < tn) {
+                    s_dig[pos[k]] = (uint8_t)dig[k];
+                    s_l[pos[k]] = (uint16_t)src[k];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++) {
+                const uint32_t q = t + 256 * k;
+                const uint32_t qc = min(q, tn - 1);
+                const uint32_t d = s_dig[qc];
+                const uint32_t v = s_idx[s_l[qc]];
+                const uint32_t dst = s_gbase[d] + (qc - s_lbase[d]);
+                if (q < tn) vals[dst] = v;
+            }
+            __syncthreads();
+            s_gbase[t] += tcount;
+        }
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------------------ blend
 
 
@@ -1426,6 +1925,43 @@ hipError_t launch_emit(const uint64_t* items0, const uint64_t* items1, const uin
         hipLaunchKernelGGL(k_emit_pairs<uint32_t>, dim3(groups), dim3(256), 0, s, items0, items1, dstats, n, groups,
                            wg_scratch, pair_capacity, tiles_x, static_cast<uint32_t*>(keys), vals);
     return hipGetLastError();
+}
+
+hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,
+                           const uint64_t* rect, int groups, uint32_t* hist, uint32_t* row_items,
+                           unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
+                           int items, hipStream_t s) {
+    if (tiles_y < 1 || tiles_y > 256 || groups < 1 || groups > kMaxSortGroups / 2 ||
+        (items != 4 && items != 8 && items != 16))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_bin_rows_count, dim3(groups), dim3(256), 0, s, items0, items1, dstats, n, rect, groups,
+                       hist);
+    hipLaunchKernelGGL(k_bin_rows_scan, dim3(256), dim3(256), 0, s, hist, groups, row_items, row_pairs);
+    auto scatter = items == 4 ? k_bin_rows_scatter<4> : items == 8 ? k_bin_rows_scatter<8> : k_bin_rows_scatter<16>;
+    hipLaunchKernelGGL(scatter, dim3(groups), dim3(256), 0, s, items0, items1, dstats, n, groups, hist, row_items,
+                       row_pairs, pair_capacity, rows_buf);
+    return hipGetLastError();
+}
+
+hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, const unsigned long long* row_pairs,
+                           uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
+                           uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,
+                           hipStream_t s) {
+    if (tiles_x < 1 || tiles_x > 256 || tiles_y < 1 || tiles_y > 256 || col_groups < 1 ||
+        (items != 4 && items != 8 && items != 16))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_bin_cols_count, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs,
+                       pair_capacity, cbins);
+    hipLaunchKernelGGL(k_bin_cols_scan, dim3(tiles_y), dim3(256), 0, s, row_items, row_pairs, pair_capacity, tiles_x,
+                       cbins, ranges, stats, host_mapped_stats);
+    auto scatter = items == 4 ? k_bin_cols_scatter<4> : items == 8 ? k_bin_cols_scatter<8> : k_bin_cols_scatter<16>;
+    hipLaunchKernelGGL(scatter, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs, pair_capacity,
+                       tiles_x, cbins, ranges, vals);
+    return hipGetLastError();
+}
+
+uint32_t bin_col_chunks_max(uint32_t pair_capacity, int tiles_y) {
+    return pair_capacity / kColChunk + (uint32_t)tiles_y + 1u;
 }
 
 template <typename K, int ITEMS>

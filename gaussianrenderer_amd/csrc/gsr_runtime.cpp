@@ -331,6 +331,13 @@ struct gsr_context {
     int depth_skip = 1;              // depth sort: skip trailing identity passes (device-side plan)
     uint32_t* dstats = nullptr;      // depth-sort pass plan: 4 final words + 4 per upsweep workgroup
     int depth_groups = 0;            // depth sort: workgroup cap (0 = default)
+    int tile_binning = 1;            // row + column binning instead of emit + tile sort (grids <= 256 x 256)
+    int bin_row_items = 8;           // binning: items per thread of a row-pass tile (4 | 8 | 16)
+    int bin_col_items = 8;           // binning: items per thread of a column-pass tile (4 | 8 | 16)
+    int bin_col_groups = 1024;       // binning: column-pass workgroups (chunks are strided over them)
+    uint64_t* binmeta = nullptr;     // binning: row pair totals (u64 x 256) then row item totals (u32 x 256)
+    uint32_t* cbins = nullptr;       // binning: column counts per chunk (256 x chunks)
+    int64_t cbins_cap = 0;
     unsigned int* queue = nullptr;   // spare device counters (blend experiments)
     int resident_groups = 2048;      // workgroups of 256 that fit on the device at once
     // frame state
@@ -379,6 +386,7 @@ int ensure_static(gsr_context* c) {
     if (int rc = realloc_dev(&c->stats, 2)) return rc;
     if (int rc = realloc_dev(&c->queue, 8)) return rc;
     if (int rc = realloc_dev(&c->dstats, 4 + 4 * (size_t)gsr::kMaxSortGroups)) return rc;
+    if (int rc = realloc_dev(&c->binmeta, 256 + 128)) return rc;
     {
         int dev = 0, cus = 0;
         HIP_TRY(hipGetDevice(&dev));
@@ -526,7 +534,8 @@ extern "C" void gsr_destroy(gsr_context* c) {
     (void)hipDeviceSynchronize();
     for (auto* p : {(void*)c->rec, (void*)c->items[0], (void*)c->items[1], (void*)c->rect, (void*)c->pairs[0],
                     (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->queue, (void*)c->dstats,
-                    (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed})
+                    (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
+                    (void*)c->cbins})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -603,6 +612,31 @@ static int sort_locked(gsr_context* c) {
                                        c->hist, c->totals, nullptr, c->stream, c->depth_skip ? c->dstats : nullptr,
                                        p));
     // result in items[passes run & 1] (device-side plan; emission picks it)
+    if (c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256) {
+        // ---- row pass, then column pass (gsr_kernels.hip "tile binning") ----
+        const uint32_t cap = (uint32_t)c->p_cap;
+        const int64_t need = 256 * (int64_t)gsr::bin_col_chunks_max(cap, c->fr.tiles_y);
+        if (need > c->cbins_cap) {
+            HIP_TRY(hipDeviceSynchronize());
+            if (int rc = realloc_dev(&c->cbins, (size_t)need)) return rc;
+            c->cbins_cap = need;
+        }
+        auto* row_pairs = reinterpret_cast<unsigned long long*>(c->binmeta);
+        auto* row_items = reinterpret_cast<uint32_t*>(c->binmeta + 256);
+        const int gb = std::min(groups_for(c->n, 1024), gsr::kMaxSortGroups / 2);
+        mark(c, GSR_STAGE_EMIT);
+        HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n, c->rect, gb,
+                                     c->hist, row_items, row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items,
+                                     c->stream));
+        mark(c, GSR_STAGE_TILE_SORT);
+        HIP_TRY(gsr::launch_bin_cols(c->pairs[0], row_items, row_pairs, c->cbins, c->bin_col_groups, cap,
+                                     c->fr.tiles_x, c->fr.tiles_y, pair_vals(c, 1), c->ranges, c->stats,
+                                     c->hstats_dev, c->bin_col_items, c->stream));
+        c->pair_buf = 1;
+        mark(c, GSR_STAGE_RANGES);
+        c->have_sort = true;
+        return GSR_OK;
+    }
     // ---- pair emission in depth order (srect staged in the free items buffer) ----
     mark(c, GSR_STAGE_EMIT);
     const int ge = groups_for(c->n, 1024);
@@ -865,6 +899,19 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         if (value != 0 && value != 8 && value != 16)
             return set_err(GSR_E_ARG, "gsr_set_tuning: depth-sort items must be 0, 8 or 16");
         c->depth_items = value;
+        return GSR_OK;
+    case GSR_TUNE_TILE_BINNING:
+        c->tile_binning = value != 0;
+        return GSR_OK;
+    case GSR_TUNE_BIN_ROW_ITEMS:
+    case GSR_TUNE_BIN_COL_ITEMS:
+        if (value != 4 && value != 8 && value != 16)
+            return set_err(GSR_E_ARG, "gsr_set_tuning: binning items per thread must be 4, 8 or 16");
+        (knob == GSR_TUNE_BIN_ROW_ITEMS ? c->bin_row_items : c->bin_col_items) = value;
+        return GSR_OK;
+    case GSR_TUNE_BIN_COL_GROUPS:
+        if (value < 1 || value > 65536) return set_err(GSR_E_ARG, "gsr_set_tuning: bad column-pass group count");
+        c->bin_col_groups = value;
         return GSR_OK;
     case GSR_TUNE_DEPTH_SORT_SKIP:
         c->depth_skip = value != 0;

@@ -206,7 +206,12 @@ enum {
     GSR_TUNE_TILE_SORT_GROUPS = 3,   /* tile sort workgroup cap (default 1024; 0 = one per tile of items) */
     GSR_TUNE_DEPTH_SORT_GROUPS = 4,  /* depth sort workgroup cap (0 = one per tile of items) */
     GSR_TUNE_TILE_SORT_SPLIT = 5,    /* tile sort digits: 1 = split evenly (default), 0 = 8 bits first */
-    GSR_TUNE_DEPTH_SORT_SKIP = 6     /* depth sort: 1 = skip trailing identity passes (default), 0 = run all 4 */
+    GSR_TUNE_DEPTH_SORT_SKIP = 6,    /* depth sort: 1 = skip trailing identity passes (default), 0 = run all 4 */
+    GSR_TUNE_TILE_BINNING = 7,       /* 1 = row + column binning (default; tile grids <= 256 x 256),
+                                        0 = pair emission + key-value tile sort */
+    GSR_TUNE_BIN_ROW_ITEMS = 8,      /* binning row pass: items per thread per tile 4 | 8 | 16 (default 8) */
+    GSR_TUNE_BIN_COL_ITEMS = 9,      /* binning column pass: items per thread per tile 4 | 8 | 16 (default 8) */
+    GSR_TUNE_BIN_COL_GROUPS = 10     /* binning column pass: workgroups (default 1024) */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Depth-sort digit passes the last sorted frame ran (1..4; trailing identity

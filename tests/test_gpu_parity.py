@@ -171,6 +171,43 @@ def test_blend_tile_schedule_parity(gpu, orc, torch, c1, ci):
         assert_image_parity(got, want)
 
 
+@pytest.mark.parametrize("knobs", [{}, {8: 4, 9: 16}, {8: 16, 9: 4, 10: 7}])
+def test_tile_binning_matches_pair_sort(gpu, orc, torch, c1, knobs):
+    """Row + column binning (default for grids <= 256 x 256 tiles) gives the same
+    tile lists as pair emission + the key-value tile sort: identical (tile,
+    Gaussian) pairs in identical order, identical images, both equal to the
+    oracle.  Knobs 8/9: items per thread of the row / column tiles (4, 16);
+    10: column-pass workgroups (7 forces the grid-stride chunk loop)."""
+    path, soa = c1
+    W, H = 1000, 700
+    scene = gpu.Scene.from_soa(soa)
+    cam = cam_for(gpu, W, H, pos=(0.4, 0.3, 3.5))
+    r_bin, r_sort = gpu.Renderer(), gpu.Renderer()
+    for kn, v in knobs.items():
+        r_bin.set_tuning(kn, v)
+    r_sort.set_tuning(7, 0)
+    got_bin, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_bin)
+    got_sort, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_sort)
+    assert np.array_equal(got_bin.view(np.uint32), got_sort.view(np.uint32))
+    pb, ps = r_bin.read_pairs(), r_sort.read_pairs()
+    assert pb.shape == ps.shape and pb.shape[0] > 10_000
+    assert np.array_equal(pb, ps)
+    assert_image_parity(got_bin, orc.render(soa, cam, W, H, 3.0))
+
+
+def test_tile_binning_wide_frame_falls_back(gpu, orc, torch, c1):
+    """More than 256 tile columns (W > 4096): the pair sort path renders it."""
+    path, soa = c1
+    W, H = 4200, 40
+    scene = gpu.Scene.from_soa(soa)
+    cam = cam_for(gpu, W, H)
+    got, r = render_gpu(gpu, torch, scene, cam, W, H)
+    assert r.tile_grid()[0] > 256
+    want = orc.render(soa, cam, W, H, 3.0)
+    assert (want != 0).sum() > 1000
+    assert_image_parity(got, want)
+
+
 @pytest.mark.parametrize("pos,look", [((0, 0, 4), (0, 0, 0)), ((0, 0, 17.3), (0, 0, 0)), ((0, 0, 4), (0, 0, 9))])
 def test_depth_pass_plan_exact(gpu, orc, torch, c1, pos, look):
     """Trailing depth-sort passes are skipped on the device when they would be
