@@ -980,11 +980,15 @@ __device__ __forceinline__ uint32_t rect_cols(uint64_t r) {
     return rect_count(r) ? (uint32_t)(((r >> 16) & 0xffffu) - (r & 0xffffu) + 1u) : 0u;
 }
 
-// Stable rank of one tile of up to 256*ITEMS items with 8-bit digits.  Item k
-// of thread t is tile element w*64*ITEMS + k*64 + lane (each wave's items are
+// Stable rank of one tile of up to 256*ITEMS items with BITS-bit digits.  Item
+// k of thread t is tile element w*64*ITEMS + k*64 + lane (each wave's items are
 // contiguous).  On return pos[k] is the item's slot in the digit-sorted tile,
 // s_lbase[d] the first slot of digit d; returns the tile's count of digit t.
-template <int ITEMS>
+// Per k-slot every lane reads its digit's running wave count and the slot's
+// leader of each digit ADDS the slot's count (ds_add, no return): LDS ops of a
+// wave execute in issue order, so slot k's read sees slots < k and nothing waits
+// on a read before the next slot is issued.
+template <int ITEMS, int BITS>
 __device__ __forceinline__ uint32_t bin_rank_tile(const uint32_t (&dig)[ITEMS], uint32_t tn,
                                                   uint32_t (&pos)[ITEMS], uint32_t (*s_wc)[256],
                                                   uint32_t* s_lbase, uint32_t* s_scr) {
@@ -993,6 +997,7 @@ __device__ __forceinline__ uint32_t bin_rank_tile(const uint32_t (&dig)[ITEMS], 
 #pragma unroll
     for (int k = 0; k < 4; k++) s_wc[k][t] = 0;
     __syncthreads();
+    uint32_t before[ITEMS], inslot[ITEMS];
 #pragma unroll
     for (int k = 0; k < ITEMS; k++) {
         const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
@@ -1000,19 +1005,18 @@ __device__ __forceinline__ uint32_t bin_rank_tile(const uint32_t (&dig)[ITEMS], 
         const uint32_t d = dig[k];
         uint64_t peers = __ballot(valid);
 #pragma unroll
-        for (int bit = 0; bit < 8; bit++) {
+        for (int bit = 0; bit < BITS; bit++) {
             const bool on = (d >> bit) & 1u;
             const uint64_t bm = __ballot(on);
             peers &= on ? bm : ~bm;
         }
-        uint32_t r = 0;
-        if (valid) {
-            const uint32_t before = s_wc[w][d];
-            r = before + (uint32_t)__popcll(peers & lt_mask);
-            if ((uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane) s_wc[w][d] = before + (uint32_t)__popcll(peers);
-        }
-        pos[k] = r;
+        inslot[k] = (uint32_t)__popcll(peers & lt_mask);
+        before[k] = s_wc[w][d];
+        if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
+            atomicAdd(&s_wc[w][d], (uint32_t)__popcll(peers));
     }
+#pragma unroll
+    for (int k = 0; k < ITEMS; k++) pos[k] = before[k] + inslot[k];
     __syncthreads();
     uint32_t tcount;
     {
@@ -1034,37 +1038,69 @@ __device__ __forceinline__ uint32_t bin_rank_tile(const uint32_t (&dig)[ITEMS], 
     return tcount;
 }
 
-// Inclusive prefix (in source order) of per-source counts held in LDS s_cnt[m]
-// (m <= 256 * PER): thread t owns sources PER*t .. PER*t + PER-1.  Writes
-// s_pref and returns the total.  Two barriers.
+// Inclusive prefix (in source order) of per-source counts cnt[] (thread t owns
+// sources PER*t .. PER*t + PER-1): writes s_pref, returns each owned source's
+// exclusive start in start[] and the total.  Two barriers.
 template <int PER>
-__device__ __forceinline__ uint32_t bin_source_prefix(const uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_scr) {
+__device__ __forceinline__ uint32_t bin_source_prefix(const uint32_t (&cnt)[PER], uint32_t (&start)[PER],
+                                                      uint32_t* s_pref, uint32_t* s_scr) {
     const uint32_t t = threadIdx.x;
-    uint32_t v[PER], loc = 0;
+    uint32_t loc = 0;
 #pragma unroll
-    for (int i = 0; i < PER; i++) {
-        v[i] = s_cnt[PER * t + i];
-        loc += v[i];
-    }
+    for (int i = 0; i < PER; i++) loc += cnt[i];
     uint32_t tot;
     uint32_t run = block_exclusive_scan<uint32_t>(loc, s_scr, tot);
 #pragma unroll
     for (int i = 0; i < PER; i++) {
-        run += v[i];
+        start[i] = run;
+        run += cnt[i];
         s_pref[PER * t + i] = run;
     }
-    __syncthreads();
     return tot;
 }
 
-// First source l in [0, M) whose inclusive prefix exceeds q (q < total).
-template <uint32_t M>
-__device__ __forceinline__ uint32_t bin_find_source(const uint32_t* s_pref, uint32_t q) {
-    uint32_t l = 0;
+// Source of every element of the tile [tb, tb + tn) of a generated stream,
+// without a per-element search: each source starting inside the tile marks its
+// first element (slot + 1) in s_own (cleared beforehand), then an in-order
+// inclusive max-scan fills the runs.  `carry` (slot + 1 owning the element
+// before the tile; 0 at a stream's start) seeds the scan and becomes the owner
+// of the tile's last element.  The scan runs thread-major inside each wave
+// (lane handles elements w*64*ITEMS + lane*ITEMS + i), so every wave scans its
+// own ITEMS*64 elements in order.  Three barriers.
+template <int ITEMS, int PER>
+__device__ __forceinline__ void bin_tile_owners(const uint32_t (&cnt)[PER], const uint32_t (&start)[PER],
+                                                uint32_t tb, uint32_t tn, uint16_t* s_own, uint32_t& carry,
+                                                uint32_t* s_wmax) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
 #pragma unroll
-    for (uint32_t st = M / 2; st >= 1; st >>= 1)
-        if (s_pref[l + st - 1] <= q) l += st;
-    return l;
+    for (int i = 0; i < PER; i++)
+        if (cnt[i] && start[i] >= tb && start[i] < tb + tn) s_own[start[i] - tb] = (uint16_t)(PER * t + i + 1);
+    __syncthreads();
+    const uint32_t base = w * 64 * ITEMS + lane * ITEMS;
+    uint32_t v[ITEMS], run = 0;
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        run = max(run, (uint32_t)s_own[base + i]);
+        v[i] = run;
+    }
+    // exclusive max over the earlier lanes of the wave, then over earlier waves
+    uint32_t x = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x = max(x, y);
+    }
+    if (lane == 63) s_wmax[w] = x;
+    uint32_t before = __shfl_up(x, 1, 64);
+    if (lane == 0) before = 0;
+    __syncthreads();
+    uint32_t cin = carry;
+    for (uint32_t k = 0; k < w; k++) cin = max(cin, s_wmax[k]);
+    cin = max(cin, before);
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) s_own[base + i] = (uint16_t)max(cin, v[i]);
+    carry = max(max(carry, max(s_wmax[0], s_wmax[1])), max(s_wmax[2], s_wmax[3]));
+    __syncthreads();
 }
 
 // Frame pair statistics (st[0]) + the sticky copy (st[1], and the host-mapped
@@ -1182,7 +1218,7 @@ __global__ __launch_bounds__(256) void k_bin_rows_scan(uint32_t* __restrict__ hi
 // row runs to rows_out (positions >= cap are dropped; the frame then overflows
 // and the column pass emits nothing).  The sorted tile holds only each item's
 // source slot: the payload (index | tx0 << 32 | tx1 << 48) is rebuilt at the write.
-template <int ITEMS>
+template <int ITEMS, int BITS>
 __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __restrict__ items0,
                                                            const uint64_t* __restrict__ items1,
                                                            const uint32_t* __restrict__ dstats, uint32_t n,
@@ -1191,9 +1227,10 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
                                                            const unsigned long long* __restrict__ row_pairs,
                                                            uint32_t cap, uint64_t* __restrict__ rows_out) {
     constexpr uint32_t kTile = 256u * ITEMS;
-    __shared__ uint32_t s_cnt[kRowSources], s_pref[kRowSources], s_idx[kRowSources];
+    __shared__ uint32_t s_pref[kRowSources], s_idx[kRowSources];
     __shared__ uint64_t s_rect[kRowSources];
-    __shared__ uint16_t s_l[kTile];
+    __shared__ uint16_t s_l[kTile], s_own[kTile];
+    __shared__ uint32_t s_wmax[4];
     __shared__ uint8_t s_dig[kTile];
     __shared__ uint32_t s_wc[4][256], s_gbase[256], s_lbase[256], s_scr[4];
     __shared__ unsigned long long s_scr64[4];
@@ -1210,31 +1247,35 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
     const uint64_t* sorted = depth_sorted(items0, items1, dstats);
     const uint64_t* srect = sorted == items0 ? items1 : items0;
     for (uint64_t c0 = b; c0 < e; c0 += kRowSources) {
+        // thread t owns sources 4t .. 4t+3 of this sub-chunk (source order)
+        uint32_t cnt[4], start[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint64_t j = c0 + t + 256 * k;
+        for (int i = 0; i < 4; i++) {
+            const uint64_t j = c0 + 4 * t + i;
             const uint64_t r = j < e ? srect[j] : kDeadRect;
-            s_idx[t + 256 * k] = j < e ? (uint32_t)sorted[j] : 0u;
-            s_rect[t + 256 * k] = r;
-            s_cnt[t + 256 * k] = rect_rows(r);
+            s_idx[4 * t + i] = j < e ? (uint32_t)sorted[j] : 0u;
+            s_rect[4 * t + i] = r;
+            cnt[i] = rect_rows(r);
         }
-        __syncthreads();
-        const uint32_t total = bin_source_prefix<4>(s_cnt, s_pref, s_scr);
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) s_own[t * ITEMS + i] = 0;
+        const uint32_t total = bin_source_prefix<4>(cnt, start, s_pref, s_scr);
+        uint32_t carry = 0;
         for (uint32_t tb = 0; tb < total; tb += kTile) {
             const uint32_t tn = min(kTile, total - tb);
-            // branch-free generation: lanes past the tile's end repeat its last
-            // item (ranked as invalid), so the ITEMS independent searches overlap
+            bin_tile_owners<ITEMS, 4>(cnt, start, tb, tn, s_own, carry, s_wmax);
             uint32_t dig[ITEMS], pos[ITEMS], src[ITEMS];
 #pragma unroll
-            for (int k = 0; k < ITEMS; k++)
-                src[k] = bin_find_source<kRowSources>(s_pref, tb + min(w * 64 * ITEMS + k * 64 + lane, tn - 1));
-#pragma unroll
             for (int k = 0; k < ITEMS; k++) {
-                const uint32_t q = tb + min(w * 64 * ITEMS + k * 64 + lane, tn - 1);
-                const uint32_t l = src[k];
-                dig[k] = (uint32_t)((s_rect[l] >> 32) & 0xffffu) + (q - (s_pref[l] - s_cnt[l]));
+                const uint32_t el = min(w * 64 * ITEMS + k * 64 + lane, tn - 1);
+                const uint32_t l = (uint32_t)s_own[el] - 1u;
+                src[k] = l;
+                const uint32_t first = l ? s_pref[l - 1] : 0u;
+                dig[k] = (uint32_t)((s_rect[l] >> 32) & 0xffffu) + (tb + el - first);
             }
-            const uint32_t tcount = bin_rank_tile<ITEMS>(dig, tn, pos, s_wc, s_lbase, s_scr);
+            const uint32_t tcount = bin_rank_tile<ITEMS, BITS>(dig, tn, pos, s_wc, s_lbase, s_scr);
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) s_own[t * ITEMS + i] = 0;   // for the next tile (rank barriers passed)
 #pragma unroll
             for (int k = 0; k < ITEMS; k++) {
                 const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
@@ -1358,7 +1399,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restric
 // Column pass, scatter: per chunk, its row items expand into one value per
 // covered column; tiles of 256*ITEMS values are ranked by column and written in
 // column runs at tile start + chunk offset.
-template <int ITEMS>
+template <int ITEMS, int BITS>
 __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __restrict__ rows_in,
                                                            const uint32_t* __restrict__ row_items,
                                                            const unsigned long long* __restrict__ row_pairs,
@@ -1369,9 +1410,9 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
     constexpr uint32_t kTile = 256u * ITEMS;
     __shared__ ColPlan pl;
     __shared__ uint32_t s_pref[kColChunk], s_idx[kColChunk];
-    __shared__ uint16_t s_cnt[kColChunk];
     __shared__ uint8_t s_tx0[kColChunk];
-    __shared__ uint16_t s_l[kTile];
+    __shared__ uint16_t s_l[kTile], s_own[kTile];
+    __shared__ uint32_t s_wmax[4];
     __shared__ uint8_t s_dig[kTile];
     __shared__ uint32_t s_wc[4][256], s_gbase[256], s_lbase[256], s_scr[4];
     __shared__ unsigned long long s_scr64[4];
@@ -1383,50 +1424,37 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
         const uint32_t ib = pl.rbase[r] + (c - pl.chbase[r]) * kColChunk;
         const uint32_t m = min(kColChunk, pl.rbase[r] + pl.rcnt[r] - ib);
         s_gbase[t] = t < (uint32_t)tiles_x ? ~ranges[r * (uint32_t)tiles_x + t].x + cbins[(size_t)c * 256 + t] : 0u;
-        uint32_t cnt[kColChunk / 256];
+        // thread t owns row items PER*t .. PER*t + PER-1 of the chunk (source order)
+        constexpr int PER = kColChunk / 256;
+        uint32_t cnt[PER], start[PER];
 #pragma unroll
-        for (int k = 0; k < (int)(kColChunk / 256); k++) {
-            const uint32_t j = t + 256 * k;
+        for (int i = 0; i < PER; i++) {
+            const uint32_t j = PER * t + i;
             const uint64_t it = j < m ? rows_in[ib + j] : 0ull;
             const uint32_t tx0 = (uint32_t)((it >> 32) & 0xffffu);
-            cnt[k] = j < m ? (uint32_t)(it >> 48) - tx0 + 1u : 0u;
+            cnt[i] = j < m ? (uint32_t)(it >> 48) - tx0 + 1u : 0u;
             s_idx[j] = (uint32_t)it;
             s_tx0[j] = (uint8_t)tx0;
-            s_cnt[j] = (uint16_t)cnt[k];
         }
-        __syncthreads();
-        uint32_t total;
-        {
-            // inclusive prefix in source order: thread t owns sources 8t .. 8t+7
-            constexpr int PER = kColChunk / 256;
-            uint32_t v[PER], loc = 0;
 #pragma unroll
-            for (int i = 0; i < PER; i++) {
-                v[i] = s_cnt[PER * t + i];
-                loc += v[i];
-            }
-            uint32_t run = block_exclusive_scan<uint32_t>(loc, s_scr, total);
-#pragma unroll
-            for (int i = 0; i < PER; i++) {
-                run += v[i];
-                s_pref[PER * t + i] = run;
-            }
-            __syncthreads();
-        }
+        for (int i = 0; i < ITEMS; i++) s_own[t * ITEMS + i] = 0;
+        const uint32_t total = bin_source_prefix<PER>(cnt, start, s_pref, s_scr);
+        uint32_t carry = 0;
         for (uint32_t tb = 0; tb < total; tb += kTile) {
             const uint32_t tn = min(kTile, total - tb);
-            // branch-free generation (see the row pass)
+            bin_tile_owners<ITEMS, PER>(cnt, start, tb, tn, s_own, carry, s_wmax);
             uint32_t dig[ITEMS], pos[ITEMS], src[ITEMS];
 #pragma unroll
-            for (int k = 0; k < ITEMS; k++)
-                src[k] = bin_find_source<kColChunk>(s_pref, tb + min(w * 64 * ITEMS + k * 64 + lane, tn - 1));
-#pragma unroll
             for (int k = 0; k < ITEMS; k++) {
-                const uint32_t q = tb + min(w * 64 * ITEMS + k * 64 + lane, tn - 1);
-                const uint32_t l = src[k];
-                dig[k] = (uint32_t)s_tx0[l] + (q - (s_pref[l] - (uint32_t)s_cnt[l]));
+                const uint32_t el = min(w * 64 * ITEMS + k * 64 + lane, tn - 1);
+                const uint32_t l = (uint32_t)s_own[el] - 1u;
+                src[k] = l;
+                const uint32_t first = l ? s_pref[l - 1] : 0u;
+                dig[k] = (uint32_t)s_tx0[l] + (tb + el - first);
             }
-            const uint32_t tcount = bin_rank_tile<ITEMS>(dig, tn, pos, s_wc, s_lbase, s_scr);
+            const uint32_t tcount = bin_rank_tile<ITEMS, BITS>(dig, tn, pos, s_wc, s_lbase, s_scr);
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) s_own[t * ITEMS + i] = 0;   // for the next tile (rank barriers passed)
 #pragma unroll
             for (int k = 0; k < ITEMS; k++) {
                 const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
@@ -1937,7 +1965,10 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
     hipLaunchKernelGGL(k_bin_rows_count, dim3(groups), dim3(256), 0, s, items0, items1, dstats, n, rect, groups,
                        hist);
     hipLaunchKernelGGL(k_bin_rows_scan, dim3(256), dim3(256), 0, s, hist, groups, row_items, row_pairs);
-    auto scatter = items == 4 ? k_bin_rows_scatter<4> : items == 8 ? k_bin_rows_scatter<8> : k_bin_rows_scatter<16>;
+    auto scatter = tiles_y <= 128 ? (items == 4 ? k_bin_rows_scatter<4, 7> : items == 8 ? k_bin_rows_scatter<8, 7>
+                                                                                    : k_bin_rows_scatter<16, 7>)
+                                  : (items == 4 ? k_bin_rows_scatter<4, 8> : items == 8 ? k_bin_rows_scatter<8, 8>
+                                                                                    : k_bin_rows_scatter<16, 8>);
     hipLaunchKernelGGL(scatter, dim3(groups), dim3(256), 0, s, items0, items1, dstats, n, groups, hist, row_items,
                        row_pairs, pair_capacity, rows_buf);
     return hipGetLastError();
@@ -1954,7 +1985,10 @@ hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, 
                        pair_capacity, cbins);
     hipLaunchKernelGGL(k_bin_cols_scan, dim3(tiles_y), dim3(256), 0, s, row_items, row_pairs, pair_capacity, tiles_x,
                        cbins, ranges, stats, host_mapped_stats);
-    auto scatter = items == 4 ? k_bin_cols_scatter<4> : items == 8 ? k_bin_cols_scatter<8> : k_bin_cols_scatter<16>;
+    auto scatter = tiles_x <= 128 ? (items == 4 ? k_bin_cols_scatter<4, 7> : items == 8 ? k_bin_cols_scatter<8, 7>
+                                                                                    : k_bin_cols_scatter<16, 7>)
+                                  : (items == 4 ? k_bin_cols_scatter<4, 8> : items == 8 ? k_bin_cols_scatter<8, 8>
+                                                                                    : k_bin_cols_scatter<16, 8>);
     hipLaunchKernelGGL(scatter, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs, pair_capacity,
                        tiles_x, cbins, ranges, vals);
     return hipGetLastError();
