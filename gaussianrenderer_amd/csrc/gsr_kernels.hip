@@ -1163,19 +1163,29 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(const uint64_t* __restri
         for (int k = 0; k < 4; k++) {
             const uint64_t j = c0 + t + 256 * k;
             if (j < e) srect[j] = r[k];
-            const uint32_t rows = rect_rows(r[k]);
-            if (rows) {
-                const uint32_t ty0 = (uint32_t)((r[k] >> 32) & 0xffffu), cols = rect_cols(r[k]);
-                for (uint32_t q = 0; q < rows; q++) {
-                    atomicAdd(&h_items[w][ty0 + q], 1u);
-                    atomicAdd(&h_pairs[w][ty0 + q], cols);
+            // difference arrays: +1 / +cols at the first row, -1 / -cols past the last
+            if (rect_count(r[k])) {
+                const uint32_t ty0 = (uint32_t)((r[k] >> 32) & 0xffffu), ty1 = (uint32_t)(r[k] >> 48);
+                const uint32_t cols = rect_cols(r[k]);
+                atomicAdd(&h_items[w][ty0], 1u);
+                atomicAdd(&h_pairs[w][ty0], cols);
+                if (ty1 < 255u) {
+                    atomicSub(&h_items[w][ty1 + 1], 1u);
+                    atomicSub(&h_pairs[w][ty1 + 1], cols);
                 }
             }
         }
     }
     __syncthreads();
-    hist[t * (uint32_t)groups + blockIdx.x] = h_items[0][t] + h_items[1][t] + h_items[2][t] + h_items[3][t];
-    hist[(256 + t) * (uint32_t)groups + blockIdx.x] = h_pairs[0][t] + h_pairs[1][t] + h_pairs[2][t] + h_pairs[3][t];
+    // prefix over rows turns the differences into per-row counts (mod 2^32)
+    uint32_t ti, tp;
+    const uint32_t di = h_items[0][t] + h_items[1][t] + h_items[2][t] + h_items[3][t];
+    const uint32_t dp = h_pairs[0][t] + h_pairs[1][t] + h_pairs[2][t] + h_pairs[3][t];
+    __shared__ uint32_t scr[4];
+    const uint32_t ci = block_exclusive_scan<uint32_t>(di, scr, ti) + di;
+    const uint32_t cp = block_exclusive_scan<uint32_t>(dp, scr, tp) + dp;
+    hist[t * (uint32_t)groups + blockIdx.x] = ci;
+    hist[(256 + t) * (uint32_t)groups + blockIdx.x] = cp;
 }
 
 // Row pass, scan: one workgroup per row.  Exclusive scan of the row's item
@@ -1382,10 +1392,18 @@ __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restric
     if (r == 0 && t == 0) publish_pair_stats(P, cap, st, host_st);
     uint32_t run = 0;
     if (P <= cap) {
-        for (uint32_t c = pl.chbase[r]; c < pl.chbase[r + 1]; c++) {
-            const uint32_t v = cbins[(size_t)c * 256 + t];
-            cbins[(size_t)c * 256 + t] = run;
-            run += v;
+        // 8 chunks per step: the loads are issued together, not one round trip per chunk
+        const uint32_t c1 = pl.chbase[r + 1];
+        for (uint32_t c0 = pl.chbase[r]; c0 < c1; c0 += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[k] = c0 + k < c1 ? cbins[(size_t)(c0 + k) * 256 + t] : 0u;
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (c0 + k < c1) {
+                    cbins[(size_t)(c0 + k) * 256 + t] = run;
+                    run += v[k];
+                }
         }
     }
     uint32_t tot;
@@ -1567,12 +1585,18 @@ __device__ __forceinline__ f2 gsr_expf_x2(f2 xc) {
 // >= -10 (float error of the 9-op form < 10), so -md2/2 lies in gsr_expf_x2's
 // proven range; finite colours make "alpha = 0 when not taken" leave the
 // accumulators bit-identical (c + (col*0)*T == c, T*(1-0) == T).
+// Every coefficient is also 0 or of magnitude >= 2^-60: the pixel offsets are
+// integers, so every intermediate of the md2 form is a multiple of 2^-83 —
+// zero or a normal number — and scaling the coefficients by -0.5 scales every
+// intermediate exactly: the form on (-a/2, -b/2, -c/2, -e/2) IS -0.5f * md2.
+__device__ __forceinline__ bool coef_ok(float v) { return v == 0.0f || fabsf(v) >= 0x1p-60f; }
 __device__ __forceinline__ bool fast_safe(float a, float b, float c, float e, float M, float r, float g,
                                           float bl) {
     const float h = 0.5f * (b + c);
     const float S = fabsf(a) + fabsf(b) + fabsf(c) + fabsf(e);
     return a > 0.0f && e > 0.0f && (a * e - h * h) > 1e-4f * (a * e) && S * M * M <= 4e7f &&
-           isfinite(S) && isfinite(r) && isfinite(g) && isfinite(bl);
+           isfinite(S) && isfinite(r) && isfinite(g) && isfinite(bl) && coef_ok(a) && coef_ok(b) && coef_ok(c) &&
+           coef_ok(e);
 }
 
 // One wave64 per 8x8 pixel block (four per 16x16 tile, one tile per
@@ -1659,10 +1683,12 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
             const int h = (int)(k & 1u);
             S[0 + h] = (float)(int)rc.x;
             S[2 + h] = (float)(int)rc.y;
-            S[4 + h] = __uint_as_float(ra.x);
-            S[6 + h] = __uint_as_float(ra.y);
-            S[8 + h] = __uint_as_float(ra.z);
-            S[10 + h] = __uint_as_float(ra.w);
+            // fast batches store the conic pre-scaled by -0.5 (exact, see fast_safe)
+            const float sc = all_fast ? -0.5f : 1.0f;
+            S[4 + h] = sc * __uint_as_float(ra.x);
+            S[6 + h] = sc * __uint_as_float(ra.y);
+            S[8 + h] = sc * __uint_as_float(ra.z);
+            S[10 + h] = sc * __uint_as_float(ra.w);
             S[12 + h] = __uint_as_float(rb.x);
             S[14 + 2 * h] = __uint_as_float(rb.y);
             S[15 + 2 * h] = __uint_as_float(rb.z);
@@ -1686,6 +1712,12 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
 
         uint64_t mm = m;
         if (all_fast) {
+            // lanes not yet saturated; the end-of-iteration ballot of T2 is the next
+            // iteration's "!(T < 1e-3)" (render.cu:328), so it is compared once
+            uint64_t live = __ballot(!(T < 1e-3f));
+            f2 TT;
+            TT.x = T;
+            TT.y = T;
             for (uint32_t j = 0; mm && alive; ++j) {
                 const int s0 = __builtin_ctzll(mm);
                 mm &= mm - 1;
@@ -1699,36 +1731,41 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 box1 = has1 ? box1 : 0ull;
                 const float4 q0 = wP4[j * 5 + 0], q1 = wP4[j * 5 + 1], q2 = wP4[j * 5 + 2];
                 const float4 q3 = wP4[j * 5 + 3], q4 = wP4[j * 5 + 4];
-                // render.cu:329-332, same operation order, both splats at once
+                // render.cu:329-332, same operation order, both splats at once; the
+                // conic is stored pre-scaled by -0.5, so this is -0.5f * md2 exactly
                 const f2 dx = (f2)fpx - (f2){q0.x, q0.y};
                 const f2 dy = (f2)fpy - (f2){q0.z, q0.w};
-                const f2 md = dx * ((f2){q1.x, q1.y} * dx + (f2){q1.z, q1.w} * dy) +
-                              dy * ((f2){q2.x, q2.y} * dx + (f2){q2.z, q2.w} * dy);
-                const f2 ee = gsr_expf_x2(-0.5f * md);
+                const f2 mdh = dx * ((f2){q1.x, q1.y} * dx + (f2){q1.z, q1.w} * dy) +
+                               dy * ((f2){q2.x, q2.y} * dx + (f2){q2.z, q2.w} * dy);
+                const f2 ee = gsr_expf_x2(mdh);
                 const f2 al = (f2){q3.x, q3.y} * ee;
                 const float al0 = fminf(al.x, 0.99f), al1 = fminf(al.y, 0.99f);
                 // render.cu:333-340: splat 2j, then splat 2j+1 against what 2j left
-                const bool in0 = __builtin_amdgcn_inverse_ballot_w64(box0);
+                const bool in0 = __builtin_amdgcn_inverse_ballot_w64(box0 & live);
                 const bool in1 = __builtin_amdgcn_inverse_ballot_w64(box1);
-                const bool take0 = in0 & !(T < 1e-3f) & !(al0 < 1e-3f);
-                const float a0 = take0 ? al0 : 0.0f;
-                const float T1 = T * (1.0f - a0);
-                const bool take1 = in1 & !(T1 < 1e-3f) & !(al1 < 1e-3f);
-                const float a1 = take1 ? al1 : 0.0f;
-                const float T2 = T1 * (1.0f - a1);
-                crg = crg + ((f2){q3.z, q3.w} * a0) * T;
-                crg = crg + ((f2){q4.x, q4.y} * a1) * T1;
-                const f2 wb = ((f2){q4.z, q4.w} * (f2){a0, a1}) * (f2){T, T1};
+                // (a0, a1) and (T, T1) live in register pairs, written in place, so
+                // the packed blue product needs no moves; TT.x carries T across
+                const bool take0 = in0 & !(al0 < 1e-3f);
+                f2 AA;
+                AA.x = take0 ? al0 : 0.0f;
+                TT.y = TT.x * (1.0f - AA.x);
+                const bool take1 = in1 & !(TT.y < 1e-3f) & !(al1 < 1e-3f);
+                AA.y = take1 ? al1 : 0.0f;
+                crg = crg + ((f2){q3.z, q3.w} * AA.x) * TT.x;
+                crg = crg + ((f2){q4.x, q4.y} * AA.y) * TT.y;
+                const f2 wb = ((f2){q4.z, q4.w} * AA) * TT;
                 cb = (cb + wb.x) + wb.y;
                 if (DIAG) {
                     dg.iter += has1 ? 2 : 1;
-                    dg.active += (uint64_t)__popcll(__ballot(in0 & !(T < 1e-3f))) +
-                                (uint64_t)__popcll(__ballot(in1 & !(T1 < 1e-3f)));
+                    dg.active += (uint64_t)__popcll(__ballot(in0)) +
+                                (uint64_t)__popcll(__ballot(in1 & !(TT.y < 1e-3f)));
                     dg.taken += (uint64_t)__popcll(__ballot(take0)) + (uint64_t)__popcll(__ballot(take1));
                 }
-                T = T2;
-                alive = __ballot(!(T < 1e-3f)) != 0ull;   // whole block saturated -> stop
+                TT.x = TT.y * (1.0f - AA.y);
+                live = __ballot(!(TT.x < 1e-3f));
+                alive = live != 0ull;   // whole block saturated -> stop
             }
+            T = TT.x;
         } else {
             // exact one-splat path (render.cu:329-340 with gsr_expf and selects)
             for (uint32_t k = 0; mm && alive; ++k) {
