@@ -57,7 +57,8 @@ hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, con
 // passes >= 1 skip themselves when they would be identities (gsr_kernels.hip).
 hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
                              int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
-                             uint2* ranges, hipStream_t s, uint32_t* dstats = nullptr, int pass = 0);
+                             uint2* ranges, hipStream_t s, uint32_t* dstats = nullptr, int pass = 0,
+                             const uint64_t* rect = nullptr, uint64_t* srect = nullptr);
 // Pair emission in depth order: tile counts (gathering each Gaussian's rect
 // once into srect, and zeroing the tile ranges), scan, then keys (uint16_t if
 // key16 else uint32_t) + values.
@@ -80,7 +81,7 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
 // row_pairs: 256 each; cbins: 256 x bin_col_chunks_max(); rows_buf: pair
 // capacity 8-B row items; vals/ranges as the tile sort's final pass.
 hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,
-                           const uint64_t* rect, int groups, uint32_t* hist, uint32_t* row_items,
+                           const uint64_t* srect, int groups, uint32_t* hist, uint32_t* row_items,
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
                            int items, hipStream_t s);
 hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, const unsigned long long* row_pairs,

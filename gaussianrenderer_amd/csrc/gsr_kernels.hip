@@ -533,15 +533,21 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
     if (threadIdx.x == 0) totals[blockIdx.x] = total;
 }
 
+// rect != nullptr (depth sort feeding the tile binning): the pass that turns
+// out to be the last one (device plan: pass 3, or pass + 1 skipped) also writes
+// srect[dst] = rect[index] for every item — the compact tile rectangles in depth
+// order.  The gather is issued right after the item load, so its latency hides
+// behind the ranking; the row pass then reads srect coalesced.
 template <int ITEMS>
 __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const uint64_t* __restrict__ in, uint64_t* __restrict__ out, const uint32_t* __restrict__ n_dev,
     uint32_t n_host, int shift, int bits, int groups, const uint32_t* __restrict__ hist,
     const uint32_t* __restrict__ totals, uint2* __restrict__ ranges, const uint32_t* __restrict__ dstats,
-    int pass) {
+    int pass, const uint64_t* __restrict__ rect, uint64_t* __restrict__ srect) {
     constexpr int kTile = kSortThreads * ITEMS;
     __shared__ uint64_t s_items[kTile];
     if (depth_pass_skipped(dstats, pass)) return;
+    const bool gather = rect && (pass == 3 || depth_pass_skipped(dstats, pass + 1));
     __shared__ uint32_t s_wc[4][256];           // per-wave digit counters, then wave bases
     __shared__ uint32_t s_gbase[256];           // running global offset per digit
     __shared__ uint32_t s_lbase[256];           // tile-local exclusive base per digit
@@ -569,13 +575,20 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
         for (int k = 0; k < 4; k++) s_wc[k][t] = 0;
         __syncthreads();
 
-        uint64_t it[ITEMS];
+        uint64_t it[ITEMS], rc[ITEMS];
         uint32_t rk[ITEMS];
         const uint32_t wbase = w * 64 * ITEMS;
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             it[k] = (el < tn) ? in[tb + el] : 0ull;
+        }
+        if (gather) {
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++) {
+                const uint32_t el = wbase + k * 64 + lane;
+                rc[k] = (el < tn) ? rect[(uint32_t)it[k]] : 0ull;
+            }
         }
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
@@ -617,6 +630,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
             if (el < tn) {
                 const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
                 s_items[s_lbase[d] + s_wc[w][d] + rk[k]] = it[k];
+                if (gather) srect[s_gbase[d] + s_wc[w][d] + rk[k]] = rc[k];
             }
         }
         __syncthreads();
@@ -1127,13 +1141,10 @@ __device__ __forceinline__ void publish_pair_stats(unsigned long long total, uin
 
 // Row pass, count: per workgroup (1024-Gaussian sub-chunks in depth order) the
 // number of row items and of pairs per tile row; hist[row][g] and
-// hist[256 + row][g].  Gathers each Gaussian's rect once and stores it in depth
-// order (srect, the free depth-sort buffer) for the scatter.
-__global__ __launch_bounds__(256) void k_bin_rows_count(const uint64_t* __restrict__ items0,
-                                                         const uint64_t* __restrict__ items1,
-                                                         const uint32_t* __restrict__ dstats, uint32_t n,
-                                                         const uint64_t* __restrict__ rect, int groups,
-                                                         uint32_t* __restrict__ hist) {
+// hist[256 + row][g].  Reads the rects in depth order (srect, written by the
+// depth sort's last downsweep).
+__global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint64_t* __restrict__ srect, int groups,
+                                                         int tiles_y, uint32_t* __restrict__ hist) {
     __shared__ uint32_t h_items[4][256], h_pairs[4][256];
     const uint32_t t = threadIdx.x, w = t >> 6;
 #pragma unroll
@@ -1142,27 +1153,17 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(const uint64_t* __restri
         h_pairs[k][t] = 0;
     }
     __syncthreads();
-    const uint64_t* sorted = depth_sorted(items0, items1, dstats);
-    uint64_t* srect = const_cast<uint64_t*>(sorted == items0 ? items1 : items0);
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, kRowSources, b, e);
     for (uint64_t c0 = b; c0 < e; c0 += 1024) {
-        uint32_t gi[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint64_t j = c0 + t + 256 * k;
-            gi[k] = j < e ? (uint32_t)sorted[j] : 0u;
-        }
         uint64_t r[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const uint64_t j = c0 + t + 256 * k;
-            r[k] = j < e ? rect[gi[k]] : kDeadRect;
+            r[k] = j < e ? srect[j] : kDeadRect;
         }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const uint64_t j = c0 + t + 256 * k;
-            if (j < e) srect[j] = r[k];
             // difference arrays: +1 / +cols at the first row, -1 / -cols past the last
             if (rect_count(r[k])) {
                 const uint32_t ty0 = (uint32_t)((r[k] >> 32) & 0xffffu), ty1 = (uint32_t)(r[k] >> 48);
@@ -1184,18 +1185,27 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(const uint64_t* __restri
     __shared__ uint32_t scr[4];
     const uint32_t ci = block_exclusive_scan<uint32_t>(di, scr, ti) + di;
     const uint32_t cp = block_exclusive_scan<uint32_t>(dp, scr, tp) + dp;
-    hist[t * (uint32_t)groups + blockIdx.x] = ci;
-    hist[(256 + t) * (uint32_t)groups + blockIdx.x] = cp;
+    if (t < (uint32_t)tiles_y) {   // rows past the grid hold nothing: no scattered writes for them
+        hist[t * (uint32_t)groups + blockIdx.x] = ci;
+        hist[(256 + t) * (uint32_t)groups + blockIdx.x] = cp;
+    }
 }
 
 // Row pass, scan: one workgroup per row.  Exclusive scan of the row's item
 // counts over the workgroups (in place) and the row's totals.
-__global__ __launch_bounds__(256) void k_bin_rows_scan(uint32_t* __restrict__ hist, int groups,
+__global__ __launch_bounds__(256) void k_bin_rows_scan(uint32_t* __restrict__ hist, int groups, int tiles_y,
                                                         uint32_t* __restrict__ row_items,
                                                         unsigned long long* __restrict__ row_pairs) {
     __shared__ uint32_t scr[4];
     __shared__ unsigned long long scr64[4];
     const uint32_t r = blockIdx.x, t = threadIdx.x;
+    if (r >= (uint32_t)tiles_y) {   // all 256 row totals are read downstream
+        if (t == 0) {
+            row_items[r] = 0;
+            row_pairs[r] = 0;
+        }
+        return;
+    }
     uint32_t* hi = hist + (size_t)r * (uint32_t)groups;
     const uint32_t* hp = hist + (size_t)(256 + r) * (uint32_t)groups;
     const int per = (groups + 255) / 256;
@@ -1231,11 +1241,12 @@ __global__ __launch_bounds__(256) void k_bin_rows_scan(uint32_t* __restrict__ hi
 template <int ITEMS, int BITS>
 __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __restrict__ items0,
                                                            const uint64_t* __restrict__ items1,
-                                                           const uint32_t* __restrict__ dstats, uint32_t n,
+                                                           const uint32_t* __restrict__ dstats,
+                                                           const uint64_t* __restrict__ srect, uint32_t n,
                                                            int groups, const uint32_t* __restrict__ hist,
                                                            const uint32_t* __restrict__ row_items,
                                                            const unsigned long long* __restrict__ row_pairs,
-                                                           uint32_t cap, uint64_t* __restrict__ rows_out) {
+                                                           uint32_t cap, int tiles_y, uint64_t* __restrict__ rows_out) {
     constexpr uint32_t kTile = 256u * ITEMS;
     __shared__ uint32_t s_pref[kRowSources], s_idx[kRowSources];
     __shared__ uint64_t s_rect[kRowSources];
@@ -1249,13 +1260,13 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
     chunk_range(n, groups, blockIdx.x, kRowSources, b, e);
     {
         uint32_t tot;
-        s_gbase[t] = block_exclusive_scan<uint32_t>(row_items[t], s_scr, tot) + hist[t * (uint32_t)groups + blockIdx.x];
+        s_gbase[t] = block_exclusive_scan<uint32_t>(row_items[t], s_scr, tot) +
+                     (t < (uint32_t)tiles_y ? hist[t * (uint32_t)groups + blockIdx.x] : 0u);
         unsigned long long ptot;
         block_exclusive_scan<unsigned long long>(row_pairs[t], s_scr64, ptot);
         if (ptot > cap || b >= e) return;   // uniform: overflow frames stop here
     }
     const uint64_t* sorted = depth_sorted(items0, items1, dstats);
-    const uint64_t* srect = sorted == items0 ? items1 : items0;
     for (uint64_t c0 = b; c0 < e; c0 += kRowSources) {
         // thread t owns sources 4t .. 4t+3 of this sub-chunk (source order)
         uint32_t cnt[4], start[4];
@@ -1349,7 +1360,7 @@ __device__ __forceinline__ uint32_t col_chunk_row(const ColPlan& pl, uint32_t c)
 __global__ __launch_bounds__(256) void k_bin_cols_count(const uint64_t* __restrict__ rows_in,
                                                          const uint32_t* __restrict__ row_items,
                                                          const unsigned long long* __restrict__ row_pairs,
-                                                         uint32_t cap, uint32_t* __restrict__ cbins) {
+                                                         uint32_t cap, int tiles_x, uint32_t* __restrict__ cbins) {
     __shared__ ColPlan pl;
     __shared__ uint32_t h[4][256], s_scr[4];
     __shared__ unsigned long long s_scr64[4];
@@ -1369,7 +1380,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_count(const uint64_t* __restri
             for (uint32_t x = tx0; x <= tx1; x++) atomicAdd(&h[w][x], 1u);
         }
         __syncthreads();
-        cbins[(size_t)c * 256 + t] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
+        if (t < (uint32_t)tiles_x) cbins[(size_t)c * 256 + t] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
         __syncthreads();
     }
 }
@@ -1391,7 +1402,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restric
     const unsigned long long P = col_plan(row_items, row_pairs, pl, s_scr, s_scr64);
     if (r == 0 && t == 0) publish_pair_stats(P, cap, st, host_st);
     uint32_t run = 0;
-    if (P <= cap) {
+    if (P <= cap && t < (uint32_t)tiles_x) {
         // 8 chunks per step: the loads are issued together, not one round trip per chunk
         const uint32_t c1 = pl.chbase[r + 1];
         for (uint32_t c0 = pl.chbase[r]; c0 < c1; c0 += 8) {
@@ -1955,23 +1966,27 @@ hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, con
 template <int ITEMS>
 static void radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host, int shift,
                        int bits, int groups, uint32_t* hist, uint32_t* totals, uint2* ranges, uint32_t* dstats,
-                       int pass, hipStream_t s) {
+                       int pass, const uint64_t* rect, uint64_t* srect, hipStream_t s) {
     const uint32_t mask = (1u << bits) - 1u;
     hipLaunchKernelGGL(k_radix_upsweep<ITEMS>, dim3(groups), dim3(kSortThreads), 0, s, in, n_dev, n_host, shift,
                        mask, groups, hist, dstats, pass);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, hist, groups, totals,
                        static_cast<const uint32_t*>(dstats), pass);
     hipLaunchKernelGGL(k_radix_downsweep<ITEMS>, dim3(groups), dim3(kSortThreads), 0, s, in, out, n_dev, n_host,
-                       shift, bits, groups, hist, totals, ranges, static_cast<const uint32_t*>(dstats), pass);
+                       shift, bits, groups, hist, totals, ranges, static_cast<const uint32_t*>(dstats), pass, rect,
+                       srect);
 }
 
 hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
                              int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
-                             uint2* ranges, hipStream_t s, uint32_t* dstats, int pass) {
+                             uint2* ranges, hipStream_t s, uint32_t* dstats, int pass, const uint64_t* rect,
+                             uint64_t* srect) {
+    if ((rect == nullptr) != (srect == nullptr)) return hipErrorInvalidValue;
     if (items == 8)
-        radix_pass<8>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, s);
+        radix_pass<8>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect, srect, s);
     else
-        radix_pass<16>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, s);
+        radix_pass<16>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect, srect,
+                       s);
     return hipGetLastError();
 }
 
@@ -1993,21 +2008,20 @@ hipError_t launch_emit(const uint64_t* items0, const uint64_t* items1, const uin
 }
 
 hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,
-                           const uint64_t* rect, int groups, uint32_t* hist, uint32_t* row_items,
+                           const uint64_t* srect, int groups, uint32_t* hist, uint32_t* row_items,
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
                            int items, hipStream_t s) {
     if (tiles_y < 1 || tiles_y > 256 || groups < 1 || groups > kMaxSortGroups / 2 ||
         (items != 4 && items != 8 && items != 16))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_bin_rows_count, dim3(groups), dim3(256), 0, s, items0, items1, dstats, n, rect, groups,
-                       hist);
-    hipLaunchKernelGGL(k_bin_rows_scan, dim3(256), dim3(256), 0, s, hist, groups, row_items, row_pairs);
+    hipLaunchKernelGGL(k_bin_rows_count, dim3(groups), dim3(256), 0, s, n, srect, groups, tiles_y, hist);
+    hipLaunchKernelGGL(k_bin_rows_scan, dim3(256), dim3(256), 0, s, hist, groups, tiles_y, row_items, row_pairs);
     auto scatter = tiles_y <= 128 ? (items == 4 ? k_bin_rows_scatter<4, 7> : items == 8 ? k_bin_rows_scatter<8, 7>
                                                                                     : k_bin_rows_scatter<16, 7>)
                                   : (items == 4 ? k_bin_rows_scatter<4, 8> : items == 8 ? k_bin_rows_scatter<8, 8>
                                                                                     : k_bin_rows_scatter<16, 8>);
-    hipLaunchKernelGGL(scatter, dim3(groups), dim3(256), 0, s, items0, items1, dstats, n, groups, hist, row_items,
-                       row_pairs, pair_capacity, rows_buf);
+    hipLaunchKernelGGL(scatter, dim3(groups), dim3(256), 0, s, items0, items1, dstats, srect, n, groups, hist,
+                       row_items, row_pairs, pair_capacity, tiles_y, rows_buf);
     return hipGetLastError();
 }
 
@@ -2019,7 +2033,7 @@ hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, 
         (items != 4 && items != 8 && items != 16))
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_bin_cols_count, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs,
-                       pair_capacity, cbins);
+                       pair_capacity, tiles_x, cbins);
     hipLaunchKernelGGL(k_bin_cols_scan, dim3(tiles_y), dim3(256), 0, s, row_items, row_pairs, pair_capacity, tiles_x,
                        cbins, ranges, stats, host_mapped_stats);
     auto scatter = tiles_x <= 128 ? (items == 4 ? k_bin_cols_scatter<4, 7> : items == 8 ? k_bin_cols_scatter<8, 7>

@@ -311,6 +311,7 @@ struct gsr_context {
     // pair buffers: p_cap u64 each, used as {keys: p_cap x 4 B, values: p_cap x 4 B}
     uint64_t* pairs[2] = {nullptr, nullptr};
     uint64_t* rect = nullptr;        // per-Gaussian tile rectangle (preprocess output)
+    uint64_t* srect = nullptr;       // the rectangles in depth order (last depth pass, binning path)
     uint32_t* hist = nullptr;
     uint32_t* totals = nullptr;
     unsigned long long* wg = nullptr;
@@ -409,6 +410,7 @@ int ensure_n(gsr_context* c, int64_t n) {
     if (int rc = realloc_dev(&c->items[0], (size_t)cap)) return rc;
     if (int rc = realloc_dev(&c->items[1], (size_t)cap)) return rc;
     if (int rc = realloc_dev(&c->rect, (size_t)cap)) return rc;
+    if (int rc = realloc_dev(&c->srect, (size_t)cap)) return rc;
     c->n_cap = cap;
     if (c->p_cap < 4 * cap) {
         const int64_t pc = std::min<int64_t>(std::max<int64_t>(4 * cap, 1 << 20), 0xffffffffLL);
@@ -535,7 +537,7 @@ extern "C" void gsr_destroy(gsr_context* c) {
     for (auto* p : {(void*)c->rec, (void*)c->items[0], (void*)c->items[1], (void*)c->rect, (void*)c->pairs[0],
                     (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->queue, (void*)c->dstats,
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
-                    (void*)c->cbins})
+                    (void*)c->cbins, (void*)c->srect})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -601,7 +603,9 @@ static uint32_t* pair_vals(gsr_context* c, int b) {
 static int sort_locked(gsr_context* c) {
     if (!c->have_pre) return set_err(GSR_E_ARG, "gsr_sort before gsr_preprocess");
     const uint32_t n = (uint32_t)c->n;
-    // ---- stable depth sort of (key << 32 | index), 4 x 8 bits ----
+    const bool bin = c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
+    // ---- stable depth sort of (key << 32 | index), 4 x 8 bits; for the binning
+    // path its last pass also writes the rects in depth order (srect) ----
     mark(c, GSR_STAGE_DEPTH_SORT);
     // smaller tiles for the 1M-item depth sort: ~500 workgroups instead of ~250
     const int di = c->depth_items ? c->depth_items : (c->n < (int64_t(4) << 20) ? 8 : 16);
@@ -610,9 +614,9 @@ static int sort_locked(gsr_context* c) {
     for (int p = 0; p < 4; p++)
         HIP_TRY(gsr::launch_radix_pass(c->items[p & 1], c->items[(p + 1) & 1], nullptr, n, 32 + 8 * p, 8, gd, di,
                                        c->hist, c->totals, nullptr, c->stream, c->depth_skip ? c->dstats : nullptr,
-                                       p));
+                                       p, bin ? c->rect : nullptr, bin ? c->srect : nullptr));
     // result in items[passes run & 1] (device-side plan; emission picks it)
-    if (c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256) {
+    if (bin) {
         // ---- row pass, then column pass (gsr_kernels.hip "tile binning") ----
         const uint32_t cap = (uint32_t)c->p_cap;
         const int64_t need = 256 * (int64_t)gsr::bin_col_chunks_max(cap, c->fr.tiles_y);
@@ -625,7 +629,7 @@ static int sort_locked(gsr_context* c) {
         auto* row_items = reinterpret_cast<uint32_t*>(c->binmeta + 256);
         const int gb = std::min(groups_for(c->n, 1024), gsr::kMaxSortGroups / 2);
         mark(c, GSR_STAGE_EMIT);
-        HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n, c->rect, gb,
+        HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n, c->srect, gb,
                                      c->hist, row_items, row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items,
                                      c->stream));
         mark(c, GSR_STAGE_TILE_SORT);
