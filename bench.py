@@ -4,7 +4,7 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|1]
 
 One step = one full frame through the native pipeline (preprocess -> depth
-sort -> pair emission -> tile sort -> ranges -> blend) on the synthetic scene
+sort -> tile binning: row pass + column pass -> blend) on the synthetic scene
 of BASELINE config 2 (1M Gaussians, 1920x1080, seed 2, camera at (0,0,4),
 fovY 50, k = 3), with the scene and the output image resident in HBM.
 
@@ -71,18 +71,29 @@ def algorithmic_blend_bytes(ntiles: int, consumed: int, W: int, H: int) -> int:
 
 
 def algorithmic_stage_bytes(n: int, m: int, pairs: int, ntiles: int, consumed: int, W: int, H: int,
-                            depth_passes: int = 4, tile_passes: int = 2) -> dict:
+                            depth_passes: int = 4, tile_passes: int = 2, row_items: int = -1) -> dict:
     """Minimal bytes each stage of this design must move (per-stage table):
     preprocess N*152 read (38 fp32 SoA arrays) + M*64 records + N*16 (item + tile rect);
-    depth sort passes*N*24 (upsweep read 8, downsweep read 8 + write 8);
-    emit N*40 (sorted items twice, rect gather, srect write/read) + P*6 (u16 key + u32 value);
-    tile sort P*14 per non-final pass, P*12 for the final one (keys 2 up, 6 read, 6|4 write) + T*8;
-    blend as algorithmic_blend_bytes."""
-    return {"preprocess": 152 * n + 64 * m + 16 * n,
-            "depth_sort": depth_passes * 24 * n,
-            "emit": 40 * n + 6 * pairs,
-            "tile_sort": 14 * pairs * (tile_passes - 1) + 12 * pairs + 8 * ntiles,
-            "blend": algorithmic_blend_bytes(ntiles, consumed, W, H)}
+    blend as algorithmic_blend_bytes.
+    Tile binning (row_items R >= 0): depth sort passes*N*24 (upsweep read 8, downsweep
+    read 8 + write 8) + N*16 (last pass: rect gather + depth-ordered rect write);
+    row pass ("emit") N*24 (rects for the count, items + rects for the scatter) +
+    R*8 row items; column pass ("tile_sort") R*16 (count + scatter reads) + P*4
+    values + T*8 ranges.
+    Pair sort (R < 0): depth sort passes*N*24; emit N*40 (sorted items twice, rect
+    gather, srect write/read) + P*6 (u16 key + u32 value); tile sort P*14 per
+    non-final pass, P*12 for the final one (keys 2 up, 6 read, 6|4 write) + T*8."""
+    out = {"preprocess": 152 * n + 64 * m + 16 * n,
+           "blend": algorithmic_blend_bytes(ntiles, consumed, W, H)}
+    if row_items >= 0:
+        out.update({"depth_sort": depth_passes * 24 * n + 16 * n,
+                    "emit": 24 * n + 8 * row_items,
+                    "tile_sort": 16 * row_items + 4 * pairs + 8 * ntiles})
+    else:
+        out.update({"depth_sort": depth_passes * 24 * n,
+                    "emit": 40 * n + 6 * pairs,
+                    "tile_sort": 14 * pairs * (tile_passes - 1) + 12 * pairs + 8 * ntiles})
+    return out
 
 
 VALU_PEAK_PER_SIMD_CYCLE = 0.5   # wave64 non-packed VALU issue: one per 2 cycles per SIMD (32 lanes)
@@ -235,6 +246,8 @@ def main():
     r.render(scene, cam, W, H, outs[0].data_ptr(), k=args.k, stream=stream, time=t_mid)
     r.sync()
     pairs = r.pair_count()
+    row_items = r.row_item_count()
+    depth_passes = r.depth_passes()
     counters = r.blend_counters()
     consumed = counters["records_loaded"]
     r.set_diagnostics(False)
@@ -314,6 +327,8 @@ def main():
                      "algorithmic_bytes": bytes_blend},
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
         "pairs": pairs,
+        "row_items": row_items,
+        "depth_passes": depth_passes,
         "pairs_consumed": consumed,
         "blend_counters": counters,
         "blend_lane_efficiency": round(counters["active_lanes"] / max(1, counters["lane_slots"]), 4),
@@ -322,7 +337,8 @@ def main():
     }
     if gather_ms is not None:
         result["gather_ms"] = round(gather_ms, 3)
-    sb = algorithmic_stage_bytes(n, visible, pairs, ntiles, consumed, W, H)
+    sb = algorithmic_stage_bytes(n, visible, pairs, ntiles, consumed, W, H, depth_passes=depth_passes,
+                                 row_items=row_items)
     result["stages_gbs"] = {k: round(sb[k] / (stages[k] * 1e-3) / 1e9, 1) for k in sb if stages.get(k)}
     result["stages_gbs"]["blend"] = round(achieved, 1)     # timed frames, not the diagnostics frame
     result["stages_algorithmic_bytes"] = sb

@@ -333,6 +333,10 @@ class Renderer:
     def pair_count(self) -> int:
         return int(lib().gsr_pair_count(self.ctx))
 
+    def row_item_count(self) -> int:
+        """(tile row, Gaussian) items of the last frame's row pass; -1 on the pair-sort path."""
+        return int(lib().gsr_row_item_count(self.ctx))
+
     def read_splats(self, n: int) -> np.ndarray:
         out = np.zeros(n, dtype=SPLAT_DTYPE)
         check(lib().gsr_read_splats(self.ctx, out.ctypes.data, n), "gsr_read_splats")

@@ -107,6 +107,7 @@ SIGNATURES = [
     ("gsr_blend", c_int, [c_void_p, c_void_p, c_void_p]),
     ("gsr_sync", c_int, [c_void_p]),
     ("gsr_pair_count", c_int64, [c_void_p]),
+    ("gsr_row_item_count", c_int64, [c_void_p]),
     ("gsr_read_splats", c_int, [c_void_p, c_void_p, c_int64]),
     ("gsr_read_depth_order", c_int, [c_void_p, c_void_p, c_int64]),
     ("gsr_read_pairs", c_int64, [c_void_p, c_void_p, c_int64]),

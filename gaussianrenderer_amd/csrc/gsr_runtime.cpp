@@ -339,6 +339,7 @@ struct gsr_context {
     uint64_t* binmeta = nullptr;     // binning: row pair totals (u64 x 256) then row item totals (u32 x 256)
     uint32_t* cbins = nullptr;       // binning: column counts per chunk (256 x chunks)
     int64_t cbins_cap = 0;
+    bool last_binned = false;        // the last sorted frame took the binning path
     unsigned int* queue = nullptr;   // spare device counters (blend experiments)
     int resident_groups = 2048;      // workgroups of 256 that fit on the device at once
     // frame state
@@ -604,6 +605,7 @@ static int sort_locked(gsr_context* c) {
     if (!c->have_pre) return set_err(GSR_E_ARG, "gsr_sort before gsr_preprocess");
     const uint32_t n = (uint32_t)c->n;
     const bool bin = c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
+    c->last_binned = bin;
     // ---- stable depth sort of (key << 32 | index), 4 x 8 bits; for the binning
     // path its last pass also writes the rects in depth order (srect) ----
     mark(c, GSR_STAGE_DEPTH_SORT);
@@ -750,6 +752,18 @@ extern "C" int64_t gsr_pair_count(gsr_context* c) {
     if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
     if (hipMemcpy(&s, c->stats, sizeof s, hipMemcpyDeviceToHost) != hipSuccess) return -1;
     return (int64_t)s.pairs_total;
+}
+
+extern "C" int64_t gsr_row_item_count(gsr_context* c) {
+    if (!c || !c->binmeta) return -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->have_sort || !c->last_binned) return -1;
+    uint32_t rows[256];
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
+    if (hipMemcpy(rows, c->binmeta + 256, sizeof rows, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    int64_t total = 0;
+    for (uint32_t v : rows) total += v;
+    return total;
 }
 
 extern "C" int gsr_read_splats(gsr_context* c, void* host, int64_t n) {

@@ -153,6 +153,9 @@ int gsr_sync(gsr_context* ctx);
 
 /* Number of (tile, Gaussian) pairs of the last frame (before capacity clamp). */
 int64_t gsr_pair_count(gsr_context* ctx);
+/* Number of (tile row, Gaussian) items the last frame's row pass produced (tile
+ * binning), or -1 if that frame used pair emission + the key-value tile sort. */
+int64_t gsr_row_item_count(gsr_context* ctx);
 /* Per-Gaussian splat records (n * GSR_SPLAT_RECORD_BYTES bytes):
  *   float inv_covar[4]; float opacity; float color[3];
  *   int32 px_x, px_y; uint32 x_range (xmin | xmax<<16); uint32 y_range;

@@ -193,6 +193,12 @@ def test_tile_binning_matches_pair_sort(gpu, orc, torch, c1, knobs):
     assert pb.shape == ps.shape and pb.shape[0] > 10_000
     assert np.array_equal(pb, ps)
     assert_image_parity(got_bin, orc.render(soa, cam, W, H, 3.0))
+    # the row pass made one item per covered tile row of every visible splat
+    spl = r_bin.read_splats(soa.shape[1])
+    live = spl["tile_count"] > 0
+    ty = spl["tile_y_range"][live]
+    assert r_bin.row_item_count() == int(((ty >> 16) - (ty & 0xFFFF) + 1).sum())
+    assert r_sort.row_item_count() == -1
 
 
 def test_tile_binning_wide_frame_falls_back(gpu, orc, torch, c1):
