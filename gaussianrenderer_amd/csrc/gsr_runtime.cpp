@@ -340,6 +340,7 @@ struct gsr_context {
     uint32_t* cbins = nullptr;       // binning: column counts per chunk (256 x chunks)
     int64_t cbins_cap = 0;
     bool last_binned = false;        // the last sorted frame took the binning path
+    int completion_events = 1;       // 0: no completion event / overflow query (stream capture)
     unsigned int* queue = nullptr;   // spare device counters (blend experiments)
     int resident_groups = 2048;      // workgroups of 256 that fit on the device at once
     // frame state
@@ -697,7 +698,7 @@ static int blend_locked(gsr_context* c, float* d_out) {
     // frames skip the record (~3 us each). The overflow stats are sticky, so reading
     // them when that older frame completes still sees every overflow so far, and
     // gsr_sync drains the stream before it reads them.
-    if (!c->pending) {
+    if (!c->pending && c->completion_events) {
         HIP_TRY(hipEventRecord(c->done_ev, c->stream));
         c->pending = true;
     }
@@ -926,6 +927,9 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         if (value != 4 && value != 8 && value != 16)
             return set_err(GSR_E_ARG, "gsr_set_tuning: binning items per thread must be 4, 8 or 16");
         (knob == GSR_TUNE_BIN_ROW_ITEMS ? c->bin_row_items : c->bin_col_items) = value;
+        return GSR_OK;
+    case GSR_TUNE_COMPLETION_EVENTS:
+        c->completion_events = value != 0;
         return GSR_OK;
     case GSR_TUNE_BIN_COL_GROUPS:
         if (value < 1 || value > 65536) return set_err(GSR_E_ARG, "gsr_set_tuning: bad column-pass group count");

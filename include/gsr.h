@@ -214,7 +214,9 @@ enum {
                                         0 = pair emission + key-value tile sort */
     GSR_TUNE_BIN_ROW_ITEMS = 8,      /* binning row pass: items per thread per tile 4 | 8 | 16 (default 8) */
     GSR_TUNE_BIN_COL_ITEMS = 9,      /* binning column pass: items per thread per tile 4 | 8 | 16 (default 8) */
-    GSR_TUNE_BIN_COL_GROUPS = 10     /* binning column pass: workgroups (default 1024) */
+    GSR_TUNE_BIN_COL_GROUPS = 10,    /* binning column pass: workgroups (default 1024) */
+    GSR_TUNE_COMPLETION_EVENTS = 11  /* 1 (default): a completion event feeds the non-blocking overflow
+                                        check; 0: none (frames captured into a graph; call gsr_sync) */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Depth-sort digit passes the last sorted frame ran (1..4; trailing identity
