@@ -5,18 +5,20 @@
 //                     colour + view/clip + 2D covariance + extent + AABB, writes a
 //                     64-B splat record, the (depth_key << 32 | index) item and
 //                     a compact 8-B tile rectangle [render.cu:472-786]
-//   radix passes      stable LSD sort of the N items by depth key (4 x 8 bits)
-//   k_emit_*          tile counts in depth order (the rect gathered once), scan,
-//                     then one (tile key, index) pair per covered 16x16 tile as
-//                     separate key / value arrays [render.cu:811-857, 788-809]
-//   k_kv_* passes     stable key-value LSD sort of the pairs by tile (2 x <= 8
-//                     bits; the last pass writes values only and records each
-//                     tile's [start, end))
-//   k_blend           one workgroup per 16x16 tile, one wave64 per 8x8 block,
-//                     one pixel per lane; 64-record batches culled against the
-//                     block, survivors compacted into LDS pair slots, two
-//                     splats per iteration with packed math; exact per-pixel
-//                     early termination [render.cu:266-367]
+//   radix passes      stable LSD sort of the N items by depth key (8-bit digits,
+//                     trailing identity passes skipped on the device); the last
+//                     pass also writes the rectangles in depth order
+//   k_bin_rows_*      tile binning, row pass: one item per covered tile row,
+//                     binned stably by row [render.cu:811-857, 788-809, 1099-1118]
+//   k_bin_cols_*      tile binning, column pass: one Gaussian index per covered
+//                     tile column, binned stably inside the row; tile ranges
+//   (k_emit_*, k_kv_*: pair emission + key-value tile sort, for grids over 256
+//                     tiles per axis)
+//   k_blend_w         one wave64 per 8x8 block, one pixel per lane; 64-record
+//                     batches culled against the block, survivors compacted into
+//                     LDS pair slots, two splats per iteration with packed math;
+//                     exact per-pixel early termination [render.cu:266-367]
+//                     (k_blend: the same per 16x16 tile workgroup)
 //
 // Every float expression restates render.cu / math.cu in the same operation
 // order; the file is compiled with -ffp-contract=off so no FMA is formed
@@ -1374,14 +1376,18 @@ __global__ __launch_bounds__(256) void k_bin_cols_count(const uint64_t* __restri
         const uint32_t r = col_chunk_row(pl, c);
         const uint32_t ib = pl.rbase[r] + (c - pl.chbase[r]) * kColChunk;
         const uint32_t ie = min(ib + kColChunk, pl.rbase[r] + pl.rcnt[r]);
+        // difference arrays: +1 at the first column, -1 past the last
         for (uint32_t i = ib + t; i < ie; i += 256) {
             const uint64_t it = rows_in[i];
             const uint32_t tx0 = (uint32_t)((it >> 32) & 0xffffu), tx1 = (uint32_t)(it >> 48);
-            for (uint32_t x = tx0; x <= tx1; x++) atomicAdd(&h[w][x], 1u);
+            atomicAdd(&h[w][tx0], 1u);
+            if (tx1 < 255u) atomicSub(&h[w][tx1 + 1], 1u);
         }
         __syncthreads();
-        if (t < (uint32_t)tiles_x) cbins[(size_t)c * 256 + t] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
-        __syncthreads();
+        const uint32_t dsum = h[0][t] + h[1][t] + h[2][t] + h[3][t];
+        uint32_t tot;
+        const uint32_t cnt = block_exclusive_scan<uint32_t>(dsum, s_scr, tot) + dsum;   // mod 2^32
+        if (t < (uint32_t)tiles_x) cbins[(size_t)c * 256 + t] = cnt;
     }
 }
 
@@ -1550,10 +1556,16 @@ __device__ __forceinline__ bool block_may_reach(float a, float b, float c, float
     // inside the err margin below
     const float ih = -h * __builtin_amdgcn_rcpf(e), iv = -h * __builtin_amdgcn_rcpf(a);
     auto q = [&](float x, float y) { return a * x * x + 2.0f * h * x * y + e * y * y; };
-    float qm = q(dx0, fminf(fmaxf(ih * dx0, dy0), dy1));
-    qm = fminf(qm, q(dx1, fminf(fmaxf(ih * dx1, dy0), dy1)));
-    qm = fminf(qm, q(fminf(fmaxf(iv * dy0, dx0), dx1), dy0));
-    qm = fminf(qm, q(fminf(fmaxf(iv * dy1, dx0), dx1), dy1));
+    // The form is convex with its minimum at the splat centre (offset 0,0), which
+    // lies outside the rectangle here.  A far edge never holds the rectangle's
+    // minimum (from any of its points the segment toward the centre enters the
+    // interior, where the form is smaller), so only the near x-edge (when 0 is not
+    // in [dx0, dx1]) and the near y-edge (when 0 is not in [dy0, dy1]) are evaluated.
+    const float xe = dx0 > 0.0f ? dx0 : dx1, ye = dy0 > 0.0f ? dy0 : dy1;
+    const float qx = q(xe, fminf(fmaxf(ih * xe, dy0), dy1));
+    const float qy = q(fminf(fmaxf(iv * ye, dx0), dx1), ye);
+    const bool x_out = dx0 > 0.0f || dx1 < 0.0f, y_out = dy0 > 0.0f || dy1 < 0.0f;
+    const float qm = fminf(x_out ? qx : 3.0e38f, y_out ? qy : 3.0e38f);
     const float M = fmaxf(fmaxf(fabsf(dx0), fabsf(dx1)), fmaxf(fabsf(dy0), fabsf(dy1)));
     const float err = 4e-6f * (fabsf(a) + fabsf(b) + fabsf(c) + fabsf(e)) * M * M + 1e-3f;
     return !(qm - err > cut);
