@@ -1252,7 +1252,10 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
     constexpr uint32_t kTile = 256u * ITEMS;
     __shared__ uint32_t s_pref[kRowSources], s_idx[kRowSources];
     __shared__ uint64_t s_rect[kRowSources];
-    __shared__ uint16_t s_l[kTile], s_own[kTile];
+    // s_own (source owners, read by the generation) and s_l (source slots of the
+    // ranked tile, written after the ranking) share storage: their lives do not overlap
+    __shared__ uint16_t s_own[kTile];
+    uint16_t* const s_l = s_own;
     __shared__ uint32_t s_wmax[4];
     __shared__ uint8_t s_dig[kTile];
     __shared__ uint32_t s_wc[4][256], s_gbase[256], s_lbase[256], s_scr[4];
@@ -1298,8 +1301,6 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
             }
             const uint32_t tcount = bin_rank_tile<ITEMS, BITS>(dig, tn, pos, s_wc, s_lbase, s_scr);
 #pragma unroll
-            for (int i = 0; i < ITEMS; i++) s_own[t * ITEMS + i] = 0;   // for the next tile (rank barriers passed)
-#pragma unroll
             for (int k = 0; k < ITEMS; k++) {
                 const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
                 if (el < tn) {
@@ -1320,6 +1321,9 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
             }
             __syncthreads();
             s_gbase[t] += tcount;
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) s_own[t * ITEMS + i] = 0;   // owners of the next tile start cleared
+            __syncthreads();
         }
     }
 }
@@ -1327,14 +1331,17 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
 // Row geometry of the column pass, rebuilt by each workgroup from the row
 // totals: item base and count per row, first chunk per row (chunks of
 // kColChunk items never cross a row), chunk total, pair base per row, P.
+// (PB: also the pair base per row — only the column scan needs it.)
+template <bool PB>
 struct ColPlan {
     uint32_t rbase[256], rcnt[256], chbase[257];
-    unsigned long long pbase[256];
+    unsigned long long pbase[PB ? 256 : 1];
 };
 
+template <bool PB>
 __device__ __forceinline__ unsigned long long col_plan(const uint32_t* __restrict__ row_items,
                                                        const unsigned long long* __restrict__ row_pairs,
-                                                       ColPlan& pl, uint32_t* s_scr,
+                                                       ColPlan<PB>& pl, uint32_t* s_scr,
                                                        unsigned long long* s_scr64) {
     const uint32_t t = threadIdx.x;
     const uint32_t cnt = row_items[t];
@@ -1344,13 +1351,15 @@ __device__ __forceinline__ unsigned long long col_plan(const uint32_t* __restric
     pl.chbase[t] = block_exclusive_scan<uint32_t>((cnt + kColChunk - 1) / kColChunk, s_scr, tot);
     if (t == 255) pl.chbase[256] = tot;
     unsigned long long ptot;
-    pl.pbase[t] = block_exclusive_scan<unsigned long long>(row_pairs[t], s_scr64, ptot);
+    const unsigned long long pb = block_exclusive_scan<unsigned long long>(row_pairs[t], s_scr64, ptot);
+    if (PB) pl.pbase[t] = pb;
     __syncthreads();
     return ptot;
 }
 
 // Row of chunk c: the last row whose first chunk is <= c (empty rows own none).
-__device__ __forceinline__ uint32_t col_chunk_row(const ColPlan& pl, uint32_t c) {
+template <bool PB>
+__device__ __forceinline__ uint32_t col_chunk_row(const ColPlan<PB>& pl, uint32_t c) {
     uint32_t l = 0;
 #pragma unroll
     for (uint32_t st = 128; st >= 1; st >>= 1)
@@ -1363,7 +1372,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_count(const uint64_t* __restri
                                                          const uint32_t* __restrict__ row_items,
                                                          const unsigned long long* __restrict__ row_pairs,
                                                          uint32_t cap, int tiles_x, uint32_t* __restrict__ cbins) {
-    __shared__ ColPlan pl;
+    __shared__ ColPlan<false> pl;
     __shared__ uint32_t h[4][256], s_scr[4];
     __shared__ unsigned long long s_scr64[4];
     const uint32_t t = threadIdx.x, w = t >> 6;
@@ -1401,7 +1410,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restric
                                                         uint32_t cap, int tiles_x, uint32_t* __restrict__ cbins,
                                                         uint2* __restrict__ ranges, Stats* __restrict__ st,
                                                         Stats* host_st) {
-    __shared__ ColPlan pl;
+    __shared__ ColPlan<true> pl;
     __shared__ uint32_t s_scr[4];
     __shared__ unsigned long long s_scr64[4];
     const uint32_t t = threadIdx.x, r = blockIdx.x;
@@ -1443,7 +1452,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
                                                            const uint2* __restrict__ ranges,
                                                            uint32_t* __restrict__ vals) {
     constexpr uint32_t kTile = 256u * ITEMS;
-    __shared__ ColPlan pl;
+    __shared__ ColPlan<false> pl;
     __shared__ uint32_t s_pref[kColChunk], s_idx[kColChunk];
     __shared__ uint8_t s_tx0[kColChunk];
     __shared__ uint16_t s_l[kTile], s_own[kTile];

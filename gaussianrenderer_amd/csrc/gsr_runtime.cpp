@@ -333,7 +333,7 @@ struct gsr_context {
     uint32_t* dstats = nullptr;      // depth-sort pass plan: 4 final words + 4 per upsweep workgroup
     int depth_groups = 0;            // depth sort: workgroup cap (0 = default)
     int tile_binning = 1;            // row + column binning instead of emit + tile sort (grids <= 256 x 256)
-    int bin_row_items = 8;           // binning: items per thread of a row-pass tile (4 | 8 | 16)
+    int bin_row_items = 4;           // binning: items per thread of a row-pass tile (4 | 8 | 16)
     int bin_col_items = 8;           // binning: items per thread of a column-pass tile (4 | 8 | 16)
     int bin_col_groups = 1024;       // binning: column-pass workgroups (chunks are strided over them)
     uint64_t* binmeta = nullptr;     // binning: row pair totals (u64 x 256) then row item totals (u32 x 256)

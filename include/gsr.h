@@ -212,7 +212,7 @@ enum {
     GSR_TUNE_DEPTH_SORT_SKIP = 6,    /* depth sort: 1 = skip trailing identity passes (default), 0 = run all 4 */
     GSR_TUNE_TILE_BINNING = 7,       /* 1 = row + column binning (default; tile grids <= 256 x 256),
                                         0 = pair emission + key-value tile sort */
-    GSR_TUNE_BIN_ROW_ITEMS = 8,      /* binning row pass: items per thread per tile 4 | 8 | 16 (default 8) */
+    GSR_TUNE_BIN_ROW_ITEMS = 8,      /* binning row pass: items per thread per tile 4 | 8 | 16 (default 4) */
     GSR_TUNE_BIN_COL_ITEMS = 9,      /* binning column pass: items per thread per tile 4 | 8 | 16 (default 8) */
     GSR_TUNE_BIN_COL_GROUPS = 10,    /* binning column pass: workgroups (default 1024) */
     GSR_TUNE_COMPLETION_EVENTS = 11  /* 1 (default): a completion event feeds the non-blocking overflow
