@@ -1681,6 +1681,9 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
     for (uint32_t base = beg; base < end && alive; base += 64) {
         const uint32_t cnt = min(64u, end - base);
         // ---- cull + lane masks + compaction (lane = record) ----
+        // pixels not yet saturated at the batch start: T only decreases, so a record
+        // whose in-box pixels are all saturated here can never be taken in this batch
+        const uint64_t live_b = __ballot(!(T < 1e-3f));
         bool hit = false, fast = true;
         uint32_t mlo = 0, mhi = 0;
         if ((uint32_t)lane < cnt) {
@@ -1695,15 +1698,16 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 const int y0 = max(ymin - by, 0), y1 = min(ymax - by, 7);
                 const float dx0 = (float)(bx + x0) - cx, dx1 = (float)(bx + x1) - cx;
                 const float dy0 = (float)(by + y0) - cy, dy1 = (float)(by + y1) - cy;
-                hit = block_may_reach(a, b, c, e, dx0, dx1, dy0, dy1, md2_cutoff(__uint_as_float(rb.x)));
-                const float M = fmaxf(fmaxf(fabsf(dx0), fabsf(dx1)), fmaxf(fabsf(dy0), fabsf(dy1)));
-                fast = fast_safe(a, b, c, e, M, __uint_as_float(rb.y), __uint_as_float(rb.z),
-                                 __uint_as_float(rb.w));
                 // bit (row * 8 + col) of the block: pixel inside the AABB
                 const uint32_t rep = ((0xffu >> (7 - (x1 - x0))) << x0) * 0x01010101u;
                 const uint64_t rows = (y1 == 7 ? ~0ull : ((1ull << (8 * (y1 + 1))) - 1ull)) & (~0ull << (8 * y0));
                 mlo = rep & (uint32_t)rows;
                 mhi = rep & (uint32_t)(rows >> 32);
+                hit = ((mlo & (uint32_t)live_b) | (mhi & (uint32_t)(live_b >> 32))) != 0u &&
+                      block_may_reach(a, b, c, e, dx0, dx1, dy0, dy1, md2_cutoff(__uint_as_float(rb.x)));
+                const float M = fmaxf(fmaxf(fabsf(dx0), fabsf(dx1)), fmaxf(fabsf(dy0), fabsf(dy1)));
+                fast = fast_safe(a, b, c, e, M, __uint_as_float(rb.y), __uint_as_float(rb.z),
+                                 __uint_as_float(rb.w));
             }
         }
         const uint64_t m = __ballot(hit);
