@@ -399,7 +399,8 @@ class Renderer:
 
     def blend_stamps(self, n_groups: int) -> np.ndarray:
         """{start, end} s_memrealtime stamps (100 MHz) per blend workgroup of the
-        last diagnostics frame rendered with schedule 2."""
+        last diagnostics frame rendered with schedule 2 (one per tile) or 3 (one
+        per 8x8 block)."""
         out = np.zeros(2 * n_groups, dtype=np.uint64)
         check(lib().gsr_blend_stamps(self.ctx, out.ctypes.data, out.size), "gsr_blend_stamps")
         return out.reshape(n_groups, 2)

@@ -1524,6 +1524,65 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
     }
 }
 
+// ------------------------------------------------------------------ blend tile order
+
+// Longest-tile-first order for the blend: one workgroup stable-sorts the tiles
+// into 32 length classes (clz of the list length: a class per power of two,
+// longest first; tile order is kept inside a class) and writes the permutation.
+// Dispatching the long tiles first leaves short ones for the drain at the end
+// of the blend kernel, where the device empties out.
+__global__ __launch_bounds__(1024) void k_tile_order(const uint2* __restrict__ ranges, int nt,
+                                                      uint32_t* __restrict__ perm) {
+    __shared__ uint32_t s_base[32], s_wc[16][32];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    auto cls = [&](int i) -> uint32_t {
+        const uint2 rr = ranges[i];
+        const uint32_t len = rr.y ? rr.y - ~rr.x : 0u;
+        return len ? min((uint32_t)__clz(len), 31u) : 31u;
+    };
+    if (t < 32) s_base[t] = 0;
+    __syncthreads();
+    for (int i = (int)t; i < nt; i += 1024) atomicAdd(&s_base[cls(i)], 1u);
+    __syncthreads();
+    if (t == 0) {
+        uint32_t run = 0;
+        for (int k = 0; k < 32; k++) {
+            const uint32_t v = s_base[k];
+            s_base[k] = run;
+            run += v;
+        }
+    }
+    for (int c0 = 0; c0 < nt; c0 += 1024) {
+        if (lane < 32) s_wc[w][lane] = 0;
+        __syncthreads();
+        const int i = c0 + (int)t;
+        const bool valid = i < nt;
+        const uint32_t d = valid ? cls(i) : 0u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 5; bit++) {
+            const bool on = (d >> bit) & 1u;
+            const uint64_t bm = __ballot(on);
+            peers &= on ? bm : ~bm;
+        }
+        if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane) s_wc[w][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = s_base[d] + (uint32_t)__popcll(peers & lt_mask);
+            for (uint32_t k = 0; k < w; k++) pos += s_wc[k][d];
+            perm[pos] = (uint32_t)i;
+        }
+        __syncthreads();
+        if (t < 32) {
+            uint32_t add = 0;
+            for (int k = 0; k < 16; k++) add += s_wc[k][t];
+            s_base[t] += add;
+        }
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------------------ blend
 
 
@@ -1881,24 +1940,55 @@ __global__ __launch_bounds__(256) void k_blend(const uint32_t* __restrict__ idx,
 // frees its wave slot at once (no waiting for the tile's other three waves).
 // Blocks are tile-major; the XCD-aware remap keeps a tile's four blocks (and
 // neighbouring tiles) on one XCD, i.e. one L2.
-template <bool DIAG>
-__global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx,
-                                                 const uint2* __restrict__ ranges,
-                                                 const uint4* __restrict__ rec, int tiles_x, int tiles_y,
-                                                 int W, int H, int cover_w, int cover_h,
-                                                 float* __restrict__ out,
-                                                 unsigned long long* __restrict__ counters) {
-    __shared__ float4 sP[32 * 20 / 4];
+template <bool DIAG, bool STAMPS = false, int WPG = 1>
+__global__ __launch_bounds__(64 * WPG) void k_blend_w(const uint32_t* __restrict__ idx,
+                                                       const uint2* __restrict__ ranges,
+                                                       const uint4* __restrict__ rec, int tiles_x, int tiles_y,
+                                                       int W, int H, int cover_w, int cover_h,
+                                                       float* __restrict__ out,
+                                                       unsigned long long* __restrict__ counters,
+                                                       const uint32_t* __restrict__ perm, int bands) {
+    // WPG waves per workgroup, one 8x8 block each (WPG = 2: the two blocks of a tile
+    // half; the waves never synchronise, only their dispatch is shared)
+    __shared__ float4 sP[WPG][32 * 20 / 4];
     const int ntiles = tiles_x * tiles_y;
-    const int b = xcd_remap(blockIdx.x, ntiles * 4);
-    const int tile = b >> 2, sub = b & 3;
+    const int wv = (int)(threadIdx.x >> 6);
+    int tile, sub;
+    if (bands > 1) {
+        // each XCD (x = b & 7) takes `bands` spatial bands spread over the image:
+        // band j of B consecutive units goes to XCD j % 8 (balances the XCDs' work
+        // while keeping neighbouring blocks on one L2); padding workgroups exit
+        const int nu = 4 * ntiles / WPG;
+        const int B = (nu + 8 * bands - 1) / (8 * bands);
+        const int b = (int)blockIdx.x, k = b >> 3;
+        const int U = ((k / B) * 8 + (b & 7)) * B + k % B;
+        if (U >= nu) return;
+        const int L = U * WPG + wv;
+        tile = L >> 2;
+        sub = L & 3;
+    } else if (perm) {
+        // longest tiles first (k_tile_order): XCD x = b & 7 takes tile ranks x, x+8, ...,
+        // each tile's four blocks consecutive in its stream (they share one L2)
+        const int b = (int)blockIdx.x, k = b >> 3;
+        const int r = (k >> 2) * 8 + (b & 7);
+        if (r >= ntiles) return;
+        tile = (int)perm[r];
+        sub = k & 3;
+    } else {
+        const int b = xcd_remap(blockIdx.x, ntiles * 4);
+        tile = b >> 2;
+        sub = b & 3;
+    }
     const int tx = tile % tiles_x, ty = tile / tiles_x;
-    const int lane = threadIdx.x;
+    const int lane = (int)(threadIdx.x & 63u);
+    const int sid = (int)blockIdx.x * WPG + wv;     // stamp slot
+    if (STAMPS && lane == 0) counters[2 * sid] = __builtin_amdgcn_s_memrealtime();
     const uint2 rr = ranges[tile];
     BlendDiag dg;
     blend_block<DIAG>(idx, rec, rr.y ? ~rr.x : 0u, rr.y, tx * GSR_TILE_PX + (sub & 1) * 8,
                       ty * GSR_TILE_PX + (sub >> 1) * 8, lane, W, H, cover_w, cover_h, out,
-                      reinterpret_cast<float*>(sP), dg);
+                      reinterpret_cast<float*>(sP[wv]), dg);
+    if (STAMPS && lane == 0) counters[2 * sid + 1] = __builtin_amdgcn_s_memrealtime();
     if (DIAG && lane == 0) {
         if (sub == 0 && dg.loaded) atomicAdd(counters, (unsigned long long)dg.loaded);
         atomicAdd(counters + 1, (unsigned long long)dg.iter);
@@ -2108,16 +2198,33 @@ hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* ke
 
 hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
                         float* out, unsigned long long* consumed, int variant, unsigned int* queue,
-                        int resident_groups, hipStream_t s) {
+                        int resident_groups, uint32_t* tile_perm, int bands, int wpg, hipStream_t s) {
     const int nt = fr.tiles_x * fr.tiles_y;
     if (nt <= 0) return hipSuccess;
-    if (variant == 0) {   // default: one wave per workgroup, one 8x8 block each
-        if (consumed)
-            hipLaunchKernelGGL(k_blend_w<true>, dim3(4 * nt), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,
-                               fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
-        else
-            hipLaunchKernelGGL(k_blend_w<false>, dim3(4 * nt), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,
-                               fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
+    if (variant == 0 || variant == 3) {   // one wave per 8x8 block, wpg blocks per workgroup
+        // bands > 1: spread spatial bands over the XCDs (grid padded to whole bands);
+        // tile_perm: longest tiles first (grid rounded up to whole XCD rounds)
+        if (bands <= 1) wpg = 1;
+        const int nu = 4 * nt / wpg;
+        const int ng = bands > 1 ? 8 * bands * ((nu + 8 * bands - 1) / (8 * bands))
+                       : tile_perm ? 4 * ((nt + 7) / 8 * 8)
+                                   : 4 * nt;
+        if (bands > 1) tile_perm = nullptr;
+        if (tile_perm) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ranges, nt, tile_perm);
+        const uint32_t* pm = tile_perm;
+#define GSR_BLEND_W(D, S, G)                                                                                 \
+    hipLaunchKernelGGL((k_blend_w<D, S, G>), dim3(ng), dim3(64 * G), 0, s, idx, ranges, rec, fr.tiles_x, fr.tiles_y, \
+                       fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, pm, bands)
+        if (wpg == 2) {
+            if (variant == 3 && consumed) GSR_BLEND_W(false, true, 2);
+            else if (consumed) GSR_BLEND_W(true, false, 2);
+            else GSR_BLEND_W(false, false, 2);
+        } else {
+            if (variant == 3 && consumed) GSR_BLEND_W(false, true, 1);
+            else if (consumed) GSR_BLEND_W(true, false, 1);
+            else GSR_BLEND_W(false, false, 1);
+        }
+#undef GSR_BLEND_W
         return hipGetLastError();
     }
     if (variant == 2 && consumed)   // timestamps into consumed[2 * nt] (diagnostics)

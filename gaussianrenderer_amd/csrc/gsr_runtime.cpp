@@ -340,6 +340,11 @@ struct gsr_context {
     uint32_t* cbins = nullptr;       // binning: column counts per chunk (256 x chunks)
     int64_t cbins_cap = 0;
     bool last_binned = false;        // the last sorted frame took the binning path
+    int blend_tile_order = 0;        // 1: blend the longest tiles first (k_tile_order), 0: spatial order
+    int blend_wpg = 1;               // blend: 8x8 blocks (waves) per workgroup, 1 | 2 (band layout only)
+    int blend_band_tiles = 4;        // blend: tiles per spatial band, bands dealt round-robin to the
+                                     // XCDs (0: one contiguous band per XCD)
+    uint32_t* tile_perm = nullptr;   // blend tile permutation (t_cap)
     int completion_events = 1;       // 0: no completion event / overflow query (stream capture)
     unsigned int* queue = nullptr;   // spare device counters (blend experiments)
     int resident_groups = 2048;      // workgroups of 256 that fit on the device at once
@@ -437,6 +442,7 @@ int ensure_tiles(gsr_context* c, int64_t t) {
     if (t <= c->t_cap) return GSR_OK;
     HIP_TRY(hipDeviceSynchronize());
     if (int rc = realloc_dev(&c->ranges, (size_t)t)) return rc;
+    if (int rc = realloc_dev(&c->tile_perm, (size_t)t)) return rc;
     c->t_cap = t;
     return GSR_OK;
 }
@@ -539,7 +545,7 @@ extern "C" void gsr_destroy(gsr_context* c) {
     for (auto* p : {(void*)c->rec, (void*)c->items[0], (void*)c->items[1], (void*)c->rect, (void*)c->pairs[0],
                     (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->queue, (void*)c->dstats,
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
-                    (void*)c->cbins, (void*)c->srect})
+                    (void*)c->cbins, (void*)c->srect, (void*)c->tile_perm})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -681,7 +687,9 @@ static int blend_locked(gsr_context* c, float* d_out) {
     mark(c, GSR_STAGE_BLEND);
     if (c->diagnostics) {
         // counters (8) or, for the timestamp schedule, 2 stamps per tile
-        const int64_t need = c->blend_variant == 2 ? std::max<int64_t>(8, 2 * (int64_t)c->ntiles) : 8;
+        const int64_t need = c->blend_variant == 2   ? std::max<int64_t>(8, 2 * (int64_t)c->ntiles)
+                             : c->blend_variant == 3 ? 12 * (int64_t)c->ntiles + 64   // >= 2 x the padded grid
+                                                     : 8;
         if (c->consumed_cap < need) {
             if (int rc = realloc_dev(&c->consumed, (size_t)need)) return rc;
             c->consumed_cap = need;
@@ -690,7 +698,11 @@ static int blend_locked(gsr_context* c, float* d_out) {
     }
     HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
                               c->diagnostics ? c->consumed : nullptr, c->blend_variant, c->queue,
-                              c->resident_groups, c->stream));
+                              c->resident_groups, c->blend_tile_order ? c->tile_perm : nullptr,
+                              c->blend_band_tiles
+                                  ? std::max(1, (c->ntiles + 8 * c->blend_band_tiles - 1) / (8 * c->blend_band_tiles))
+                                  : 1,
+                              c->blend_wpg, c->stream));
     mark(c, GSR_NUM_STAGES);
     if (c->timing && c->timing_now) c->ev_frames.push_back(c->cur);
     c->cur = FrameEvents{};
@@ -907,7 +919,7 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     std::lock_guard<std::mutex> lk(c->mu);
     switch (knob) {
     case GSR_TUNE_BLEND_SCHEDULE:
-        if (value < 0 || value > 2) return set_err(GSR_E_ARG, "gsr_set_tuning: blend schedule must be 0, 1 or 2");
+        if (value < 0 || value > 3) return set_err(GSR_E_ARG, "gsr_set_tuning: blend schedule must be 0..3");
         c->blend_variant = value;
         return GSR_OK;
     case GSR_TUNE_TILE_SORT_ITEMS:
@@ -927,6 +939,17 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         if (value != 4 && value != 8 && value != 16)
             return set_err(GSR_E_ARG, "gsr_set_tuning: binning items per thread must be 4, 8 or 16");
         (knob == GSR_TUNE_BIN_ROW_ITEMS ? c->bin_row_items : c->bin_col_items) = value;
+        return GSR_OK;
+    case GSR_TUNE_BLEND_TILE_ORDER:
+        c->blend_tile_order = value != 0;
+        return GSR_OK;
+    case GSR_TUNE_BLEND_WAVES_PER_GROUP:
+        if (value != 1 && value != 2) return set_err(GSR_E_ARG, "gsr_set_tuning: blend waves per group must be 1 or 2");
+        c->blend_wpg = value;
+        return GSR_OK;
+    case GSR_TUNE_BLEND_BAND_TILES:
+        if (value < 0 || value > 65536) return set_err(GSR_E_ARG, "gsr_set_tuning: blend band tiles must be 0..65536");
+        c->blend_band_tiles = value;
         return GSR_OK;
     case GSR_TUNE_COMPLETION_EVENTS:
         c->completion_events = value != 0;
@@ -953,8 +976,8 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
 
 extern "C" int gsr_set_blend_variant(gsr_context* c, int variant) {
     if (!c) return set_err(GSR_E_ARG, "null context");
-    if (variant < 0 || variant > 2)
-        return set_err(GSR_E_ARG, "gsr_set_blend_variant: variant must be 0, 1 or 2");
+    if (variant < 0 || variant > 3)
+        return set_err(GSR_E_ARG, "gsr_set_blend_variant: variant must be 0..3");
     std::lock_guard<std::mutex> lk(c->mu);
     c->blend_variant = variant;
     return GSR_OK;

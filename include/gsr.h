@@ -197,7 +197,8 @@ int gsr_blend_counters(gsr_context* ctx, int64_t* out8);
 /* Blend schedule (tuning knob for A/B experiments, tools/ab_blend.py):
  * 0 = one 64-thread workgroup per 8x8 pixel block (default); 1 = one
  * 256-thread workgroup per 16x16 tile (four blocks); 2 = schedule 1 with
- * per-workgroup timestamps (see gsr_blend_stamps).  Every schedule culls each
+ * per-workgroup timestamps, 3 = schedule 0 with per-workgroup timestamps (see
+ * gsr_blend_stamps; diagnostics frames only).  Every schedule culls each
  * 64-record batch against its block, compacts the survivors into LDS pair
  * slots and composites two splats per iteration; all are bit-identical. */
 int gsr_set_blend_variant(gsr_context* ctx, int variant);
@@ -215,8 +216,12 @@ enum {
     GSR_TUNE_BIN_ROW_ITEMS = 8,      /* binning row pass: items per thread per tile 4 | 8 | 16 (default 4) */
     GSR_TUNE_BIN_COL_ITEMS = 9,      /* binning column pass: items per thread per tile 4 | 8 | 16 (default 8) */
     GSR_TUNE_BIN_COL_GROUPS = 10,    /* binning column pass: workgroups (default 1024) */
-    GSR_TUNE_COMPLETION_EVENTS = 11  /* 1 (default): a completion event feeds the non-blocking overflow
+    GSR_TUNE_COMPLETION_EVENTS = 11, /* 1 (default): a completion event feeds the non-blocking overflow
                                         check; 0: none (frames captured into a graph; call gsr_sync) */
+    GSR_TUNE_BLEND_TILE_ORDER = 12,  /* blend schedule 0: 1 = longest tiles first, 0 = spatial (default) */
+    GSR_TUNE_BLEND_BAND_TILES = 13,  /* blend schedule 0: tiles per spatial band, bands dealt round-robin
+                                        to the 8 XCDs (default 4); 0 = one contiguous band per XCD */
+    GSR_TUNE_BLEND_WAVES_PER_GROUP = 14 /* blend schedule 0 with bands: 8x8 blocks per workgroup, 1 | 2 */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Depth-sort digit passes the last sorted frame ran (1..4; trailing identity

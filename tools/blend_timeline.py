@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Blend workgroup timeline (schedule 2: per-workgroup s_memrealtime stamps).
+"""Blend workgroup timeline (per-workgroup s_memrealtime stamps: schedule 2 =
+the tile-per-workgroup kernel, schedule 3 = the default block-per-workgroup one).
 
 Reports the kernel span, the workgroup-duration distribution, how many
 workgroups were in flight over time, and the share of the span spent in the
@@ -24,6 +25,9 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--orbit", type=float, default=0.0)
     ap.add_argument("--resident", type=int, default=2048, help="workgroups the device holds at once")
+    ap.add_argument("--schedule", type=int, default=2, choices=(2, 3))
+    ap.add_argument("--tile-order", type=int, default=None, help="schedule 3: GSR_TUNE_BLEND_TILE_ORDER value")
+    ap.add_argument("--band-tiles", type=int, default=None, help="schedule 3: GSR_TUNE_BLEND_BAND_TILES value")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -45,14 +49,23 @@ def main():
     for _ in range(3):
         r.render(scene, cam, W, H, out.data_ptr())
     r.sync()
-    r.set_blend_variant(2)
+    r.set_blend_variant(args.schedule)
+    if args.tile_order is not None:
+        r.set_tuning(12, args.tile_order)
+    if args.band_tiles is not None:
+        r.set_tuning(13, args.band_tiles)
     r.set_diagnostics(True)
     res = []
     for rep in range(3):
         r.render(scene, cam, W, H, out.data_ptr())
         r.sync()
         tx, ty = r.tile_grid()
-        st = r.blend_stamps(tx * ty).astype(np.int64)
+        # schedule 3: the grid may be padded (band layout): read it whole, skip blocks
+        # that exited without stamps
+        st = r.blend_stamps(6 * tx * ty + 32 if args.schedule == 3 else tx * ty).astype(np.int64)
+        keep = st[:, 0] != 0
+        xcd = np.nonzero(keep)[0] % 8
+        st = st[keep]
         t0 = st[:, 0].min()
         s, e = (st[:, 0] - t0) * 10.0, (st[:, 1] - t0) * 10.0       # 100 MHz -> ns
         span = e.max()
@@ -76,7 +89,10 @@ def main():
                     "starts_by_tenth": np.histogram(s, bins=10, range=(0, span))[0].tolist(),
                     "dur_by_start_tenth_us": [round(float(dur[(s >= span * q / 10) & (s < span * (q + 1) / 10)].mean()) / 1e3, 1)
                                               if ((s >= span * q / 10) & (s < span * (q + 1) / 10)).any() else 0.0
-                                              for q in range(10)]})
+                                              for q in range(10)],
+                    # hardware dispatch sends workgroup b to XCD b % 8
+                    "xcd_end_us": [round(float(e[xcd == x].max()) / 1e3, 1) for x in range(8)],
+                    "xcd_busy_us": [round(float(dur[xcd == x].sum()) / 1e3 / 1024, 1) for x in range(8)]})
     print(json.dumps({"config": args.config, "runs": res}, indent=1))
 
 
