@@ -1531,19 +1531,25 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
 // longest first; tile order is kept inside a class) and writes the permutation.
 // Dispatching the long tiles first leaves short ones for the drain at the end
 // of the blend kernel, where the device empties out.
-__global__ __launch_bounds__(1024) void k_tile_order(const uint2* __restrict__ ranges, int nt,
+// Bands of bt consecutive tiles (bt = 1: single tiles) are the units: a band's
+// work is the sum of its tiles' list lengths.
+__global__ __launch_bounds__(1024) void k_tile_order(const uint2* __restrict__ ranges, int nt, int bt,
                                                       uint32_t* __restrict__ perm) {
     __shared__ uint32_t s_base[32], s_wc[16][32];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    auto cls = [&](int i) -> uint32_t {
-        const uint2 rr = ranges[i];
-        const uint32_t len = rr.y ? rr.y - ~rr.x : 0u;
+    const int nbands = (nt + bt - 1) / bt;
+    auto cls = [&](int j) -> uint32_t {
+        uint32_t len = 0;
+        for (int i = j * bt; i < min(nt, (j + 1) * bt); i++) {
+            const uint2 rr = ranges[i];
+            len += rr.y ? rr.y - ~rr.x : 0u;
+        }
         return len ? min((uint32_t)__clz(len), 31u) : 31u;
     };
     if (t < 32) s_base[t] = 0;
     __syncthreads();
-    for (int i = (int)t; i < nt; i += 1024) atomicAdd(&s_base[cls(i)], 1u);
+    for (int i = (int)t; i < nbands; i += 1024) atomicAdd(&s_base[cls(i)], 1u);
     __syncthreads();
     if (t == 0) {
         uint32_t run = 0;
@@ -1553,11 +1559,11 @@ __global__ __launch_bounds__(1024) void k_tile_order(const uint2* __restrict__ r
             run += v;
         }
     }
-    for (int c0 = 0; c0 < nt; c0 += 1024) {
+    for (int c0 = 0; c0 < nbands; c0 += 1024) {
         if (lane < 32) s_wc[w][lane] = 0;
         __syncthreads();
         const int i = c0 + (int)t;
-        const bool valid = i < nt;
+        const bool valid = i < nbands;
         const uint32_t d = valid ? cls(i) : 0u;
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -1954,7 +1960,19 @@ __global__ __launch_bounds__(64 * WPG) void k_blend_w(const uint32_t* __restrict
     const int ntiles = tiles_x * tiles_y;
     const int wv = (int)(threadIdx.x >> 6);
     int tile, sub;
-    if (bands > 1) {
+    if (perm && bands > 1) {
+        // bands of `bands` tiles, heaviest first (k_tile_order over bands): XCD
+        // x = b & 7 takes band ranks x, x+8, ..., a band's blocks consecutive in its stream
+        const int bb = 4 * bands / WPG;                 // units per band
+        const int b = (int)blockIdx.x, k = b >> 3;
+        const int r = (k / bb) * 8 + (b & 7);
+        const int nbnd = (ntiles + bands - 1) / bands;
+        if (r >= nbnd) return;
+        const int L = (int)perm[r] * 4 * bands + (k % bb) * WPG + wv;
+        if (L >= 4 * ntiles) return;
+        tile = L >> 2;
+        sub = L & 3;
+    } else if (bands > 1) {
         // each XCD (x = b & 7) takes `bands` spatial bands spread over the image:
         // band j of B consecutive units goes to XCD j % 8 (balances the XCDs' work
         // while keeping neighbouring blocks on one L2); padding workgroups exit
@@ -2198,19 +2216,36 @@ hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* ke
 
 hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
                         float* out, unsigned long long* consumed, int variant, unsigned int* queue,
-                        int resident_groups, uint32_t* tile_perm, int bands, int wpg, hipStream_t s) {
+                        int resident_groups, uint32_t* tile_perm, int band_tiles, int wpg, hipStream_t s) {
     const int nt = fr.tiles_x * fr.tiles_y;
     if (nt <= 0) return hipSuccess;
     if (variant == 0 || variant == 3) {   // one wave per 8x8 block, wpg blocks per workgroup
         // bands > 1: spread spatial bands over the XCDs (grid padded to whole bands);
         // tile_perm: longest tiles first (grid rounded up to whole XCD rounds)
-        if (bands <= 1) wpg = 1;
-        const int nu = 4 * nt / wpg;
-        const int ng = bands > 1 ? 8 * bands * ((nu + 8 * bands - 1) / (8 * bands))
-                       : tile_perm ? 4 * ((nt + 7) / 8 * 8)
-                                   : 4 * nt;
-        if (bands > 1) tile_perm = nullptr;
-        if (tile_perm) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ranges, nt, tile_perm);
+        // band_tiles > 0: bands of that many tiles; with tile_perm heaviest band first,
+        // else dealt round-robin in image order.  band_tiles == 0: one contiguous band
+        // per XCD, or with tile_perm heaviest single tile first.
+        const int bt = band_tiles;
+        if (bt == 0) wpg = 1;
+        int ng, bands;
+        if (bt > 0 && tile_perm) {
+            bands = bt;                                      // kernel: tiles per band
+            const int nbnd = (nt + bt - 1) / bt;
+            ng = 8 * ((nbnd + 7) / 8) * (4 * bt / wpg);
+            hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ranges, nt, bt, tile_perm);
+        } else if (bt > 0 && (nt + 8 * bt - 1) / (8 * bt) > 1) {
+            bands = (nt + 8 * bt - 1) / (8 * bt);                // kernel: bands per XCD
+            const int nu = 4 * nt / wpg;
+            ng = 8 * bands * ((nu + 8 * bands - 1) / (8 * bands));
+        } else if (bt > 0) {                                     // image too small for bands
+            wpg = 1;
+            bands = 1;
+            ng = 4 * nt;                                         // xcd_remap covers exactly 4 nt blocks
+        } else {
+            bands = 1;
+            ng = tile_perm ? 4 * ((nt + 7) / 8 * 8) : 4 * nt;
+            if (tile_perm) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ranges, nt, 1, tile_perm);
+        }
         const uint32_t* pm = tile_perm;
 #define GSR_BLEND_W(D, S, G)                                                                                 \
     hipLaunchKernelGGL((k_blend_w<D, S, G>), dim3(ng), dim3(64 * G), 0, s, idx, ranges, rec, fr.tiles_x, fr.tiles_y, \

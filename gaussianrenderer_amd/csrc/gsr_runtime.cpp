@@ -699,10 +699,7 @@ static int blend_locked(gsr_context* c, float* d_out) {
     HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
                               c->diagnostics ? c->consumed : nullptr, c->blend_variant, c->queue,
                               c->resident_groups, c->blend_tile_order ? c->tile_perm : nullptr,
-                              c->blend_band_tiles
-                                  ? std::max(1, (c->ntiles + 8 * c->blend_band_tiles - 1) / (8 * c->blend_band_tiles))
-                                  : 1,
-                              c->blend_wpg, c->stream));
+                              c->blend_band_tiles, c->blend_wpg, c->stream));
     mark(c, GSR_NUM_STAGES);
     if (c->timing && c->timing_now) c->ev_frames.push_back(c->cur);
     c->cur = FrameEvents{};

@@ -171,6 +171,23 @@ def test_blend_tile_schedule_parity(gpu, orc, torch, c1, ci):
         assert_image_parity(got, want)
 
 
+@pytest.mark.parametrize("knobs", [{13: 0}, {13: 0, 12: 1}, {13: 1}, {13: 4, 14: 2}, {13: 4, 12: 1},
+                                   {13: 5, 12: 1, 14: 2}, {13: 64}])
+def test_blend_block_mappings_parity(gpu, orc, torch, c1, knobs):
+    """Every block-to-workgroup mapping of the default blend schedule is bit-exact vs
+    the oracle: 13 = tiles per band (0: one contiguous band per XCD), 12 = heaviest
+    first, 14 = blocks per workgroup; frames small enough to fall back to one band."""
+    path, soa = c1
+    scene = gpu.Scene.from_soa(soa)
+    for W, H in ((640, 480), (333, 217), (37, 23), (1, 1)):
+        cam = cam_for(gpu, W, H, **CAMS[1])
+        r = gpu.Renderer()
+        for kn, v in knobs.items():
+            r.set_tuning(kn, v)
+        got, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
+        assert_image_parity(got, orc.render(soa, cam, W, H, 3.0))
+
+
 @pytest.mark.parametrize("knobs", [{}, {8: 4, 9: 16}, {8: 16, 9: 4, 10: 7}])
 def test_tile_binning_matches_pair_sort(gpu, orc, torch, c1, knobs):
     """Row + column binning (default for grids <= 256 x 256 tiles) gives the same
