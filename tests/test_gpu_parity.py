@@ -218,6 +218,24 @@ def test_tile_binning_matches_pair_sort(gpu, orc, torch, c1, knobs):
     assert r_sort.row_item_count() == -1
 
 
+def test_tile_binning_8bit_digits(gpu, orc, torch, c1):
+    """More than 128 tiles per axis (2100 x 2060: 132 x 129 tiles): both binning
+    scatters rank 8-bit digits; pairs and image equal the pair-sort path and the oracle."""
+    path, soa = c1
+    W, H = 2100, 2060
+    scene = gpu.Scene.from_soa(soa)
+    cam = cam_for(gpu, W, H, pos=(0.3, -0.2, 3.2), fov=60)
+    r_bin, r_sort = gpu.Renderer(), gpu.Renderer()
+    r_sort.set_tuning(7, 0)
+    got, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_bin)
+    ref, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_sort)
+    tx, ty = r_bin.tile_grid()
+    assert tx > 128 and ty > 128 and r_bin.row_item_count() > 0
+    assert np.array_equal(r_bin.read_pairs(), r_sort.read_pairs())
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert_image_parity(got, orc.render(soa, cam, W, H, 3.0))
+
+
 def test_tile_binning_wide_frame_falls_back(gpu, orc, torch, c1):
     """More than 256 tile columns (W > 4096): the pair sort path renders it."""
     path, soa = c1
