@@ -2000,13 +2000,23 @@ __global__ __launch_bounds__(64 * WPG) void k_blend_w(const uint32_t* __restrict
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int lane = (int)(threadIdx.x & 63u);
     const int sid = (int)blockIdx.x * WPG + wv;     // stamp slot
-    if (STAMPS && lane == 0) counters[2 * sid] = __builtin_amdgcn_s_memrealtime();
+    uint64_t t_start = 0, place = 0;
+    if (STAMPS && lane == 0) {
+        // placement: XCC (3 bits) above HW_ID's SE / SH / CU / SIMD / wave slot (low 16 bits)
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        place = ((uint64_t)(xcc & 7u) << 16) | (hw & 0xffffu);
+        t_start = __builtin_amdgcn_s_memrealtime();
+        counters[2 * sid] = t_start;
+    }
     const uint2 rr = ranges[tile];
     BlendDiag dg;
     blend_block<DIAG>(idx, rec, rr.y ? ~rr.x : 0u, rr.y, tx * GSR_TILE_PX + (sub & 1) * 8,
                       ty * GSR_TILE_PX + (sub >> 1) * 8, lane, W, H, cover_w, cover_h, out,
                       reinterpret_cast<float*>(sP[wv]), dg);
-    if (STAMPS && lane == 0) counters[2 * sid + 1] = __builtin_amdgcn_s_memrealtime();
+    // second word: duration (100 MHz ticks, 40 bits) | placement << 40
+    if (STAMPS && lane == 0) counters[2 * sid + 1] = ((__builtin_amdgcn_s_memrealtime() - t_start) & ((1ull << 40) - 1)) | (place << 40);
     if (DIAG && lane == 0) {
         if (sub == 0 && dg.loaded) atomicAdd(counters, (unsigned long long)dg.loaded);
         atomicAdd(counters + 1, (unsigned long long)dg.iter);

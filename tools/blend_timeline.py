@@ -66,6 +66,10 @@ def main():
         keep = st[:, 0] != 0
         xcd = np.nonzero(keep)[0] % 8
         st = st[keep]
+        place = None
+        if args.schedule == 3:   # second word: duration (40 bits) | placement << 40
+            place = (st[:, 1] >> 40).astype(np.int64)
+            st[:, 1] = st[:, 0] + (st[:, 1] & ((1 << 40) - 1))
         t0 = st[:, 0].min()
         s, e = (st[:, 0] - t0) * 10.0, (st[:, 1] - t0) * 10.0       # 100 MHz -> ns
         span = e.max()
@@ -93,6 +97,19 @@ def main():
                     # hardware dispatch sends workgroup b to XCD b % 8
                     "xcd_end_us": [round(float(e[xcd == x].max()) / 1e3, 1) for x in range(8)],
                     "xcd_busy_us": [round(float(dur[xcd == x].sum()) / 1e3 / 1024, 1) for x in range(8)]})
+        if place is not None:
+            # HW_ID (gfx9 layout): wave 3:0, SIMD 5:4, CU 11:8, SH 12, SE 15:13; XCC above
+            cu = place >> 8   # XCC / SE / SH / CU
+            cus, inv = np.unique(cu, return_inverse=True)
+            mid = span * 0.5
+            live = (s <= mid) & (e >= mid)
+            per_cu_mid = np.bincount(inv[live], minlength=len(cus))
+            res[-1]["cus_seen"] = int(len(cus))
+            res[-1]["waves_per_cu_at_mid"] = {"min": int(per_cu_mid.min()), "mean": round(float(per_cu_mid.mean()), 2),
+                                              "max": int(per_cu_mid.max()),
+                                              "hist": np.bincount(per_cu_mid).tolist()}
+            slot = place & 0xF
+            res[-1]["wave_slot_ids_seen"] = sorted(set(slot.tolist()))
     print(json.dumps({"config": args.config, "runs": res}, indent=1))
 
 
