@@ -283,6 +283,36 @@ class Renderer:
             raise GsrError(rc, "gsr_render")
         return rc
 
+    def set_frames_in_flight(self, frames: int):
+        """Frames render_path runs concurrently (1..8; lanes 1.. own private workspaces)."""
+        check(lib().gsr_set_frames_in_flight(self.ctx, int(frames)), "gsr_set_frames_in_flight")
+
+    def frames_in_flight(self) -> int:
+        return int(lib().gsr_frames_in_flight(self.ctx))
+
+    def render_path(self, scene, cams, W: int, H: int, out_ptrs, k: float = 3.0, tiling=None, stream: int = 0,
+                    layout: int = LAYOUT_SCENE_BLOCK, n: int | None = None, times=None) -> int:
+        """Enqueue len(cams) frames (camera cams[i], 4D time times[i]) into the device
+        buffers out_ptrs[i] with up to frames_in_flight() of them concurrent
+        (gsr_render_path, include/gsr.h).  Stream-ordered on `stream` at entry and exit.
+        Same returns as render()."""
+        ptr = scene.ptr if isinstance(scene, Scene) else int(scene)
+        n = scene.n if n is None else n
+        if isinstance(scene, Scene) and layout == LAYOUT_SCENE_BLOCK:
+            layout = scene.layout
+        nf = len(cams)
+        if len(out_ptrs) != nf or (times is not None and len(times) != nf):
+            raise ValueError("render_path: cams, out_ptrs and times must have the same length")
+        cam_arr = (Camera * max(1, nf))(*cams)
+        out_arr = (c_void_p * max(1, nf))(*[int(p) for p in out_ptrs])
+        t_arr = (c_float * nf)(*[float(t) for t in times]) if times is not None else None
+        t = tiling or TilingInformation(1, 1, H, W)
+        rc = lib().gsr_render_path(self.ctx, ptr, layout, n, cam_arr, t_arr, nf, W, H, t.num_tile_x,
+                                   t.num_tile_y, t.width_stride, t.height_stride, k, out_arr, stream or None)
+        if rc not in (_native.GSR_OK, _native.GSR_E_OVERFLOW):
+            raise GsrError(rc, "gsr_render_path")
+        return rc
+
     def render_display(self, target: "DisplayTarget", scene, cam: Camera, W: int, H: int, k: float = 3.0,
                        tiling=None, stream: int = 0, layout: int = LAYOUT_SCENE_BLOCK, n: int | None = None,
                        time: float | None = None) -> int:

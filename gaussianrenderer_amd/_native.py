@@ -101,6 +101,10 @@ SIGNATURES = [
     ("gsr_reserve", c_int, [c_void_p, c_int64, c_int64]),
     ("gsr_render", c_int, [c_void_p, c_void_p, c_int, c_int64, POINTER(Camera), c_int, c_int, c_int, c_int,
                            c_int, c_int, c_float, c_void_p, c_void_p]),
+    ("gsr_render_path", c_int, [c_void_p, c_void_p, c_int, c_int64, POINTER(Camera), c_void_p, c_int, c_int,
+                                c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p]),
+    ("gsr_set_frames_in_flight", c_int, [c_void_p, c_int]),
+    ("gsr_frames_in_flight", c_int, [c_void_p]),
     ("gsr_preprocess", c_int, [c_void_p, c_void_p, c_int, c_int64, POINTER(Camera), c_int, c_int, c_int, c_int,
                                c_int, c_int, c_float, c_void_p]),
     ("gsr_sort", c_int, [c_void_p, c_void_p]),

@@ -368,6 +368,15 @@ struct gsr_context {
     // drop-in helpers
     float* out_tmp = nullptr;
     int64_t out_cap = 0;
+    // frames in flight (gsr_render_path): lane 0 is this context on the caller's
+    // stream; lane l >= 1 is a private child context (own workspace) on its own
+    // non-blocking stream.  Children are only touched under this context's mutex.
+    int inflight = 3;
+    std::vector<gsr_context*> lanes;          // lanes[l - 1] = child of lane l
+    std::vector<hipStream_t> lane_streams;    // lane_streams[l - 1]
+    hipEvent_t fork_ev = nullptr;
+    std::vector<hipEvent_t> join_evs;         // one per child lane
+    std::vector<hipEvent_t> alias_evs;        // ring of `inflight` events: output reuse across lanes
 };
 
 namespace {
@@ -542,6 +551,11 @@ extern "C" gsr_context* gsr_create(void) { return new gsr_context(); }
 extern "C" void gsr_destroy(gsr_context* c) {
     if (!c) return;
     (void)hipDeviceSynchronize();
+    for (auto* l : c->lanes) gsr_destroy(l);
+    for (auto s : c->lane_streams) (void)hipStreamDestroy(s);
+    for (auto e : c->join_evs) (void)hipEventDestroy(e);
+    for (auto e : c->alias_evs) (void)hipEventDestroy(e);
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     for (auto* p : {(void*)c->rec, (void*)c->items[0], (void*)c->items[1], (void*)c->rect, (void*)c->pairs[0],
                     (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->queue, (void*)c->dstats,
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
@@ -746,11 +760,151 @@ extern "C" int gsr_render(gsr_context* c, const void* scene, int layout, int64_t
     return rc;
 }
 
+// ------------------------------------------------------------------ frames in flight
+
+namespace {
+
+// Everything that selects kernels or schedules (all settings are bit-identical);
+// diagnostics and timing stay on lane 0 only.
+void copy_settings(gsr_context* d, const gsr_context* s) {
+    d->blend_variant = s->blend_variant == 2 || s->blend_variant == 3 ? 0 : s->blend_variant;
+    d->tile_items = s->tile_items;
+    d->depth_items = s->depth_items;
+    d->tile_groups = s->tile_groups;
+    d->tile_split_even = s->tile_split_even;
+    d->depth_skip = s->depth_skip;
+    d->depth_groups = s->depth_groups;
+    d->tile_binning = s->tile_binning;
+    d->bin_row_items = s->bin_row_items;
+    d->bin_col_items = s->bin_col_items;
+    d->bin_col_groups = s->bin_col_groups;
+    d->blend_tile_order = s->blend_tile_order;
+    d->blend_wpg = s->blend_wpg;
+    d->blend_band_tiles = s->blend_band_tiles;
+    d->completion_events = s->completion_events;
+}
+
+// Lanes 1..F-1: child contexts, streams and events, created once and kept.
+int ensure_lanes(gsr_context* c, int F) {
+    if (!c->fork_ev) HIP_TRY(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+    while ((int)c->lanes.size() < F - 1) {
+        gsr_context* l = new gsr_context();
+        l->inflight = 1;
+        hipStream_t s = nullptr;
+        hipEvent_t e = nullptr;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            if (s) (void)hipStreamDestroy(s);
+            gsr_destroy(l);
+            return set_err(GSR_E_HIP, "frames in flight: stream/event creation failed");
+        }
+        c->lanes.push_back(l);
+        c->lane_streams.push_back(s);
+        c->join_evs.push_back(e);
+    }
+    while ((int)c->alias_evs.size() < F) {
+        hipEvent_t e = nullptr;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->alias_evs.push_back(e);
+    }
+    for (int l = 0; l < F - 1; l++) copy_settings(c->lanes[l], c);
+    return GSR_OK;
+}
+
+int render_one_locked(gsr_context* c, const void* scene, int layout, int64_t n, const gsr_camera* cam, int W,
+                      int H, int nx, int ny, int ws, int hs, float k, float* d_out, hipStream_t s) {
+    int rc = preprocess_locked(c, scene, layout, n, cam, W, H, nx, ny, ws, hs, k, s);
+    if (rc != GSR_OK && rc != GSR_E_OVERFLOW) return rc;
+    if (int r2 = sort_locked(c)) return r2;
+    if (int r3 = blend_locked(c, d_out)) return r3;
+    return rc;
+}
+
+}  // namespace
+
+extern "C" int gsr_set_frames_in_flight(gsr_context* c, int frames) {
+    if (!c || frames < 1 || frames > GSR_MAX_FRAMES_IN_FLIGHT)
+        return set_err(GSR_E_ARG, "gsr_set_frames_in_flight: frames must be 1..%d", GSR_MAX_FRAMES_IN_FLIGHT);
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->inflight = frames;
+    return GSR_OK;
+}
+
+extern "C" int gsr_frames_in_flight(gsr_context* c) {
+    if (!c) return set_err(GSR_E_ARG, "null context");
+    return c->inflight;
+}
+
+extern "C" int gsr_render_path(gsr_context* c, const void* scene, int layout, int64_t n, const gsr_camera* cams,
+                               const float* times, int nframes, int W, int H, int nx, int ny, int ws, int hs,
+                               float k, float* const* d_outs, void* stream) {
+    if (!c) return set_err(GSR_E_ARG, "null context");
+    if (nframes < 0 || (nframes > 0 && (!cams || !d_outs)))
+        return set_err(GSR_E_ARG, "gsr_render_path: bad frame arrays");
+    for (int i = 0; i < nframes; i++)
+        if (!d_outs[i]) return set_err(GSR_E_ARG, "gsr_render_path: null output for frame %d", i);
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (nframes == 0) return GSR_OK;
+    const hipStream_t S = static_cast<hipStream_t>(stream);
+    const int F = std::max(1, std::min(c->inflight, nframes));
+    if (int rc = ensure_lanes(c, F)) return rc;
+    if (int rc = ensure_static(c)) return rc;
+    // children start at the parent's pair high-water mark (each still grows on its own overflow)
+    for (int l = 0; l < F - 1; l++) {
+        gsr_context* ch = c->lanes[l];
+        if (int rc = ensure_static(ch)) return rc;
+        if (ch->p_cap < c->p_cap && c->p_cap > 0) {
+            if (int rc = ensure_n(ch, std::max<int64_t>(n, 1))) return rc;
+            if (int rc = ensure_pairs(ch, c->p_cap)) return rc;
+        }
+    }
+    // fork: every lane starts after the work already queued on the caller's stream
+    if (F > 1) {
+        HIP_TRY(hipEventRecord(c->fork_ev, S));
+        for (int l = 0; l < F - 1; l++) HIP_TRY(hipStreamWaitEvent(c->lane_streams[l], c->fork_ev, 0));
+    }
+    int result = GSR_OK;
+    const float t_saved = c->time;
+    for (int i = 0; i < nframes; i++) {
+        const int lane = i % F;
+        gsr_context* lc = lane == 0 ? c : c->lanes[lane - 1];
+        const hipStream_t ls = lane == 0 ? S : c->lane_streams[lane - 1];
+        // an output written by an earlier frame still in flight on ANOTHER lane: wait for it
+        for (int j = std::max(0, i - F + 1); j < i; j++)
+            if (d_outs[j] == d_outs[i] && j % F != lane) HIP_TRY(hipStreamWaitEvent(ls, c->alias_evs[j % F], 0));
+        if (times) lc->time = times[i];
+        else lc->time = t_saved;
+        const int rc = render_one_locked(lc, scene, layout, n, &cams[i], W, H, nx, ny, ws, hs, k, d_outs[i], ls);
+        if (rc == GSR_E_OVERFLOW) result = GSR_E_OVERFLOW;
+        else if (rc != GSR_OK) return rc;
+        bool reused = false;
+        for (int j = i + 1; j < std::min(nframes, i + F) && !reused; j++)
+            reused = d_outs[j] == d_outs[i] && j % F != lane;
+        if (reused) HIP_TRY(hipEventRecord(c->alias_evs[i % F], ls));
+    }
+    c->time = t_saved;
+    // join: work queued on the caller's stream afterwards sees every frame
+    for (int l = 0; l < F - 1 && l + 1 < nframes; l++) {
+        HIP_TRY(hipEventRecord(c->join_evs[l], c->lane_streams[l]));
+        HIP_TRY(hipStreamWaitEvent(S, c->join_evs[l], 0));
+    }
+    c->stream = S;
+    return result;
+}
+
 extern "C" int gsr_sync(gsr_context* c) {
     if (!c) return set_err(GSR_E_ARG, "null context");
     std::lock_guard<std::mutex> lk(c->mu);
+    int result = GSR_OK;
+    for (size_t l = 0; l < c->lanes.size(); l++) {
+        HIP_TRY(hipStreamSynchronize(c->lane_streams[l]));
+        const int rc = check_overflow(c->lanes[l], true);
+        if (rc == GSR_E_OVERFLOW) result = GSR_E_OVERFLOW;
+        else if (rc != GSR_OK) return rc;
+    }
     if (c->stream || c->pending) HIP_TRY(hipStreamSynchronize(c->stream));
-    return check_overflow(c, true);
+    const int rc = check_overflow(c, true);
+    return rc != GSR_OK ? rc : result;
 }
 
 // ------------------------------------------------------------------ readback

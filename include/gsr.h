@@ -130,6 +130,30 @@ int gsr_render(gsr_context* ctx, const void* d_scene, int layout, int64_t n,
                const gsr_camera* cam, int W, int H, int num_tile_x, int num_tile_y,
                int width_stride, int height_stride, float k, float* d_out, void* stream);
 
+/* Offline camera path (config 4 on one GPU; the reference has no batch entry
+ * point — it renders one frame per preprocessCUDAGaussians call, render.cu:871):
+ * frame i renders cams[i] (at times[i] for 4D scenes; times may be NULL) into
+ * the DEVICE buffer d_outs[i], each frame exactly as gsr_render would.  Up to
+ * gsr_set_frames_in_flight() frames run concurrently: frame i goes to lane
+ * i % F, lane 0 being this context on `stream` and lanes 1..F-1 private child
+ * contexts (own workspaces) on their own streams, so one frame's latency-bound
+ * sort and binning kernels overlap another frame's VALU-bound blend.
+ * Stream-ordered: the frames start after the work already queued on `stream`
+ * (fork event), and work queued on `stream` after the call sees all nframes
+ * images (join events).  Outputs may repeat (e.g. a ring of buffers); a frame
+ * whose output an in-flight frame of another lane also writes waits for it.
+ * Readbacks, timing and diagnostics refer to lane 0's last frame.  Returns
+ * GSR_E_OVERFLOW when an earlier frame of any lane overflowed its pair buffer
+ * (grown; re-render), as gsr_render. */
+#define GSR_MAX_FRAMES_IN_FLIGHT 8
+int gsr_render_path(gsr_context* ctx, const void* d_scene, int layout, int64_t n, const gsr_camera* cams,
+                    const float* times, int nframes, int W, int H, int num_tile_x, int num_tile_y,
+                    int width_stride, int height_stride, float k, float* const* d_outs, void* stream);
+/* Frames in flight for gsr_render_path: 1..GSR_MAX_FRAMES_IN_FLIGHT (default 3;
+ * 1 = strictly sequential on `stream`).  Each extra lane holds its own workspace. */
+int gsr_set_frames_in_flight(gsr_context* ctx, int frames);
+int gsr_frames_in_flight(gsr_context* ctx);
+
 /* The three stages of gsr_render, callable separately (same stream). */
 int gsr_preprocess(gsr_context* ctx, const void* d_scene, int layout, int64_t n,
                    const gsr_camera* cam, int W, int H, int num_tile_x, int num_tile_y,
