@@ -84,12 +84,21 @@ def algorithmic_stage_bytes(n: int, m: int, pairs: int, ntiles: int, consumed: i
     row pass ("emit") N*24 (rects for the count, items + rects for the scatter) +
     R*8 row items; column pass ("tile_sort") R*16 (count + scatter reads) + P*4
     values + T*8 ranges.
+    Per-tile depth order (depth_passes 0): the binning as above over Gaussians in index
+    order, then "depth_sort" = P*16 (list read, key gather, list write).
     Pair sort (R < 0): depth sort passes*N*24; emit N*40 (sorted items twice, rect
     gather, srect write/read) + P*6 (u16 key + u32 value); tile sort P*14 per
     non-final pass, P*12 for the final one (keys 2 up, 6 read, 6|4 write) + T*8."""
     out = {"preprocess": 152 * n + 64 * m + 16 * n,
            "blend": algorithmic_blend_bytes(ntiles, consumed, W, H)}
-    if row_items >= 0:
+    if row_items >= 0 and depth_passes == 0:
+        # per-tile depth order: binning in index order (rects + items read as in the
+        # depth-ordered case), then every tile list re-read (4), its keys gathered
+        # (8-B items) and written back in depth order (4)
+        out.update({"depth_sort": 16 * pairs,
+                    "emit": 24 * n + 8 * row_items,
+                    "tile_sort": 16 * row_items + 4 * pairs + 8 * ntiles})
+    elif row_items >= 0:
         out.update({"depth_sort": depth_passes * 24 * n + 16 * n,
                     "emit": 24 * n + 8 * row_items,
                     "tile_sort": 16 * row_items + 4 * pairs + 8 * ntiles})
@@ -285,8 +294,8 @@ def main():
     consumed = counters["records_loaded"]
     r.set_diagnostics(False)
     tiles_x, tiles_y = r.tile_grid()
-    # visible Gaussians M (depth key != 0xFFFFFFFF after the depth sort), untimed
-    visible = int(((r.read_depth_order(n) >> 32) != 0xFFFFFFFF).sum())
+    # visible Gaussians M (depth key != 0xFFFFFFFF), untimed
+    visible = int((r.read_splats(n)["depth_key"] != 0xFFFFFFFF).sum())
 
     def timed(fn):
         if dist:

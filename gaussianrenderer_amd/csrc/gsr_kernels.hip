@@ -866,7 +866,7 @@ __global__ __launch_bounds__(256) void k_emit_scan(unsigned long long* __restric
             run += v;
         }
     if (threadIdx.x == 0) {
-        Stats s;
+        Stats s{};
         s.pairs_total = total;
         s.pairs_eff = (uint32_t)(total < cap ? total : cap);
         s.overflow = total > cap ? 1u : 0u;
@@ -1123,7 +1123,7 @@ __device__ __forceinline__ void bin_tile_owners(const uint32_t (&cnt)[PER], cons
 // mirror) the non-blocking overflow check reads.
 __device__ __forceinline__ void publish_pair_stats(unsigned long long total, uint32_t cap, Stats* st,
                                                    Stats* host_st) {
-    Stats s;
+    Stats s{};
     s.pairs_total = total;
     s.pairs_eff = (uint32_t)(total < cap ? total : cap);
     s.overflow = total > cap ? 1u : 0u;
@@ -1519,6 +1519,351 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
             }
             __syncthreads();
             s_gbase[t] += tcount;
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ per-tile depth order
+//
+// The other way to reach the same tile lists: bin the Gaussians in INDEX order
+// (the row and column passes above, fed by the preprocess items and rects
+// directly — no global depth sort), which leaves every tile's list in index
+// order, then sort each list stably by depth key.  The result is the order the
+// reference's stable SortPairs on (tile << 32 | key) defines (render.cu:1099-1118,
+// ties by index), identical to global depth sort + stable binning.
+//
+// Opt-in (GSR_TUNE_DEPTH_ORDER = 1): measured slower than the global depth sort
+// on config 2 (k_tile_depth_sort_wave 70 us for 5.4M entries vs 80 us for the
+// whole global sort; 8-bit ballot ranking costs ~60 VALU per 64 entries per pass,
+// and a tile's list needs 3 passes), so it is kept as a tested alternative.
+// Lists of up to 1024 entries: one wave each (k_tile_depth_sort_wave); longer
+// ones: a workgroup each, sorted in LDS up to 256 * 16 entries (keys gathered
+// once from the 8-B items, passes from the list's key span: 8-bit LSD digits of
+// key - min, ranked with bin_rank_tile), beyond that a chunked LSD through
+// global scratch (stable: chunks in order, running digit bases), counted in the
+// frame stats (big_tiles).
+
+constexpr uint32_t kTdsCap = 256u * 16u;            // largest list sorted in LDS
+
+__device__ __forceinline__ void block_min_max(uint32_t& kmin, uint32_t& kmax, uint32_t* s_mm) {
+    const uint32_t w = threadIdx.x >> 6;
+    kmin = ~wave_max_u32(~kmin);
+    kmax = wave_max_u32(kmax);
+    if ((threadIdx.x & 63u) == 0) {
+        s_mm[w] = kmin;
+        s_mm[4 + w] = kmax;
+    }
+    __syncthreads();
+    kmin = min(min(s_mm[0], s_mm[1]), min(s_mm[2], s_mm[3]));
+    kmax = max(max(s_mm[4], s_mm[5]), max(s_mm[6], s_mm[7]));
+    __syncthreads();
+}
+
+__device__ __forceinline__ int key_passes(uint32_t span) { return span ? (32 - __clz((int)span) + 7) / 8 : 0; }
+
+template <int ITEMS>
+__device__ __forceinline__ void tds_sort_lds(uint32_t* __restrict__ vals, uint32_t start, uint32_t L,
+                                             const uint64_t* __restrict__ items, uint32_t* s_key,
+                                             uint32_t* s_idx, uint32_t (*s_wc)[256], uint32_t* s_lbase,
+                                             uint32_t* s_scr, uint32_t* s_mm) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    uint32_t key[ITEMS], idx[ITEMS];
+#pragma unroll
+    for (int k = 0; k < ITEMS; k++) {
+        const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
+        idx[k] = el < L ? vals[start + el] : 0u;
+    }
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+    for (int k = 0; k < ITEMS; k++) {
+        const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
+        key[k] = el < L ? (uint32_t)(items[idx[k]] >> 32) : 0u;
+        if (el < L) {
+            kmin = min(kmin, key[k]);
+            kmax = max(kmax, key[k]);
+        }
+    }
+    block_min_max(kmin, kmax, s_mm);
+    const int passes = key_passes(kmax - kmin);   // 0: all keys equal, index order is the answer
+    for (int p = 0; p < passes; p++) {
+        uint32_t dig[ITEMS], pos[ITEMS];
+#pragma unroll
+        for (int k = 0; k < ITEMS; k++) dig[k] = ((key[k] - kmin) >> (8 * p)) & 0xffu;
+        bin_rank_tile<ITEMS, 8>(dig, L, pos, s_wc, s_lbase, s_scr);
+        if (p == passes - 1) {
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++)
+                if (w * 64 * ITEMS + k * 64 + lane < L) vals[start + pos[k]] = idx[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++)
+                if (w * 64 * ITEMS + k * 64 + lane < L) {
+                    s_key[pos[k]] = key[k];
+                    s_idx[pos[k]] = idx[k];
+                }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++) {
+                const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
+                if (el < L) {
+                    key[k] = s_key[el];
+                    idx[k] = s_idx[el];
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Lists longer than kTdsCap: LSD passes through global scratch, A = u64
+// (key << 32 | index) and B = (scr_keys, vals), alternating A, B, A, ...; each pass
+// counts its digits over the whole list, then ranks and scatters it chunk by
+// chunk in list order.  An odd number of passes ends in A and copies back.
+__device__ void tds_sort_global(uint32_t* __restrict__ vals, uint32_t start, uint32_t L,
+                                const uint64_t* __restrict__ items, uint64_t* __restrict__ scr_a,
+                                uint32_t* __restrict__ scr_keys, uint32_t (*s_wc)[256], uint32_t* s_lbase,
+                                uint32_t* s_gbase, uint32_t* s_scr, uint32_t* s_mm) {
+    constexpr int ITEMS = 16;
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+    for (uint32_t i = t; i < L; i += 256) {
+        const uint32_t k = (uint32_t)(items[vals[start + i]] >> 32);
+        kmin = min(kmin, k);
+        kmax = max(kmax, k);
+    }
+    block_min_max(kmin, kmax, s_mm);
+    const int passes = key_passes(kmax - kmin);
+    auto load = [&](int p, uint32_t i, uint32_t& key, uint32_t& idx) {
+        if (p == 0) {
+            idx = vals[start + i];
+            key = (uint32_t)(items[idx] >> 32);
+        } else if (p & 1) {   // previous pass wrote A
+            const uint64_t v = scr_a[start + i];
+            key = (uint32_t)(v >> 32);
+            idx = (uint32_t)v;
+        } else {              // previous pass wrote B
+            key = scr_keys[start + i];
+            idx = vals[start + i];
+        }
+    };
+    for (int p = 0; p < passes; p++) {
+        const int sh = 8 * p;
+        // digit counts of the whole list -> running global bases
+        s_gbase[t] = 0;
+        __syncthreads();
+        for (uint32_t i = t; i < L; i += 256) {
+            uint32_t key, idx;
+            load(p, i, key, idx);
+            atomicAdd(&s_gbase[((key - kmin) >> sh) & 0xffu], 1u);
+        }
+        __syncthreads();
+        {
+            uint32_t tot;
+            const uint32_t c = s_gbase[t];
+            __syncthreads();
+            s_gbase[t] = block_exclusive_scan<uint32_t>(c, s_scr, tot);
+        }
+        const bool to_a = (p & 1) == 0;
+        for (uint32_t c0 = 0; c0 < L; c0 += kTdsCap) {
+            const uint32_t tn = min(kTdsCap, L - c0);
+            uint32_t key[ITEMS], idx[ITEMS], dig[ITEMS], pos[ITEMS];
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++) {
+                const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
+                key[k] = 0u;
+                idx[k] = 0u;
+                if (el < tn) load(p, c0 + el, key[k], idx[k]);
+                dig[k] = ((key[k] - kmin) >> sh) & 0xffu;
+            }
+            // (the loads of this chunk precede bin_rank_tile's barriers, so the
+            // scatter below never overwrites an element another thread still reads:
+            // source and destination are different buffers anyway)
+            const uint32_t tcount = bin_rank_tile<ITEMS, 8>(dig, tn, pos, s_wc, s_lbase, s_scr);
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++) {
+                if (w * 64 * ITEMS + k * 64 + lane < tn) {
+                    const uint32_t dst = start + s_gbase[dig[k]] + (pos[k] - s_lbase[dig[k]]);
+                    if (to_a) {
+                        scr_a[dst] = ((uint64_t)key[k] << 32) | idx[k];
+                    } else {
+                        scr_keys[dst] = key[k];
+                        vals[dst] = idx[k];
+                    }
+                }
+            }
+            __syncthreads();
+            s_gbase[t] += tcount;
+            __syncthreads();
+        }
+    }
+    if (passes & 1) {   // the last pass wrote A: indices back into vals
+        __threadfence_block();
+        for (uint32_t i = t; i < L; i += 256) vals[start + i] = (uint32_t)scr_a[start + i];
+    }
+}
+
+// Lists of up to kTdsWaveCap entries: one wave per tile, wave-synchronous (no
+// workgroup barrier; a wave's LDS operations execute in issue order).  Entry e
+// of the list is slot e / 64, lane e % 64 (slot-major, so every load is one
+// coalesced wave access).  Per pass: digit counts ranked slot by slot with
+// ballot matching (a slot's read of the running count sees the earlier slots'
+// adds), a wave scan of the 256 counts, then the entries move through the wave's
+// LDS slice (or, in the last pass, straight to their final slot in vals).
+// Longer lists are appended to big_list for k_tile_depth_sort_big.
+constexpr uint32_t kTdsWaveCap = 1024;
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(64) void k_tile_depth_sort_wave(const uint2* __restrict__ ranges,
+                                                              const uint64_t* __restrict__ items,
+                                                              uint32_t* __restrict__ vals,
+                                                              uint32_t* __restrict__ big_list,
+                                                              uint32_t* __restrict__ big_count) {
+    constexpr int IT = kTdsWaveCap / 64;
+    __shared__ uint32_t s_key[kTdsWaveCap], s_idx[kTdsWaveCap], s_cnt[256];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t tile = blockIdx.x;
+    const uint2 rr = ranges[tile];                      // {~start, end}, zero = empty
+    if (!rr.y) return;
+    const uint32_t start = ~rr.x, L = rr.y - start;
+    if (L < 2) return;
+    if (L > kTdsWaveCap) {
+        if (lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
+        return;
+    }
+    const uint32_t nslot = (L + 63u) / 64u;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t key[IT], idx[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        const uint32_t e = (uint32_t)k * 64u + lane;
+        idx[k] = ((uint32_t)k < nslot && e < L) ? vals[start + e] : 0u;
+    }
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+        const uint32_t e = (uint32_t)k * 64u + lane;
+        if ((uint32_t)k < nslot && e < L) {
+            key[k] = (uint32_t)(items[idx[k]] >> 32);
+            kmin = min(kmin, key[k]);
+            kmax = max(kmax, key[k]);
+        } else {
+            key[k] = 0u;
+        }
+    }
+    kmin = ~wave_max_u32(~kmin);
+    kmax = wave_max_u32(kmax);
+    const int passes = key_passes(kmax - kmin);        // 0: all keys equal, index order stands
+    for (int p = 0; p < passes; p++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) s_cnt[4 * lane + j] = 0u;
+        wave_lds_sync();
+        uint32_t dig[IT], pos[IT];
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            dig[k] = 0u;
+            pos[k] = 0u;
+            if ((uint32_t)k >= nslot) continue;            // uniform
+            const bool valid = (uint32_t)k * 64u + lane < L;
+            const uint32_t d = ((key[k] - kmin) >> (8 * p)) & 0xffu;
+            dig[k] = d;
+            uint64_t peers = __ballot(valid);
+#pragma unroll
+            for (int bit = 0; bit < 8; bit++) {
+                const bool on = (d >> bit) & 1u;
+                const uint64_t bm = __ballot(on);
+                peers &= on ? bm : ~bm;
+            }
+            pos[k] = s_cnt[d] + (uint32_t)__popcll(peers & lt_mask);
+            if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
+                atomicAdd(&s_cnt[d], (uint32_t)__popcll(peers));
+        }
+        wave_lds_sync();
+        // exclusive scan of the 256 digit counts (4 per lane), bases back into s_cnt
+        {
+            uint32_t c[4], sum = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                c[j] = s_cnt[4 * lane + j];
+                sum += c[j];
+            }
+            uint32_t x = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if (lane >= (uint32_t)o) x += y;
+            }
+            uint32_t run = x - sum;
+            wave_lds_sync();
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                s_cnt[4 * lane + j] = run;
+                run += c[j];
+            }
+        }
+        wave_lds_sync();
+        const bool last = p == passes - 1;
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            if ((uint32_t)k * 64u + lane < L) {
+                const uint32_t q = s_cnt[dig[k]] + pos[k];
+                if (last) {
+                    vals[start + q] = idx[k];
+                } else {
+                    s_key[q] = key[k];
+                    s_idx[q] = idx[k];
+                }
+            }
+        }
+        if (last) break;
+        wave_lds_sync();
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const uint32_t e = (uint32_t)k * 64u + lane;
+            if (e < L) {
+                key[k] = s_key[e];
+                idx[k] = s_idx[e];
+            }
+        }
+        wave_lds_sync();
+    }
+}
+
+// Lists over kTdsWaveCap (big_list, filled by the wave kernel): one workgroup per
+// list, in LDS up to kTdsCap, chunked through global scratch beyond (counted in
+// the frame stats, big_tiles).  The
+// workgroups stride over the list; the count of the NEXT frame parity is zeroed.
+__global__ __launch_bounds__(256) void k_tile_depth_sort_big(const uint2* __restrict__ ranges,
+                                                              const uint64_t* __restrict__ items,
+                                                              uint32_t* __restrict__ vals,
+                                                              uint64_t* __restrict__ scr_a,
+                                                              uint32_t* __restrict__ scr_keys,
+                                                              const uint32_t* __restrict__ big_list,
+                                                              uint32_t* __restrict__ big_counts, int parity,
+                                                              Stats* __restrict__ st, Stats* host_st) {
+    __shared__ uint32_t s_key[kTdsCap], s_idx[kTdsCap];
+    __shared__ uint32_t s_wc[4][256], s_lbase[256], s_gbase[256], s_scr[4], s_mm[8];
+    const uint32_t nbig = big_counts[parity];
+    if (blockIdx.x == 0 && threadIdx.x == 0) big_counts[parity ^ 1] = 0u;
+    for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
+        const uint2 rr = ranges[big_list[b]];
+        const uint32_t start = ~rr.x, L = rr.y - start;
+        if (L <= kTdsCap) {
+            tds_sort_lds<16>(vals, start, L, items, s_key, s_idx, s_wc, s_lbase, s_scr, s_mm);
+        } else {
+            if (threadIdx.x == 0) {
+                atomicAdd(&st[1].big_tiles, 1u);
+                if (host_st) {
+                    host_st->big_tiles = 1u;
+                    __threadfence_system();
+                }
+            }
+            tds_sort_global(vals, start, L, items, scr_a, scr_keys, s_wc, s_lbase, s_gbase, s_scr, s_mm);
         }
         __syncthreads();
     }
@@ -2185,6 +2530,19 @@ hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, 
                                                                                     : k_bin_cols_scatter<16, 8>);
     hipLaunchKernelGGL(scatter, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs, pair_capacity,
                        tiles_x, cbins, ranges, vals);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_depth_sort(const uint2* ranges, int ntiles, const uint64_t* items, uint32_t* vals,
+                                  uint64_t* scr_a, uint32_t* scr_keys, uint32_t* big_list, uint32_t* big_counts,
+                                  int parity, int big_groups, Stats* stats, Stats* host_mapped_stats,
+                                  hipStream_t s) {
+    if (ntiles < 0 || big_groups < 1 || (parity & ~1)) return hipErrorInvalidValue;
+    if (ntiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_tile_depth_sort_wave, dim3(ntiles), dim3(64), 0, s, ranges, items, vals, big_list,
+                       big_counts + parity);
+    hipLaunchKernelGGL(k_tile_depth_sort_big, dim3(big_groups), dim3(256), 0, s, ranges, items, vals, scr_a,
+                       scr_keys, big_list, big_counts, parity, stats, host_mapped_stats);
     return hipGetLastError();
 }
 

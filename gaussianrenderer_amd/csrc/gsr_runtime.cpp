@@ -345,7 +345,12 @@ struct gsr_context {
     int blend_band_tiles = 4;        // blend: tiles per spatial band, bands dealt round-robin to the
                                      // XCDs (0: one contiguous band per XCD)
     uint32_t* tile_perm = nullptr;   // blend tile permutation (t_cap)
+    uint32_t* big_list = nullptr;    // per-tile depth order: tiles with lists over one wave's cap (t_cap)
+    uint32_t* big_counts = nullptr;  // their count, one word per frame parity
+    int tds_parity = 0;              // parity of the next per-tile depth-order frame
     int completion_events = 1;       // 0: no completion event / overflow query (stream capture)
+    int depth_order = 0;             // binning path: 0 = global depth sort, 1 = per-tile depth sort
+    bool last_tile_order = false;    // the last sorted frame used the per-tile depth sort
     unsigned int* queue = nullptr;   // spare device counters (blend experiments)
     int resident_groups = 2048;      // workgroups of 256 that fit on the device at once
     // frame state
@@ -404,6 +409,8 @@ int ensure_static(gsr_context* c) {
     if (int rc = realloc_dev(&c->queue, 8)) return rc;
     if (int rc = realloc_dev(&c->dstats, 4 + 4 * (size_t)gsr::kMaxSortGroups)) return rc;
     if (int rc = realloc_dev(&c->binmeta, 256 + 128)) return rc;
+    if (int rc = realloc_dev(&c->big_counts, 2)) return rc;
+    HIP_TRY(hipMemset(c->big_counts, 0, 2 * sizeof(uint32_t)));
     {
         int dev = 0, cus = 0;
         HIP_TRY(hipGetDevice(&dev));
@@ -452,6 +459,7 @@ int ensure_tiles(gsr_context* c, int64_t t) {
     HIP_TRY(hipDeviceSynchronize());
     if (int rc = realloc_dev(&c->ranges, (size_t)t)) return rc;
     if (int rc = realloc_dev(&c->tile_perm, (size_t)t)) return rc;
+    if (int rc = realloc_dev(&c->big_list, (size_t)t)) return rc;
     c->t_cap = t;
     return GSR_OK;
 }
@@ -559,7 +567,7 @@ extern "C" void gsr_destroy(gsr_context* c) {
     for (auto* p : {(void*)c->rec, (void*)c->items[0], (void*)c->items[1], (void*)c->rect, (void*)c->pairs[0],
                     (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->queue, (void*)c->dstats,
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
-                    (void*)c->cbins, (void*)c->srect, (void*)c->tile_perm})
+                    (void*)c->cbins, (void*)c->srect, (void*)c->tile_perm, (void*)c->big_list, (void*)c->big_counts})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -622,14 +630,22 @@ static uint32_t* pair_vals(gsr_context* c, int b) {
     return reinterpret_cast<uint32_t*>(c->pairs[b]) + c->p_cap;
 }
 
-static int sort_locked(gsr_context* c) {
-    if (!c->have_pre) return set_err(GSR_E_ARG, "gsr_sort before gsr_preprocess");
+// Column-pass chunk counts for the current capacity and grid.
+static int ensure_cbins(gsr_context* c) {
+    const int64_t need = 256 * (int64_t)gsr::bin_col_chunks_max((uint32_t)c->p_cap, c->fr.tiles_y);
+    if (need > c->cbins_cap) {
+        HIP_TRY(hipDeviceSynchronize());
+        if (int rc = realloc_dev(&c->cbins, (size_t)need)) return rc;
+        c->cbins_cap = need;
+    }
+    return GSR_OK;
+}
+
+// Global stable depth sort of the preprocess items (key << 32 | index), 4 x 8-bit
+// passes with the device-side pass plan; with rects (binning) the last pass also
+// writes them in depth order (srect).  Result in items[passes run & 1].
+static int depth_sort_locked(gsr_context* c, bool with_rects) {
     const uint32_t n = (uint32_t)c->n;
-    const bool bin = c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
-    c->last_binned = bin;
-    // ---- stable depth sort of (key << 32 | index), 4 x 8 bits; for the binning
-    // path its last pass also writes the rects in depth order (srect) ----
-    mark(c, GSR_STAGE_DEPTH_SORT);
     // smaller tiles for the 1M-item depth sort: ~500 workgroups instead of ~250
     const int di = c->depth_items ? c->depth_items : (c->n < (int64_t(4) << 20) ? 8 : 16);
     int gd = groups_for(c->n, 256 * di);
@@ -637,17 +653,50 @@ static int sort_locked(gsr_context* c) {
     for (int p = 0; p < 4; p++)
         HIP_TRY(gsr::launch_radix_pass(c->items[p & 1], c->items[(p + 1) & 1], nullptr, n, 32 + 8 * p, 8, gd, di,
                                        c->hist, c->totals, nullptr, c->stream, c->depth_skip ? c->dstats : nullptr,
-                                       p, bin ? c->rect : nullptr, bin ? c->srect : nullptr));
+                                       p, with_rects ? c->rect : nullptr, with_rects ? c->srect : nullptr));
+    return GSR_OK;
+}
+
+static int sort_locked(gsr_context* c) {
+    if (!c->have_pre) return set_err(GSR_E_ARG, "gsr_sort before gsr_preprocess");
+    const uint32_t n = (uint32_t)c->n;
+    const bool bin = c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
+    c->last_binned = bin;
+    // per-tile depth order (knob): bin in index order, then sort each tile's list by depth
+    const bool per_tile = bin && c->depth_order == 1;
+    c->last_tile_order = per_tile;
+    if (per_tile) {
+        if (int rc = ensure_cbins(c)) return rc;
+        auto* row_pairs = reinterpret_cast<unsigned long long*>(c->binmeta);
+        auto* row_items = reinterpret_cast<uint32_t*>(c->binmeta + 256);
+        const uint32_t cap = (uint32_t)c->p_cap;
+        const int gb = std::min(groups_for(c->n, 1024), gsr::kMaxSortGroups / 2);
+        mark(c, GSR_STAGE_EMIT);
+        HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], nullptr, n, c->rect, gb, c->hist, row_items,
+                                     row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items, c->stream));
+        mark(c, GSR_STAGE_TILE_SORT);
+        HIP_TRY(gsr::launch_bin_cols(c->pairs[0], row_items, row_pairs, c->cbins, c->bin_col_groups, cap,
+                                     c->fr.tiles_x, c->fr.tiles_y, pair_vals(c, 1), c->ranges, c->stats,
+                                     c->hstats_dev, c->bin_col_items, c->stream));
+        mark(c, GSR_STAGE_DEPTH_SORT);
+        HIP_TRY(gsr::launch_tile_depth_sort(c->ranges, c->ntiles, c->items[0], pair_vals(c, 1), c->pairs[0],
+                                            reinterpret_cast<uint32_t*>(pair_keys(c, 1)), c->big_list,
+                                            c->big_counts, c->tds_parity, std::min(c->ntiles, 1024), c->stats,
+                                            c->hstats_dev, c->stream));
+        c->tds_parity ^= 1;
+        c->pair_buf = 1;
+        c->have_sort = true;
+        return GSR_OK;
+    }
+    // ---- stable depth sort of (key << 32 | index), 4 x 8 bits; for the binning
+    // path its last pass also writes the rects in depth order (srect) ----
+    mark(c, GSR_STAGE_DEPTH_SORT);
+    if (int rc = depth_sort_locked(c, bin)) return rc;
     // result in items[passes run & 1] (device-side plan; emission picks it)
     if (bin) {
         // ---- row pass, then column pass (gsr_kernels.hip "tile binning") ----
         const uint32_t cap = (uint32_t)c->p_cap;
-        const int64_t need = 256 * (int64_t)gsr::bin_col_chunks_max(cap, c->fr.tiles_y);
-        if (need > c->cbins_cap) {
-            HIP_TRY(hipDeviceSynchronize());
-            if (int rc = realloc_dev(&c->cbins, (size_t)need)) return rc;
-            c->cbins_cap = need;
-        }
+        if (int rc = ensure_cbins(c)) return rc;
         auto* row_pairs = reinterpret_cast<unsigned long long*>(c->binmeta);
         auto* row_items = reinterpret_cast<uint32_t*>(c->binmeta + 256);
         const int gb = std::min(groups_for(c->n, 1024), gsr::kMaxSortGroups / 2);
@@ -782,6 +831,7 @@ void copy_settings(gsr_context* d, const gsr_context* s) {
     d->blend_wpg = s->blend_wpg;
     d->blend_band_tiles = s->blend_band_tiles;
     d->completion_events = s->completion_events;
+    d->depth_order = s->depth_order;
 }
 
 // Lanes 1..F-1: child contexts, streams and events, created once and kept.
@@ -955,6 +1005,7 @@ static int depth_passes_locked(gsr_context* c, int* passes) {
 extern "C" int gsr_depth_passes(gsr_context* c) {
     if (!c || !c->have_sort) return set_err(GSR_E_ARG, "gsr_depth_passes: no sorted frame");
     std::lock_guard<std::mutex> lk(c->mu);
+    if (c->last_tile_order) return 0;   // per-tile depth order: no global passes ran
     HIP_TRY(hipStreamSynchronize(c->stream));
     int p = 4;
     if (int rc = depth_passes_locked(c, &p)) return rc;
@@ -964,6 +1015,14 @@ extern "C" int gsr_depth_passes(gsr_context* c) {
 extern "C" int gsr_read_depth_order(gsr_context* c, uint64_t* host, int64_t n) {
     if (!c || !host || n < 0 || n > c->n || !c->have_sort) return set_err(GSR_E_ARG, "gsr_read_depth_order: bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
+    if (c->last_tile_order) {
+        // per-tile depth order: the frame never sorted globally; sort its preprocess
+        // items now (same kernels and plan as the global path; the frame's tile
+        // lists are already final, and items are not read after the frame)
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (int rc = depth_sort_locked(c, false)) return rc;
+        c->last_tile_order = false;
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     int p = 4;
     if (int rc = depth_passes_locked(c, &p)) return rc;
@@ -1034,14 +1093,24 @@ extern "C" int gsr_stage_times(gsr_context* c, double* ms, int64_t* frames) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (int s = 0; s < GSR_NUM_STAGES; s++) ms[s] = 0.0;
     for (auto& f : c->ev_frames) {
+        // stages may be recorded out of index order (per-tile depth order runs its
+        // depth stage after the binning passes): each stage lasts until the next
+        // recorded boundary in TIME order
+        hipEvent_t e0 = nullptr;
+        for (int s = 0; s <= GSR_NUM_STAGES && !e0; s++) e0 = f.ev[s];
+        float at[GSR_NUM_STAGES + 1];
+        for (int s = 0; s <= GSR_NUM_STAGES; s++) {
+            at[s] = -1.0f;
+            if (f.ev[s] && e0 && hipEventElapsedTime(&at[s], e0, f.ev[s]) != hipSuccess) at[s] = -1.0f;
+        }
         for (int s = 0; s < GSR_NUM_STAGES; s++) {
-            hipEvent_t a = f.ev[s];
-            hipEvent_t b = nullptr;
-            for (int q = s + 1; q <= GSR_NUM_STAGES && !b; q++) b = f.ev[q];
-            if (a && b) {
-                float t = 0.0f;
-                if (hipEventElapsedTime(&t, a, b) == hipSuccess) ms[s] += t;
-            }
+            if (!f.ev[s] || at[s] < 0.0f) continue;
+            float next = -1.0f;
+            for (int q = 0; q <= GSR_NUM_STAGES; q++)
+                if (q != s && f.ev[q] && at[q] >= 0.0f && (at[q] > at[s] || (at[q] == at[s] && q > s)) &&
+                    (next < 0.0f || at[q] < next))
+                    next = at[q];
+            if (next >= 0.0f) ms[s] += next - at[s];
         }
         for (auto e : f.ev)
             if (e) c->ev_pool.push_back(e);
@@ -1097,6 +1166,10 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     case GSR_TUNE_BLEND_WAVES_PER_GROUP:
         if (value != 1 && value != 2) return set_err(GSR_E_ARG, "gsr_set_tuning: blend waves per group must be 1 or 2");
         c->blend_wpg = value;
+        return GSR_OK;
+    case GSR_TUNE_DEPTH_ORDER:
+        if (value < 0 || value > 1) return set_err(GSR_E_ARG, "gsr_set_tuning: depth order must be 0 or 1");
+        c->depth_order = value;
         return GSR_OK;
     case GSR_TUNE_BLEND_BAND_TILES:
         if (value < 0 || value > 65536) return set_err(GSR_E_ARG, "gsr_set_tuning: blend band tiles must be 0..65536");

@@ -66,9 +66,11 @@ enum {
 /* Stage indices for gsr_stage_times(). */
 enum {
     GSR_STAGE_PREPROCESS = 0,     /* cull + SH colour + projection + covariance + AABB */
-    GSR_STAGE_DEPTH_SORT = 1,     /* stable radix sort of (depth, index) */
-    GSR_STAGE_EMIT = 2,           /* scan of tile counts + (tile, index) pair emission */
-    GSR_STAGE_TILE_SORT = 3,      /* stable radix sort of pairs by tile */
+    GSR_STAGE_DEPTH_SORT = 1,     /* stable radix sort of (depth, index); per-tile depth order
+                                     (GSR_TUNE_DEPTH_ORDER): each tile's list sorted by depth,
+                                     which runs after the two binning passes */
+    GSR_STAGE_EMIT = 2,           /* pair emission, or the binning row pass */
+    GSR_STAGE_TILE_SORT = 3,      /* stable radix sort of pairs by tile, or the binning column pass */
     GSR_STAGE_RANGES = 4,         /* per-tile [start, end) from sorted pairs */
     GSR_STAGE_BLEND = 5,          /* front-to-back alpha compositing */
     GSR_NUM_STAGES = 6
@@ -187,7 +189,9 @@ int64_t gsr_row_item_count(gsr_context* ctx);
  * Culled / invalid Gaussians have tile_count 0 and depth_key 0xFFFFFFFF;
  * their other fields are unspecified. */
 int gsr_read_splats(gsr_context* ctx, void* host_records, int64_t n);
-/* (depth_key << 32 | index) items after the depth sort, n of them. */
+/* (depth_key << 32 | index) items after the depth sort, n of them.  A frame
+ * that used the per-tile depth order has no global one: it is computed here
+ * (stable sort of that frame's keys, the same kernels as the global path). */
 int gsr_read_depth_order(gsr_context* ctx, uint64_t* host_items, int64_t n);
 /* (tile << 32 | index) pairs after the tile sort; returns the count copied. */
 int64_t gsr_read_pairs(gsr_context* ctx, uint64_t* host_pairs, int64_t cap);
@@ -245,11 +249,16 @@ enum {
     GSR_TUNE_BLEND_TILE_ORDER = 12,  /* blend schedule 0: 1 = longest tiles first, 0 = spatial (default) */
     GSR_TUNE_BLEND_BAND_TILES = 13,  /* blend schedule 0: tiles per spatial band, bands dealt round-robin
                                         to the 8 XCDs (default 4); 0 = one contiguous band per XCD */
-    GSR_TUNE_BLEND_WAVES_PER_GROUP = 14 /* blend schedule 0 with bands: 8x8 blocks per workgroup, 1 | 2 */
+    GSR_TUNE_BLEND_WAVES_PER_GROUP = 14, /* blend schedule 0 with bands: 8x8 blocks per workgroup, 1 | 2 */
+    GSR_TUNE_DEPTH_ORDER = 15        /* tile binning path: 0 (default) = global depth sort before binning;
+                                        1 = bin in index order, then sort every tile's list by depth (one
+                                        wave per list <= 1024, a workgroup per longer list, lists over 4096
+                                        chunked through global scratch); same pairs, same image */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Depth-sort digit passes the last sorted frame ran (1..4; trailing identity
- * passes are skipped on the device), or a negative error code. */
+ * passes are skipped on the device; 0 when the frame used the per-tile depth
+ * order, GSR_TUNE_DEPTH_ORDER), or a negative error code. */
 int gsr_depth_passes(gsr_context* ctx);
 /* Schedule 2 = schedule 0 with per-workgroup timestamps instead of counters:
  * with diagnostics on, the last frame's blend stores {start, end} of the

@@ -188,7 +188,7 @@ def test_blend_block_mappings_parity(gpu, orc, torch, c1, knobs):
         assert_image_parity(got, orc.render(soa, cam, W, H, 3.0))
 
 
-@pytest.mark.parametrize("knobs", [{}, {8: 4, 9: 16}, {8: 16, 9: 4, 10: 7}])
+@pytest.mark.parametrize("knobs", [{}, {8: 4, 9: 16}, {8: 16, 9: 4, 10: 7}, {15: 1}, {15: 1, 8: 16, 10: 7}])
 def test_tile_binning_matches_pair_sort(gpu, orc, torch, c1, knobs):
     """Row + column binning (default for grids <= 256 x 256 tiles) gives the same
     tile lists as pair emission + the key-value tile sort: identical (tile,
@@ -263,6 +263,7 @@ def test_depth_pass_plan_exact(gpu, orc, torch, c1, pos, look):
     orders = []
     for skip in (1, 0):
         r = gpu.Renderer()
+        r.set_tuning(15, 0)      # global depth sort (the per-tile order has no passes to plan)
         r.set_tuning(6, skip)
         got, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
         assert_image_parity(got, orc.render(soa, cam, W, H, 3.0))

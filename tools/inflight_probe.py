@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=200)
-    ap.add_argument("--inflight", type=int, nargs="+", default=[1, 2, 3])
+    ap.add_argument("--inflight", type=int, nargs="+", default=[1, 2, 3, 4])
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     import torch
@@ -63,6 +63,40 @@ def main():
                 assert torch.equal(outs[f], ref), f"inflight {k}: context {f} image differs"
     for k in a.inflight:
         print(f"inflight {k}: fps " + " ".join(f"{v:.1f}" for v in res[k]) + f"  best {max(res[k]):.1f}", flush=True)
+
+    # stage split over two streams per context: preprocess + sort on one, blend on the
+    # other, with the given priorities (HIP: lower number = higher priority)
+    lo_p, hi_p = torch.cuda.Stream.priority_range()
+    print(f"stream priority range: low {lo_p} high {hi_p}", flush=True)
+    for name, ps, pb in (("split equal", 0, 0), ("split sort-high", hi_p, lo_p), ("split blend-high", lo_p, hi_p)):
+        for k in a.inflight:
+            if k == 1:
+                continue
+            ss = [torch.cuda.Stream(priority=ps) for _ in range(k)]
+            sb = [torch.cuda.Stream(priority=pb) for _ in range(k)]
+            ev_sorted = [torch.cuda.Event() for _ in range(k)]
+            ev_done = [torch.cuda.Event() for _ in range(k)]
+            best = []
+            for _ in range(a.rounds):
+                torch.cuda.synchronize()
+                for f in range(k):
+                    ev_done[f].record(sb[f])
+                t0 = time.perf_counter()
+                for i in range(a.frames):
+                    f = i % k
+                    ss[f].wait_event(ev_done[f])
+                    rs[f].preprocess(scene, cam, W, H, stream=ss[f].cuda_stream)
+                    rs[f].sort(stream=ss[f].cuda_stream)
+                    ev_sorted[f].record(ss[f])
+                    sb[f].wait_event(ev_sorted[f])
+                    rs[f].blend(outs[f].data_ptr(), stream=sb[f].cuda_stream)
+                    ev_done[f].record(sb[f])
+                torch.cuda.synchronize()
+                best.append(a.frames / (time.perf_counter() - t0))
+                for f in range(k):
+                    assert torch.equal(outs[f], ref), f"{name} {k}: context {f} image differs"
+            print(f"{name} inflight {k}: fps " + " ".join(f"{v:.1f}" for v in best) + f"  best {max(best):.1f}",
+                  flush=True)
 
 
 if __name__ == "__main__":
