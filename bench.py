@@ -128,7 +128,9 @@ def load_pmc_counter(config: int, kernel: str, counter: str):
 def load_pmc_traffic(config: int, kernel: str):
     """HBM bytes per launch of `kernel` from the committed PMC summary of the same
     workload (tools/profile.sh: separate FETCH_SIZE / WRITE_SIZE passes, KiB x 1024,
-    FETCH doubled per the gfx950 correction), or None."""
+    FETCH corrected per access pattern: x2 for wide coalesced streams (the guide's
+    gfx950 correction), x1 for the blend's scattered 64-B record gathers, which our
+    calibration shows are counted exactly — profiles/r01_fetch_calibration.txt), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         d = json.load(open(p))

@@ -4,8 +4,10 @@
 Per kernel: calls, average duration (kernel trace), and per-launch HBM traffic
 from the separate FETCH_SIZE / WRITE_SIZE passes.  Units and gfx950
 corrections follow MI355X_MICROARCH.md section HBM: the counters are in KiB
-(x1024) and FETCH_SIZE reads half the bytes of a wide coalesced stream, so the
-corrected read traffic is reported as 2 x FETCH_SIZE next to the raw value.
+(x1024) and FETCH_SIZE reads half the bytes of a wide coalesced stream but
+exactly the bytes of scattered 64-B record gathers (own calibration), so the
+corrected read traffic is reported next to the raw value: x2 for streaming
+kernels, x1 for the blend (fetch_factor).
 
     python tools/summarize_prof.py gpurun_out/prof > profiles/r01_rocprof_summary.txt
 """
@@ -14,6 +16,18 @@ import csv
 import os
 import re
 import sys
+
+
+# FETCH_SIZE correction per access pattern (tools/microbench/gather_fetch.hip,
+# profiles/r01_fetch_calibration.txt): wide coalesced streams issue 128-B
+# requests tallied at 64 B (x2, the guide's correction); scattered 64-B record
+# gathers (the blend's splat records, 48 or 64 B of a 64-B record per lane) issue
+# one 64-B request each and are counted exactly (x1).
+GATHER_KERNELS = ("k_blend_w", "k_blend<")
+
+
+def fetch_factor(kernel: str) -> float:
+    return 1.0 if kernel.startswith(GATHER_KERNELS) else 2.0
 
 
 def short(name: str) -> str:
@@ -35,17 +49,18 @@ def main(d):
             agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)
         pmc[c] = {k: sum(v) / len(v) for k, v in agg.items()}
     print("rocprofv3 --kernel-trace --stats; PMC FETCH_SIZE and WRITE_SIZE in separate passes")
-    print(f"{'kernel':<34}{'calls':>7}{'avg_us':>10}{'pct':>7}{'FETCH_MB':>10}{'2xFETCH_MB':>12}{'WRITE_MB':>10}{'GB/s(2xF+W)':>13}")
+    print(f"{'kernel':<34}{'calls':>7}{'avg_us':>10}{'pct':>7}{'FETCH_MB':>10}{'corrFETCH_MB':>13}{'WRITE_MB':>10}{'GB/s(cF+W)':>12}")
     for r in stats:
         k = short(r["Name"])
         avg_us = float(r["AverageNs"]) / 1e3
         f = pmc.get("FETCH_SIZE", {}).get(k)
         w = pmc.get("WRITE_SIZE", {}).get(k)
         fmt = lambda v: f"{v / 1e6:10.2f}" if v is not None else f"{'-':>10}"
-        gbs = (2 * f + w) / (avg_us * 1e-6) / 1e9 if (f is not None and w is not None and avg_us > 0) else None
+        cf = fetch_factor(k) * f if f is not None else None
+        gbs = (cf + w) / (avg_us * 1e-6) / 1e9 if (f is not None and w is not None and avg_us > 0) else None
         print(f"{k:<34}{int(r['Calls']):>7}{avg_us:>10.2f}{float(r['Percentage']):>7.2f}{fmt(f)}"
-              f"{(f'{2 * f / 1e6:12.2f}' if f is not None else f'{chr(45):>12}')}{fmt(w)}"
-              f"{(f'{gbs:13.1f}' if gbs is not None else f'{chr(45):>13}')}")
+              f"{(f'{cf / 1e6:13.2f}' if f is not None else f'{chr(45):>13}')}{fmt(w)}"
+              f"{(f'{gbs:12.1f}' if gbs is not None else f'{chr(45):>12}')}")
 
 
 def write_json(d, out, config, source):
@@ -61,8 +76,9 @@ def write_json(d, out, config, source):
         pm[c] = {k: sum(v) / len(v) for k, v in agg.items()}
     for k in pm["FETCH_SIZE"]:
         if k in pm["WRITE_SIZE"]:
-            res[k] = {"fetch_bytes_raw": pm["FETCH_SIZE"][k], "fetch_bytes_corrected": 2 * pm["FETCH_SIZE"][k],
-                      "write_bytes": pm["WRITE_SIZE"][k]}
+            res[k] = {"fetch_bytes_raw": pm["FETCH_SIZE"][k],
+                      "fetch_bytes_corrected": fetch_factor(k) * pm["FETCH_SIZE"][k],
+                      "fetch_correction": fetch_factor(k), "write_bytes": pm["WRITE_SIZE"][k]}
     # any other counter passes present (SQ_*): per-kernel mean per launch, latest process only
     import glob
     for f in glob.glob(os.path.join(d, "pmc_*", "pmc_counter_collection.csv")):
