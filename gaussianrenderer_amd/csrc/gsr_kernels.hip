@@ -153,11 +153,6 @@ __device__ __forceinline__ void mv4(const float* M, const float* v, float* out) 
     }
 }
 
-__device__ __forceinline__ uint4 dead_record_d() {
-    // tile ranges empty, count 0, depth key 0xFFFFFFFF (sorts last)
-    return make_uint4(0u, 0u, 0u, 0xffffffffu);
-}
-
 // Compact tile rectangle of one Gaussian for the emission: tx0 | tx1 << 16 |
 // ty0 << 32 | ty1 << 48; tile count (tx1 - tx0 + 1) * (ty1 - ty0 + 1), which
 // is 0 for the dead value below (tx0 = ty0 = 1, tx1 = ty1 = 0).
@@ -166,6 +161,66 @@ __device__ __forceinline__ uint32_t rect_count(uint64_t r) {
     const int tx0 = (int)(r & 0xffffu), tx1 = (int)((r >> 16) & 0xffffu);
     const int ty0 = (int)((r >> 32) & 0xffffu), ty1 = (int)(r >> 48);
     return (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1));
+}
+
+// ------------------------------------------------------------------ blend cull words
+//
+// The blend culls every record of its tile list against each 8x8 block (the
+// ellipse-vs-block test and the fast-path proof below).  Everything in those
+// tests that depends on the record alone is computed once here, in
+// k_preprocess, and stored as the record's fourth 16-B word (the blend's record
+// gather fetches the whole 64-B line anyway: profiles/r01_fetch_calibration.txt):
+//   { cut, ih, iv, S }
+// cut  md2 cutoff (md2_cutoff) if the conic is robustly positive definite, else +inf
+//      (+inf or NaN: the block test never culls)
+// ih   -h / e, iv = -h / a (edge minimisers of the quadratic form), h = (b + c) / 2
+// S    |a| + |b| + |c| + |e| if the record passes the per-record part of the
+//      fast-path proof (robustly PD, finite S and colour, coefficients 0 or
+//      >= 2^-60), else +inf (then the per-block part S M^2 <= 4e7 fails, and the
+//      block test's rounding margin is infinite: conservative, never culls)
+
+// md2 cutoff of one splat: alpha = fminf(op * exp(-md2/2), 0.99) < 1e-3 holds
+// for every md2 > 2 ln(1000 op) (exp and the product are within a few ulp), so
+// lanes beyond the returned bound can never composite.  The bound is padded by
+// 1e-5 relative + 1e-3 absolute — orders of magnitude above the rounding of
+// gsr_expf, the product and the hardware log2 used here — and is NaN (never
+// skip) for NaN opacity, +inf for infinite opacity, -inf for op <= 0.  It only
+// decides whether a wave may SKIP work; it never changes a composited value.
+__device__ __forceinline__ float md2_cutoff(float op) {
+    const float l = __log2f(op * 1000.0f);                   // v_log_f32
+    return (l * 1.38629436111989061f) * 1.00001f + 1e-3f;     // 2 ln2 log2(1000 op)
+}
+
+// Fast-path proof for one splat on one block (exactness, not a heuristic):
+// finite conic that is robustly positive definite with |a|+|b|+|c|+|e| times
+// the squared largest block offset <= 4e7 keeps every in-box md2 finite and
+// >= -10 (float error of the 9-op form < 10), so -md2/2 lies in gsr_expf_x2's
+// proven range; finite colours make "alpha = 0 when not taken" leave the
+// accumulators bit-identical (c + (col*0)*T == c, T*(1-0) == T).
+// Every coefficient is also 0 or of magnitude >= 2^-60: the pixel offsets are
+// integers, so every intermediate of the md2 form is a multiple of 2^-83 —
+// zero or a normal number — and scaling the coefficients by -0.5 scales every
+// intermediate exactly: the form on (-a/2, -b/2, -c/2, -e/2) IS -0.5f * md2.
+// The per-record part is the cull word's S; the per-block part, in the blend,
+// is S * M * M <= 4e7.
+__device__ __forceinline__ bool coef_ok(float v) { return v == 0.0f || fabsf(v) >= 0x1p-60f; }
+
+__device__ __forceinline__ uint4 cull_word(float a, float b, float c, float e, float op, float r, float g,
+                                           float bl) {
+    const float inf = __builtin_huge_valf();
+    const float h = 0.5f * (b + c);
+    const bool pd = a > 0.0f && e > 0.0f && (a * e - h * h) > 1e-4f * (a * e);
+    const float cut = md2_cutoff(op);
+    const float S = fabsf(a) + fabsf(b) + fabsf(c) + fabsf(e);
+    const bool fast = pd && isfinite(S) && isfinite(r) && isfinite(g) && isfinite(bl) && coef_ok(a) &&
+                      coef_ok(b) && coef_ok(c) && coef_ok(e);
+    // edge minimisers; v_rcp_f32 (~1 ulp) moves them by ~1e-7 relative, which
+    // changes an edge minimum only at second order (e * delta^2), far inside the
+    // block test's rounding margin
+    const float ih = pd ? -h * __builtin_amdgcn_rcpf(e) : 0.0f;
+    const float iv = pd ? -h * __builtin_amdgcn_rcpf(a) : 0.0f;
+    return make_uint4(__float_as_uint(pd && cut < 3.0e38f ? cut : inf), __float_as_uint(ih), __float_as_uint(iv),
+                      __float_as_uint(fast ? S : inf));
 }
 
 // Temporal state of a 4D (Spacetime-Gaussian style) Gaussian at time t, in
@@ -201,7 +256,6 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     float tmp_xyz[4], new_xyz[4];
     mv4(fr.V, old_xyz, tmp_xyz);
     if (!isfinite(tmp_xyz[0]) || !isfinite(tmp_xyz[1]) || !isfinite(tmp_xyz[2])) {
-        R[3] = dead_record_d();
         rect[i] = kDeadRect;
         return;
     }
@@ -211,7 +265,6 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     new_xyz[2] = new_xyz[2] / new_xyz[3];
     if (!isfinite(new_xyz[0]) || !isfinite(new_xyz[1]) || !isfinite(new_xyz[2]) ||
         tmp_xyz[2] >= -fr.znear || new_xyz[2] < -1.0f || new_xyz[2] > 1.0f) {
-        R[3] = dead_record_d();
         rect[i] = kDeadRect;
         return;
     }
@@ -259,7 +312,6 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     S2[3] = (H * 0.5f) * (H * 0.5f) * S2[3];
     const float det = S2[0] * S2[3] - S2[1] * S2[2];
     if (!isfinite(det) || det < 1e-8f) {                        // render.cu:690
-        R[3] = dead_record_d();
         rect[i] = kDeadRect;
         return;
     }
@@ -273,7 +325,6 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
         const float opt = arr[GSR_A_OPACITY * stride + i] * tfac;
         const float hh = 0.5f * (ic1 + ic2);
         if (opt < 0.9e-3f && ic0 > 0.0f && ic3 > 0.0f && (ic0 * ic3 - hh * hh) > 1e-4f * (ic0 * ic3)) {
-            R[3] = dead_record_d();
             rect[i] = kDeadRect;
             return;
         }
@@ -300,7 +351,6 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     float xmin = new_xyz[0] - ex, xmax = new_xyz[0] + ex;
     float ymin = new_xyz[1] - ey, ymax = new_xyz[1] + ey;
     if (xmax < -0.99f || xmin > 0.99f || ymax < -0.99f || ymin > 0.99f) {   // render.cu:737
-        R[3] = dead_record_d();
         rect[i] = kDeadRect;
         return;
     }
@@ -321,7 +371,6 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     const int tx1 = min(fr.tiles_x - 1, xmax_px / GSR_TILE_PX);
     const int ty0 = ymin_px / GSR_TILE_PX;
     const int ty1 = min(fr.tiles_y - 1, ymax_px / GSR_TILE_PX);
-    const uint32_t count = (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1));
 
     // ---- SH colour, bands 0..2 (render.cu:500-534), only for survivors ----
     float dir[3] = {gx - fr.campos[0], gy - fr.campos[1], gz - fr.campos[2]};
@@ -384,7 +433,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
                       __float_as_uint(col[2]));
     R[2] = make_uint4((uint32_t)px_x, (uint32_t)px_y, (uint32_t)xmin_px | ((uint32_t)xmax_px << 16),
                       (uint32_t)ymin_px | ((uint32_t)ymax_px << 16));
-    R[3] = make_uint4((uint32_t)tx0 | ((uint32_t)tx1 << 16), (uint32_t)ty0 | ((uint32_t)ty1 << 16), count, key);
+    R[3] = cull_word(ic0, ic1, ic2, ic3, opacity, col[0], col[1], col[2]);
     rect[i] = (uint64_t)((uint32_t)tx0 | ((uint32_t)tx1 << 16)) | ((uint64_t)((uint32_t)ty0 | ((uint32_t)ty1 << 16)) << 32);
     items[i] = ((uint64_t)key << 32) | (uint64_t)(uint32_t)i;
 }
@@ -1944,36 +1993,20 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
-// md2 cutoff of one splat: alpha = fminf(op * exp(-md2/2), 0.99) < 1e-3 holds
-// for every md2 > 2 ln(1000 op) (exp and the product are within a few ulp), so
-// lanes beyond the returned bound can never composite.  The bound is padded by
-// 1e-5 relative + 1e-3 absolute — orders of magnitude above the rounding of
-// gsr_expf, the product and the hardware log2 used here — and is NaN (never
-// skip) for NaN opacity, +inf for infinite opacity, -inf for op <= 0.  It only
-// decides whether a wave may SKIP work; it never changes a composited value.
-__device__ __forceinline__ float md2_cutoff(float op) {
-    const float l = __log2f(op * 1000.0f);                   // v_log_f32
-    return (l * 1.38629436111989061f) * 1.00001f + 1e-3f;     // 2 ln2 log2(1000 op)
-}
-
 // Can any pixel of an integer rectangle reach md2 <= cut?  dx0..dy1 bound the
 // (float)pixel - (float)centre offsets of the rectangle's pixels (monotone, so
 // every pixel's dx lies in [dx0, dx1]).  Returns false only when the exact
 // minimum of the quadratic form a dx^2 + (b+c) dx dy + e dy^2 over that
 // rectangle exceeds cut by more than a bound on the float rounding of md2
 // (<= ~6 ulp of |a|dx^2 + (|b|+|c|)|dx dy| + |e|dy^2, padded 10x) — so a culled
-// splat could never have composited onto this block.  Not positive definite
-// (robustly), NaN or inf inputs: never culled.
-__device__ __forceinline__ bool block_may_reach(float a, float b, float c, float e, float dx0, float dx1,
-                                                float dy0, float dy1, float cut) {
+// splat could never have composited onto this block.  cut, ih, iv and S come
+// from the record's cull word (cull_word): a conic that is not robustly
+// positive definite has cut = +inf, a record without the per-record fast proof
+// S = +inf (infinite margin); NaN anywhere: never culled.
+__device__ __forceinline__ bool block_may_reach(float a, float b, float c, float e, float ih, float iv, float S,
+                                                float dx0, float dx1, float dy0, float dy1, float M, float cut) {
     if (dx0 <= 0.0f && dx1 >= 0.0f && dy0 <= 0.0f && dy1 >= 0.0f) return true;
     const float h = 0.5f * (b + c);
-    const float det = a * e - h * h;
-    if (!(a > 0.0f && e > 0.0f && det > 1e-4f * (a * e)) || !(cut < 3.0e38f)) return true;
-    // minimiser along each edge; v_rcp_f32 (~1 ulp) moves it by ~1e-7 relative,
-    // which changes the edge minimum only at second order (e * delta^2), far
-    // inside the err margin below
-    const float ih = -h * __builtin_amdgcn_rcpf(e), iv = -h * __builtin_amdgcn_rcpf(a);
     auto q = [&](float x, float y) { return a * x * x + 2.0f * h * x * y + e * y * y; };
     // The form is convex with its minimum at the splat centre (offset 0,0), which
     // lies outside the rectangle here.  A far edge never holds the rectangle's
@@ -1985,8 +2018,7 @@ __device__ __forceinline__ bool block_may_reach(float a, float b, float c, float
     const float qy = q(fminf(fmaxf(iv * ye, dx0), dx1), ye);
     const bool x_out = dx0 > 0.0f || dx1 < 0.0f, y_out = dy0 > 0.0f || dy1 < 0.0f;
     const float qm = fminf(x_out ? qx : 3.0e38f, y_out ? qy : 3.0e38f);
-    const float M = fmaxf(fmaxf(fabsf(dx0), fabsf(dx1)), fmaxf(fabsf(dy0), fabsf(dy1)));
-    const float err = 4e-6f * (fabsf(a) + fabsf(b) + fabsf(c) + fabsf(e)) * M * M + 1e-3f;
+    const float err = 4e-6f * S * M * M + 1e-3f;
     return !(qm - err > cut);
 }
 
@@ -2019,26 +2051,6 @@ __device__ __forceinline__ f2 gsr_expf_x2(f2 xc) {
     res.x = __builtin_amdgcn_ldexpf(y.x, (int)n.x);
     res.y = __builtin_amdgcn_ldexpf(y.y, (int)n.y);
     return res;
-}
-
-// Fast-path proof for one splat on one block (exactness, not a heuristic):
-// finite conic that is robustly positive definite with |a|+|b|+|c|+|e| times
-// the squared largest block offset <= 4e7 keeps every in-box md2 finite and
-// >= -10 (float error of the 9-op form < 10), so -md2/2 lies in gsr_expf_x2's
-// proven range; finite colours make "alpha = 0 when not taken" leave the
-// accumulators bit-identical (c + (col*0)*T == c, T*(1-0) == T).
-// Every coefficient is also 0 or of magnitude >= 2^-60: the pixel offsets are
-// integers, so every intermediate of the md2 form is a multiple of 2^-83 —
-// zero or a normal number — and scaling the coefficients by -0.5 scales every
-// intermediate exactly: the form on (-a/2, -b/2, -c/2, -e/2) IS -0.5f * md2.
-__device__ __forceinline__ bool coef_ok(float v) { return v == 0.0f || fabsf(v) >= 0x1p-60f; }
-__device__ __forceinline__ bool fast_safe(float a, float b, float c, float e, float M, float r, float g,
-                                          float bl) {
-    const float h = 0.5f * (b + c);
-    const float S = fabsf(a) + fabsf(b) + fabsf(c) + fabsf(e);
-    return a > 0.0f && e > 0.0f && (a * e - h * h) > 1e-4f * (a * e) && S * M * M <= 4e7f &&
-           isfinite(S) && isfinite(r) && isfinite(g) && isfinite(bl) && coef_ok(a) && coef_ok(b) && coef_ok(c) &&
-           coef_ok(e);
 }
 
 // One wave64 per 8x8 pixel block (four per 16x16 tile, one tile per
@@ -2078,13 +2090,14 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
     float cb = 0.0f;
     const float4* wP4 = reinterpret_cast<const float4*>(wP);
 
-    uint4 ra = make_uint4(0, 0, 0, 0), rb = ra, rc = ra;
+    uint4 ra = make_uint4(0, 0, 0, 0), rb = ra, rc = ra, rd = ra;
     uint32_t nidx = 0;
     if (beg + lane < end) {
         const uint4* R = rec + 4 * (uint64_t)idx[beg + lane];
         ra = R[0];
         rb = R[1];
         rc = R[2];
+        rd = R[3];
     }
     if (beg + 64 + lane < end) nidx = idx[beg + 64 + lane];
     bool alive = __ballot(!(T < 1e-3f)) != 0ull;
@@ -2113,11 +2126,13 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 const uint64_t rows = (y1 == 7 ? ~0ull : ((1ull << (8 * (y1 + 1))) - 1ull)) & (~0ull << (8 * y0));
                 mlo = rep & (uint32_t)rows;
                 mhi = rep & (uint32_t)(rows >> 32);
-                hit = ((mlo & (uint32_t)live_b) | (mhi & (uint32_t)(live_b >> 32))) != 0u &&
-                      block_may_reach(a, b, c, e, dx0, dx1, dy0, dy1, md2_cutoff(__uint_as_float(rb.x)));
+                // cull word (cull_word): per-record parts of the block test and the proof
+                const float S = __uint_as_float(rd.w);
                 const float M = fmaxf(fmaxf(fabsf(dx0), fabsf(dx1)), fmaxf(fabsf(dy0), fabsf(dy1)));
-                fast = fast_safe(a, b, c, e, M, __uint_as_float(rb.y), __uint_as_float(rb.z),
-                                 __uint_as_float(rb.w));
+                hit = ((mlo & (uint32_t)live_b) | (mhi & (uint32_t)(live_b >> 32))) != 0u &&
+                      block_may_reach(a, b, c, e, __uint_as_float(rd.y), __uint_as_float(rd.z), S, dx0, dx1, dy0,
+                                      dy1, M, __uint_as_float(rd.x));
+                fast = S * M * M <= 4e7f;   // per-block part of the fast-path proof
             }
         }
         const uint64_t m = __ballot(hit);
@@ -2129,7 +2144,7 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
             const int h = (int)(k & 1u);
             S[0 + h] = (float)(int)rc.x;
             S[2 + h] = (float)(int)rc.y;
-            // fast batches store the conic pre-scaled by -0.5 (exact, see fast_safe)
+            // fast batches store the conic pre-scaled by -0.5 (exact, see coef_ok)
             const float sc = all_fast ? -0.5f : 1.0f;
             S[4 + h] = sc * __uint_as_float(ra.x);
             S[6 + h] = sc * __uint_as_float(ra.y);
@@ -2153,6 +2168,7 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
             ra = R[0];
             rb = R[1];
             rc = R[2];
+            rd = R[3];
         }
         if (base + 128 + lane < end) nidx = idx[base + 128 + lane];
 

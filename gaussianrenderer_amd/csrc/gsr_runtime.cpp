@@ -980,11 +980,40 @@ extern "C" int64_t gsr_row_item_count(gsr_context* c) {
     return total;
 }
 
+static int depth_passes_locked(gsr_context* c, int* passes);
+
+// The device record's fourth word is the blend's cull word (gsr_kernels.hip
+// cull_word); the readback layout's fourth word {tile x range, tile y range,
+// tile count, depth key} is rebuilt from the preprocess tile rects (index order)
+// and the frame's depth items: (key << 32 | index) in index order right after
+// preprocess or in a per-tile-order frame, depth-sorted after a global sort.
 extern "C" int gsr_read_splats(gsr_context* c, void* host, int64_t n) {
     if (!c || !host || n < 0 || n > c->n) return set_err(GSR_E_ARG, "gsr_read_splats: bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (n) HIP_TRY(hipMemcpy(host, c->rec, (size_t)n * GSR_SPLAT_RECORD_BYTES, hipMemcpyDeviceToHost));
+    if (!n) return GSR_OK;
+    if (!c->have_pre) return set_err(GSR_E_ARG, "gsr_read_splats: no preprocessed frame");
+    HIP_TRY(hipMemcpy(host, c->rec, (size_t)n * GSR_SPLAT_RECORD_BYTES, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> rect((size_t)n), items((size_t)c->n);
+    HIP_TRY(hipMemcpy(rect.data(), c->rect, (size_t)n * 8, hipMemcpyDeviceToHost));
+    int p = 0;
+    if (c->have_sort && !c->last_tile_order)
+        if (int rc = depth_passes_locked(c, &p)) return rc;
+    HIP_TRY(hipMemcpy(items.data(), c->items[p & 1], (size_t)c->n * 8, hipMemcpyDeviceToHost));
+    auto* w = static_cast<uint32_t*>(host);
+    for (uint64_t it : items) {
+        const uint32_t i = (uint32_t)it;
+        if (i < (uint64_t)n) w[(size_t)i * 16 + 15] = (uint32_t)(it >> 32);
+    }
+    for (int64_t i = 0; i < n; i++) {
+        const uint64_t r = rect[(size_t)i];
+        const int tx0 = (int)(r & 0xffffu), tx1 = (int)((r >> 16) & 0xffffu);
+        const int ty0 = (int)((r >> 32) & 0xffffu), ty1 = (int)(r >> 48);
+        uint32_t* q = w + (size_t)i * 16;
+        q[12] = (uint32_t)r;
+        q[13] = (uint32_t)(r >> 32);
+        q[14] = (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1));
+    }
     return GSR_OK;
 }
 
