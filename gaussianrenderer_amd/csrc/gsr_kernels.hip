@@ -431,7 +431,8 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     R[0] = make_uint4(__float_as_uint(ic0), __float_as_uint(ic1), __float_as_uint(ic2), __float_as_uint(ic3));
     R[1] = make_uint4(__float_as_uint(opacity), __float_as_uint(col[0]), __float_as_uint(col[1]),
                       __float_as_uint(col[2]));
-    R[2] = make_uint4((uint32_t)px_x, (uint32_t)px_y, (uint32_t)xmin_px | ((uint32_t)xmax_px << 16),
+    // centre pixel stored as the float the blend computes with ((float)px, render.cu:329)
+    R[2] = make_uint4(__float_as_uint((float)px_x), __float_as_uint((float)px_y), (uint32_t)xmin_px | ((uint32_t)xmax_px << 16),
                       (uint32_t)ymin_px | ((uint32_t)ymax_px << 16));
     R[3] = cull_word(ic0, ic1, ic2, ic3, opacity, col[0], col[1], col[2]);
     rect[i] = (uint64_t)((uint32_t)tx0 | ((uint32_t)tx1 << 16)) | ((uint64_t)((uint32_t)ty0 | ((uint32_t)ty1 << 16)) << 32);
@@ -2114,7 +2115,7 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
             const int ymin = (int)(rc.w & 0xffffu), ymax = (int)(rc.w >> 16);
             hit = !(xmax < bx || xmin > bx + 7 || ymax < by || ymin > by + 7);
             if (hit) {
-                const float cx = (float)(int)rc.x, cy = (float)(int)rc.y;
+                const float cx = __uint_as_float(rc.x), cy = __uint_as_float(rc.y);
                 const float a = __uint_as_float(ra.x), b = __uint_as_float(ra.y);
                 const float c = __uint_as_float(ra.z), e = __uint_as_float(ra.w);
                 const int x0 = max(xmin - bx, 0), x1 = min(xmax - bx, 7);
@@ -2142,8 +2143,8 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             float* S = wP + (k >> 1) * kSlot;
             const int h = (int)(k & 1u);
-            S[0 + h] = (float)(int)rc.x;
-            S[2 + h] = (float)(int)rc.y;
+            S[0 + h] = __uint_as_float(rc.x);
+            S[2 + h] = __uint_as_float(rc.y);
             // fast batches store the conic pre-scaled by -0.5 (exact, see coef_ok)
             const float sc = all_fast ? -0.5f : 1.0f;
             S[4 + h] = sc * __uint_as_float(ra.x);
@@ -2158,8 +2159,9 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
         const uint32_t nsurv = (uint32_t)__popcll(m);
         if ((nsurv & 1u) && lane < 10) {
             // odd count: zero the unused second half of the last slot (mask 0 keeps it inert)
-            static constexpr int kHalf1[10] = {1, 3, 5, 7, 9, 11, 13, 16, 17, 19};
-            wP[(nsurv >> 1) * kSlot + kHalf1[lane]] = 0.0f;
+            // second-half dwords of a slot: 1 3 5 7 9 11 13 | 16 17 | 19 (arithmetic, not a
+            // table: a table load would stall the wave on memory once per odd batch)
+            wP[(nsurv >> 1) * kSlot + (lane < 7 ? 2 * lane + 1 : lane + 9 + (lane == 9))] = 0.0f;
         }
         if (DIAG) dg.loaded += cnt;
         // ---- prefetch: records of batch k+1, indices of batch k+2 ----

@@ -1010,6 +1010,14 @@ extern "C" int gsr_read_splats(gsr_context* c, void* host, int64_t n) {
         const int tx0 = (int)(r & 0xffffu), tx1 = (int)((r >> 16) & 0xffffu);
         const int ty0 = (int)((r >> 32) & 0xffffu), ty1 = (int)(r >> 48);
         uint32_t* q = w + (size_t)i * 16;
+        // the device keeps the centre pixel as the float the blend uses; the
+        // readback layout's int32 (exact for |px| <= 2^24, saturating like gsr_f2i_sat)
+        for (int k = 8; k < 10; k++) {
+            float f;
+            std::memcpy(&f, q + k, 4);
+            const int32_t v = f >= 2147483648.0f ? INT32_MAX : (f < -2147483648.0f ? INT32_MIN : (int32_t)f);
+            std::memcpy(q + k, &v, 4);
+        }
         q[12] = (uint32_t)r;
         q[13] = (uint32_t)(r >> 32);
         q[14] = (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1));
