@@ -279,6 +279,36 @@ def test_depth_pass_plan_exact(gpu, orc, torch, c1, pos, look):
     assert np.array_equal(orders[0], orders[1])
 
 
+def test_blend_slow_path_and_degenerate_records(gpu, orc, torch, c1):
+    """Records without the blend's fast-path proof (cull word S = inf: needle-thin
+    Gaussians whose conic is not robustly positive definite and has coefficients
+    ~1e7) and records with NaN opacity (md2 cutoff NaN: never culled; alpha =
+    fminf(NaN, 0.99)) run the exact one-splat path; the image must still equal the
+    oracle bit for bit, and the diagnostics must show the slow path ran."""
+    path, soa = c1
+    s = soa.copy()
+    rng = np.random.default_rng(7)
+    n = s.shape[1]
+    thin = rng.choice(n, 300, replace=False)
+    s[4, thin] = 1e-6                       # scale0: needle along one axis
+    s[5, thin] = 0.05
+    s[6, thin] = 0.05
+    nan_op = rng.choice(np.setdiff1d(np.arange(n), thin), 40, replace=False)
+    s[3, nan_op] = np.nan
+    W, H = 640, 480
+    cam = cam_for(gpu, W, H)
+    want = orc.render(s, cam, W, H, 3.0)
+    for variant in (0, 1):
+        r = gpu.Renderer()
+        r.set_blend_variant(variant)
+        got, _ = render_gpu(gpu, torch, gpu.Scene.from_soa(s), cam, W, H, renderer=r)
+        assert_image_parity(got, want)
+        r.set_diagnostics(True)
+        got2, _ = render_gpu(gpu, torch, gpu.Scene.from_soa(s), cam, W, H, renderer=r)
+        assert np.array_equal(got2.view(np.uint32), want.view(np.uint32))
+        assert r.blend_counters()["slow_path_iters"] > 0
+
+
 @pytest.mark.parametrize("ci", [0, 1, 3])
 def test_sh3_mode_parity(gpu, orc, torch, c1, ci):
     """Opt-in "Inria-correct" SH-3 scenes (degree-3 colour, channel-major f_rest)
