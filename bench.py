@@ -173,9 +173,33 @@ def cpu_baseline(soa, cam, W, H, k, seconds, four_d=False):
         el = time.perf_counter() - t0
         if el >= seconds or frames >= 50:
             break
+    # one frame on one thread beside it (single-thread and all-core runs)
+    t1 = time.perf_counter()
+    if four_d:
+        _oracle.render(_oracle.temporal(soa, frame_time(0)), cam, W, H, k, threads=1)
+    else:
+        _oracle.render(soa, cam, W, H, k, threads=1)
+    el1 = time.perf_counter() - t1
     return {"value": frames / el, "unit": "frames/sec", "cores": threads, "kind": "port",
             "sample": f"{frames} full frame(s) of the same workload by the C oracle (oracle/gsr_oracle.c, "
-                      f"OpenMP {threads} threads), {el:.1f} s"}
+                      f"OpenMP {threads} threads), {el:.1f} s",
+            "single_thread": {"value": 1.0 / el1, "unit": "frames/sec", "cores": 1,
+                              "sample": f"1 full frame, {el1:.1f} s"},
+            "host": host_cpu()}
+
+
+def host_cpu() -> dict:
+    """CPU model string and logical CPU count of the host the baseline ran on."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"model": model, "logical_cpus": os.cpu_count()}
 
 
 def frame_time(i: int) -> float:

@@ -2316,77 +2316,83 @@ __global__ __launch_bounds__(64 * WPG) void k_blend_w(const uint32_t* __restrict
                                                        int W, int H, int cover_w, int cover_h,
                                                        float* __restrict__ out,
                                                        unsigned long long* __restrict__ counters,
-                                                       const uint32_t* __restrict__ perm, int bands) {
+                                                       const uint32_t* __restrict__ perm, int bands, int seq) {
     // WPG waves per workgroup, one 8x8 block each (WPG = 2: the two blocks of a tile
     // half; the waves never synchronise, only their dispatch is shared)
     __shared__ float4 sP[WPG][32 * 20 / 4];
     const int ntiles = tiles_x * tiles_y;
     const int wv = (int)(threadIdx.x >> 6);
-    int tile, sub;
-    if (perm && bands > 1) {
-        // bands of `bands` tiles, heaviest first (k_tile_order over bands): XCD
-        // x = b & 7 takes band ranks x, x+8, ..., a band's blocks consecutive in its stream
-        const int bb = 4 * bands / WPG;                 // units per band
-        const int b = (int)blockIdx.x, k = b >> 3;
-        const int r = (k / bb) * 8 + (b & 7);
-        const int nbnd = (ntiles + bands - 1) / bands;
-        if (r >= nbnd) return;
-        const int L = (int)perm[r] * 4 * bands + (k % bb) * WPG + wv;
-        if (L >= 4 * ntiles) return;
-        tile = L >> 2;
-        sub = L & 3;
-    } else if (bands > 1) {
-        // each XCD (x = b & 7) takes `bands` spatial bands spread over the image:
-        // band j of B consecutive units goes to XCD j % 8 (balances the XCDs' work
-        // while keeping neighbouring blocks on one L2); padding workgroups exit
-        const int nu = 4 * ntiles / WPG;
-        const int B = (nu + 8 * bands - 1) / (8 * bands);
-        const int b = (int)blockIdx.x, k = b >> 3;
-        const int U = ((k / B) * 8 + (b & 7)) * B + k % B;
-        if (U >= nu) return;
-        const int L = U * WPG + wv;
-        tile = L >> 2;
-        sub = L & 3;
-    } else if (perm) {
-        // longest tiles first (k_tile_order): XCD x = b & 7 takes tile ranks x, x+8, ...,
-        // each tile's four blocks consecutive in its stream (they share one L2)
-        const int b = (int)blockIdx.x, k = b >> 3;
-        const int r = (k >> 2) * 8 + (b & 7);
-        if (r >= ntiles) return;
-        tile = (int)perm[r];
-        sub = k & 3;
-    } else {
-        const int b = xcd_remap(blockIdx.x, ntiles * 4);
-        tile = b >> 2;
-        sub = b & 3;
-    }
-    const int tx = tile % tiles_x, ty = tile / tiles_x;
-    const int lane = (int)(threadIdx.x & 63u);
-    const int sid = (int)blockIdx.x * WPG + wv;     // stamp slot
-    uint64_t t_start = 0, place = 0;
-    if (STAMPS && lane == 0) {
-        // placement: XCC (3 bits) above HW_ID's SE / SH / CU / SIMD / wave slot (low 16 bits)
-        uint32_t hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        place = ((uint64_t)(xcc & 7u) << 16) | (hw & 0xffffu);
-        t_start = __builtin_amdgcn_s_memrealtime();
-        counters[2 * sid] = t_start;
-    }
-    const uint2 rr = ranges[tile];
-    BlendDiag dg;
-    blend_block<DIAG>(idx, rec, rr.y ? ~rr.x : 0u, rr.y, tx * GSR_TILE_PX + (sub & 1) * 8,
-                      ty * GSR_TILE_PX + (sub >> 1) * 8, lane, W, H, cover_w, cover_h, out,
-                      reinterpret_cast<float*>(sP[wv]), dg);
-    // second word: duration (100 MHz ticks, 40 bits) | placement << 40
-    if (STAMPS && lane == 0) counters[2 * sid + 1] = ((__builtin_amdgcn_s_memrealtime() - t_start) & ((1ull << 40) - 1)) | (place << 40);
-    if (DIAG && lane == 0) {
-        if (sub == 0 && dg.loaded) atomicAdd(counters, (unsigned long long)dg.loaded);
-        atomicAdd(counters + 1, (unsigned long long)dg.iter);
-        atomicAdd(counters + 2, (unsigned long long)dg.active);
-        atomicAdd(counters + 3, (unsigned long long)dg.taken);
-        atomicAdd(counters + 4, (unsigned long long)dg.slow);
-        atomicAdd(counters + 6, (unsigned long long)(dg.iter * 64));
+    // seq > 1: the workgroup blends `seq` units of its XCD's stream one after the
+    // other (virtual workgroups vb = ((g / 8) * seq + j) * 8 + g % 8 keep g's XCD)
+    for (int j = 0; j < seq; j++) {
+        const int vb = (((int)blockIdx.x >> 3) * seq + j) * 8 + ((int)blockIdx.x & 7);
+        int tile, sub;
+        if (perm && bands > 1) {
+            // bands of `bands` tiles, heaviest first (k_tile_order over bands): XCD
+            // x = b & 7 takes band ranks x, x+8, ..., a band's blocks consecutive in its stream
+            const int bb = 4 * bands / WPG;                 // units per band
+            const int b = vb, k = b >> 3;
+            const int r = (k / bb) * 8 + (b & 7);
+            const int nbnd = (ntiles + bands - 1) / bands;
+            if (r >= nbnd) continue;
+            const int L = (int)perm[r] * 4 * bands + (k % bb) * WPG + wv;
+            if (L >= 4 * ntiles) continue;
+            tile = L >> 2;
+            sub = L & 3;
+        } else if (bands > 1) {
+            // each XCD (x = b & 7) takes `bands` spatial bands spread over the image:
+            // band j of B consecutive units goes to XCD j % 8 (balances the XCDs' work
+            // while keeping neighbouring blocks on one L2); padding workgroups exit
+            const int nu = 4 * ntiles / WPG;
+            const int B = (nu + 8 * bands - 1) / (8 * bands);
+            const int b = vb, k = b >> 3;
+            const int U = ((k / B) * 8 + (b & 7)) * B + k % B;
+            if (U >= nu) continue;
+            const int L = U * WPG + wv;
+            tile = L >> 2;
+            sub = L & 3;
+        } else if (perm) {
+            // longest tiles first (k_tile_order): XCD x = b & 7 takes tile ranks x, x+8, ...,
+            // each tile's four blocks consecutive in its stream (they share one L2)
+            const int b = vb, k = b >> 3;
+            const int r = (k >> 2) * 8 + (b & 7);
+            if (r >= ntiles) continue;
+            tile = (int)perm[r];
+            sub = k & 3;
+        } else {
+            if (vb >= ntiles * 4) continue;
+            const int b = xcd_remap(vb, ntiles * 4);
+            tile = b >> 2;
+            sub = b & 3;
+        }
+        const int tx = tile % tiles_x, ty = tile / tiles_x;
+        const int lane = (int)(threadIdx.x & 63u);
+        const int sid = vb * WPG + wv;     // stamp slot
+        uint64_t t_start = 0, place = 0;
+        if (STAMPS && lane == 0) {
+            // placement: XCC (3 bits) above HW_ID's SE / SH / CU / SIMD / wave slot (low 16 bits)
+            uint32_t hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            place = ((uint64_t)(xcc & 7u) << 16) | (hw & 0xffffu);
+            t_start = __builtin_amdgcn_s_memrealtime();
+            counters[2 * sid] = t_start;
+        }
+        const uint2 rr = ranges[tile];
+        BlendDiag dg;
+        blend_block<DIAG>(idx, rec, rr.y ? ~rr.x : 0u, rr.y, tx * GSR_TILE_PX + (sub & 1) * 8,
+                          ty * GSR_TILE_PX + (sub >> 1) * 8, lane, W, H, cover_w, cover_h, out,
+                          reinterpret_cast<float*>(sP[wv]), dg);
+        // second word: duration (100 MHz ticks, 40 bits) | placement << 40
+        if (STAMPS && lane == 0) counters[2 * sid + 1] = ((__builtin_amdgcn_s_memrealtime() - t_start) & ((1ull << 40) - 1)) | (place << 40);
+        if (DIAG && lane == 0) {
+            if (sub == 0 && dg.loaded) atomicAdd(counters, (unsigned long long)dg.loaded);
+            atomicAdd(counters + 1, (unsigned long long)dg.iter);
+            atomicAdd(counters + 2, (unsigned long long)dg.active);
+            atomicAdd(counters + 3, (unsigned long long)dg.taken);
+            atomicAdd(counters + 4, (unsigned long long)dg.slow);
+            atomicAdd(counters + 6, (unsigned long long)(dg.iter * 64));
+        }
     }
 }
 
@@ -2602,7 +2608,8 @@ hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* ke
 
 hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
                         float* out, unsigned long long* consumed, int variant, unsigned int* queue,
-                        int resident_groups, uint32_t* tile_perm, int band_tiles, int wpg, hipStream_t s) {
+                        int resident_groups, uint32_t* tile_perm, int band_tiles, int wpg, int seq,
+                        hipStream_t s) {
     const int nt = fr.tiles_x * fr.tiles_y;
     if (nt <= 0) return hipSuccess;
     if (variant == 0 || variant == 3) {   // one wave per 8x8 block, wpg blocks per workgroup
@@ -2633,9 +2640,13 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
             if (tile_perm) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ranges, nt, 1, tile_perm);
         }
         const uint32_t* pm = tile_perm;
+        // seq blocks per wave: grid = whole XCD rounds of ng / seq (virtual workgroups past
+        // ng exit: every mapping bounds-checks its unit)
+        const int sq = std::max(1, seq);
+        const int ngw = 8 * (((ng + 7) / 8 + sq - 1) / sq);   // >= 8: tiny frames have ng < 8
 #define GSR_BLEND_W(D, S, G)                                                                                 \
-    hipLaunchKernelGGL((k_blend_w<D, S, G>), dim3(ng), dim3(64 * G), 0, s, idx, ranges, rec, fr.tiles_x, fr.tiles_y, \
-                       fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, pm, bands)
+    hipLaunchKernelGGL((k_blend_w<D, S, G>), dim3(ngw), dim3(64 * G), 0, s, idx, ranges, rec, fr.tiles_x, fr.tiles_y, \
+                       fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, pm, bands, sq)
         if (wpg == 2) {
             if (variant == 3 && consumed) GSR_BLEND_W(false, true, 2);
             else if (consumed) GSR_BLEND_W(true, false, 2);

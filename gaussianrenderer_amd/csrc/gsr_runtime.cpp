@@ -341,6 +341,7 @@ struct gsr_context {
     int64_t cbins_cap = 0;
     bool last_binned = false;        // the last sorted frame took the binning path
     int blend_tile_order = 0;        // 1: blend the longest tiles first (k_tile_order), 0: spatial order
+    int blend_seq = 1;               // blend: 8x8 blocks each wave blends one after the other
     int blend_wpg = 1;               // blend: 8x8 blocks (waves) per workgroup, 1 | 2 (band layout only)
     int blend_band_tiles = 4;        // blend: tiles per spatial band, bands dealt round-robin to the
                                      // XCDs (0: one contiguous band per XCD)
@@ -762,7 +763,7 @@ static int blend_locked(gsr_context* c, float* d_out) {
     HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
                               c->diagnostics ? c->consumed : nullptr, c->blend_variant, c->queue,
                               c->resident_groups, c->blend_tile_order ? c->tile_perm : nullptr,
-                              c->blend_band_tiles, c->blend_wpg, c->stream));
+                              c->blend_band_tiles, c->blend_wpg, c->blend_seq, c->stream));
     mark(c, GSR_NUM_STAGES);
     if (c->timing && c->timing_now) c->ev_frames.push_back(c->cur);
     c->cur = FrameEvents{};
@@ -832,6 +833,7 @@ void copy_settings(gsr_context* d, const gsr_context* s) {
     d->blend_band_tiles = s->blend_band_tiles;
     d->completion_events = s->completion_events;
     d->depth_order = s->depth_order;
+    d->blend_seq = s->blend_seq;
 }
 
 // Lanes 1..F-1: child contexts, streams and events, created once and kept.
@@ -1218,6 +1220,10 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     case GSR_TUNE_BIN_COL_GROUPS:
         if (value < 1 || value > 65536) return set_err(GSR_E_ARG, "gsr_set_tuning: bad column-pass group count");
         c->bin_col_groups = value;
+        return GSR_OK;
+    case GSR_TUNE_BLEND_BLOCKS_PER_WAVE:
+        if (value < 1 || value > 64) return set_err(GSR_E_ARG, "gsr_set_tuning: blend blocks per wave must be 1..64");
+        c->blend_seq = value;
         return GSR_OK;
     case GSR_TUNE_DEPTH_SORT_SKIP:
         c->depth_skip = value != 0;

@@ -250,10 +250,12 @@ enum {
     GSR_TUNE_BLEND_BAND_TILES = 13,  /* blend schedule 0: tiles per spatial band, bands dealt round-robin
                                         to the 8 XCDs (default 4); 0 = one contiguous band per XCD */
     GSR_TUNE_BLEND_WAVES_PER_GROUP = 14, /* blend schedule 0 with bands: 8x8 blocks per workgroup, 1 | 2 */
-    GSR_TUNE_DEPTH_ORDER = 15        /* tile binning path: 0 (default) = global depth sort before binning;
+    GSR_TUNE_DEPTH_ORDER = 15,       /* tile binning path: 0 (default) = global depth sort before binning;
                                         1 = bin in index order, then sort every tile's list by depth (one
                                         wave per list <= 1024, a workgroup per longer list, lists over 4096
                                         chunked through global scratch); same pairs, same image */
+    GSR_TUNE_BLEND_BLOCKS_PER_WAVE = 16 /* blend schedule 0: 8x8 blocks each wave blends one after the other
+                                        (default 1); same blocks, same image */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Depth-sort digit passes the last sorted frame ran (1..4; trailing identity
