@@ -2025,6 +2025,21 @@ __device__ __forceinline__ bool block_may_reach(float a, float b, float c, float
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
+// Packed products with the HIGH half of one operand broadcast to both lanes, in
+// one v_pk_mul_f32 through op_sel (the compiler otherwise copies that half into
+// a fresh register pair first: one v_mov per use in the compositing loop).
+// Same IEEE products as the plain expressions (multiplication commutes exactly).
+__device__ __forceinline__ f2 pk_mul_a_hi(f2 a, f2 b) {   // (a.y * b.x, a.y * b.y)
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f2 pk_mul_b_hi(f2 a, f2 b) {   // (a.x * b.y, a.y * b.y)
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // gsr_expf on two lanes at once (v_pk_* for every float op that has a packed
 // form), for inputs the caller has PROVEN finite and in [-2e7, 88.75]: there the
 // clamps and the NaN select of gsr_expf do not change the result, and every
@@ -2216,7 +2231,7 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 const bool take1 = in1 & !(TT.y < 1e-3f) & !(al1 < 1e-3f);
                 AA.y = take1 ? al1 : 0.0f;
                 crg = crg + ((f2){q3.z, q3.w} * AA.x) * TT.x;
-                crg = crg + ((f2){q4.x, q4.y} * AA.y) * TT.y;
+                crg = crg + pk_mul_a_hi(TT, pk_mul_b_hi((f2){q4.x, q4.y}, AA));   // (col1 * AA.y) * TT.y
                 const f2 wb = ((f2){q4.z, q4.w} * AA) * TT;
                 cb = (cb + wb.x) + wb.y;
                 if (DIAG) {
