@@ -2088,6 +2088,15 @@ struct BlendDiag {
     uint64_t loaded = 0, iter = 0, active = 0, taken = 0, slow = 0;
 };
 
+// 64-bit pixel mask (bit row * 8 + col) of a box descriptor built in the cull:
+// bits 0-7 the column byte, 8-15 = 56 - 8 (y1 - y0), 16-23 = 8 y0.  Uniform input,
+// so it compiles to scalar instructions.
+__device__ __forceinline__ uint64_t box_mask(uint32_t d) {
+    const uint32_t rep = (d & 0xffu) * 0x01010101u;
+    const uint64_t rows = (~0ull >> ((d >> 8) & 0xffu)) << ((d >> 16) & 0xffu);
+    return rows & (((uint64_t)rep << 32) | rep);
+}
+
 // One 8x8 pixel block (bx, by) blended by one wave over the tile list
 // idx[beg, end), using the wave's private LDS slice wP (32 pair slots).
 template <bool DIAG>
@@ -2124,7 +2133,7 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
         // whose in-box pixels are all saturated here can never be taken in this batch
         const uint64_t live_b = __ballot(!(T < 1e-3f));
         bool hit = false, fast = true;
-        uint32_t mlo = 0, mhi = 0;
+        uint32_t mlo = 0, mhi = 0, dsc = 0;
         if ((uint32_t)lane < cnt) {
             const int xmin = (int)(rc.z & 0xffffu), xmax = (int)(rc.z >> 16);
             const int ymin = (int)(rc.w & 0xffffu), ymax = (int)(rc.w >> 16);
@@ -2142,6 +2151,9 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 const uint64_t rows = (y1 == 7 ? ~0ull : ((1ull << (8 * (y1 + 1))) - 1ull)) & (~0ull << (8 * y0));
                 mlo = rep & (uint32_t)rows;
                 mhi = rep & (uint32_t)(rows >> 32);
+                // the same box as a descriptor the compositing loop expands on the
+                // scalar unit (box_mask): column byte | (56 - 8 (y1 - y0)) << 8 | 8 y0 << 16
+                dsc = (rep & 0xffu) | ((uint32_t)(56 - 8 * (y1 - y0)) << 8) | ((uint32_t)(8 * y0) << 16);
                 // cull word (cull_word): per-record parts of the block test and the proof
                 const float S = __uint_as_float(rd.w);
                 const float M = fmaxf(fmaxf(fabsf(dx0), fabsf(dx1)), fmaxf(fabsf(dy0), fabsf(dy1)));
@@ -2203,11 +2215,11 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 const bool has1 = mm != 0ull;
                 const int s1 = has1 ? __builtin_ctzll(mm) : s0;
                 if (has1) mm &= mm - 1;
-                const uint64_t box0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mhi, s0) << 32) |
-                                      (uint32_t)__builtin_amdgcn_readlane((int)mlo, s0);
-                uint64_t box1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mhi, s1) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)mlo, s1);
-                box1 = has1 ? box1 : 0ull;
+                // one v_readlane per splat; the 64-bit lane masks are rebuilt from the
+                // descriptors by scalar instructions (the VALU is the kernel's bound)
+                const uint64_t box0 = box_mask((uint32_t)__builtin_amdgcn_readlane((int)dsc, s0));
+                const uint64_t box1 = box_mask((uint32_t)__builtin_amdgcn_readlane((int)dsc, s1)) &
+                                      (has1 ? ~0ull : 0ull);
                 const float4 q0 = wP4[j * 5 + 0], q1 = wP4[j * 5 + 1], q2 = wP4[j * 5 + 2];
                 const float4 q3 = wP4[j * 5 + 3], q4 = wP4[j * 5 + 4];
                 // render.cu:329-332, same operation order, both splats at once; the
@@ -2230,9 +2242,17 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 TT.y = TT.x * (1.0f - AA.x);
                 const bool take1 = in1 & !(TT.y < 1e-3f) & !(al1 < 1e-3f);
                 AA.y = take1 ? al1 : 0.0f;
-                crg = crg + ((f2){q3.z, q3.w} * AA.x) * TT.x;
-                crg = crg + pk_mul_a_hi(TT, pk_mul_b_hi((f2){q4.x, q4.y}, AA));   // (col1 * AA.y) * TT.y
-                const f2 wb = ((f2){q4.z, q4.w} * AA) * TT;
+                // the three colour products first, then the three transmittance
+                // products, then the sums in list order (independent packed ops
+                // adjacent: no wait states between dependent v_pk_* instructions)
+                const f2 p0 = (f2){q3.z, q3.w} * AA.x;
+                const f2 p1 = pk_mul_b_hi((f2){q4.x, q4.y}, AA);     // col1 * AA.y
+                const f2 pb = (f2){q4.z, q4.w} * AA;
+                const f2 w0 = p0 * TT.x;
+                const f2 w1 = pk_mul_a_hi(TT, p1);                   // (col1 * AA.y) * TT.y
+                const f2 wb = pb * TT;
+                crg = crg + w0;
+                crg = crg + w1;
                 cb = (cb + wb.x) + wb.y;
                 if (DIAG) {
                     dg.iter += has1 ? 2 : 1;
