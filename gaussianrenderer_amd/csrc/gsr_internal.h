@@ -88,7 +88,8 @@ hipError_t launch_tile_depth_sort(const uint2* ranges, int ntiles, const uint64_
 // per-wave block queue (queue: 8 device uints; resident_groups: grid size).
 hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
                         float* out, unsigned long long* consumed, int variant, unsigned int* queue,
-                        int resident_groups, uint32_t* tile_perm, int band_tiles, int wpg, int seq, hipStream_t s);
+                        int resident_groups, uint32_t* tile_perm, int band_tiles, int wpg, int seq, int lds_pad,
+                        hipStream_t s);
 // Tile binning (row pass + column pass, tile grids <= 256 x 256): replaces
 // launch_emit + the key-value tile sort.  hist: 512 x groups; row_items /
 // row_pairs: 256 each; cbins: 256 x bin_col_chunks_max(); rows_buf: pair

@@ -2644,7 +2644,7 @@ hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* ke
 hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
                         float* out, unsigned long long* consumed, int variant, unsigned int* queue,
                         int resident_groups, uint32_t* tile_perm, int band_tiles, int wpg, int seq,
-                        hipStream_t s) {
+                        int lds_pad, hipStream_t s) {
     const int nt = fr.tiles_x * fr.tiles_y;
     if (nt <= 0) return hipSuccess;
     if (variant == 0 || variant == 3) {   // one wave per 8x8 block, wpg blocks per workgroup
@@ -2680,7 +2680,8 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
         const int sq = std::max(1, seq);
         const int ngw = 8 * (((ng + 7) / 8 + sq - 1) / sq);   // >= 8: tiny frames have ng < 8
 #define GSR_BLEND_W(D, S, G)                                                                                 \
-    hipLaunchKernelGGL((k_blend_w<D, S, G>), dim3(ngw), dim3(64 * G), 0, s, idx, ranges, rec, fr.tiles_x, fr.tiles_y, \
+    hipLaunchKernelGGL((k_blend_w<D, S, G>), dim3(ngw), dim3(64 * G), (size_t)lds_pad, s, idx, ranges, rec, fr.tiles_x, \
+                       fr.tiles_y, \
                        fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, pm, bands, sq)
         if (wpg == 2) {
             if (variant == 3 && consumed) GSR_BLEND_W(false, true, 2);

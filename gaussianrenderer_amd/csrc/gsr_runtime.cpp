@@ -342,6 +342,7 @@ struct gsr_context {
     bool last_binned = false;        // the last sorted frame took the binning path
     int blend_tile_order = 0;        // 1: blend the longest tiles first (k_tile_order), 0: spatial order
     int blend_seq = 1;               // blend: 8x8 blocks each wave blends one after the other
+    int blend_lds_pad = 0;           // blend: extra LDS bytes per workgroup (caps waves per CU)
     int blend_wpg = 1;               // blend: 8x8 blocks (waves) per workgroup, 1 | 2 (band layout only)
     int blend_band_tiles = 4;        // blend: tiles per spatial band, bands dealt round-robin to the
                                      // XCDs (0: one contiguous band per XCD)
@@ -763,7 +764,7 @@ static int blend_locked(gsr_context* c, float* d_out) {
     HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
                               c->diagnostics ? c->consumed : nullptr, c->blend_variant, c->queue,
                               c->resident_groups, c->blend_tile_order ? c->tile_perm : nullptr,
-                              c->blend_band_tiles, c->blend_wpg, c->blend_seq, c->stream));
+                              c->blend_band_tiles, c->blend_wpg, c->blend_seq, c->blend_lds_pad, c->stream));
     mark(c, GSR_NUM_STAGES);
     if (c->timing && c->timing_now) c->ev_frames.push_back(c->cur);
     c->cur = FrameEvents{};
@@ -834,6 +835,7 @@ void copy_settings(gsr_context* d, const gsr_context* s) {
     d->completion_events = s->completion_events;
     d->depth_order = s->depth_order;
     d->blend_seq = s->blend_seq;
+    d->blend_lds_pad = s->blend_lds_pad;
 }
 
 // Lanes 1..F-1: child contexts, streams and events, created once and kept.
@@ -1220,6 +1222,10 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     case GSR_TUNE_BIN_COL_GROUPS:
         if (value < 1 || value > 65536) return set_err(GSR_E_ARG, "gsr_set_tuning: bad column-pass group count");
         c->bin_col_groups = value;
+        return GSR_OK;
+    case GSR_TUNE_BLEND_LDS_PAD:
+        if (value < 0 || value > 65536) return set_err(GSR_E_ARG, "gsr_set_tuning: blend LDS pad must be 0..65536 bytes");
+        c->blend_lds_pad = value;
         return GSR_OK;
     case GSR_TUNE_BLEND_BLOCKS_PER_WAVE:
         if (value < 1 || value > 64) return set_err(GSR_E_ARG, "gsr_set_tuning: blend blocks per wave must be 1..64");

@@ -254,8 +254,11 @@ enum {
                                         1 = bin in index order, then sort every tile's list by depth (one
                                         wave per list <= 1024, a workgroup per longer list, lists over 4096
                                         chunked through global scratch); same pairs, same image */
-    GSR_TUNE_BLEND_BLOCKS_PER_WAVE = 16 /* blend schedule 0: 8x8 blocks each wave blends one after the other
+    GSR_TUNE_BLEND_BLOCKS_PER_WAVE = 16, /* blend schedule 0: 8x8 blocks each wave blends one after the other
                                         (default 1); same blocks, same image */
+    GSR_TUNE_BLEND_LDS_PAD = 17      /* blend schedule 0: extra LDS bytes reserved per blend workgroup
+                                        (0..65536, default 0): caps the blend's waves per CU, leaving
+                                        slots to other frames' kernels in flight; same image */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Depth-sort digit passes the last sorted frame ran (1..4; trailing identity
