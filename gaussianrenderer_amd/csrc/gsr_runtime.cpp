@@ -1224,7 +1224,7 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         c->bin_col_groups = value;
         return GSR_OK;
     case GSR_TUNE_BLEND_LDS_PAD:
-        if (value < 0 || value > 65536) return set_err(GSR_E_ARG, "gsr_set_tuning: blend LDS pad must be 0..65536 bytes");
+        if (value < 0 || value > 32768) return set_err(GSR_E_ARG, "gsr_set_tuning: blend LDS pad must be 0..32768 bytes");
         c->blend_lds_pad = value;
         return GSR_OK;
     case GSR_TUNE_BLEND_BLOCKS_PER_WAVE:

@@ -257,7 +257,7 @@ enum {
     GSR_TUNE_BLEND_BLOCKS_PER_WAVE = 16, /* blend schedule 0: 8x8 blocks each wave blends one after the other
                                         (default 1); same blocks, same image */
     GSR_TUNE_BLEND_LDS_PAD = 17      /* blend schedule 0: extra LDS bytes reserved per blend workgroup
-                                        (0..65536, default 0): caps the blend's waves per CU, leaving
+                                        (0..32768, default 0): caps the blend's waves per CU, leaving
                                         slots to other frames' kernels in flight; same image */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);

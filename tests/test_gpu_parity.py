@@ -174,7 +174,7 @@ def test_blend_tile_schedule_parity(gpu, orc, torch, c1, ci):
 @pytest.mark.parametrize("knobs", [{13: 0}, {13: 0, 12: 1}, {13: 1}, {13: 4, 14: 2}, {13: 4, 12: 1},
                                    {13: 5, 12: 1, 14: 2}, {13: 64}, {16: 2}, {13: 0, 16: 3},
                                    {13: 4, 12: 1, 16: 4}, {13: 5, 14: 2, 16: 3}, {17: 4096},
-                                   {13: 0, 17: 65536}])
+                                   {13: 0, 17: 32768}])
 def test_blend_block_mappings_parity(gpu, orc, torch, c1, knobs):
     """Every block-to-workgroup mapping of the default blend schedule is bit-exact vs
     the oracle: 13 = tiles per band (0: one contiguous band per XCD), 12 = heaviest
