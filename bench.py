@@ -65,6 +65,8 @@ def parse():
                     help="frames in flight per GPU (gsr_render_path lanes); 1 = one frame at a time")
     ap.add_argument("--chunk", type=int, default=8,
                     help="N>1 with --gather step: frames per render_path call (one RCCL gather per frame)")
+    ap.add_argument("--tune", default="",
+                    help="gsr_set_tuning knob=value pairs, comma-separated (include/gsr.h GSR_TUNE_*; A/B runs)")
     return ap.parse_args()
 
 
@@ -239,6 +241,9 @@ def main():
     cam = multi.orbit_camera(rank, W, H)      # rank 0: camera (0,0,4); config 4: orbit 45 deg * rank
 
     r = gsr.Renderer()
+    for kv in filter(None, args.tune.split(",")):
+        knob, val = kv.split("=")
+        r.set_tuning(int(knob), int(val))
     F = max(1, min(8, args.inflight))
     r.set_frames_in_flight(F)
     gloo = dist is not None and args.dist_backend == "gloo"

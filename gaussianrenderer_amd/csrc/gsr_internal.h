@@ -90,6 +90,11 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
                         float* out, unsigned long long* consumed, int variant, unsigned int* queue,
                         int resident_groups, uint32_t* tile_perm, int band_tiles, int wpg, int seq, int lds_pad,
                         hipStream_t s);
+// Stable partition of the preprocess items: visible first, culled last (both in
+// index order), visible count into *n_live; culled tail to out only, with dead
+// rects in srect (gsr_kernels.hip "live partition").  counts: groups words.
+hipError_t launch_partition(const uint64_t* in, uint32_t n, int groups, uint32_t* counts, uint32_t* n_live,
+                            uint64_t* out, uint64_t* srect, hipStream_t s);
 // Tile binning (row pass + column pass, tile grids <= 256 x 256): replaces
 // launch_emit + the key-value tile sort.  hist: 512 x groups; row_items /
 // row_pairs: 256 each; cbins: 256 x bin_col_chunks_max(); rows_buf: pair

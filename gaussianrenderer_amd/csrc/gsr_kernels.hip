@@ -1574,6 +1574,92 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
     }
 }
 
+// ------------------------------------------------------------------ live partition
+//
+// Stable partition of the preprocess items ahead of the global depth sort
+// (GSR_TUNE_DEPTH_COMPACT): visible items (key != 0xFFFFFFFF) first, in index
+// order, then the culled ones, in index order.  The full sort puts the culled
+// items last in index order anyway (their key is the maximum, ties by index), so
+// sorting only the visible prefix (n_dev = the visible count) gives the same
+// order.  The culled tail is written to `out` only, with kDeadRect in srect at
+// the same positions; the binning never reads items whose rect is dead, and
+// gsr_read_depth_order takes the tail from `out`.  Three launches: per-chunk
+// visible counts, their exclusive scan (+ total), the scatter.
+__global__ __launch_bounds__(256) void k_part_count(const uint64_t* __restrict__ in, uint32_t n, int groups,
+                                                     uint32_t* __restrict__ counts) {
+    __shared__ uint32_t s_scr[4];
+    uint64_t b, e;
+    chunk_range(n, groups, blockIdx.x, 256, b, e);
+    uint32_t c = 0;
+    for (uint64_t i = b + threadIdx.x; i < e; i += 256) c += (uint32_t)(in[i] >> 32) != 0xffffffffu ? 1u : 0u;
+    uint32_t tot;
+    (void)block_exclusive_scan<uint32_t>(c, s_scr, tot);
+    if (threadIdx.x == 0) counts[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_part_scan(uint32_t* __restrict__ counts, int groups,
+                                                    uint32_t* __restrict__ n_live) {
+    __shared__ uint32_t s_scr[4];
+    const int per = (groups + 255) / 256;
+    const int b = (int)threadIdx.x * per;
+    uint32_t local = 0;
+    for (int k = 0; k < per; k++)
+        if (b + k < groups) local += counts[b + k];
+    uint32_t total;
+    uint32_t run = block_exclusive_scan<uint32_t>(local, s_scr, total);
+    for (int k = 0; k < per; k++)
+        if (b + k < groups) {
+            const uint32_t v = counts[b + k];
+            counts[b + k] = run;
+            run += v;
+        }
+    if (threadIdx.x == 0) *n_live = total;
+}
+
+__global__ __launch_bounds__(256) void k_part_scatter(const uint64_t* __restrict__ in, uint32_t n, int groups,
+                                                       const uint32_t* __restrict__ offs,
+                                                       const uint32_t* __restrict__ n_live,
+                                                       uint64_t* __restrict__ out, uint64_t* __restrict__ srect) {
+    __shared__ uint32_t s_w[4];
+    uint64_t b, e;
+    chunk_range(n, groups, blockIdx.x, 256, b, e);
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint32_t live_base = offs[blockIdx.x];
+    // culled items before this chunk = b - visible items before it
+    uint32_t dead_base = *n_live + (uint32_t)(b - live_base);
+    for (uint64_t c0 = b; c0 < e; c0 += 256) {
+        const uint64_t i = c0 + t;
+        const bool valid = i < e;
+        const uint64_t v = valid ? in[i] : 0ull;
+        const bool live = valid && (uint32_t)(v >> 32) != 0xffffffffu;
+        const bool dead = valid && !live;
+        const uint64_t bl = __ballot(live), bd = __ballot(dead);
+        if (lane == 0) s_w[w] = (uint32_t)__popcll(bl) | ((uint32_t)__popcll(bd) << 16);
+        __syncthreads();
+        uint32_t lb = 0, db = 0, ltot = 0, dtot = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t x = s_w[k];
+            if (k < w) {
+                lb += x & 0xffffu;
+                db += x >> 16;
+            }
+            ltot += x & 0xffffu;
+            dtot += x >> 16;
+        }
+        if (live) out[live_base + lb + (uint32_t)__popcll(bl & lt)] = v;
+        if (dead) {
+            const uint32_t q = dead_base + db + (uint32_t)__popcll(bd & lt);
+            out[q] = v;
+            srect[q] = kDeadRect;
+        }
+        live_base += ltot;
+        dead_base += dtot;
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------------------ per-tile depth order
 //
 // The other way to reach the same tile lists: bin the Gaussians in INDEX order
@@ -2551,6 +2637,15 @@ hipError_t launch_emit(const uint64_t* items0, const uint64_t* items1, const uin
     else
         hipLaunchKernelGGL(k_emit_pairs<uint32_t>, dim3(groups), dim3(256), 0, s, items0, items1, dstats, n, groups,
                            wg_scratch, pair_capacity, tiles_x, static_cast<uint32_t*>(keys), vals);
+    return hipGetLastError();
+}
+
+hipError_t launch_partition(const uint64_t* in, uint32_t n, int groups, uint32_t* counts, uint32_t* n_live,
+                            uint64_t* out, uint64_t* srect, hipStream_t s) {
+    if (groups < 1 || groups > kMaxSortGroups) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_part_count, dim3(groups), dim3(256), 0, s, in, n, groups, counts);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(256), 0, s, counts, groups, n_live);
+    hipLaunchKernelGGL(k_part_scatter, dim3(groups), dim3(256), 0, s, in, n, groups, counts, n_live, out, srect);
     return hipGetLastError();
 }
 

@@ -331,6 +331,10 @@ struct gsr_context {
     int tile_split_even = 1;         // tile sort: digits split evenly over the passes
     int depth_skip = 1;              // depth sort: skip trailing identity passes (device-side plan)
     uint32_t* dstats = nullptr;      // depth-sort pass plan: 4 final words + 4 per upsweep workgroup
+    uint32_t* nlive = nullptr;       // visible count of the live partition (device word)
+    int depth_compact = 2;           // live partition before the depth sort: 0 off, 1 on, 2 4D scenes only
+    bool compact_frame = false;      // this frame's preprocess items went to items[1] for the partition
+    bool last_compact = false;       // the last sorted frame sorted only its visible prefix
     int depth_groups = 0;            // depth sort: workgroup cap (0 = default)
     int tile_binning = 1;            // row + column binning instead of emit + tile sort (grids <= 256 x 256)
     int bin_row_items = 4;           // binning: items per thread of a row-pass tile (4 | 8 | 16)
@@ -410,6 +414,7 @@ int ensure_static(gsr_context* c) {
     if (int rc = realloc_dev(&c->stats, 2)) return rc;
     if (int rc = realloc_dev(&c->queue, 8)) return rc;
     if (int rc = realloc_dev(&c->dstats, 4 + 4 * (size_t)gsr::kMaxSortGroups)) return rc;
+    if (int rc = realloc_dev(&c->nlive, 1)) return rc;
     if (int rc = realloc_dev(&c->binmeta, 256 + 128)) return rc;
     if (int rc = realloc_dev(&c->big_counts, 2)) return rc;
     HIP_TRY(hipMemset(c->big_counts, 0, 2 * sizeof(uint32_t)));
@@ -569,7 +574,7 @@ extern "C" void gsr_destroy(gsr_context* c) {
     for (auto* p : {(void*)c->rec, (void*)c->items[0], (void*)c->items[1], (void*)c->rect, (void*)c->pairs[0],
                     (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->queue, (void*)c->dstats,
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
-                    (void*)c->cbins, (void*)c->srect, (void*)c->tile_perm, (void*)c->big_list, (void*)c->big_counts})
+                    (void*)c->cbins, (void*)c->srect, (void*)c->tile_perm, (void*)c->big_list, (void*)c->big_counts, (void*)c->nlive})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -619,7 +624,11 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     } else {
         arrays = reinterpret_cast<const float*>(static_cast<const char*>(scene) + GSR_SCENE_HEADER_BYTES);
     }
-    HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[0], c->rect,
+    // live partition (global depth sort on the binning path): the items go to
+    // items[1] and the partition writes the visible-first order into items[0]
+    c->compact_frame = n > 0 && (c->depth_compact == 1 || (c->depth_compact == 2 && layout == GSR_LAYOUT_SCENE_BLOCK_4D)) &&
+                       c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256 && c->depth_order == 0;
+    HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[c->compact_frame ? 1 : 0], c->rect,
                                    layout == GSR_LAYOUT_SCENE_BLOCK_4D, layout == GSR_LAYOUT_SCENE_BLOCK_SH3, c->time,
                                    c->stream));
     c->have_pre = true;
@@ -652,8 +661,16 @@ static int depth_sort_locked(gsr_context* c, bool with_rects) {
     const int di = c->depth_items ? c->depth_items : (c->n < (int64_t(4) << 20) ? 8 : 16);
     int gd = groups_for(c->n, 256 * di);
     if (c->depth_groups) gd = std::min(gd, c->depth_groups);
+    const bool part = with_rects && c->compact_frame;
+    if (part)   // visible items first (index order) into items[0]; the passes sort only those
+        HIP_TRY(gsr::launch_partition(c->items[1], n, std::min(groups_for(c->n, 4096), gsr::kMaxSortGroups), c->hist,
+                                      c->nlive, c->items[0], c->srect, c->stream));
+    c->last_compact = part;
+    // items[1] is the sort's scratch from here on; a repeated sort of this frame sorts
+    // the whole partitioned items[0] (same order: visible and culled keys never tie)
+    if (part) c->compact_frame = false;
     for (int p = 0; p < 4; p++)
-        HIP_TRY(gsr::launch_radix_pass(c->items[p & 1], c->items[(p + 1) & 1], nullptr, n, 32 + 8 * p, 8, gd, di,
+        HIP_TRY(gsr::launch_radix_pass(c->items[p & 1], c->items[(p + 1) & 1], part ? c->nlive : nullptr, n, 32 + 8 * p, 8, gd, di,
                                        c->hist, c->totals, nullptr, c->stream, c->depth_skip ? c->dstats : nullptr,
                                        p, with_rects ? c->rect : nullptr, with_rects ? c->srect : nullptr));
     return GSR_OK;
@@ -667,6 +684,10 @@ static int sort_locked(gsr_context* c) {
     // per-tile depth order (knob): bin in index order, then sort each tile's list by depth
     const bool per_tile = bin && c->depth_order == 1;
     c->last_tile_order = per_tile;
+    if (c->compact_frame && (!bin || per_tile)) {   // knobs changed since gsr_preprocess
+        HIP_TRY(hipMemcpyAsync(c->items[0], c->items[1], (size_t)n * 8, hipMemcpyDeviceToDevice, c->stream));
+        c->compact_frame = false;
+    }
     if (per_tile) {
         if (int rc = ensure_cbins(c)) return rc;
         auto* row_pairs = reinterpret_cast<unsigned long long*>(c->binmeta);
@@ -836,6 +857,7 @@ void copy_settings(gsr_context* d, const gsr_context* s) {
     d->depth_order = s->depth_order;
     d->blend_seq = s->blend_seq;
     d->blend_lds_pad = s->blend_lds_pad;
+    d->depth_compact = s->depth_compact;
 }
 
 // Lanes 1..F-1: child contexts, streams and events, created once and kept.
@@ -985,6 +1007,7 @@ extern "C" int64_t gsr_row_item_count(gsr_context* c) {
 }
 
 static int depth_passes_locked(gsr_context* c, int* passes);
+static int sorted_items_locked(gsr_context* c, uint64_t* host, int64_t n);
 
 // The device record's fourth word is the blend's cull word (gsr_kernels.hip
 // cull_word); the readback layout's fourth word {tile x range, tile y range,
@@ -1000,10 +1023,12 @@ extern "C" int gsr_read_splats(gsr_context* c, void* host, int64_t n) {
     HIP_TRY(hipMemcpy(host, c->rec, (size_t)n * GSR_SPLAT_RECORD_BYTES, hipMemcpyDeviceToHost));
     std::vector<uint64_t> rect((size_t)n), items((size_t)c->n);
     HIP_TRY(hipMemcpy(rect.data(), c->rect, (size_t)n * 8, hipMemcpyDeviceToHost));
-    int p = 0;
-    if (c->have_sort && !c->last_tile_order)
-        if (int rc = depth_passes_locked(c, &p)) return rc;
-    HIP_TRY(hipMemcpy(items.data(), c->items[p & 1], (size_t)c->n * 8, hipMemcpyDeviceToHost));
+    if (c->have_sort && !c->last_tile_order) {
+        if (int rc = sorted_items_locked(c, items.data(), c->n)) return rc;
+    } else {   // preprocess order (items[1] when the frame is set up for the live partition)
+        HIP_TRY(hipMemcpy(items.data(), c->items[c->compact_frame && !c->have_sort ? 1 : 0], (size_t)c->n * 8,
+                          hipMemcpyDeviceToHost));
+    }
     auto* w = static_cast<uint32_t*>(host);
     for (uint64_t it : items) {
         const uint32_t i = (uint32_t)it;
@@ -1043,6 +1068,22 @@ static int depth_passes_locked(gsr_context* c, int* passes) {
     return GSR_OK;
 }
 
+// First n items of the last globally sorted frame's depth order (stream drained).
+static int sorted_items_locked(gsr_context* c, uint64_t* host, int64_t n) {
+    int p = 4;
+    if (int rc = depth_passes_locked(c, &p)) return rc;
+    int64_t head = n;
+    if (c->last_compact) {   // sorted visible prefix in items[p & 1], culled tail (index order) in items[0]
+        uint32_t live = 0;
+        HIP_TRY(hipMemcpy(&live, c->nlive, sizeof live, hipMemcpyDeviceToHost));
+        head = std::min<int64_t>(n, live);
+        if (n > head)
+            HIP_TRY(hipMemcpy(host + head, c->items[0] + head, (size_t)(n - head) * 8, hipMemcpyDeviceToHost));
+    }
+    if (head) HIP_TRY(hipMemcpy(host, c->items[p & 1], (size_t)head * 8, hipMemcpyDeviceToHost));
+    return GSR_OK;
+}
+
 extern "C" int gsr_depth_passes(gsr_context* c) {
     if (!c || !c->have_sort) return set_err(GSR_E_ARG, "gsr_depth_passes: no sorted frame");
     std::lock_guard<std::mutex> lk(c->mu);
@@ -1065,10 +1106,7 @@ extern "C" int gsr_read_depth_order(gsr_context* c, uint64_t* host, int64_t n) {
         c->last_tile_order = false;
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
-    int p = 4;
-    if (int rc = depth_passes_locked(c, &p)) return rc;
-    if (n) HIP_TRY(hipMemcpy(host, c->items[p & 1], (size_t)n * 8, hipMemcpyDeviceToHost));
-    return GSR_OK;
+    return sorted_items_locked(c, host, n);
 }
 
 extern "C" int64_t gsr_read_pairs(gsr_context* c, uint64_t* host, int64_t cap) {
@@ -1222,6 +1260,10 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     case GSR_TUNE_BIN_COL_GROUPS:
         if (value < 1 || value > 65536) return set_err(GSR_E_ARG, "gsr_set_tuning: bad column-pass group count");
         c->bin_col_groups = value;
+        return GSR_OK;
+    case GSR_TUNE_DEPTH_COMPACT:
+        if (value < 0 || value > 2) return set_err(GSR_E_ARG, "gsr_set_tuning: depth compaction must be 0, 1 or 2");
+        c->depth_compact = value;
         return GSR_OK;
     case GSR_TUNE_BLEND_LDS_PAD:
         if (value < 0 || value > 32768) return set_err(GSR_E_ARG, "gsr_set_tuning: blend LDS pad must be 0..32768 bytes");

@@ -256,9 +256,12 @@ enum {
                                         chunked through global scratch); same pairs, same image */
     GSR_TUNE_BLEND_BLOCKS_PER_WAVE = 16, /* blend schedule 0: 8x8 blocks each wave blends one after the other
                                         (default 1); same blocks, same image */
-    GSR_TUNE_BLEND_LDS_PAD = 17      /* blend schedule 0: extra LDS bytes reserved per blend workgroup
+    GSR_TUNE_BLEND_LDS_PAD = 17,     /* blend schedule 0: extra LDS bytes reserved per blend workgroup
                                         (0..32768, default 0): caps the blend's waves per CU, leaving
                                         slots to other frames' kernels in flight; same image */
+    GSR_TUNE_DEPTH_COMPACT = 18      /* global depth sort on the binning path: 1 = stable partition of the
+                                        visible Gaussians first, the passes sort only those; 0 = sort all;
+                                        2 (default) = partition for 4D scenes only; same order, same image */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Depth-sort digit passes the last sorted frame ran (1..4; trailing identity
