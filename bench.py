@@ -61,7 +61,7 @@ def parse():
                     help="N>1: nccl (= RCCL over xGMI, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--gather", choices=("step", "end", "none"), default="step",
                     help="N>1: RCCL gather of finished frames to rank 0 every step (overlapped) or once at the end")
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=4,
                     help="frames in flight per GPU (gsr_render_path lanes); 1 = one frame at a time")
     ap.add_argument("--chunk", type=int, default=8,
                     help="N>1 with --gather step: frames per render_path call (one RCCL gather per frame)")
