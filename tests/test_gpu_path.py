@@ -39,7 +39,7 @@ def render_path_checked(r, scene, cams, W, H, ptrs, **kw):
     raise AssertionError("render_path kept overflowing")
 
 
-@pytest.mark.parametrize("F", [1, 2, 3, 8])
+@pytest.mark.parametrize("F", [1, 2, 3, 4, 8])
 def test_path_distinct_outputs_match_oracle(gpu, orc, torch, c1, F):
     path, soa = c1
     W, H = 320, 240
