@@ -38,7 +38,7 @@ $(LIB): $(OBJDIR)/gsr_kernels.o $(OBJDIR)/gsr_runtime.o $(OBJDIR)/gsr_ply.o $(OB
 	mkdir -p $(dir $(LIB))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -ldl -Wl,-soname,libgsr.so
 
-oracle:
+oracle: $(LIB)
 	$(MAKE) -C oracle
 
 clean:

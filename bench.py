@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--k", type=float, default=3.0)
+    ap.add_argument("--warm-ms", type=float, default=1000.0,
+                    help="untimed frames in flight for at least this long right before the timed regions")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-oracle sample length")
     ap.add_argument("--scene-dir", default=None)
@@ -164,7 +166,8 @@ def dropin_rate(gsr, scene, cam, W, H, k, frames=20):
 def cpu_baseline(soa, cam, W, H, k, seconds, four_d=False):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle  # test infrastructure: CPU baseline leg only
-    threads = min(16, os.cpu_count() or 1)
+    share = cpu_share()
+    threads = share["threads"]
     frames, t0 = 0, time.perf_counter()
     while True:
         if four_d:   # temporal state of the frame, then the 3D render (no cull)
@@ -187,7 +190,23 @@ def cpu_baseline(soa, cam, W, H, k, seconds, four_d=False):
                       f"OpenMP {threads} threads), {el:.1f} s",
             "single_thread": {"value": 1.0 / el1, "unit": "frames/sec", "cores": 1,
                               "sample": f"1 full frame, {el1:.1f} s"},
-            "host": host_cpu()}
+            "host": dict(host_cpu(), **{k: v for k, v in share.items() if k != "threads"})}
+
+
+def cpu_share() -> dict:
+    """Host CPUs this process may run on: the affinity mask (os.sched_getaffinity),
+    capped by the cgroup's CPU quota when one is set (cpu.max: a quota of 16 CPUs on
+    a 256-CPU mask runs 16 at a time, so more OpenMP threads only time-slice)."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return {"threads": min(affinity, quota) if quota else affinity, "affinity_cpus": affinity,
+            "cgroup_quota_cpus": quota}
 
 
 def host_cpu() -> dict:
@@ -204,16 +223,51 @@ def host_cpu() -> dict:
     return {"model": model, "logical_cpus": os.cpu_count()}
 
 
+def gpu_telemetry() -> dict | None:
+    """Clocks, power and temperature of the card(s) from rocm-smi (host-side child
+    process, read outside the timed region), or None when it is unavailable."""
+    import subprocess
+    try:
+        out = subprocess.run(["rocm-smi", "--showpower", "--showclocks", "--showtemp", "--json"],
+                             capture_output=True, text=True, timeout=30).stdout
+        d = json.loads(out[out.index("{"):])
+    except (OSError, ValueError, subprocess.SubprocessError):
+        return None
+    keep = ("power", "sclk", "mclk", "fclk", "socclk", "junction", "memory")
+    return {card: {k: v for k, v in vals.items() if any(w in k.lower() for w in keep)}
+            for card, vals in d.items() if isinstance(vals, dict)}
+
+
 def frame_time(i: int) -> float:
     """Config 5: frame i renders timestep i mod 120 of [0, 1]."""
     return (i % TIMESTEPS_4D) / (TIMESTEPS_4D - 1)
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` (N > 1) started without RANK in the environment: start N
+    ranks under torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1)
+    as a CHILD process and return its exit code.  Nothing here touches the GPU: the
+    parent only picks a free port and waits."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     import torch  # noqa: E402  (before gaussianrenderer_amd: one HIP runtime)
     from gaussianrenderer_amd import multi
     info = multi.rank_info()
+    if info.world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {info.world}")
     rank, world, local_rank = info.rank, info.world, info.local_rank
     device = local_rank % max(1, torch.cuda.device_count())   # == local_rank on a full node
     torch.cuda.set_device(device)
@@ -247,51 +301,11 @@ def main():
     F = max(1, min(8, args.inflight))
     r.set_frames_in_flight(F)
     gloo = dist is not None and args.dist_backend == "gloo"
-    step_gather = dist is not None and args.gather == "step"
     stream = torch.cuda.current_stream().cuda_stream
-    chunk = max(1, args.chunk) if step_gather else args.steps
-    # output buffers: a ring of F (one per lane) or, with per-step gathers, two sets
-    # of `chunk` (one set renders while the other's gathers drain)
-    nsets = 2 if step_gather else 1
-    per_set = chunk if step_gather else F
-    outs = [torch.empty(3 * W * H, dtype=torch.float32, device="cuda") for _ in range(nsets * per_set)]
-    recv = ([[torch.empty_like(outs[0], device="cpu" if gloo else outs[0].device) for _ in range(world)]
-             for _ in range(len(outs))] if (step_gather and rank == 0) else None)
-    pending = [None] * len(outs)
-
-    def wait_pending(b):
-        if pending[b] is not None:
-            pending[b].wait()                   # stream-wait: gather of this buffer done
-            pending[b] = None
-
-    def gather(b):
-        # gloo rehearsal: host copies, synchronous; nccl (RCCL): device buffers, overlapped
-        src = outs[b].cpu() if gloo else outs[b]
-        pending[b] = dist.gather(src, recv[b] if recv else None, dst=0, async_op=not gloo)
-
-    def frame(i=0, b=0):
-        """One frame on the caller's stream (sequential: the viewer's one-at-a-time use)."""
-        r.render(scene, cam, W, H, outs[b].data_ptr(), k=args.k, stream=stream,
-                 time=frame_time(i) if four_d else None)
-
-    def path(i0, m, bufs):
-        """Frames i0 .. i0+m-1 through gsr_render_path (F lanes in flight) into outs[bufs[j]]."""
-        r.render_path(scene, [cam] * m, W, H, [outs[b].data_ptr() for b in bufs], k=args.k, stream=stream,
-                      times=[frame_time(i0 + j) for j in range(m)] if four_d else None)
-
-    def run_pipelined(steps):
-        if not step_gather:
-            path(0, steps, [j % F for j in range(steps)])
-            return
-        for c0 in range(0, steps, chunk):
-            m = min(chunk, steps - c0)
-            base = ((c0 // chunk) % nsets) * per_set
-            bufs = [base + j for j in range(m)]
-            for b in bufs:
-                wait_pending(b)
-            path(c0, m, bufs)
-            for b in bufs:
-                gather(b)
+    shard = multi.FrameShard(dist, r, scene, cam, W, H, k=args.k, steps=args.steps, gather=args.gather,
+                             inflight=F, chunk=args.chunk, gloo=gloo, frame_time=frame_time if four_d else None,
+                             stream=stream)
+    outs, frame, path = shard.outs, shard.frame, shard.path
 
     # warmup (+ grow every lane's pair buffer to the high-water mark)
     for i in range(max(1, args.warmup)):
@@ -299,10 +313,23 @@ def main():
     while r.sync() != 0:
         frame()
     for _ in range(3):
-        path(0, max(F, args.warmup), [j % F for j in range(max(F, args.warmup))])
-        if r.sync() == 0:
+        rc = path(0, max(F, args.warmup), [j % min(F, len(outs)) for j in range(max(F, args.warmup))])
+        if r.sync() == 0 and rc == 0:
             break
     torch.cuda.synchronize()
+
+    def warm(ms):
+        """Untimed frames in flight for at least `ms` of wall time; returns the count."""
+        frames, w0 = 0, time.perf_counter()
+        while (time.perf_counter() - w0) * 1e3 < ms:
+            m = 4 * F
+            path(0, m, [j % min(F, len(outs)) for j in range(m)])
+            frames += m
+            torch.cuda.synchronize()
+        r.sync()
+        return frames
+
+    warm(min(300.0, args.warm_ms))   # stage times below are taken on a warm card too
 
     # untimed frames: the per-stage breakdown averaged over STAGE_FRAMES plain
     # frames (events between stages), then P, Pc and the blend counters from the
@@ -334,12 +361,21 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         fn()
-        for b in range(len(outs)):
-            wait_pending(b)
+        shard.drain()
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         return time.perf_counter() - t0
+
+    # clocks and power before the timed regions (a ~1 s host-side child process, so it
+    # runs before the sustained warmup, never between warmup and timing)
+    telemetry_before = gpu_telemetry() if rank == 0 else None
+    # sustained warmup: the card leaves its idle power state over tens of ms, so a
+    # short K (the driver's --steps 20 is ~10 ms of frames) would otherwise be timed on
+    # the ramp.  Frames in flight for at least --warm-ms of wall time, untimed.
+    warm_frames = warm(args.warm_ms)
+    if dist:
+        dist.barrier()
 
     # sequential segment: K frames one at a time on one stream (the viewer's use and the
     # frame latency), HIP events around the blend launch of every TIMING_STRIDE-th frame
@@ -358,14 +394,15 @@ def main():
     # pipelined timed region (the reported value): the same K frames through
     # gsr_render_path with F frames in flight; blend events on lane 0's launches
     # measure the kernel while it shares the GPU with the other lanes
-    if F > 1 or step_gather:
+    if F > 1 or shard.step_gather:
         r.set_timing(1, TIMING_STRIDE)
-        elapsed = timed(lambda: run_pipelined(args.steps))
+        elapsed = timed(lambda: shard.run(args.steps))
         blend_times_pipe, timed_frames_pipe = r.stage_times()
         r.set_timing(0)
     else:
         elapsed, blend_times_pipe, timed_frames_pipe = seq_elapsed, blend_times, timed_frames
     overflow = r.sync() or seq_overflow
+    telemetry_after = gpu_telemetry() if rank == 0 else None
 
     max_elapsed = multi.max_over_ranks(dist, elapsed, "cpu" if gloo else "cuda")
     max_seq = multi.max_over_ranks(dist, seq_elapsed, "cpu" if gloo else "cuda")
@@ -433,6 +470,8 @@ def main():
         "image_mean": float(img.mean().item()),
         "overflow_after_timed": overflow,
     }
+    result["gpu_telemetry"] = {"before_warmup": telemetry_before, "after_timed": telemetry_after}
+    result["sustained_warmup"] = {"frames": warm_frames, "min_ms": args.warm_ms}
     if gather_ms is not None:
         result["gather_ms"] = round(gather_ms, 3)
     sb = algorithmic_stage_bytes(n, visible, pairs, ntiles, consumed, W, H, depth_passes=depth_passes,

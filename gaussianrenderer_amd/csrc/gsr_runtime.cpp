@@ -16,6 +16,7 @@
 #include <random>
 #include <sstream>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -939,24 +940,39 @@ extern "C" int gsr_render_path(gsr_context* c, const void* scene, int layout, in
         HIP_TRY(hipEventRecord(c->fork_ev, S));
         for (int l = 0; l < F - 1; l++) HIP_TRY(hipStreamWaitEvent(c->lane_streams[l], c->fork_ev, 0));
     }
+    // Output reuse: a frame writing a buffer that an earlier frame of this call wrote on
+    // ANOTHER lane must wait for that writer, however far back it ran (lanes are not
+    // ordered with each other).  prev[i] = the last earlier frame writing d_outs[i];
+    // a writer whose buffer is reused on another lane records its lane's event after
+    // it, and the reuser waits on that event's latest record (at or after the writer
+    // on the same stream, so the wait covers it).
+    std::vector<int> prev(nframes, -1);
+    std::vector<char> record(nframes, 0);
+    {
+        std::unordered_map<const float*, int> last;
+        last.reserve(2 * (size_t)nframes);
+        for (int i = 0; i < nframes; i++) {
+            auto it = last.find(d_outs[i]);
+            if (it != last.end()) {
+                prev[i] = it->second;
+                if (it->second % F != i % F) record[it->second] = 1;
+            }
+            last[d_outs[i]] = i;
+        }
+    }
     int result = GSR_OK;
     const float t_saved = c->time;
     for (int i = 0; i < nframes; i++) {
         const int lane = i % F;
         gsr_context* lc = lane == 0 ? c : c->lanes[lane - 1];
         const hipStream_t ls = lane == 0 ? S : c->lane_streams[lane - 1];
-        // an output written by an earlier frame still in flight on ANOTHER lane: wait for it
-        for (int j = std::max(0, i - F + 1); j < i; j++)
-            if (d_outs[j] == d_outs[i] && j % F != lane) HIP_TRY(hipStreamWaitEvent(ls, c->alias_evs[j % F], 0));
+        if (prev[i] >= 0 && prev[i] % F != lane) HIP_TRY(hipStreamWaitEvent(ls, c->alias_evs[prev[i] % F], 0));
         if (times) lc->time = times[i];
         else lc->time = t_saved;
         const int rc = render_one_locked(lc, scene, layout, n, &cams[i], W, H, nx, ny, ws, hs, k, d_outs[i], ls);
         if (rc == GSR_E_OVERFLOW) result = GSR_E_OVERFLOW;
         else if (rc != GSR_OK) return rc;
-        bool reused = false;
-        for (int j = i + 1; j < std::min(nframes, i + F) && !reused; j++)
-            reused = d_outs[j] == d_outs[i] && j % F != lane;
-        if (reused) HIP_TRY(hipEventRecord(c->alias_evs[i % F], ls));
+        if (record[i]) HIP_TRY(hipEventRecord(c->alias_evs[lane], ls));
     }
     c->time = t_saved;
     // join: work queued on the caller's stream afterwards sees every frame
@@ -1359,9 +1375,12 @@ int gsr::dropin_render_device(gsr_gaussian* d_gaussians, int num_gaussians, cons
     if (num_gaussians > 0 && d_gaussians) {
         gsr_scene_header h{};
         *what = "scene";
-        HIP_TRY(hipMemcpy(&h, d_gaussians, sizeof h, hipMemcpyDeviceToHost));
+        // the magic first (16 B fit inside any 240-B AoS record), the rest of the
+        // header only once it is known to be our block
+        HIP_TRY(hipMemcpy(&h.magic, d_gaussians, sizeof h.magic, hipMemcpyDeviceToHost));
         if (h.magic[0] == GSR_SCENE_MAGIC0 && h.magic[1] == GSR_SCENE_MAGIC1 && h.magic[2] == GSR_SCENE_MAGIC2 &&
             h.magic[3] == GSR_SCENE_MAGIC3) {
+            HIP_TRY(hipMemcpy(&h, d_gaussians, sizeof h, hipMemcpyDeviceToHost));
             // 4D blocks render at the drop-in context's time (gsr_set_time on it is not
             // reachable through this ABI, so t = 0: the sequence's first frame)
             layout = h.narrays == GSR_SCENE4D_NARRAYS    ? GSR_LAYOUT_SCENE_BLOCK_4D

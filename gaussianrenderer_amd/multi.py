@@ -61,3 +61,81 @@ def gather_frames(dist, frame, root: int = 0):
     out = [torch.empty_like(frame) for _ in range(world)] if dist.get_rank() == root else None
     dist.gather(frame, out, dst=root)
     return out
+
+
+class FrameShard:
+    """One rank's frame loop for bench.py --gpus N (config 4): K frames of this rank's
+    camera through Renderer.render_path (F lanes in flight), and with gather="step"
+    every finished frame handed to rank 0 — issued asynchronously (RCCL) right after
+    its chunk is enqueued and overlapped with the next chunk's render.
+
+    Buffers: with per-step gathers, two sets of `chunk` output buffers (one set
+    renders while the other's gathers drain; a buffer is reused only after its
+    pending gather completes); otherwise a ring of F.  On rank 0, `recv[b]` holds
+    the last frame gathered from every rank into buffer b.  gloo (the CPU / shared-GPU
+    rehearsal) gathers host copies synchronously."""
+
+    def __init__(self, dist, renderer, scene, cam, W: int, H: int, k: float = 3.0, steps: int = 1,
+                 gather: str = "step", inflight: int = 1, chunk: int = 8, gloo: bool = False,
+                 frame_time=None, stream: int = 0):
+        import torch
+        self.dist, self.r, self.scene, self.cam = dist, renderer, scene, cam
+        self.W, self.H, self.k, self.stream = W, H, k, stream
+        self.F = max(1, inflight)
+        self.gloo = gloo
+        self.frame_time = frame_time
+        self.step_gather = dist is not None and gather == "step"
+        self.chunk = max(1, chunk) if self.step_gather else max(1, steps)
+        self.nsets = 2 if self.step_gather else 1
+        self.per_set = self.chunk if self.step_gather else self.F
+        self.outs = [torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+                     for _ in range(self.nsets * self.per_set)]
+        rank = dist.get_rank() if dist is not None else 0
+        world = dist.get_world_size() if dist is not None else 1
+        self.recv = ([[torch.empty_like(self.outs[0], device="cpu" if gloo else self.outs[0].device)
+                       for _ in range(world)] for _ in range(len(self.outs))]
+                     if (self.step_gather and rank == 0) else None)
+        self.pending = [None] * len(self.outs)
+
+    def _times(self, i0: int, m: int):
+        return [self.frame_time(i0 + j) for j in range(m)] if self.frame_time else None
+
+    def wait_pending(self, b: int):
+        if self.pending[b] is not None:
+            self.pending[b].wait()          # nccl: stream-wait until the gather of buffer b is done
+            self.pending[b] = None
+
+    def drain(self):
+        for b in range(len(self.outs)):
+            self.wait_pending(b)
+
+    def gather(self, b: int):
+        src = self.outs[b].cpu() if self.gloo else self.outs[b]
+        self.pending[b] = self.dist.gather(src, self.recv[b] if self.recv else None, dst=0,
+                                           async_op=not self.gloo)
+
+    def frame(self, i: int = 0, b: int = 0):
+        """One frame on the caller's stream (sequential: the viewer's one-at-a-time use)."""
+        self.r.render(self.scene, self.cam, self.W, self.H, self.outs[b].data_ptr(), k=self.k,
+                      stream=self.stream, time=self.frame_time(i) if self.frame_time else None)
+
+    def path(self, i0: int, m: int, bufs):
+        """Frames i0 .. i0+m-1 through gsr_render_path into outs[bufs[j]]; returns its code
+        (GSR_E_OVERFLOW: some frame of the call overflowed and must be re-rendered)."""
+        return self.r.render_path(self.scene, [self.cam] * m, self.W, self.H, [self.outs[b].data_ptr() for b in bufs],
+                           k=self.k, stream=self.stream, times=self._times(i0, m))
+
+    def run(self, steps: int):
+        """K frames in flight, gathered per step when enabled (not drained: call drain())."""
+        if not self.step_gather:
+            self.path(0, steps, [j % self.F for j in range(steps)])
+            return
+        for c0 in range(0, steps, self.chunk):
+            m = min(self.chunk, steps - c0)
+            base = ((c0 // self.chunk) % self.nsets) * self.per_set
+            bufs = [base + j for j in range(m)]
+            for b in bufs:
+                self.wait_pending(b)
+            self.path(c0, m, bufs)
+            for b in bufs:
+                self.gather(b)

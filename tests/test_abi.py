@@ -86,3 +86,26 @@ def test_tiling_information_matches_reference(gsr):
     assert (t.width_stride, t.height_stride) == (39, 22)
     t.resize(480, 640, 50, 50)
     assert (t.width_stride, t.height_stride) == (13, 10)
+
+
+VIEWER_LINK = os.path.join(ROOT, "oracle", "_ref", "viewer_link")
+LOADER_MANGLED = "_Z23loadGaussianCudaFromPlyRKNSt7__cxx1112basic_stringIcSt11char_traitsIcESaIcEEEPi"
+
+
+def test_viewer_tu_links_against_reference_headers(gsr):
+    """tests/link/viewer_link.cpp includes the reference's own render.cuh / camera.hpp /
+    gaussians.hpp (unmodified), static_asserts every Camera / Gaussian /
+    lightWeightGaussian field offset against include/gsr_types.h, and links libgsr.so:
+    both drop-in symbols (the extern "C" render call and the C++-mangled loader) must be
+    imported from libgsr.so and resolve at load time (LD_BIND_NOW)."""
+    if not os.path.exists(VIEWER_LINK):
+        pytest.skip("oracle/_ref/viewer_link not built (needs /root/reference at build time)")
+    undefined = subprocess.run(["nm", "-D", "--undefined-only", VIEWER_LINK], capture_output=True, text=True,
+                               check=True).stdout.split()
+    assert "preprocessCUDAGaussians" in undefined and LOADER_MANGLED in undefined
+    from gaussianrenderer_amd import _native
+    assert {"preprocessCUDAGaussians", LOADER_MANGLED} <= exported_symbols(_native.LIB_PATH)
+    out = subprocess.run([VIEWER_LINK, "--layout"], capture_output=True, text=True, timeout=60,
+                         env=dict(os.environ, LD_BIND_NOW="1"))
+    assert out.returncode == 0, out.stderr
+    assert "Camera 484 B, Gaussian 240 B" in out.stdout

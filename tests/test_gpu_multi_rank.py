@@ -1,0 +1,97 @@
+"""World-size-2 run of the multi-GPU frame loop (multi.FrameShard, the code behind
+bench.py --gpus N) with the HIP renderer: two gloo ranks share cuda:0, each renders
+its orbit camera (azimuth 45 deg * rank, camera.cpp:130-158) through
+Renderer.render_path with frames in flight, hands every frame to rank 0 per step
+(double-buffered chunks, pending-gather reuse), and max-reduces the elapsed time.
+Rank 0's gathered frames must equal the oracle's renders of cameras 0 and 1 bit for
+bit.  Also: bench.py --gpus 2 launches two real ranks and prints n_gpus 2."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, ply, W, H, steps, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    import gaussianrenderer_amd as gsr
+    from gaussianrenderer_amd import multi
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    scene = gsr.Scene.from_ply(ply)
+    r = gsr.Renderer()
+    r.set_frames_in_flight(2)
+    cam = multi.orbit_camera(rank, W, H)
+    shard = multi.FrameShard(dist, r, scene, cam, W, H, steps=steps, gather="step", inflight=2, chunk=2,
+                             gloo=True, stream=torch.cuda.current_stream().cuda_stream)
+    shard.run(steps)
+    shard.drain()
+    torch.cuda.synchronize()
+    assert r.sync() == 0
+    elapsed = multi.max_over_ranks(dist, 0.25 + rank, "cpu")
+    if rank == 0:
+        q.put((elapsed, [[f.numpy().copy() for f in shard.recv[b]] for b in range(len(shard.recv))]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_hip_frames_gathered(gpu, orc, tmp_path):
+    W, H, world, steps = 320, 240, 2, 3       # chunks of 2: buffers 0, 1 then 2 (second set)
+    ply = str(tmp_path / "s.ply")
+    gpu.write_synthetic_ply(ply, 10_000, 4)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, ply, W, H, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        elapsed, recv = q.get(timeout=100)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert elapsed == pytest.approx(1.25)          # MAX over ranks
+    soa = gpu.read_ply(ply)
+    from gaussianrenderer_amd import multi
+    wants = [orc.render(soa, multi.orbit_camera(r, W, H), W, H, 3.0).reshape(-1) for r in range(world)]
+    assert not np.array_equal(wants[0], wants[1])
+    for b in range(steps):
+        for r in range(world):
+            assert np.array_equal(recv[b][r], wants[r]), f"buffer {b}, rank {r}"
+
+
+def test_bench_launches_ranks(gpu, tmp_path):
+    """bench.py --gpus 2 (no RANK in the environment) starts two ranks itself; gloo so
+    both can share the one GPU of a test box.  Rank 0 prints n_gpus 2."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "1",
+                          "--steps", "6", "--warmup", "2", "--dist-backend", "gloo", "--chunk", "3",
+                          "--scene-dir", str(tmp_path)],
+                         capture_output=True, text=True, timeout=110, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    res = lines[0]
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "frames2"
+    assert res["value"] > 0 and res["steps"] == 6

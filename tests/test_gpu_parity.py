@@ -9,7 +9,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import scene_soa
+from conftest import ROOT, scene_soa
 
 pytestmark = pytest.mark.gpu
 
@@ -492,4 +492,29 @@ def test_config3_full_parity_and_properties(gpu, orc, torch, tmp_path_factory):
     again, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
     assert np.array_equal(got.view(np.uint32), again.view(np.uint32))
     want = orc.render(soa, cam, W, H, 3.0, threads=min(16, os.cpu_count() or 1))
+    assert_image_parity(got, want)
+
+
+@pytest.mark.parametrize("azimuth", [0.0, 135.0])
+def test_viewer_link_binary_renders_like_oracle(gpu, orc, tmp_path, azimuth):
+    """The viewer-style C++ binary (tests/link/viewer_link.cpp: reference headers,
+    reference camera.cpp, by-value Camera across a real C++ call into libgsr.so, 50x50
+    TilingInformation, host image) renders the oracle's image bit for bit."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "_ref", "viewer_link")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/viewer_link was not built")
+    W, H = 400, 300
+    ply, img = str(tmp_path / "s.ply"), str(tmp_path / "img.f32")
+    gpu.write_synthetic_ply(ply, 20_000, 7)
+    out = subprocess.run([exe, ply, str(W), str(H), img, str(azimuth)], capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr
+    got = np.fromfile(img, dtype=np.float32).reshape(3, H, W)
+    cam = cam_for(gpu, W, H)
+    if azimuth:
+        gpu.orbit(cam, azimuth, 0.0)
+    t = gpu.TilingInformation(50, 50, H, W)
+    want = orc.render(gpu.read_ply(ply), cam, W, H, 3.0, tiling=(t.num_tile_x, t.num_tile_y, t.width_stride,
+                                                                     t.height_stride))
+    assert (want != 0).sum() > 1000
     assert_image_parity(got, want)

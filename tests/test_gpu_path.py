@@ -33,8 +33,8 @@ def orbit_cams(gsr, W, H, m):
 def render_path_checked(r, scene, cams, W, H, ptrs, **kw):
     """render_path, re-rendered once if an earlier frame overflowed (as the bench warmup does)."""
     for _ in range(3):
-        r.render_path(scene, cams, W, H, ptrs, **kw)
-        if r.sync() == 0:
+        rc = r.render_path(scene, cams, W, H, ptrs, **kw)   # overflow of an earlier frame of the call
+        if r.sync() == 0 and rc == 0:                         # ... or of the last ones, seen at sync
             return
     raise AssertionError("render_path kept overflowing")
 
@@ -68,6 +68,24 @@ def test_path_ring_outputs_shared_across_lanes(gpu, orc, torch, c1):
     render_path_checked(r, scene, cams, W, H, [bufs[i % 2].data_ptr() for i in range(m)])
     for b in range(2):
         last = max(i for i in range(m) if i % 2 == b)
+        assert_image_parity(bufs[b].view(3, H, W).cpu().numpy(), orc.render(soa, cams[last], W, H, 3.0))
+
+
+@pytest.mark.parametrize("F,ring,m", [(2, 3, 9), (4, 5, 13), (3, 4, 10)])
+def test_path_ring_longer_than_lanes(gpu, orc, torch, c1, F, ring, m):
+    """A ring of more buffers than lanes: frame i and frame i + ring write the same
+    buffer from lanes that are not ordered with each other (and more than F - 1 frames
+    apart), so the later frame must still wait for the earlier writer."""
+    path, soa = c1
+    W, H = 320, 240
+    cams = orbit_cams(gpu, W, H, m)
+    scene = gpu.Scene.from_soa(soa)
+    r = gpu.Renderer()
+    r.set_frames_in_flight(F)
+    bufs = [torch.full((3 * W * H,), -1.0, device="cuda") for _ in range(ring)]
+    render_path_checked(r, scene, cams, W, H, [bufs[i % ring].data_ptr() for i in range(m)])
+    for b in range(ring):
+        last = max(i for i in range(m) if i % ring == b)
         assert_image_parity(bufs[b].view(3, H, W).cpu().numpy(), orc.render(soa, cams[last], W, H, 3.0))
 
 
