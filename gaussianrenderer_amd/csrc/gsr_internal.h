@@ -40,7 +40,6 @@ struct Stats {
     unsigned long long pairs_total;   // P before the capacity clamp
     uint32_t pairs_eff;               // min(P, capacity): what sort/ranges/blend consume
     uint32_t overflow;                // 1 if P > capacity
-    uint32_t big_tiles;               // tiles whose list exceeded the per-tile LDS sort (sticky copy: count)
     uint32_t pad;
 };
 
@@ -73,23 +72,12 @@ hipError_t launch_emit(const uint64_t* items0, const uint64_t* items1, const uin
 hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* keys_out, uint32_t* vals_out,
                           bool key16, const uint32_t* n_dev, int shift, int bits, int groups, int items,
                           uint32_t* hist, uint32_t* totals, uint2* ranges, hipStream_t s);
-// Per-tile depth order (tile binning in index order): sort each tile's index list
-// in vals stably by depth key (items: preprocess output, key in the high word).
-// One wave per list of <= 1024 entries; longer lists go through big_list (>= ntiles
-// entries) to big_groups workgroups.  big_counts: 2 words, [parity] zero on entry
-// (the launch zeroes [parity ^ 1] for the next frame).  scr_a (u64) and scr_keys
-// (u32), both >= the pair count, are scratch for lists over 4096 entries
-// (counted in stats[1].big_tiles / host_st).
-hipError_t launch_tile_depth_sort(const uint2* ranges, int ntiles, const uint64_t* items, uint32_t* vals,
-                                  uint64_t* scr_a, uint32_t* scr_keys, uint32_t* big_list, uint32_t* big_counts,
-                                  int parity, int big_groups, Stats* stats, Stats* host_mapped_stats,
-                                  hipStream_t s);
-// consumed: optional device counters (diagnostics).  variant 1 = persistent
-// per-wave block queue (queue: 8 device uints; resident_groups: grid size).
+// One wave per 8x8 block (k_blend_w).  consumed: optional device counters
+// (diagnostics), or with stamps the per-wave timeline (tools/blend_timeline.py).
+// band_tiles > 0: bands of that many tiles dealt round-robin to the XCDs; 0: one
+// contiguous run of blocks per XCD.
 hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
-                        float* out, unsigned long long* consumed, int variant, unsigned int* queue,
-                        int resident_groups, uint32_t* tile_perm, int band_tiles, int wpg, int seq, int lds_pad,
-                        hipStream_t s);
+                        float* out, unsigned long long* consumed, bool stamps, int band_tiles, hipStream_t s);
 // Stable partition of the preprocess items: visible first, culled last (both in
 // index order), visible count into *n_live; culled tail to out only, with dead
 // rects in srect (gsr_kernels.hip "live partition").  counts: groups words.

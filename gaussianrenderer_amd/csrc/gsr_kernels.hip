@@ -1660,416 +1660,6 @@ __global__ __launch_bounds__(256) void k_part_scatter(const uint64_t* __restrict
     }
 }
 
-// ------------------------------------------------------------------ per-tile depth order
-//
-// The other way to reach the same tile lists: bin the Gaussians in INDEX order
-// (the row and column passes above, fed by the preprocess items and rects
-// directly — no global depth sort), which leaves every tile's list in index
-// order, then sort each list stably by depth key.  The result is the order the
-// reference's stable SortPairs on (tile << 32 | key) defines (render.cu:1099-1118,
-// ties by index), identical to global depth sort + stable binning.
-//
-// Opt-in (GSR_TUNE_DEPTH_ORDER = 1): measured slower than the global depth sort
-// on config 2 (k_tile_depth_sort_wave 70 us for 5.4M entries vs 80 us for the
-// whole global sort; 8-bit ballot ranking costs ~60 VALU per 64 entries per pass,
-// and a tile's list needs 3 passes), so it is kept as a tested alternative.
-// Lists of up to 1024 entries: one wave each (k_tile_depth_sort_wave); longer
-// ones: a workgroup each, sorted in LDS up to 256 * 16 entries (keys gathered
-// once from the 8-B items, passes from the list's key span: 8-bit LSD digits of
-// key - min, ranked with bin_rank_tile), beyond that a chunked LSD through
-// global scratch (stable: chunks in order, running digit bases), counted in the
-// frame stats (big_tiles).
-
-constexpr uint32_t kTdsCap = 256u * 16u;            // largest list sorted in LDS
-
-__device__ __forceinline__ void block_min_max(uint32_t& kmin, uint32_t& kmax, uint32_t* s_mm) {
-    const uint32_t w = threadIdx.x >> 6;
-    kmin = ~wave_max_u32(~kmin);
-    kmax = wave_max_u32(kmax);
-    if ((threadIdx.x & 63u) == 0) {
-        s_mm[w] = kmin;
-        s_mm[4 + w] = kmax;
-    }
-    __syncthreads();
-    kmin = min(min(s_mm[0], s_mm[1]), min(s_mm[2], s_mm[3]));
-    kmax = max(max(s_mm[4], s_mm[5]), max(s_mm[6], s_mm[7]));
-    __syncthreads();
-}
-
-__device__ __forceinline__ int key_passes(uint32_t span) { return span ? (32 - __clz((int)span) + 7) / 8 : 0; }
-
-template <int ITEMS>
-__device__ __forceinline__ void tds_sort_lds(uint32_t* __restrict__ vals, uint32_t start, uint32_t L,
-                                             const uint64_t* __restrict__ items, uint32_t* s_key,
-                                             uint32_t* s_idx, uint32_t (*s_wc)[256], uint32_t* s_lbase,
-                                             uint32_t* s_scr, uint32_t* s_mm) {
-    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    uint32_t key[ITEMS], idx[ITEMS];
-#pragma unroll
-    for (int k = 0; k < ITEMS; k++) {
-        const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
-        idx[k] = el < L ? vals[start + el] : 0u;
-    }
-    uint32_t kmin = 0xffffffffu, kmax = 0u;
-#pragma unroll
-    for (int k = 0; k < ITEMS; k++) {
-        const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
-        key[k] = el < L ? (uint32_t)(items[idx[k]] >> 32) : 0u;
-        if (el < L) {
-            kmin = min(kmin, key[k]);
-            kmax = max(kmax, key[k]);
-        }
-    }
-    block_min_max(kmin, kmax, s_mm);
-    const int passes = key_passes(kmax - kmin);   // 0: all keys equal, index order is the answer
-    for (int p = 0; p < passes; p++) {
-        uint32_t dig[ITEMS], pos[ITEMS];
-#pragma unroll
-        for (int k = 0; k < ITEMS; k++) dig[k] = ((key[k] - kmin) >> (8 * p)) & 0xffu;
-        bin_rank_tile<ITEMS, 8>(dig, L, pos, s_wc, s_lbase, s_scr);
-        if (p == passes - 1) {
-#pragma unroll
-            for (int k = 0; k < ITEMS; k++)
-                if (w * 64 * ITEMS + k * 64 + lane < L) vals[start + pos[k]] = idx[k];
-        } else {
-#pragma unroll
-            for (int k = 0; k < ITEMS; k++)
-                if (w * 64 * ITEMS + k * 64 + lane < L) {
-                    s_key[pos[k]] = key[k];
-                    s_idx[pos[k]] = idx[k];
-                }
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < ITEMS; k++) {
-                const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
-                if (el < L) {
-                    key[k] = s_key[el];
-                    idx[k] = s_idx[el];
-                }
-            }
-            __syncthreads();
-        }
-    }
-}
-
-// Lists longer than kTdsCap: LSD passes through global scratch, A = u64
-// (key << 32 | index) and B = (scr_keys, vals), alternating A, B, A, ...; each pass
-// counts its digits over the whole list, then ranks and scatters it chunk by
-// chunk in list order.  An odd number of passes ends in A and copies back.
-__device__ void tds_sort_global(uint32_t* __restrict__ vals, uint32_t start, uint32_t L,
-                                const uint64_t* __restrict__ items, uint64_t* __restrict__ scr_a,
-                                uint32_t* __restrict__ scr_keys, uint32_t (*s_wc)[256], uint32_t* s_lbase,
-                                uint32_t* s_gbase, uint32_t* s_scr, uint32_t* s_mm) {
-    constexpr int ITEMS = 16;
-    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    uint32_t kmin = 0xffffffffu, kmax = 0u;
-    for (uint32_t i = t; i < L; i += 256) {
-        const uint32_t k = (uint32_t)(items[vals[start + i]] >> 32);
-        kmin = min(kmin, k);
-        kmax = max(kmax, k);
-    }
-    block_min_max(kmin, kmax, s_mm);
-    const int passes = key_passes(kmax - kmin);
-    auto load = [&](int p, uint32_t i, uint32_t& key, uint32_t& idx) {
-        if (p == 0) {
-            idx = vals[start + i];
-            key = (uint32_t)(items[idx] >> 32);
-        } else if (p & 1) {   // previous pass wrote A
-            const uint64_t v = scr_a[start + i];
-            key = (uint32_t)(v >> 32);
-            idx = (uint32_t)v;
-        } else {              // previous pass wrote B
-            key = scr_keys[start + i];
-            idx = vals[start + i];
-        }
-    };
-    for (int p = 0; p < passes; p++) {
-        const int sh = 8 * p;
-        // digit counts of the whole list -> running global bases
-        s_gbase[t] = 0;
-        __syncthreads();
-        for (uint32_t i = t; i < L; i += 256) {
-            uint32_t key, idx;
-            load(p, i, key, idx);
-            atomicAdd(&s_gbase[((key - kmin) >> sh) & 0xffu], 1u);
-        }
-        __syncthreads();
-        {
-            uint32_t tot;
-            const uint32_t c = s_gbase[t];
-            __syncthreads();
-            s_gbase[t] = block_exclusive_scan<uint32_t>(c, s_scr, tot);
-        }
-        const bool to_a = (p & 1) == 0;
-        for (uint32_t c0 = 0; c0 < L; c0 += kTdsCap) {
-            const uint32_t tn = min(kTdsCap, L - c0);
-            uint32_t key[ITEMS], idx[ITEMS], dig[ITEMS], pos[ITEMS];
-#pragma unroll
-            for (int k = 0; k < ITEMS; k++) {
-                const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
-                key[k] = 0u;
-                idx[k] = 0u;
-                if (el < tn) load(p, c0 + el, key[k], idx[k]);
-                dig[k] = ((key[k] - kmin) >> sh) & 0xffu;
-            }
-            // (the loads of this chunk precede bin_rank_tile's barriers, so the
-            // scatter below never overwrites an element another thread still reads:
-            // source and destination are different buffers anyway)
-            const uint32_t tcount = bin_rank_tile<ITEMS, 8>(dig, tn, pos, s_wc, s_lbase, s_scr);
-#pragma unroll
-            for (int k = 0; k < ITEMS; k++) {
-                if (w * 64 * ITEMS + k * 64 + lane < tn) {
-                    const uint32_t dst = start + s_gbase[dig[k]] + (pos[k] - s_lbase[dig[k]]);
-                    if (to_a) {
-                        scr_a[dst] = ((uint64_t)key[k] << 32) | idx[k];
-                    } else {
-                        scr_keys[dst] = key[k];
-                        vals[dst] = idx[k];
-                    }
-                }
-            }
-            __syncthreads();
-            s_gbase[t] += tcount;
-            __syncthreads();
-        }
-    }
-    if (passes & 1) {   // the last pass wrote A: indices back into vals
-        __threadfence_block();
-        for (uint32_t i = t; i < L; i += 256) vals[start + i] = (uint32_t)scr_a[start + i];
-    }
-}
-
-// Lists of up to kTdsWaveCap entries: one wave per tile, wave-synchronous (no
-// workgroup barrier; a wave's LDS operations execute in issue order).  Entry e
-// of the list is slot e / 64, lane e % 64 (slot-major, so every load is one
-// coalesced wave access).  Per pass: digit counts ranked slot by slot with
-// ballot matching (a slot's read of the running count sees the earlier slots'
-// adds), a wave scan of the 256 counts, then the entries move through the wave's
-// LDS slice (or, in the last pass, straight to their final slot in vals).
-// Longer lists are appended to big_list for k_tile_depth_sort_big.
-constexpr uint32_t kTdsWaveCap = 1024;
-
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__global__ __launch_bounds__(64) void k_tile_depth_sort_wave(const uint2* __restrict__ ranges,
-                                                              const uint64_t* __restrict__ items,
-                                                              uint32_t* __restrict__ vals,
-                                                              uint32_t* __restrict__ big_list,
-                                                              uint32_t* __restrict__ big_count) {
-    constexpr int IT = kTdsWaveCap / 64;
-    __shared__ uint32_t s_key[kTdsWaveCap], s_idx[kTdsWaveCap], s_cnt[256];
-    const uint32_t lane = threadIdx.x;
-    const uint32_t tile = blockIdx.x;
-    const uint2 rr = ranges[tile];                      // {~start, end}, zero = empty
-    if (!rr.y) return;
-    const uint32_t start = ~rr.x, L = rr.y - start;
-    if (L < 2) return;
-    if (L > kTdsWaveCap) {
-        if (lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
-        return;
-    }
-    const uint32_t nslot = (L + 63u) / 64u;
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint32_t key[IT], idx[IT];
-#pragma unroll
-    for (int k = 0; k < IT; k++) {
-        const uint32_t e = (uint32_t)k * 64u + lane;
-        idx[k] = ((uint32_t)k < nslot && e < L) ? vals[start + e] : 0u;
-    }
-    uint32_t kmin = 0xffffffffu, kmax = 0u;
-#pragma unroll
-    for (int k = 0; k < IT; k++) {
-        const uint32_t e = (uint32_t)k * 64u + lane;
-        if ((uint32_t)k < nslot && e < L) {
-            key[k] = (uint32_t)(items[idx[k]] >> 32);
-            kmin = min(kmin, key[k]);
-            kmax = max(kmax, key[k]);
-        } else {
-            key[k] = 0u;
-        }
-    }
-    kmin = ~wave_max_u32(~kmin);
-    kmax = wave_max_u32(kmax);
-    const int passes = key_passes(kmax - kmin);        // 0: all keys equal, index order stands
-    for (int p = 0; p < passes; p++) {
-#pragma unroll
-        for (int j = 0; j < 4; j++) s_cnt[4 * lane + j] = 0u;
-        wave_lds_sync();
-        uint32_t dig[IT], pos[IT];
-#pragma unroll
-        for (int k = 0; k < IT; k++) {
-            dig[k] = 0u;
-            pos[k] = 0u;
-            if ((uint32_t)k >= nslot) continue;            // uniform
-            const bool valid = (uint32_t)k * 64u + lane < L;
-            const uint32_t d = ((key[k] - kmin) >> (8 * p)) & 0xffu;
-            dig[k] = d;
-            uint64_t peers = __ballot(valid);
-#pragma unroll
-            for (int bit = 0; bit < 8; bit++) {
-                const bool on = (d >> bit) & 1u;
-                const uint64_t bm = __ballot(on);
-                peers &= on ? bm : ~bm;
-            }
-            pos[k] = s_cnt[d] + (uint32_t)__popcll(peers & lt_mask);
-            if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
-                atomicAdd(&s_cnt[d], (uint32_t)__popcll(peers));
-        }
-        wave_lds_sync();
-        // exclusive scan of the 256 digit counts (4 per lane), bases back into s_cnt
-        {
-            uint32_t c[4], sum = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                c[j] = s_cnt[4 * lane + j];
-                sum += c[j];
-            }
-            uint32_t x = sum;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o, 64);
-                if (lane >= (uint32_t)o) x += y;
-            }
-            uint32_t run = x - sum;
-            wave_lds_sync();
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                s_cnt[4 * lane + j] = run;
-                run += c[j];
-            }
-        }
-        wave_lds_sync();
-        const bool last = p == passes - 1;
-#pragma unroll
-        for (int k = 0; k < IT; k++) {
-            if ((uint32_t)k * 64u + lane < L) {
-                const uint32_t q = s_cnt[dig[k]] + pos[k];
-                if (last) {
-                    vals[start + q] = idx[k];
-                } else {
-                    s_key[q] = key[k];
-                    s_idx[q] = idx[k];
-                }
-            }
-        }
-        if (last) break;
-        wave_lds_sync();
-#pragma unroll
-        for (int k = 0; k < IT; k++) {
-            const uint32_t e = (uint32_t)k * 64u + lane;
-            if (e < L) {
-                key[k] = s_key[e];
-                idx[k] = s_idx[e];
-            }
-        }
-        wave_lds_sync();
-    }
-}
-
-// Lists over kTdsWaveCap (big_list, filled by the wave kernel): one workgroup per
-// list, in LDS up to kTdsCap, chunked through global scratch beyond (counted in
-// the frame stats, big_tiles).  The
-// workgroups stride over the list; the count of the NEXT frame parity is zeroed.
-__global__ __launch_bounds__(256) void k_tile_depth_sort_big(const uint2* __restrict__ ranges,
-                                                              const uint64_t* __restrict__ items,
-                                                              uint32_t* __restrict__ vals,
-                                                              uint64_t* __restrict__ scr_a,
-                                                              uint32_t* __restrict__ scr_keys,
-                                                              const uint32_t* __restrict__ big_list,
-                                                              uint32_t* __restrict__ big_counts, int parity,
-                                                              Stats* __restrict__ st, Stats* host_st) {
-    __shared__ uint32_t s_key[kTdsCap], s_idx[kTdsCap];
-    __shared__ uint32_t s_wc[4][256], s_lbase[256], s_gbase[256], s_scr[4], s_mm[8];
-    const uint32_t nbig = big_counts[parity];
-    if (blockIdx.x == 0 && threadIdx.x == 0) big_counts[parity ^ 1] = 0u;
-    for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
-        const uint2 rr = ranges[big_list[b]];
-        const uint32_t start = ~rr.x, L = rr.y - start;
-        if (L <= kTdsCap) {
-            tds_sort_lds<16>(vals, start, L, items, s_key, s_idx, s_wc, s_lbase, s_scr, s_mm);
-        } else {
-            if (threadIdx.x == 0) {
-                atomicAdd(&st[1].big_tiles, 1u);
-                if (host_st) {
-                    host_st->big_tiles = 1u;
-                    __threadfence_system();
-                }
-            }
-            tds_sort_global(vals, start, L, items, scr_a, scr_keys, s_wc, s_lbase, s_gbase, s_scr, s_mm);
-        }
-        __syncthreads();
-    }
-}
-
-// ------------------------------------------------------------------ blend tile order
-
-// Longest-tile-first order for the blend: one workgroup stable-sorts the tiles
-// into 32 length classes (clz of the list length: a class per power of two,
-// longest first; tile order is kept inside a class) and writes the permutation.
-// Dispatching the long tiles first leaves short ones for the drain at the end
-// of the blend kernel, where the device empties out.
-// Bands of bt consecutive tiles (bt = 1: single tiles) are the units: a band's
-// work is the sum of its tiles' list lengths.
-__global__ __launch_bounds__(1024) void k_tile_order(const uint2* __restrict__ ranges, int nt, int bt,
-                                                      uint32_t* __restrict__ perm) {
-    __shared__ uint32_t s_base[32], s_wc[16][32];
-    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int nbands = (nt + bt - 1) / bt;
-    auto cls = [&](int j) -> uint32_t {
-        uint32_t len = 0;
-        for (int i = j * bt; i < min(nt, (j + 1) * bt); i++) {
-            const uint2 rr = ranges[i];
-            len += rr.y ? rr.y - ~rr.x : 0u;
-        }
-        return len ? min((uint32_t)__clz(len), 31u) : 31u;
-    };
-    if (t < 32) s_base[t] = 0;
-    __syncthreads();
-    for (int i = (int)t; i < nbands; i += 1024) atomicAdd(&s_base[cls(i)], 1u);
-    __syncthreads();
-    if (t == 0) {
-        uint32_t run = 0;
-        for (int k = 0; k < 32; k++) {
-            const uint32_t v = s_base[k];
-            s_base[k] = run;
-            run += v;
-        }
-    }
-    for (int c0 = 0; c0 < nbands; c0 += 1024) {
-        if (lane < 32) s_wc[w][lane] = 0;
-        __syncthreads();
-        const int i = c0 + (int)t;
-        const bool valid = i < nbands;
-        const uint32_t d = valid ? cls(i) : 0u;
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int bit = 0; bit < 5; bit++) {
-            const bool on = (d >> bit) & 1u;
-            const uint64_t bm = __ballot(on);
-            peers &= on ? bm : ~bm;
-        }
-        if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane) s_wc[w][d] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = s_base[d] + (uint32_t)__popcll(peers & lt_mask);
-            for (uint32_t k = 0; k < w; k++) pos += s_wc[k][d];
-            perm[pos] = (uint32_t)i;
-        }
-        __syncthreads();
-        if (t < 32) {
-            uint32_t add = 0;
-            for (int k = 0; k < 16; k++) add += s_wc[k][t];
-            s_base[t] += add;
-        }
-        __syncthreads();
-    }
-}
-
 // ------------------------------------------------------------------ blend
 
 
@@ -2394,126 +1984,64 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
     }
 }
 
-// STAMPS: timing diagnostics only (no counters): per workgroup, its launch
-// order slot gets {start, end} of the s_memrealtime clock (100 MHz) in
-// counters[2 * blockIdx.x ...] (end = max over the four waves).
+// One-wave workgroups: workgroup g blends one 8x8 block, so a finished block
+// frees its wave slot at once (no waiting for the tile's other three waves).
+// Hardware dispatch sends workgroup g to XCD g mod 8.  bands > 1: the blocks
+// (tile-major, a tile's four blocks consecutive) are cut into bands of B
+// consecutive blocks and band j goes to XCD j mod 8, so each XCD's L2 serves runs
+// of neighbouring tiles while heavy and light image regions spread over all XCDs;
+// padding workgroups past the last block exit.  bands <= 1: one contiguous run of
+// blocks per XCD (xcd_remap).
+// STAMPS (timeline diagnostics, no counters): counters[2 * g] = start of the
+// s_memrealtime clock (100 MHz), counters[2 * g + 1] = duration (40 bits) |
+// placement << 40 (XCC id and HW_ID's SE / SH / CU / SIMD / slot).
 template <bool DIAG, bool STAMPS = false>
-__global__ __launch_bounds__(256) void k_blend(const uint32_t* __restrict__ idx,
-                                                const uint2* __restrict__ ranges,
-                                                const uint4* __restrict__ rec, int tiles_x, int tiles_y,
-                                                int W, int H, int cover_w, int cover_h,
-                                                float* __restrict__ out,
-                                                unsigned long long* __restrict__ counters) {
-    __shared__ float4 sP[4][32 * 20 / 4];
+__global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx,
+                                                 const uint2* __restrict__ ranges,
+                                                 const uint4* __restrict__ rec, int tiles_x, int tiles_y,
+                                                 int W, int H, int cover_w, int cover_h,
+                                                 float* __restrict__ out,
+                                                 unsigned long long* __restrict__ counters, int bands) {
+    __shared__ float4 sP[32 * 20 / 4];
     const int ntiles = tiles_x * tiles_y;
-    const int tile = xcd_remap(blockIdx.x, ntiles);
+    const int vb = (int)blockIdx.x;
+    int L;
+    if (bands > 1) {
+        const int nu = 4 * ntiles;
+        const int B = (nu + 8 * bands - 1) / (8 * bands);
+        const int k = vb >> 3;
+        L = ((k / B) * 8 + (vb & 7)) * B + k % B;
+        if (L >= nu) return;
+    } else {
+        if (vb >= ntiles * 4) return;
+        L = xcd_remap(vb, ntiles * 4);
+    }
+    const int tile = L >> 2, sub = L & 3;
     const int tx = tile % tiles_x, ty = tile / tiles_x;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    if (STAMPS && t == 0) counters[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    const int lane = (int)(threadIdx.x & 63u);
+    uint64_t t_start = 0, place = 0;
+    if (STAMPS && lane == 0) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        place = ((uint64_t)(xcc & 7u) << 16) | (hw & 0xffffu);
+        t_start = __builtin_amdgcn_s_memrealtime();
+        counters[2 * vb] = t_start;
+    }
     const uint2 rr = ranges[tile];                          // {~start, end}, zero = empty
     BlendDiag dg;
-    blend_block<DIAG>(idx, rec, rr.y ? ~rr.x : 0u, rr.y, tx * GSR_TILE_PX + (w & 1) * 8,
-                      ty * GSR_TILE_PX + (w >> 1) * 8, lane, W, H, cover_w, cover_h, out,
-                      reinterpret_cast<float*>(sP[w]), dg);
-    if (STAMPS && lane == 0) atomicMax(counters + 2 * blockIdx.x + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    blend_block<DIAG>(idx, rec, rr.y ? ~rr.x : 0u, rr.y, tx * GSR_TILE_PX + (sub & 1) * 8,
+                      ty * GSR_TILE_PX + (sub >> 1) * 8, lane, W, H, cover_w, cover_h, out,
+                      reinterpret_cast<float*>(sP), dg);
+    if (STAMPS && lane == 0)
+        counters[2 * vb + 1] = ((__builtin_amdgcn_s_memrealtime() - t_start) & ((1ull << 40) - 1)) | (place << 40);
     if (DIAG && lane == 0) {
-        if (w == 0 && dg.loaded) atomicAdd(counters, (unsigned long long)dg.loaded);
+        if (sub == 0 && dg.loaded) atomicAdd(counters, (unsigned long long)dg.loaded);
         atomicAdd(counters + 1, (unsigned long long)dg.iter);
         atomicAdd(counters + 2, (unsigned long long)dg.active);
         atomicAdd(counters + 3, (unsigned long long)dg.taken);
         atomicAdd(counters + 4, (unsigned long long)dg.slow);
         atomicAdd(counters + 6, (unsigned long long)(dg.iter * 64));
-    }
-}
-
-// One-wave workgroups: workgroup g blends one 8x8 block, so a finished block
-// frees its wave slot at once (no waiting for the tile's other three waves).
-// Blocks are tile-major; the XCD-aware remap keeps a tile's four blocks (and
-// neighbouring tiles) on one XCD, i.e. one L2.
-template <bool DIAG, bool STAMPS = false, int WPG = 1>
-__global__ __launch_bounds__(64 * WPG) void k_blend_w(const uint32_t* __restrict__ idx,
-                                                       const uint2* __restrict__ ranges,
-                                                       const uint4* __restrict__ rec, int tiles_x, int tiles_y,
-                                                       int W, int H, int cover_w, int cover_h,
-                                                       float* __restrict__ out,
-                                                       unsigned long long* __restrict__ counters,
-                                                       const uint32_t* __restrict__ perm, int bands, int seq) {
-    // WPG waves per workgroup, one 8x8 block each (WPG = 2: the two blocks of a tile
-    // half; the waves never synchronise, only their dispatch is shared)
-    __shared__ float4 sP[WPG][32 * 20 / 4];
-    const int ntiles = tiles_x * tiles_y;
-    const int wv = (int)(threadIdx.x >> 6);
-    // seq > 1: the workgroup blends `seq` units of its XCD's stream one after the
-    // other (virtual workgroups vb = ((g / 8) * seq + j) * 8 + g % 8 keep g's XCD)
-    for (int j = 0; j < seq; j++) {
-        const int vb = (((int)blockIdx.x >> 3) * seq + j) * 8 + ((int)blockIdx.x & 7);
-        int tile, sub;
-        if (perm && bands > 1) {
-            // bands of `bands` tiles, heaviest first (k_tile_order over bands): XCD
-            // x = b & 7 takes band ranks x, x+8, ..., a band's blocks consecutive in its stream
-            const int bb = 4 * bands / WPG;                 // units per band
-            const int b = vb, k = b >> 3;
-            const int r = (k / bb) * 8 + (b & 7);
-            const int nbnd = (ntiles + bands - 1) / bands;
-            if (r >= nbnd) continue;
-            const int L = (int)perm[r] * 4 * bands + (k % bb) * WPG + wv;
-            if (L >= 4 * ntiles) continue;
-            tile = L >> 2;
-            sub = L & 3;
-        } else if (bands > 1) {
-            // each XCD (x = b & 7) takes `bands` spatial bands spread over the image:
-            // band j of B consecutive units goes to XCD j % 8 (balances the XCDs' work
-            // while keeping neighbouring blocks on one L2); padding workgroups exit
-            const int nu = 4 * ntiles / WPG;
-            const int B = (nu + 8 * bands - 1) / (8 * bands);
-            const int b = vb, k = b >> 3;
-            const int U = ((k / B) * 8 + (b & 7)) * B + k % B;
-            if (U >= nu) continue;
-            const int L = U * WPG + wv;
-            tile = L >> 2;
-            sub = L & 3;
-        } else if (perm) {
-            // longest tiles first (k_tile_order): XCD x = b & 7 takes tile ranks x, x+8, ...,
-            // each tile's four blocks consecutive in its stream (they share one L2)
-            const int b = vb, k = b >> 3;
-            const int r = (k >> 2) * 8 + (b & 7);
-            if (r >= ntiles) continue;
-            tile = (int)perm[r];
-            sub = k & 3;
-        } else {
-            if (vb >= ntiles * 4) continue;
-            const int b = xcd_remap(vb, ntiles * 4);
-            tile = b >> 2;
-            sub = b & 3;
-        }
-        const int tx = tile % tiles_x, ty = tile / tiles_x;
-        const int lane = (int)(threadIdx.x & 63u);
-        const int sid = vb * WPG + wv;     // stamp slot
-        uint64_t t_start = 0, place = 0;
-        if (STAMPS && lane == 0) {
-            // placement: XCC (3 bits) above HW_ID's SE / SH / CU / SIMD / wave slot (low 16 bits)
-            uint32_t hw, xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            place = ((uint64_t)(xcc & 7u) << 16) | (hw & 0xffffu);
-            t_start = __builtin_amdgcn_s_memrealtime();
-            counters[2 * sid] = t_start;
-        }
-        const uint2 rr = ranges[tile];
-        BlendDiag dg;
-        blend_block<DIAG>(idx, rec, rr.y ? ~rr.x : 0u, rr.y, tx * GSR_TILE_PX + (sub & 1) * 8,
-                          ty * GSR_TILE_PX + (sub >> 1) * 8, lane, W, H, cover_w, cover_h, out,
-                          reinterpret_cast<float*>(sP[wv]), dg);
-        // second word: duration (100 MHz ticks, 40 bits) | placement << 40
-        if (STAMPS && lane == 0) counters[2 * sid + 1] = ((__builtin_amdgcn_s_memrealtime() - t_start) & ((1ull << 40) - 1)) | (place << 40);
-        if (DIAG && lane == 0) {
-            if (sub == 0 && dg.loaded) atomicAdd(counters, (unsigned long long)dg.loaded);
-            atomicAdd(counters + 1, (unsigned long long)dg.iter);
-            atomicAdd(counters + 2, (unsigned long long)dg.active);
-            atomicAdd(counters + 3, (unsigned long long)dg.taken);
-            atomicAdd(counters + 4, (unsigned long long)dg.slow);
-            atomicAdd(counters + 6, (unsigned long long)(dg.iter * 64));
-        }
     }
 }
 
@@ -2687,19 +2215,6 @@ hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, 
     return hipGetLastError();
 }
 
-hipError_t launch_tile_depth_sort(const uint2* ranges, int ntiles, const uint64_t* items, uint32_t* vals,
-                                  uint64_t* scr_a, uint32_t* scr_keys, uint32_t* big_list, uint32_t* big_counts,
-                                  int parity, int big_groups, Stats* stats, Stats* host_mapped_stats,
-                                  hipStream_t s) {
-    if (ntiles < 0 || big_groups < 1 || (parity & ~1)) return hipErrorInvalidValue;
-    if (ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_tile_depth_sort_wave, dim3(ntiles), dim3(64), 0, s, ranges, items, vals, big_list,
-                       big_counts + parity);
-    hipLaunchKernelGGL(k_tile_depth_sort_big, dim3(big_groups), dim3(256), 0, s, ranges, items, vals, scr_a,
-                       scr_keys, big_list, big_counts, parity, stats, host_mapped_stats);
-    return hipGetLastError();
-}
-
 uint32_t bin_col_chunks_max(uint32_t pair_capacity, int tiles_y) {
     return pair_capacity / kColChunk + (uint32_t)tiles_y + 1u;
 }
@@ -2737,68 +2252,26 @@ hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* ke
 }
 
 hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
-                        float* out, unsigned long long* consumed, int variant, unsigned int* queue,
-                        int resident_groups, uint32_t* tile_perm, int band_tiles, int wpg, int seq,
-                        int lds_pad, hipStream_t s) {
+                        float* out, unsigned long long* consumed, bool stamps, int band_tiles, hipStream_t s) {
     const int nt = fr.tiles_x * fr.tiles_y;
     if (nt <= 0) return hipSuccess;
-    if (variant == 0 || variant == 3) {   // one wave per 8x8 block, wpg blocks per workgroup
-        // bands > 1: spread spatial bands over the XCDs (grid padded to whole bands);
-        // tile_perm: longest tiles first (grid rounded up to whole XCD rounds)
-        // band_tiles > 0: bands of that many tiles; with tile_perm heaviest band first,
-        // else dealt round-robin in image order.  band_tiles == 0: one contiguous band
-        // per XCD, or with tile_perm heaviest single tile first.
-        const int bt = band_tiles;
-        if (bt == 0) wpg = 1;
-        int ng, bands;
-        if (bt > 0 && tile_perm) {
-            bands = bt;                                      // kernel: tiles per band
-            const int nbnd = (nt + bt - 1) / bt;
-            ng = 8 * ((nbnd + 7) / 8) * (4 * bt / wpg);
-            hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ranges, nt, bt, tile_perm);
-        } else if (bt > 0 && (nt + 8 * bt - 1) / (8 * bt) > 1) {
-            bands = (nt + 8 * bt - 1) / (8 * bt);                // kernel: bands per XCD
-            const int nu = 4 * nt / wpg;
-            ng = 8 * bands * ((nu + 8 * bands - 1) / (8 * bands));
-        } else if (bt > 0) {                                     // image too small for bands
-            wpg = 1;
-            bands = 1;
-            ng = 4 * nt;                                         // xcd_remap covers exactly 4 nt blocks
-        } else {
-            bands = 1;
-            ng = tile_perm ? 4 * ((nt + 7) / 8 * 8) : 4 * nt;
-            if (tile_perm) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, ranges, nt, 1, tile_perm);
-        }
-        const uint32_t* pm = tile_perm;
-        // seq blocks per wave: grid = whole XCD rounds of ng / seq (virtual workgroups past
-        // ng exit: every mapping bounds-checks its unit)
-        const int sq = std::max(1, seq);
-        const int ngw = 8 * (((ng + 7) / 8 + sq - 1) / sq);   // >= 8: tiny frames have ng < 8
-#define GSR_BLEND_W(D, S, G)                                                                                 \
-    hipLaunchKernelGGL((k_blend_w<D, S, G>), dim3(ngw), dim3(64 * G), (size_t)lds_pad, s, idx, ranges, rec, fr.tiles_x, \
-                       fr.tiles_y, \
-                       fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, pm, bands, sq)
-        if (wpg == 2) {
-            if (variant == 3 && consumed) GSR_BLEND_W(false, true, 2);
-            else if (consumed) GSR_BLEND_W(true, false, 2);
-            else GSR_BLEND_W(false, false, 2);
-        } else {
-            if (variant == 3 && consumed) GSR_BLEND_W(false, true, 1);
-            else if (consumed) GSR_BLEND_W(true, false, 1);
-            else GSR_BLEND_W(false, false, 1);
-        }
-#undef GSR_BLEND_W
-        return hipGetLastError();
+    // bands of band_tiles tiles (4 blocks each) dealt round-robin to the 8 XCDs; the
+    // grid is padded to whole rounds of bands.  Images too small for two rounds:
+    // one contiguous run per XCD.
+    int bands = 1, ng = 4 * nt;
+    if (band_tiles > 0 && (nt + 8 * band_tiles - 1) / (8 * band_tiles) > 1) {
+        bands = (nt + 8 * band_tiles - 1) / (8 * band_tiles);          // bands per XCD
+        ng = 8 * bands * ((4 * nt + 8 * bands - 1) / (8 * bands));
     }
-    if (variant == 2 && consumed)   // timestamps into consumed[2 * nt] (diagnostics)
-        hipLaunchKernelGGL((k_blend<false, true>), dim3(nt), dim3(256), 0, s, idx, ranges, rec, fr.tiles_x,
-                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
+    if (stamps && consumed)
+        hipLaunchKernelGGL((k_blend_w<false, true>), dim3(ng), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,
+                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, bands);
     else if (consumed)
-        hipLaunchKernelGGL(k_blend<true>, dim3(nt), dim3(256), 0, s, idx, ranges, rec, fr.tiles_x, fr.tiles_y,
-                           fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
+        hipLaunchKernelGGL((k_blend_w<true, false>), dim3(ng), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,
+                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, bands);
     else
-        hipLaunchKernelGGL(k_blend<false>, dim3(nt), dim3(256), 0, s, idx, ranges, rec, fr.tiles_x, fr.tiles_y,
-                           fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed);
+        hipLaunchKernelGGL((k_blend_w<false, false>), dim3(ng), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,
+                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, bands);
     return hipGetLastError();
 }
 

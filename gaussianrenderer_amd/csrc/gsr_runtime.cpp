@@ -345,21 +345,9 @@ struct gsr_context {
     uint32_t* cbins = nullptr;       // binning: column counts per chunk (256 x chunks)
     int64_t cbins_cap = 0;
     bool last_binned = false;        // the last sorted frame took the binning path
-    int blend_tile_order = 0;        // 1: blend the longest tiles first (k_tile_order), 0: spatial order
-    int blend_seq = 1;               // blend: 8x8 blocks each wave blends one after the other
-    int blend_lds_pad = 0;           // blend: extra LDS bytes per workgroup (caps waves per CU)
-    int blend_wpg = 1;               // blend: 8x8 blocks (waves) per workgroup, 1 | 2 (band layout only)
     int blend_band_tiles = 4;        // blend: tiles per spatial band, bands dealt round-robin to the
                                      // XCDs (0: one contiguous band per XCD)
-    uint32_t* tile_perm = nullptr;   // blend tile permutation (t_cap)
-    uint32_t* big_list = nullptr;    // per-tile depth order: tiles with lists over one wave's cap (t_cap)
-    uint32_t* big_counts = nullptr;  // their count, one word per frame parity
-    int tds_parity = 0;              // parity of the next per-tile depth-order frame
     int completion_events = 1;       // 0: no completion event / overflow query (stream capture)
-    int depth_order = 0;             // binning path: 0 = global depth sort, 1 = per-tile depth sort
-    bool last_tile_order = false;    // the last sorted frame used the per-tile depth sort
-    unsigned int* queue = nullptr;   // spare device counters (blend experiments)
-    int resident_groups = 2048;      // workgroups of 256 that fit on the device at once
     // frame state
     Frame fr{};
     int64_t n = 0;
@@ -413,18 +401,9 @@ int ensure_static(gsr_context* c) {
     if (int rc = realloc_dev(&c->totals, 256)) return rc;
     if (int rc = realloc_dev(&c->wg, (size_t)gsr::kMaxSortGroups)) return rc;
     if (int rc = realloc_dev(&c->stats, 2)) return rc;
-    if (int rc = realloc_dev(&c->queue, 8)) return rc;
     if (int rc = realloc_dev(&c->dstats, 4 + 4 * (size_t)gsr::kMaxSortGroups)) return rc;
     if (int rc = realloc_dev(&c->nlive, 1)) return rc;
     if (int rc = realloc_dev(&c->binmeta, 256 + 128)) return rc;
-    if (int rc = realloc_dev(&c->big_counts, 2)) return rc;
-    HIP_TRY(hipMemset(c->big_counts, 0, 2 * sizeof(uint32_t)));
-    {
-        int dev = 0, cus = 0;
-        HIP_TRY(hipGetDevice(&dev));
-        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        c->resident_groups = std::max(8, cus * 8);      // 8 workgroups of 4 waves per CU (VGPR-limited)
-    }
     HIP_TRY(hipMemset(c->stats, 0, 2 * sizeof(Stats)));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->hstats), sizeof(Stats), hipHostMallocMapped));
     std::memset(c->hstats, 0, sizeof(Stats));
@@ -466,8 +445,6 @@ int ensure_tiles(gsr_context* c, int64_t t) {
     if (t <= c->t_cap) return GSR_OK;
     HIP_TRY(hipDeviceSynchronize());
     if (int rc = realloc_dev(&c->ranges, (size_t)t)) return rc;
-    if (int rc = realloc_dev(&c->tile_perm, (size_t)t)) return rc;
-    if (int rc = realloc_dev(&c->big_list, (size_t)t)) return rc;
     c->t_cap = t;
     return GSR_OK;
 }
@@ -573,9 +550,9 @@ extern "C" void gsr_destroy(gsr_context* c) {
     for (auto e : c->alias_evs) (void)hipEventDestroy(e);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     for (auto* p : {(void*)c->rec, (void*)c->items[0], (void*)c->items[1], (void*)c->rect, (void*)c->pairs[0],
-                    (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->queue, (void*)c->dstats,
+                    (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->dstats,
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
-                    (void*)c->cbins, (void*)c->srect, (void*)c->tile_perm, (void*)c->big_list, (void*)c->big_counts, (void*)c->nlive})
+                    (void*)c->cbins, (void*)c->srect, (void*)c->nlive})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -628,7 +605,7 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     // live partition (global depth sort on the binning path): the items go to
     // items[1] and the partition writes the visible-first order into items[0]
     c->compact_frame = n > 0 && (c->depth_compact == 1 || (c->depth_compact == 2 && layout == GSR_LAYOUT_SCENE_BLOCK_4D)) &&
-                       c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256 && c->depth_order == 0;
+                       c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
     HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[c->compact_frame ? 1 : 0], c->rect,
                                    layout == GSR_LAYOUT_SCENE_BLOCK_4D, layout == GSR_LAYOUT_SCENE_BLOCK_SH3, c->time,
                                    c->stream));
@@ -682,35 +659,9 @@ static int sort_locked(gsr_context* c) {
     const uint32_t n = (uint32_t)c->n;
     const bool bin = c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
     c->last_binned = bin;
-    // per-tile depth order (knob): bin in index order, then sort each tile's list by depth
-    const bool per_tile = bin && c->depth_order == 1;
-    c->last_tile_order = per_tile;
-    if (c->compact_frame && (!bin || per_tile)) {   // knobs changed since gsr_preprocess
+    if (c->compact_frame && !bin) {   // knobs changed since gsr_preprocess
         HIP_TRY(hipMemcpyAsync(c->items[0], c->items[1], (size_t)n * 8, hipMemcpyDeviceToDevice, c->stream));
         c->compact_frame = false;
-    }
-    if (per_tile) {
-        if (int rc = ensure_cbins(c)) return rc;
-        auto* row_pairs = reinterpret_cast<unsigned long long*>(c->binmeta);
-        auto* row_items = reinterpret_cast<uint32_t*>(c->binmeta + 256);
-        const uint32_t cap = (uint32_t)c->p_cap;
-        const int gb = std::min(groups_for(c->n, 1024), gsr::kMaxSortGroups / 2);
-        mark(c, GSR_STAGE_EMIT);
-        HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], nullptr, n, c->rect, gb, c->hist, row_items,
-                                     row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items, c->stream));
-        mark(c, GSR_STAGE_TILE_SORT);
-        HIP_TRY(gsr::launch_bin_cols(c->pairs[0], row_items, row_pairs, c->cbins, c->bin_col_groups, cap,
-                                     c->fr.tiles_x, c->fr.tiles_y, pair_vals(c, 1), c->ranges, c->stats,
-                                     c->hstats_dev, c->bin_col_items, c->stream));
-        mark(c, GSR_STAGE_DEPTH_SORT);
-        HIP_TRY(gsr::launch_tile_depth_sort(c->ranges, c->ntiles, c->items[0], pair_vals(c, 1), c->pairs[0],
-                                            reinterpret_cast<uint32_t*>(pair_keys(c, 1)), c->big_list,
-                                            c->big_counts, c->tds_parity, std::min(c->ntiles, 1024), c->stats,
-                                            c->hstats_dev, c->stream));
-        c->tds_parity ^= 1;
-        c->pair_buf = 1;
-        c->have_sort = true;
-        return GSR_OK;
     }
     // ---- stable depth sort of (key << 32 | index), 4 x 8 bits; for the binning
     // path its last pass also writes the rects in depth order (srect) ----
@@ -773,10 +724,9 @@ static int blend_locked(gsr_context* c, float* d_out) {
     if (!d_out) return set_err(GSR_E_ARG, "null output");
     mark(c, GSR_STAGE_BLEND);
     if (c->diagnostics) {
-        // counters (8) or, for the timestamp schedule, 2 stamps per tile
-        const int64_t need = c->blend_variant == 2   ? std::max<int64_t>(8, 2 * (int64_t)c->ntiles)
-                             : c->blend_variant == 3 ? 12 * (int64_t)c->ntiles + 64   // >= 2 x the padded grid
-                                                     : 8;
+        // counters (8) or, for the timestamp schedule, 2 stamps per wave
+        const int64_t need = c->blend_variant == 3 ? 12 * (int64_t)c->ntiles + 64   // >= 2 x the padded grid
+                                                   : 8;
         if (c->consumed_cap < need) {
             if (int rc = realloc_dev(&c->consumed, (size_t)need)) return rc;
             c->consumed_cap = need;
@@ -784,9 +734,8 @@ static int blend_locked(gsr_context* c, float* d_out) {
         HIP_TRY(hipMemsetAsync(c->consumed, 0, (size_t)need * sizeof(unsigned long long), c->stream));
     }
     HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
-                              c->diagnostics ? c->consumed : nullptr, c->blend_variant, c->queue,
-                              c->resident_groups, c->blend_tile_order ? c->tile_perm : nullptr,
-                              c->blend_band_tiles, c->blend_wpg, c->blend_seq, c->blend_lds_pad, c->stream));
+                              c->diagnostics ? c->consumed : nullptr, c->blend_variant == 3,
+                              c->blend_band_tiles, c->stream));
     mark(c, GSR_NUM_STAGES);
     if (c->timing && c->timing_now) c->ev_frames.push_back(c->cur);
     c->cur = FrameEvents{};
@@ -840,7 +789,6 @@ namespace {
 // Everything that selects kernels or schedules (all settings are bit-identical);
 // diagnostics and timing stay on lane 0 only.
 void copy_settings(gsr_context* d, const gsr_context* s) {
-    d->blend_variant = s->blend_variant == 2 || s->blend_variant == 3 ? 0 : s->blend_variant;
     d->tile_items = s->tile_items;
     d->depth_items = s->depth_items;
     d->tile_groups = s->tile_groups;
@@ -851,13 +799,8 @@ void copy_settings(gsr_context* d, const gsr_context* s) {
     d->bin_row_items = s->bin_row_items;
     d->bin_col_items = s->bin_col_items;
     d->bin_col_groups = s->bin_col_groups;
-    d->blend_tile_order = s->blend_tile_order;
-    d->blend_wpg = s->blend_wpg;
     d->blend_band_tiles = s->blend_band_tiles;
     d->completion_events = s->completion_events;
-    d->depth_order = s->depth_order;
-    d->blend_seq = s->blend_seq;
-    d->blend_lds_pad = s->blend_lds_pad;
     d->depth_compact = s->depth_compact;
 }
 
@@ -1039,7 +982,7 @@ extern "C" int gsr_read_splats(gsr_context* c, void* host, int64_t n) {
     HIP_TRY(hipMemcpy(host, c->rec, (size_t)n * GSR_SPLAT_RECORD_BYTES, hipMemcpyDeviceToHost));
     std::vector<uint64_t> rect((size_t)n), items((size_t)c->n);
     HIP_TRY(hipMemcpy(rect.data(), c->rect, (size_t)n * 8, hipMemcpyDeviceToHost));
-    if (c->have_sort && !c->last_tile_order) {
+    if (c->have_sort) {
         if (int rc = sorted_items_locked(c, items.data(), c->n)) return rc;
     } else {   // preprocess order (items[1] when the frame is set up for the live partition)
         HIP_TRY(hipMemcpy(items.data(), c->items[c->compact_frame && !c->have_sort ? 1 : 0], (size_t)c->n * 8,
@@ -1103,7 +1046,6 @@ static int sorted_items_locked(gsr_context* c, uint64_t* host, int64_t n) {
 extern "C" int gsr_depth_passes(gsr_context* c) {
     if (!c || !c->have_sort) return set_err(GSR_E_ARG, "gsr_depth_passes: no sorted frame");
     std::lock_guard<std::mutex> lk(c->mu);
-    if (c->last_tile_order) return 0;   // per-tile depth order: no global passes ran
     HIP_TRY(hipStreamSynchronize(c->stream));
     int p = 4;
     if (int rc = depth_passes_locked(c, &p)) return rc;
@@ -1113,14 +1055,6 @@ extern "C" int gsr_depth_passes(gsr_context* c) {
 extern "C" int gsr_read_depth_order(gsr_context* c, uint64_t* host, int64_t n) {
     if (!c || !host || n < 0 || n > c->n || !c->have_sort) return set_err(GSR_E_ARG, "gsr_read_depth_order: bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
-    if (c->last_tile_order) {
-        // per-tile depth order: the frame never sorted globally; sort its preprocess
-        // items now (same kernels and plan as the global path; the frame's tile
-        // lists are already final, and items are not read after the frame)
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        if (int rc = depth_sort_locked(c, false)) return rc;
-        c->last_tile_order = false;
-    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     return sorted_items_locked(c, host, n);
 }
@@ -1234,7 +1168,8 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     std::lock_guard<std::mutex> lk(c->mu);
     switch (knob) {
     case GSR_TUNE_BLEND_SCHEDULE:
-        if (value < 0 || value > 3) return set_err(GSR_E_ARG, "gsr_set_tuning: blend schedule must be 0..3");
+        if (value != 0 && value != 3)
+            return set_err(GSR_E_ARG, "gsr_set_tuning: blend schedule must be 0 (default) or 3 (timeline stamps)");
         c->blend_variant = value;
         return GSR_OK;
     case GSR_TUNE_TILE_SORT_ITEMS:
@@ -1255,17 +1190,6 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
             return set_err(GSR_E_ARG, "gsr_set_tuning: binning items per thread must be 4, 8 or 16");
         (knob == GSR_TUNE_BIN_ROW_ITEMS ? c->bin_row_items : c->bin_col_items) = value;
         return GSR_OK;
-    case GSR_TUNE_BLEND_TILE_ORDER:
-        c->blend_tile_order = value != 0;
-        return GSR_OK;
-    case GSR_TUNE_BLEND_WAVES_PER_GROUP:
-        if (value != 1 && value != 2) return set_err(GSR_E_ARG, "gsr_set_tuning: blend waves per group must be 1 or 2");
-        c->blend_wpg = value;
-        return GSR_OK;
-    case GSR_TUNE_DEPTH_ORDER:
-        if (value < 0 || value > 1) return set_err(GSR_E_ARG, "gsr_set_tuning: depth order must be 0 or 1");
-        c->depth_order = value;
-        return GSR_OK;
     case GSR_TUNE_BLEND_BAND_TILES:
         if (value < 0 || value > 65536) return set_err(GSR_E_ARG, "gsr_set_tuning: blend band tiles must be 0..65536");
         c->blend_band_tiles = value;
@@ -1280,14 +1204,6 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     case GSR_TUNE_DEPTH_COMPACT:
         if (value < 0 || value > 2) return set_err(GSR_E_ARG, "gsr_set_tuning: depth compaction must be 0, 1 or 2");
         c->depth_compact = value;
-        return GSR_OK;
-    case GSR_TUNE_BLEND_LDS_PAD:
-        if (value < 0 || value > 32768) return set_err(GSR_E_ARG, "gsr_set_tuning: blend LDS pad must be 0..32768 bytes");
-        c->blend_lds_pad = value;
-        return GSR_OK;
-    case GSR_TUNE_BLEND_BLOCKS_PER_WAVE:
-        if (value < 1 || value > 64) return set_err(GSR_E_ARG, "gsr_set_tuning: blend blocks per wave must be 1..64");
-        c->blend_seq = value;
         return GSR_OK;
     case GSR_TUNE_DEPTH_SORT_SKIP:
         c->depth_skip = value != 0;
@@ -1307,8 +1223,8 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
 
 extern "C" int gsr_set_blend_variant(gsr_context* c, int variant) {
     if (!c) return set_err(GSR_E_ARG, "null context");
-    if (variant < 0 || variant > 3)
-        return set_err(GSR_E_ARG, "gsr_set_blend_variant: variant must be 0..3");
+    if (variant != 0 && variant != 3)
+        return set_err(GSR_E_ARG, "gsr_set_blend_variant: variant must be 0 (default) or 3 (timeline stamps)");
     std::lock_guard<std::mutex> lk(c->mu);
     c->blend_variant = variant;
     return GSR_OK;

@@ -66,9 +66,7 @@ enum {
 /* Stage indices for gsr_stage_times(). */
 enum {
     GSR_STAGE_PREPROCESS = 0,     /* cull + SH colour + projection + covariance + AABB */
-    GSR_STAGE_DEPTH_SORT = 1,     /* stable radix sort of (depth, index); per-tile depth order
-                                     (GSR_TUNE_DEPTH_ORDER): each tile's list sorted by depth,
-                                     which runs after the two binning passes */
+    GSR_STAGE_DEPTH_SORT = 1,     /* stable radix sort of (depth, index) */
     GSR_STAGE_EMIT = 2,           /* pair emission, or the binning row pass */
     GSR_STAGE_TILE_SORT = 3,      /* stable radix sort of pairs by tile, or the binning column pass */
     GSR_STAGE_RANGES = 4,         /* per-tile [start, end) from sorted pairs */
@@ -222,13 +220,11 @@ int64_t gsr_blend_records_loaded(gsr_context* ctx);
  * (64 x pixels per lane x iterations), 0};
  * lane efficiency = active / slots. */
 int gsr_blend_counters(gsr_context* ctx, int64_t* out8);
-/* Blend schedule (tuning knob for A/B experiments, tools/ab_blend.py):
- * 0 = one 64-thread workgroup per 8x8 pixel block (default); 1 = one
- * 256-thread workgroup per 16x16 tile (four blocks); 2 = schedule 1 with
- * per-workgroup timestamps, 3 = schedule 0 with per-workgroup timestamps (see
- * gsr_blend_stamps; diagnostics frames only).  Every schedule culls each
- * 64-record batch against its block, compacts the survivors into LDS pair
- * slots and composites two splats per iteration; all are bit-identical. */
+/* Blend schedule: 0 = one 64-thread workgroup per 8x8 pixel block (the
+ * kernel); 3 = the same with per-wave timestamps instead of counters (see
+ * gsr_blend_stamps; diagnostics frames only).  Other values are refused (the
+ * tile-per-workgroup schedule, longest-tiles-first, several blocks per wave or
+ * workgroup and LDS-capped occupancy were measured slower and removed). */
 int gsr_set_blend_variant(gsr_context* ctx, int variant);
 /* Tuning knobs for A/B experiments (all settings give bit-identical output). */
 enum {
@@ -246,31 +242,23 @@ enum {
     GSR_TUNE_BIN_COL_GROUPS = 10,    /* binning column pass: workgroups (default 1024) */
     GSR_TUNE_COMPLETION_EVENTS = 11, /* 1 (default): a completion event feeds the non-blocking overflow
                                         check; 0: none (frames captured into a graph; call gsr_sync) */
-    GSR_TUNE_BLEND_TILE_ORDER = 12,  /* blend schedule 0: 1 = longest tiles first, 0 = spatial (default) */
+    /* 12 reserved (removed: longest tiles first) */
     GSR_TUNE_BLEND_BAND_TILES = 13,  /* blend schedule 0: tiles per spatial band, bands dealt round-robin
                                         to the 8 XCDs (default 4); 0 = one contiguous band per XCD */
-    GSR_TUNE_BLEND_WAVES_PER_GROUP = 14, /* blend schedule 0 with bands: 8x8 blocks per workgroup, 1 | 2 */
-    GSR_TUNE_DEPTH_ORDER = 15,       /* tile binning path: 0 (default) = global depth sort before binning;
-                                        1 = bin in index order, then sort every tile's list by depth (one
-                                        wave per list <= 1024, a workgroup per longer list, lists over 4096
-                                        chunked through global scratch); same pairs, same image */
-    GSR_TUNE_BLEND_BLOCKS_PER_WAVE = 16, /* blend schedule 0: 8x8 blocks each wave blends one after the other
-                                        (default 1); same blocks, same image */
-    GSR_TUNE_BLEND_LDS_PAD = 17,     /* blend schedule 0: extra LDS bytes reserved per blend workgroup
-                                        (0..32768, default 0): caps the blend's waves per CU, leaving
-                                        slots to other frames' kernels in flight; same image */
+    /* 14-17 reserved (removed, all measured slower: two blocks per workgroup, per-tile depth
+       order after index-order binning (config 3: 1.53 ms vs 0.24 ms), several blocks per wave,
+       LDS-capped blend occupancy) */
     GSR_TUNE_DEPTH_COMPACT = 18      /* global depth sort on the binning path: 1 = stable partition of the
                                         visible Gaussians first, the passes sort only those; 0 = sort all;
                                         2 (default) = partition for 4D scenes only; same order, same image */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Depth-sort digit passes the last sorted frame ran (1..4; trailing identity
- * passes are skipped on the device; 0 when the frame used the per-tile depth
- * order, GSR_TUNE_DEPTH_ORDER), or a negative error code. */
+ * passes are skipped on the device), or a negative error code. */
 int gsr_depth_passes(gsr_context* ctx);
-/* Schedule 2 = schedule 0 with per-workgroup timestamps instead of counters:
- * with diagnostics on, the last frame's blend stores {start, end} of the
- * 100 MHz s_memrealtime clock per workgroup (launch order); read n values. */
+/* Schedule 3: with diagnostics on, the last frame's blend stores per wave
+ * (launch order) {start of the 100 MHz s_memrealtime clock, duration (40 bits) |
+ * placement << 40 (XCC id, HW_ID)}; read n values. */
 int gsr_blend_stamps(gsr_context* ctx, uint64_t* out, int64_t n);
 
 /* ---------------------------------------------------------------- scenes */

@@ -151,35 +151,11 @@ def test_image_config1_parity(gpu, orc, torch, c1, ci):
     assert_image_parity(got, want)
 
 
-@pytest.mark.parametrize("ci", [0, 2])
-def test_blend_tile_schedule_parity(gpu, orc, torch, c1, ci):
-    """The tile-per-workgroup blend (schedule 1) is bit-exact vs the oracle,
-    including tiny frames, partial coverage and
-    sizes that are not multiples of the 8x8 blocks."""
-    path, soa = c1
-    scene = gpu.Scene.from_soa(soa)
-    for W, H, tiling in ((640, 480, None), (37, 23, None), (1, 1, None), (640, 480, (7, 3, 92, 160))):
-        cam = cam_for(gpu, W, H, **CAMS[ci])
-        r = gpu.Renderer()
-        r.set_blend_variant(1)
-        t = None
-        if tiling is not None:
-            t = gpu.TilingInformation(1, 1, H, W)
-            t.num_tile_x, t.num_tile_y, t.width_stride, t.height_stride = tiling
-        got, _ = render_gpu(gpu, torch, scene, cam, W, H, tiling=t, renderer=r)
-        want = orc.render(soa, cam, W, H, 3.0, tiling=tiling)
-        assert_image_parity(got, want)
-
-
-@pytest.mark.parametrize("knobs", [{13: 0}, {13: 0, 12: 1}, {13: 1}, {13: 4, 14: 2}, {13: 4, 12: 1},
-                                   {13: 5, 12: 1, 14: 2}, {13: 64}, {16: 2}, {13: 0, 16: 3},
-                                   {13: 4, 12: 1, 16: 4}, {13: 5, 14: 2, 16: 3}, {17: 4096},
-                                   {13: 0, 17: 32768}])
+@pytest.mark.parametrize("knobs", [{}, {13: 0}, {13: 1}, {13: 64}])
 def test_blend_block_mappings_parity(gpu, orc, torch, c1, knobs):
-    """Every block-to-workgroup mapping of the default blend schedule is bit-exact vs
-    the oracle: 13 = tiles per band (0: one contiguous band per XCD), 12 = heaviest
-    first, 14 = blocks per workgroup, 16 = blocks each wave blends in turn, 17 = LDS pad; frames
-    small enough to fall back to one band."""
+    """Every block-to-workgroup mapping of the blend is bit-exact vs the oracle:
+    13 = tiles per band (default 4; 0: one contiguous run per XCD), including frames
+    small enough to fall back to one run per XCD.  The removed knobs are refused."""
     path, soa = c1
     scene = gpu.Scene.from_soa(soa)
     for W, H in ((640, 480), (333, 217), (37, 23), (1, 1)):
@@ -189,9 +165,16 @@ def test_blend_block_mappings_parity(gpu, orc, torch, c1, knobs):
             r.set_tuning(kn, v)
         got, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
         assert_image_parity(got, orc.render(soa, cam, W, H, 3.0))
+    r = gpu.Renderer()
+    for kn in (12, 14, 15, 16, 17):
+        with pytest.raises(gpu.GsrError):
+            r.set_tuning(kn, 1)
+    for v in (1, 2):
+        with pytest.raises(gpu.GsrError):
+            r.set_blend_variant(v)
 
 
-@pytest.mark.parametrize("knobs", [{}, {8: 4, 9: 16}, {8: 16, 9: 4, 10: 7}, {15: 1}, {15: 1, 8: 16, 10: 7}])
+@pytest.mark.parametrize("knobs", [{}, {8: 4, 9: 16}, {8: 16, 9: 4, 10: 7}])
 def test_tile_binning_matches_pair_sort(gpu, orc, torch, c1, knobs):
     """Row + column binning (default for grids <= 256 x 256 tiles) gives the same
     tile lists as pair emission + the key-value tile sort: identical (tile,
@@ -266,7 +249,6 @@ def test_depth_pass_plan_exact(gpu, orc, torch, c1, pos, look):
     orders = []
     for skip in (1, 0):
         r = gpu.Renderer()
-        r.set_tuning(15, 0)      # global depth sort (the per-tile order has no passes to plan)
         r.set_tuning(6, skip)
         got, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
         assert_image_parity(got, orc.render(soa, cam, W, H, 3.0))
@@ -301,9 +283,8 @@ def test_blend_slow_path_and_degenerate_records(gpu, orc, torch, c1):
     W, H = 640, 480
     cam = cam_for(gpu, W, H)
     want = orc.render(s, cam, W, H, 3.0)
-    for variant in (0, 1):
+    for _ in range(1):
         r = gpu.Renderer()
-        r.set_blend_variant(variant)
         got, _ = render_gpu(gpu, torch, gpu.Scene.from_soa(s), cam, W, H, renderer=r)
         assert_image_parity(got, want)
         r.set_diagnostics(True)

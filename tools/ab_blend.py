@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Interleaved A/B timing of the blend schedules (gsr_set_blend_variant) in ONE
+"""Interleaved A/B timing of blend builds / schedules (gsr_set_blend_variant: 0, or 3
+with timeline stamps) in ONE
 process on one scene: every round renders K frames per variant (HIP events
 around each blend launch), so clock/thermal drift hits all variants alike.
 Also checks that every variant's image is bit-identical to variant 0's and

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Blend workgroup timeline (per-workgroup s_memrealtime stamps: schedule 2 =
-the tile-per-workgroup kernel, schedule 3 = the default block-per-workgroup one).
+"""Blend workgroup timeline (per-wave s_memrealtime stamps of the one-wave-per-
+8x8-block kernel, blend schedule 3).
 
 Reports the kernel span, the workgroup-duration distribution, how many
 workgroups were in flight over time, and the share of the span spent in the
@@ -25,8 +25,7 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--orbit", type=float, default=0.0)
     ap.add_argument("--resident", type=int, default=2048, help="workgroups the device holds at once")
-    ap.add_argument("--schedule", type=int, default=2, choices=(2, 3))
-    ap.add_argument("--tile-order", type=int, default=None, help="schedule 3: GSR_TUNE_BLEND_TILE_ORDER value")
+    ap.add_argument("--schedule", type=int, default=3, choices=(3,))
     ap.add_argument("--band-tiles", type=int, default=None, help="schedule 3: GSR_TUNE_BLEND_BAND_TILES value")
     args = ap.parse_args()
     import numpy as np
@@ -50,8 +49,6 @@ def main():
         r.render(scene, cam, W, H, out.data_ptr())
     r.sync()
     r.set_blend_variant(args.schedule)
-    if args.tile_order is not None:
-        r.set_tuning(12, args.tile_order)
     if args.band_tiles is not None:
         r.set_tuning(13, args.band_tiles)
     r.set_diagnostics(True)
