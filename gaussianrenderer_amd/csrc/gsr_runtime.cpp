@@ -340,7 +340,8 @@ struct gsr_context {
     int tile_binning = 1;            // row + column binning instead of emit + tile sort (grids <= 256 x 256)
     int bin_row_items = 4;           // binning: items per thread of a row-pass tile (4 | 8 | 16)
     int bin_col_items = 8;           // binning: items per thread of a column-pass tile (4 | 8 | 16)
-    int bin_col_groups = 1024;       // binning: column-pass workgroups (chunks are strided over them)
+    int bin_col_groups = 0;          // binning: column-pass workgroups (chunks are strided over them);
+                                     // 0 = by scene size (n / 1024 clamped to 1024..4096)
     uint64_t* binmeta = nullptr;     // binning: row pair totals (u64 x 256) then row item totals (u32 x 256)
     uint32_t* cbins = nullptr;       // binning: column counts per chunk (256 x chunks)
     int64_t cbins_cap = 0;
@@ -680,7 +681,11 @@ static int sort_locked(gsr_context* c) {
                                      c->hist, row_items, row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items,
                                      c->stream));
         mark(c, GSR_STAGE_TILE_SORT);
-        HIP_TRY(gsr::launch_bin_cols(c->pairs[0], row_items, row_pairs, c->cbins, c->bin_col_groups, cap,
+        // column-pass workgroups: ~one 2048-item chunk each (config 3: 2048-4096 groups 12 us
+        // faster than 1024; config 2: 1024 best, profiles/r02_ab_col_groups.txt)
+        const int gcol = c->bin_col_groups ? c->bin_col_groups
+                                           : (int)std::min<int64_t>(4096, std::max<int64_t>(1024, c->n / 1024));
+        HIP_TRY(gsr::launch_bin_cols(c->pairs[0], row_items, row_pairs, c->cbins, gcol, cap,
                                      c->fr.tiles_x, c->fr.tiles_y, pair_vals(c, 1), c->ranges, c->stats,
                                      c->hstats_dev, c->bin_col_items, c->stream));
         c->pair_buf = 1;
@@ -1198,7 +1203,7 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         c->completion_events = value != 0;
         return GSR_OK;
     case GSR_TUNE_BIN_COL_GROUPS:
-        if (value < 1 || value > 65536) return set_err(GSR_E_ARG, "gsr_set_tuning: bad column-pass group count");
+        if (value < 0 || value > 65536) return set_err(GSR_E_ARG, "gsr_set_tuning: bad column-pass group count");
         c->bin_col_groups = value;
         return GSR_OK;
     case GSR_TUNE_DEPTH_COMPACT:

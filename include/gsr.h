@@ -239,7 +239,8 @@ enum {
                                         0 = pair emission + key-value tile sort */
     GSR_TUNE_BIN_ROW_ITEMS = 8,      /* binning row pass: items per thread per tile 4 | 8 | 16 (default 4) */
     GSR_TUNE_BIN_COL_ITEMS = 9,      /* binning column pass: items per thread per tile 4 | 8 | 16 (default 8) */
-    GSR_TUNE_BIN_COL_GROUPS = 10,    /* binning column pass: workgroups (default 1024) */
+    GSR_TUNE_BIN_COL_GROUPS = 10,    /* binning column pass: workgroups (default 0 = n / 1024 clamped
+                                        to 1024..4096) */
     GSR_TUNE_COMPLETION_EVENTS = 11, /* 1 (default): a completion event feeds the non-blocking overflow
                                         check; 0: none (frames captured into a graph; call gsr_sync) */
     /* 12 reserved (removed: longest tiles first) */
