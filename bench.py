@@ -44,7 +44,7 @@ TIMESTEPS_4D = 120
 TIMING_STRIDE = 8
 STAGE_FRAMES = 10     # untimed frames averaged for stages_ms
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
-BLEND_KERNEL = "k_blend_w<false, false, 1>"   # default blend schedule (one 64-thread workgroup per 8x8 block)
+BLEND_KERNEL = "k_blend_w<false, false>"   # the blend (one 64-thread workgroup per 8x8 block)
 
 
 def parse():

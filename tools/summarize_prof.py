@@ -23,7 +23,7 @@ import sys
 # requests tallied at 64 B (x2, the guide's correction); scattered 64-B record
 # gathers (the blend's splat records, 48 or 64 B of a 64-B record per lane) issue
 # one 64-B request each and are counted exactly (x1).
-GATHER_KERNELS = ("k_blend_w", "k_blend<")
+GATHER_KERNELS = ("k_blend_w",)
 
 
 def fetch_factor(kernel: str) -> float:
