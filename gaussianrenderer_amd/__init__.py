@@ -410,7 +410,7 @@ class Renderer:
         v = np.zeros(8, dtype=np.int64)
         check(lib().gsr_blend_counters(self.ctx, v.ctypes.data), "gsr_blend_counters")
         keys = ("records_loaded", "wave_splat_iters", "active_lanes", "taken_lanes", "slow_path_iters",
-                "iters_skipped_cutoff", "lane_slots")
+                "zero_taken_iters", "lane_slots", "no_candidate_pair_iters")
         return dict(zip(keys, (int(x) for x in v)))
 
     def set_blend_variant(self, variant: int):

@@ -47,8 +47,8 @@ struct Stats {
 hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, int64_t stride,
                              hipStream_t s);
 hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
-                             uint4* rec, uint64_t* items, uint64_t* rect, bool four_d, bool sh3, float t,
-                             hipStream_t s);
+                             uint4* rec, uint64_t* items, uint64_t* rect, bool packed, bool four_d, bool sh3,
+                             float t, hipStream_t s);
 // One stable LSD pass over u64 items on bits [shift, shift + bits) (bits <= 8).
 // n = n_dev ? *n_dev : n_host.  hist: 256 * groups u32, totals: 256 u32.
 // ranges (nullable, final tile-sort pass): per-tile {~start, end} of key (item >> 32),
@@ -59,7 +59,8 @@ hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, con
 hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
                              int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
                              uint2* ranges, hipStream_t s, uint32_t* dstats = nullptr, int pass = 0,
-                             const uint64_t* rect = nullptr, uint64_t* srect = nullptr);
+                             const uint32_t* rect = nullptr, int rect_direct = 0, uint32_t* pay0 = nullptr,
+                             uint32_t* pay1 = nullptr);
 // Pair emission in depth order: tile counts (gathering each Gaussian's rect
 // once into srect, and zeroing the tile ranges), scan, then keys (uint16_t if
 // key16 else uint32_t) + values.
@@ -82,13 +83,14 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
 // index order), visible count into *n_live; culled tail to out only, with dead
 // rects in srect (gsr_kernels.hip "live partition").  counts: groups words.
 hipError_t launch_partition(const uint64_t* in, uint32_t n, int groups, uint32_t* counts, uint32_t* n_live,
-                            uint64_t* out, uint64_t* srect, hipStream_t s);
+                            uint64_t* out, const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, hipStream_t s);
 // Tile binning (row pass + column pass, tile grids <= 256 x 256): replaces
 // launch_emit + the key-value tile sort.  hist: 512 x groups; row_items /
 // row_pairs: 256 each; cbins: 256 x bin_col_chunks_max(); rows_buf: pair
 // capacity 8-B row items; vals/ranges as the tile sort's final pass.
 hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,
-                           const uint64_t* srect, int groups, uint32_t* hist, uint32_t* row_items,
+                           const uint32_t* pay0, const uint32_t* pay1, int groups, uint32_t* hist,
+                           uint32_t* row_items,
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
                            int items, hipStream_t s);
 hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, const unsigned long long* row_pairs,

@@ -163,6 +163,27 @@ __device__ __forceinline__ uint32_t rect_count(uint64_t r) {
     return (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1));
 }
 
+// 4-B form of a tile rectangle for grids of at most 256 tiles per axis (the
+// binning path): tx0 | tx1 << 8 | ty0 << 16 | ty1 << 24.  Lossless there (every
+// coordinate is < 256; the dead value packs to 0x00010001 and unpacks to kDeadRect).
+__device__ __forceinline__ uint32_t pack_rect(uint64_t r) {
+    return (uint32_t)(r & 0xffu) | (uint32_t)((r >> 8) & 0xff00u) | (uint32_t)((r >> 16) & 0xff0000u) |
+           (uint32_t)((r >> 24) & 0xff000000u);
+}
+__device__ __forceinline__ uint64_t unpack_rect(uint32_t p) {
+    return (uint64_t)(p & 0xffu) | ((uint64_t)((p >> 8) & 0xffu) << 16) | ((uint64_t)((p >> 16) & 0xffu) << 32) |
+           ((uint64_t)(p >> 24) << 48);
+}
+
+// The preprocess's tile rect of Gaussian i: 8 B, or packed to 4 B (pack_rect) for the
+// binning path (`packed`: the buffer then holds u32 rects in index order).
+__device__ __forceinline__ void put_rect(uint64_t* rect, int64_t i, uint64_t r, int packed) {
+    if (packed)
+        reinterpret_cast<uint32_t*>(rect)[i] = pack_rect(r);
+    else
+        rect[i] = r;
+}
+
 // ------------------------------------------------------------------ blend cull words
 //
 // The blend culls every record of its tile list against each 8x8 block (the
@@ -231,6 +252,7 @@ template <bool T4D, bool SH3>
 __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ arr, int64_t stride,
                                                     int64_t n, Frame fr, uint4* __restrict__ rec,
                                                     uint64_t* __restrict__ items, uint64_t* __restrict__ rect,
+                                                    int packed,
                                                     float tnow) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
@@ -256,7 +278,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     float tmp_xyz[4], new_xyz[4];
     mv4(fr.V, old_xyz, tmp_xyz);
     if (!isfinite(tmp_xyz[0]) || !isfinite(tmp_xyz[1]) || !isfinite(tmp_xyz[2])) {
-        rect[i] = kDeadRect;
+        put_rect(rect, i, kDeadRect, packed);
         return;
     }
     mv4(fr.P, tmp_xyz, new_xyz);
@@ -265,7 +287,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     new_xyz[2] = new_xyz[2] / new_xyz[3];
     if (!isfinite(new_xyz[0]) || !isfinite(new_xyz[1]) || !isfinite(new_xyz[2]) ||
         tmp_xyz[2] >= -fr.znear || new_xyz[2] < -1.0f || new_xyz[2] > 1.0f) {
-        rect[i] = kDeadRect;
+        put_rect(rect, i, kDeadRect, packed);
         return;
     }
 
@@ -312,7 +334,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     S2[3] = (H * 0.5f) * (H * 0.5f) * S2[3];
     const float det = S2[0] * S2[3] - S2[1] * S2[2];
     if (!isfinite(det) || det < 1e-8f) {                        // render.cu:690
-        rect[i] = kDeadRect;
+        put_rect(rect, i, kDeadRect, packed);
         return;
     }
     const float invDet = 1.0f / det;
@@ -325,7 +347,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
         const float opt = arr[GSR_A_OPACITY * stride + i] * tfac;
         const float hh = 0.5f * (ic1 + ic2);
         if (opt < 0.9e-3f && ic0 > 0.0f && ic3 > 0.0f && (ic0 * ic3 - hh * hh) > 1e-4f * (ic0 * ic3)) {
-            rect[i] = kDeadRect;
+            put_rect(rect, i, kDeadRect, packed);
             return;
         }
     }
@@ -351,7 +373,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     float xmin = new_xyz[0] - ex, xmax = new_xyz[0] + ex;
     float ymin = new_xyz[1] - ey, ymax = new_xyz[1] + ey;
     if (xmax < -0.99f || xmin > 0.99f || ymax < -0.99f || ymin > 0.99f) {   // render.cu:737
-        rect[i] = kDeadRect;
+        put_rect(rect, i, kDeadRect, packed);
         return;
     }
     xmin = fmaxf(xmin, -1.0f);
@@ -435,7 +457,9 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     R[2] = make_uint4(__float_as_uint((float)px_x), __float_as_uint((float)px_y), (uint32_t)xmin_px | ((uint32_t)xmax_px << 16),
                       (uint32_t)ymin_px | ((uint32_t)ymax_px << 16));
     R[3] = cull_word(ic0, ic1, ic2, ic3, opacity, col[0], col[1], col[2]);
-    rect[i] = (uint64_t)((uint32_t)tx0 | ((uint32_t)tx1 << 16)) | ((uint64_t)((uint32_t)ty0 | ((uint32_t)ty1 << 16)) << 32);
+    put_rect(rect, i,
+             (uint64_t)((uint32_t)tx0 | ((uint32_t)tx1 << 16)) | ((uint64_t)((uint32_t)ty0 | ((uint32_t)ty1 << 16)) << 32),
+             packed);
     items[i] = ((uint64_t)key << 32) | (uint64_t)(uint32_t)i;
 }
 
@@ -585,21 +609,28 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
     if (threadIdx.x == 0) totals[blockIdx.x] = total;
 }
 
-// rect != nullptr (depth sort feeding the tile binning): the pass that turns
-// out to be the last one (device plan: pass 3, or pass + 1 skipped) also writes
-// srect[dst] = rect[index] for every item — the compact tile rectangles in depth
-// order.  The gather is issued right after the item load, so its latency hides
-// behind the ranking; the row pass then reads srect coalesced.
+// pay_out != nullptr (depth sort feeding the tile binning): every pass carries
+// each item's tile rectangle as a 4-B payload (pack_rect: grids <= 256 tiles per
+// axis) and writes it at the item's destination, so the pass that turns out to be
+// the last one leaves the rects in depth order (pay_out[np & 1] for np passes run)
+// for the row pass to read coalesced.  Pass 0 takes it from the live partition's
+// payloads (pay_in), or from the preprocess's packed rects: rect[position] when its
+// input is the preprocess order (rect_direct: item j has index j), else rect[index]
+// (a repeated sort).
+// Payloads leave through the items' LDS slots, in the same digit runs.
+// (The rects used to be gathered in the last pass only: a random 8-B read per item
+// that cost the 5M-Gaussian frame 76 us of its 110-us pass, profiles/r02_geom_pmc.txt.)
 template <int ITEMS>
 __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const uint64_t* __restrict__ in, uint64_t* __restrict__ out, const uint32_t* __restrict__ n_dev,
     uint32_t n_host, int shift, int bits, int groups, const uint32_t* __restrict__ hist,
     const uint32_t* __restrict__ totals, uint2* __restrict__ ranges, const uint32_t* __restrict__ dstats,
-    int pass, const uint64_t* __restrict__ rect, uint64_t* __restrict__ srect) {
+    int pass, const uint32_t* __restrict__ rect, int rect_direct, const uint32_t* __restrict__ pay_in,
+    uint32_t* __restrict__ pay_out) {
     constexpr int kTile = kSortThreads * ITEMS;
     __shared__ uint64_t s_items[kTile];
     if (depth_pass_skipped(dstats, pass)) return;
-    const bool gather = rect && (pass == 3 || depth_pass_skipped(dstats, pass + 1));
+    const bool carry = pay_out != nullptr;
     __shared__ uint32_t s_wc[4][256];           // per-wave digit counters, then wave bases
     __shared__ uint32_t s_gbase[256];           // running global offset per digit
     __shared__ uint32_t s_lbase[256];           // tile-local exclusive base per digit
@@ -627,19 +658,29 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
         for (int k = 0; k < 4; k++) s_wc[k][t] = 0;
         __syncthreads();
 
-        uint64_t it[ITEMS], rc[ITEMS];
-        uint32_t rk[ITEMS];
+        uint64_t it[ITEMS];
+        uint32_t rk[ITEMS], pv[ITEMS];
         const uint32_t wbase = w * 64 * ITEMS;
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             it[k] = (el < tn) ? in[tb + el] : 0ull;
         }
-        if (gather) {
+        if (carry) {
+            // uniform branches: the position-indexed reads must not wait for the item loads
+            const uint32_t* src = pay_in ? pay_in : rect;
+            if (pay_in || rect_direct) {
 #pragma unroll
-            for (int k = 0; k < ITEMS; k++) {
-                const uint32_t el = wbase + k * 64 + lane;
-                rc[k] = (el < tn) ? rect[(uint32_t)it[k]] : 0ull;
+                for (int k = 0; k < ITEMS; k++) {
+                    const uint32_t el = wbase + k * 64 + lane;
+                    pv[k] = (el < tn) ? src[tb + el] : 0u;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < ITEMS; k++) {
+                    const uint32_t el = wbase + k * 64 + lane;
+                    pv[k] = (el < tn) ? rect[(uint32_t)it[k]] : 0u;
+                }
             }
         }
 #pragma unroll
@@ -682,23 +723,48 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
             if (el < tn) {
                 const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
                 s_items[s_lbase[d] + s_wc[w][d] + rk[k]] = it[k];
-                if (gather) srect[s_gbase[d] + s_wc[w][d] + rk[k]] = rc[k];
             }
         }
         __syncthreads();
-        for (uint32_t q = t; q < tn; q += kSortThreads) {
-            const uint64_t v = s_items[q];
-            const uint32_t d = (uint32_t)(v >> shift) & mask;
-            const uint32_t dst = s_gbase[d] + (q - s_lbase[d]);
-            out[dst] = v;
-            if (ranges) {
-                // final pass of the tile sort: the LDS tile is fully sorted, so each
-                // run of one tile key is contiguous; record its global [start, end)
-                // as {~start, end} with atomicMax, so a zeroed array means "empty"
-                // (replaces a separate boundary-detection kernel).
-                const uint32_t key = (uint32_t)(v >> 32);
-                if (q == 0 || (uint32_t)(s_items[q - 1] >> 32) != key) atomicMax(&ranges[key].x, ~dst);
-                if (q == tn - 1 || (uint32_t)(s_items[q + 1] >> 32) != key) atomicMax(&ranges[key].y, dst + 1);
+        uint32_t dq[ITEMS];
+#pragma unroll
+        for (int k = 0; k < ITEMS; k++) {
+            const uint32_t q = t + k * kSortThreads;
+            if (q < tn) {
+                const uint64_t v = s_items[q];
+                const uint32_t d = (uint32_t)(v >> shift) & mask;
+                const uint32_t dst = s_gbase[d] + (q - s_lbase[d]);
+                out[dst] = v;
+                dq[k] = dst;
+                if (ranges) {
+                    // final pass of the tile sort: the LDS tile is fully sorted, so each
+                    // run of one tile key is contiguous; record its global [start, end)
+                    // as {~start, end} with atomicMax, so a zeroed array means "empty"
+                    // (replaces a separate boundary-detection kernel).
+                    const uint32_t key = (uint32_t)(v >> 32);
+                    if (q == 0 || (uint32_t)(s_items[q - 1] >> 32) != key) atomicMax(&ranges[key].x, ~dst);
+                    if (q == tn - 1 || (uint32_t)(s_items[q + 1] >> 32) != key) atomicMax(&ranges[key].y, dst + 1);
+                }
+            }
+        }
+        if (carry) {
+            // the payloads take the items' LDS slots once every item is read, so their
+            // stores leave in the same digit runs as the items' (coalesced)
+            uint32_t* s_pay = reinterpret_cast<uint32_t*>(s_items);
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++) {
+                const uint32_t el = wbase + k * 64 + lane;
+                if (el < tn) {
+                    const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
+                    s_pay[s_lbase[d] + s_wc[w][d] + rk[k]] = pv[k];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < ITEMS; k++) {
+                const uint32_t q = t + k * kSortThreads;
+                if (q < tn) pay_out[dq[k]] = s_pay[q];
             }
         }
         __syncthreads();
@@ -854,6 +920,12 @@ __global__ __launch_bounds__(kSortThreads) void k_kv_downsweep(
 __device__ __forceinline__ const uint64_t* depth_sorted(const uint64_t* items0, const uint64_t* items1,
                                                         const uint32_t* dstats) {
     return (depth_passes_run(dstats) & 1) ? items1 : items0;
+}
+// The depth-ordered rect payloads the binning's depth sort carries (k_radix_downsweep):
+// same parity as the items.
+__device__ __forceinline__ const uint32_t* depth_sorted_rects(const uint32_t* pay0, const uint32_t* pay1,
+                                                             const uint32_t* dstats) {
+    return (depth_passes_run(dstats) & 1) ? pay1 : pay0;
 }
 
 __global__ __launch_bounds__(256) void k_emit_count(const uint64_t* __restrict__ items0,
@@ -1193,9 +1265,11 @@ __device__ __forceinline__ void publish_pair_stats(unsigned long long total, uin
 
 // Row pass, count: per workgroup (1024-Gaussian sub-chunks in depth order) the
 // number of row items and of pairs per tile row; hist[row][g] and
-// hist[256 + row][g].  Reads the rects in depth order (srect, written by the
-// depth sort's last downsweep).
-__global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint64_t* __restrict__ srect, int groups,
+// hist[256 + row][g].  Reads the rects in depth order (the payloads the depth
+// sort carried, depth_sorted_rects).
+__global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint32_t* __restrict__ pay0,
+                                                         const uint32_t* __restrict__ pay1,
+                                                         const uint32_t* __restrict__ dstats, int groups,
                                                          int tiles_y, uint32_t* __restrict__ hist) {
     __shared__ uint32_t h_items[4][256], h_pairs[4][256];
     const uint32_t t = threadIdx.x, w = t >> 6;
@@ -1205,6 +1279,7 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint64
         h_pairs[k][t] = 0;
     }
     __syncthreads();
+    const uint32_t* srect = depth_sorted_rects(pay0, pay1, dstats);
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, kRowSources, b, e);
     for (uint64_t c0 = b; c0 < e; c0 += 1024) {
@@ -1212,7 +1287,7 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint64
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const uint64_t j = c0 + t + 256 * k;
-            r[k] = j < e ? srect[j] : kDeadRect;
+            r[k] = j < e ? unpack_rect(srect[j]) : kDeadRect;
         }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -1294,7 +1369,8 @@ template <int ITEMS, int BITS>
 __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __restrict__ items0,
                                                            const uint64_t* __restrict__ items1,
                                                            const uint32_t* __restrict__ dstats,
-                                                           const uint64_t* __restrict__ srect, uint32_t n,
+                                                           const uint32_t* __restrict__ pay0,
+                                                           const uint32_t* __restrict__ pay1, uint32_t n,
                                                            int groups, const uint32_t* __restrict__ hist,
                                                            const uint32_t* __restrict__ row_items,
                                                            const unsigned long long* __restrict__ row_pairs,
@@ -1322,13 +1398,14 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
         if (ptot > cap || b >= e) return;   // uniform: overflow frames stop here
     }
     const uint64_t* sorted = depth_sorted(items0, items1, dstats);
+    const uint32_t* srect = depth_sorted_rects(pay0, pay1, dstats);
     for (uint64_t c0 = b; c0 < e; c0 += kRowSources) {
         // thread t owns sources 4t .. 4t+3 of this sub-chunk (source order)
         uint32_t cnt[4], start[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint64_t j = c0 + 4 * t + i;
-            const uint64_t r = j < e ? srect[j] : kDeadRect;
+            const uint64_t r = j < e ? unpack_rect(srect[j]) : kDeadRect;
             s_idx[4 * t + i] = j < e ? (uint32_t)sorted[j] : 0u;
             s_rect[4 * t + i] = r;
             cnt[i] = rect_rows(r);
@@ -1581,9 +1658,11 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
 // order, then the culled ones, in index order.  The full sort puts the culled
 // items last in index order anyway (their key is the maximum, ties by index), so
 // sorting only the visible prefix (n_dev = the visible count) gives the same
-// order.  The culled tail is written to `out` only, with kDeadRect in srect at
-// the same positions; the binning never reads items whose rect is dead, and
-// gsr_read_depth_order takes the tail from `out`.  Three launches: per-chunk
+// order.  The visible items' rect payloads go to pay0 (pass 0 reads them there).
+// The culled tail is written to `out` only, with the dead rect in both payload
+// buffers at the same positions (the passes never touch the tail, and which buffer
+// ends depth-ordered is decided on the device); the binning never reads items whose
+// rect is dead, and gsr_read_depth_order takes the tail from `out`.  Three launches: per-chunk
 // visible counts, their exclusive scan (+ total), the scatter.
 __global__ __launch_bounds__(256) void k_part_count(const uint64_t* __restrict__ in, uint32_t n, int groups,
                                                      uint32_t* __restrict__ counts) {
@@ -1619,7 +1698,9 @@ __global__ __launch_bounds__(256) void k_part_scan(uint32_t* __restrict__ counts
 __global__ __launch_bounds__(256) void k_part_scatter(const uint64_t* __restrict__ in, uint32_t n, int groups,
                                                        const uint32_t* __restrict__ offs,
                                                        const uint32_t* __restrict__ n_live,
-                                                       uint64_t* __restrict__ out, uint64_t* __restrict__ srect) {
+                                                       uint64_t* __restrict__ out,
+                                                       const uint32_t* __restrict__ rect,
+                                                       uint32_t* __restrict__ pay0, uint32_t* __restrict__ pay1) {
     __shared__ uint32_t s_w[4];
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, 256, b, e);
@@ -1648,11 +1729,16 @@ __global__ __launch_bounds__(256) void k_part_scatter(const uint64_t* __restrict
             ltot += x & 0xffffu;
             dtot += x >> 16;
         }
-        if (live) out[live_base + lb + (uint32_t)__popcll(bl & lt)] = v;
+        if (live) {
+            const uint32_t q = live_base + lb + (uint32_t)__popcll(bl & lt);
+            out[q] = v;
+            pay0[q] = rect[(uint32_t)v];   // pass 0 reads the payloads from pay0
+        }
         if (dead) {
             const uint32_t q = dead_base + db + (uint32_t)__popcll(bd & lt);
             out[q] = v;
-            srect[q] = kDeadRect;
+            pay0[q] = pack_rect(kDeadRect);   // the sort's result parity is decided on the device
+            pay1[q] = pack_rect(kDeadRect);
         }
         live_base += ltot;
         dead_base += dtot;
@@ -1761,7 +1847,7 @@ __device__ __forceinline__ f2 gsr_expf_x2(f2 xc) {
 //   [0+h] cx  [2+h] cy  [4+h] a  [6+h] b  [8+h] c  [10+h] e  [12+h] opacity
 //   [14+2h] red  [15+2h] green  [18+h] blue
 struct BlendDiag {
-    uint64_t loaded = 0, iter = 0, active = 0, taken = 0, slow = 0;
+    uint64_t loaded = 0, iter = 0, active = 0, taken = 0, slow = 0, zero_taken = 0, no_cand_pairs = 0;
 };
 
 // 64-bit pixel mask (bit row * 8 + col) of a box descriptor built in the cull:
@@ -1867,6 +1953,7 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
             wP[(nsurv >> 1) * kSlot + (lane < 7 ? 2 * lane + 1 : lane + 9 + (lane == 9))] = 0.0f;
         }
         if (DIAG) dg.loaded += cnt;
+        const float cut_l = DIAG ? __uint_as_float(rd.x) : 0.0f;   // diagnostics: md2 cutoff of record `lane`
         // ---- prefetch: records of batch k+1, indices of batch k+2 ----
         if (base + 64 + lane < end) {
             const uint4* R = rec + 4 * (uint64_t)nidx;
@@ -1931,6 +2018,14 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 crg = crg + w1;
                 cb = (cb + wb.x) + wb.y;
                 if (DIAG) {
+                    // splat-iterations with no taken lane; pair-iterations in which no live
+                    // in-box lane of either splat passes md2 <= cut (a pre-exp skip test)
+                    const float cut0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cut_l), s0));
+                    const float cut1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cut_l), s1));
+                    const bool cand0 = in0 && !(mdh.x < -0.5f * cut0);
+                    const bool cand1 = has1 && in1 && !(TT.x < 1e-3f) && !(mdh.y < -0.5f * cut1);
+                    dg.zero_taken += (__ballot(take0) == 0ull ? 1 : 0) + (has1 && __ballot(take1) == 0ull ? 1 : 0);
+                    dg.no_cand_pairs += (__ballot(cand0 || cand1) == 0ull) ? 1 : 0;
                     dg.iter += has1 ? 2 : 1;
                     dg.active += (uint64_t)__popcll(__ballot(in0)) +
                                 (uint64_t)__popcll(__ballot(in1 & !(TT.y < 1e-3f)));
@@ -2041,6 +2136,8 @@ __global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx
         atomicAdd(counters + 2, (unsigned long long)dg.active);
         atomicAdd(counters + 3, (unsigned long long)dg.taken);
         atomicAdd(counters + 4, (unsigned long long)dg.slow);
+        atomicAdd(counters + 5, (unsigned long long)dg.zero_taken);
+        atomicAdd(counters + 7, (unsigned long long)dg.no_cand_pairs);
         atomicAdd(counters + 6, (unsigned long long)(dg.iter * 64));
     }
 }
@@ -2110,44 +2207,54 @@ hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, 
 }
 
 hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
-                             uint4* rec, uint64_t* items, uint64_t* rect, bool four_d, bool sh3, float t,
-                             hipStream_t s) {
+                             uint4* rec, uint64_t* items, uint64_t* rect, bool packed, bool four_d, bool sh3,
+                             float t, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const dim3 g(grid_for(n, 256));
+    const int pk = packed ? 1 : 0;
     if (four_d)
-        hipLaunchKernelGGL((k_preprocess<true, false>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect, t);
+        hipLaunchKernelGGL((k_preprocess<true, false>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect,
+                           pk, t);
     else if (sh3)
-        hipLaunchKernelGGL((k_preprocess<false, true>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect, t);
+        hipLaunchKernelGGL((k_preprocess<false, true>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect,
+                           pk, t);
     else
         hipLaunchKernelGGL((k_preprocess<false, false>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect,
-                           t);
+                           pk, t);
     return hipGetLastError();
 }
 
 template <int ITEMS>
 static void radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host, int shift,
                        int bits, int groups, uint32_t* hist, uint32_t* totals, uint2* ranges, uint32_t* dstats,
-                       int pass, const uint64_t* rect, uint64_t* srect, hipStream_t s) {
+                       int pass, const uint32_t* rect, int rect_direct, uint32_t* pay0, uint32_t* pay1,
+                       hipStream_t s) {
     const uint32_t mask = (1u << bits) - 1u;
     hipLaunchKernelGGL(k_radix_upsweep<ITEMS>, dim3(groups), dim3(kSortThreads), 0, s, in, n_dev, n_host, shift,
                        mask, groups, hist, dstats, pass);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, hist, groups, totals,
                        static_cast<const uint32_t*>(dstats), pass);
+    // rect payloads (binning): pass p reads pay[p & 1] (pass 0: rect, or pay[0] when
+    // rect_direct < 0 — the live partition wrote it) and writes pay[(p + 1) & 1]
+    const uint32_t* pay_in = pay0 && (pass > 0 || rect_direct < 0) ? ((pass & 1) ? pay1 : pay0) : nullptr;
+    uint32_t* pay_out = pay0 ? ((pass & 1) ? pay0 : pay1) : nullptr;
     hipLaunchKernelGGL(k_radix_downsweep<ITEMS>, dim3(groups), dim3(kSortThreads), 0, s, in, out, n_dev, n_host,
                        shift, bits, groups, hist, totals, ranges, static_cast<const uint32_t*>(dstats), pass, rect,
-                       srect);
+                       rect_direct > 0 ? 1 : 0, pay_in, pay_out);
 }
 
 hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
                              int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
-                             uint2* ranges, hipStream_t s, uint32_t* dstats, int pass, const uint64_t* rect,
-                             uint64_t* srect) {
-    if ((rect == nullptr) != (srect == nullptr)) return hipErrorInvalidValue;
+                             uint2* ranges, hipStream_t s, uint32_t* dstats, int pass, const uint32_t* rect,
+                             int rect_direct, uint32_t* pay0, uint32_t* pay1) {
+    if ((rect == nullptr) != (pay0 == nullptr) || (pay0 == nullptr) != (pay1 == nullptr))
+        return hipErrorInvalidValue;
     if (items == 8)
-        radix_pass<8>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect, srect, s);
+        radix_pass<8>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
+                      rect_direct, pay0, pay1, s);
     else
-        radix_pass<16>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect, srect,
-                       s);
+        radix_pass<16>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
+                       rect_direct, pay0, pay1, s);
     return hipGetLastError();
 }
 
@@ -2169,28 +2276,31 @@ hipError_t launch_emit(const uint64_t* items0, const uint64_t* items1, const uin
 }
 
 hipError_t launch_partition(const uint64_t* in, uint32_t n, int groups, uint32_t* counts, uint32_t* n_live,
-                            uint64_t* out, uint64_t* srect, hipStream_t s) {
+                            uint64_t* out, const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, hipStream_t s) {
     if (groups < 1 || groups > kMaxSortGroups) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_part_count, dim3(groups), dim3(256), 0, s, in, n, groups, counts);
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(256), 0, s, counts, groups, n_live);
-    hipLaunchKernelGGL(k_part_scatter, dim3(groups), dim3(256), 0, s, in, n, groups, counts, n_live, out, srect);
+    hipLaunchKernelGGL(k_part_scatter, dim3(groups), dim3(256), 0, s, in, n, groups, counts, n_live, out, rect,
+                       pay0, pay1);
     return hipGetLastError();
 }
 
 hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,
-                           const uint64_t* srect, int groups, uint32_t* hist, uint32_t* row_items,
+                           const uint32_t* pay0, const uint32_t* pay1, int groups, uint32_t* hist,
+                           uint32_t* row_items,
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
                            int items, hipStream_t s) {
     if (tiles_y < 1 || tiles_y > 256 || groups < 1 || groups > kMaxSortGroups / 2 ||
         (items != 4 && items != 8 && items != 16))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_bin_rows_count, dim3(groups), dim3(256), 0, s, n, srect, groups, tiles_y, hist);
+    hipLaunchKernelGGL(k_bin_rows_count, dim3(groups), dim3(256), 0, s, n, pay0, pay1, dstats, groups, tiles_y,
+                       hist);
     hipLaunchKernelGGL(k_bin_rows_scan, dim3(256), dim3(256), 0, s, hist, groups, tiles_y, row_items, row_pairs);
     auto scatter = tiles_y <= 128 ? (items == 4 ? k_bin_rows_scatter<4, 7> : items == 8 ? k_bin_rows_scatter<8, 7>
                                                                                     : k_bin_rows_scatter<16, 7>)
                                   : (items == 4 ? k_bin_rows_scatter<4, 8> : items == 8 ? k_bin_rows_scatter<8, 8>
                                                                                     : k_bin_rows_scatter<16, 8>);
-    hipLaunchKernelGGL(scatter, dim3(groups), dim3(256), 0, s, items0, items1, dstats, srect, n, groups, hist,
+    hipLaunchKernelGGL(scatter, dim3(groups), dim3(256), 0, s, items0, items1, dstats, pay0, pay1, n, groups, hist,
                        row_items, row_pairs, pair_capacity, tiles_y, rows_buf);
     return hipGetLastError();
 }

@@ -312,7 +312,9 @@ struct gsr_context {
     // pair buffers: p_cap u64 each, used as {keys: p_cap x 4 B, values: p_cap x 4 B}
     uint64_t* pairs[2] = {nullptr, nullptr};
     uint64_t* rect = nullptr;        // per-Gaussian tile rectangle (preprocess output)
-    uint64_t* srect = nullptr;       // the rectangles in depth order (last depth pass, binning path)
+    bool rect_packed = false;        // this frame's rects are packed (binning path, set by gsr_preprocess)
+    uint64_t* srect = nullptr;       // binning path: two u32 rect-payload buffers the depth sort carries
+                                     // (pack_rect), one of them depth-ordered at its end
     uint32_t* hist = nullptr;
     uint32_t* totals = nullptr;
     unsigned long long* wg = nullptr;
@@ -607,9 +609,12 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     // items[1] and the partition writes the visible-first order into items[0]
     c->compact_frame = n > 0 && (c->depth_compact == 1 || (c->depth_compact == 2 && layout == GSR_LAYOUT_SCENE_BLOCK_4D)) &&
                        c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
+    // the binning path takes the tile rects packed to 4 B (pack_rect), the pair path 8 B;
+    // the sort follows the path chosen here (rect_packed)
+    c->rect_packed = c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
     HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[c->compact_frame ? 1 : 0], c->rect,
-                                   layout == GSR_LAYOUT_SCENE_BLOCK_4D, layout == GSR_LAYOUT_SCENE_BLOCK_SH3, c->time,
-                                   c->stream));
+                                   c->rect_packed, layout == GSR_LAYOUT_SCENE_BLOCK_4D,
+                                   layout == GSR_LAYOUT_SCENE_BLOCK_SH3, c->time, c->stream));
     c->have_pre = true;
     c->have_sort = false;
     return rc_over;
@@ -631,9 +636,14 @@ static int ensure_cbins(gsr_context* c) {
     return GSR_OK;
 }
 
+// Rect payload buffer b (0 or 1) of the binning's depth sort: the two u32 halves of srect.
+static uint32_t* pay_buf(gsr_context* c, int b) {
+    return reinterpret_cast<uint32_t*>(c->srect) + (b ? c->n_cap : 0);
+}
+
 // Global stable depth sort of the preprocess items (key << 32 | index), 4 x 8-bit
-// passes with the device-side pass plan; with rects (binning) the last pass also
-// writes them in depth order (srect).  Result in items[passes run & 1].
+// passes with the device-side pass plan; with rects (binning) the passes carry them and
+// leaves them in depth order (pay_buf(c, passes run & 1)).  Result in items[passes run & 1].
 static int depth_sort_locked(gsr_context* c, bool with_rects) {
     const uint32_t n = (uint32_t)c->n;
     // smaller tiles for the 1M-item depth sort: ~500 workgroups instead of ~250
@@ -643,29 +653,35 @@ static int depth_sort_locked(gsr_context* c, bool with_rects) {
     const bool part = with_rects && c->compact_frame;
     if (part)   // visible items first (index order) into items[0]; the passes sort only those
         HIP_TRY(gsr::launch_partition(c->items[1], n, std::min(groups_for(c->n, 4096), gsr::kMaxSortGroups), c->hist,
-                                      c->nlive, c->items[0], c->srect, c->stream));
+                                      c->nlive, c->items[0], reinterpret_cast<const uint32_t*>(c->rect),
+                                      pay_buf(c, 0), pay_buf(c, 1), c->stream));
     c->last_compact = part;
+    // pass 0's rect payloads: from the partition (-1), read at the item's position when
+    // items[0] is still the preprocess order (1: item j has index j), else gathered (0)
+    const int rect_mode = part ? -1 : (c->have_sort ? 0 : 1);
     // items[1] is the sort's scratch from here on; a repeated sort of this frame sorts
     // the whole partitioned items[0] (same order: visible and culled keys never tie)
     if (part) c->compact_frame = false;
     for (int p = 0; p < 4; p++)
         HIP_TRY(gsr::launch_radix_pass(c->items[p & 1], c->items[(p + 1) & 1], part ? c->nlive : nullptr, n, 32 + 8 * p, 8, gd, di,
                                        c->hist, c->totals, nullptr, c->stream, c->depth_skip ? c->dstats : nullptr,
-                                       p, with_rects ? c->rect : nullptr, with_rects ? c->srect : nullptr));
+                                       p, with_rects ? reinterpret_cast<const uint32_t*>(c->rect) : nullptr, rect_mode,
+                                       with_rects ? pay_buf(c, 0) : nullptr,
+                                       with_rects ? pay_buf(c, 1) : nullptr));
     return GSR_OK;
 }
 
 static int sort_locked(gsr_context* c) {
     if (!c->have_pre) return set_err(GSR_E_ARG, "gsr_sort before gsr_preprocess");
     const uint32_t n = (uint32_t)c->n;
-    const bool bin = c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
+    const bool bin = c->rect_packed;   // the path gsr_preprocess chose (its rect format)
     c->last_binned = bin;
     if (c->compact_frame && !bin) {   // knobs changed since gsr_preprocess
         HIP_TRY(hipMemcpyAsync(c->items[0], c->items[1], (size_t)n * 8, hipMemcpyDeviceToDevice, c->stream));
         c->compact_frame = false;
     }
     // ---- stable depth sort of (key << 32 | index), 4 x 8 bits; for the binning
-    // path its last pass also writes the rects in depth order (srect) ----
+    // path the passes carry the rects, depth-ordered at the end (pay_buf) ----
     mark(c, GSR_STAGE_DEPTH_SORT);
     if (int rc = depth_sort_locked(c, bin)) return rc;
     // result in items[passes run & 1] (device-side plan; emission picks it)
@@ -677,7 +693,8 @@ static int sort_locked(gsr_context* c) {
         auto* row_items = reinterpret_cast<uint32_t*>(c->binmeta + 256);
         const int gb = std::min(groups_for(c->n, 1024), gsr::kMaxSortGroups / 2);
         mark(c, GSR_STAGE_EMIT);
-        HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n, c->srect, gb,
+        HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n, pay_buf(c, 0),
+                                     pay_buf(c, 1), gb,
                                      c->hist, row_items, row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items,
                                      c->stream));
         mark(c, GSR_STAGE_TILE_SORT);
@@ -986,7 +1003,15 @@ extern "C" int gsr_read_splats(gsr_context* c, void* host, int64_t n) {
     if (!c->have_pre) return set_err(GSR_E_ARG, "gsr_read_splats: no preprocessed frame");
     HIP_TRY(hipMemcpy(host, c->rec, (size_t)n * GSR_SPLAT_RECORD_BYTES, hipMemcpyDeviceToHost));
     std::vector<uint64_t> rect((size_t)n), items((size_t)c->n);
-    HIP_TRY(hipMemcpy(rect.data(), c->rect, (size_t)n * 8, hipMemcpyDeviceToHost));
+    if (c->rect_packed) {   // 4-B rects (gsr_kernels.hip pack_rect): tx0 | tx1 << 8 | ty0 << 16 | ty1 << 24
+        std::vector<uint32_t> p((size_t)n);
+        HIP_TRY(hipMemcpy(p.data(), c->rect, (size_t)n * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < (size_t)n; i++)
+            rect[i] = (uint64_t)(p[i] & 0xffu) | ((uint64_t)((p[i] >> 8) & 0xffu) << 16) |
+                      ((uint64_t)((p[i] >> 16) & 0xffu) << 32) | ((uint64_t)(p[i] >> 24) << 48);
+    } else {
+        HIP_TRY(hipMemcpy(rect.data(), c->rect, (size_t)n * 8, hipMemcpyDeviceToHost));
+    }
     if (c->have_sort) {
         if (int rc = sorted_items_locked(c, items.data(), c->n)) return rc;
     } else {   // preprocess order (items[1] when the frame is set up for the live partition)

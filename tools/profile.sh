@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${OUT:-gpurun_out/prof}
 mkdir -p "$OUT"
 fatal() { case $1 in 124|134|137|139) echo "FATAL rc=$1 in $2; stopping"; exit "$1";; esac; }
 B="bench.py --steps ${STEPS:-50} --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-}"
@@ -14,7 +14,7 @@ rc=$?; echo "kernel-trace rc=$rc"; fatal $rc kt
 IFS=';' read -ra GROUPS_ <<< "${PMC_GROUPS:-FETCH_SIZE;WRITE_SIZE}"
 for G in "${GROUPS_[@]}"; do
   TAG=$(echo $G | awk '{print $1}')
-  timeout -k 10 600 rocprofv3 --pmc $G -d "$OUT/pmc_$TAG" -o pmc --output-format csv -- python3 $B > "$OUT/pmc_$TAG.log" 2>&1
+  timeout -k 10 ${PMC_TIMEOUT:-600} rocprofv3 --pmc $G -d "$OUT/pmc_$TAG" -o pmc --output-format csv -- python3 $B > "$OUT/pmc_$TAG.log" 2>&1
   rc=$?; echo "pmc [$G] rc=$rc"; fatal $rc "pmc $G"
 done
 find "$OUT" -name "*.csv" | head -20
