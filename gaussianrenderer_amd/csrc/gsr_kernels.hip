@@ -463,6 +463,28 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     items[i] = ((uint64_t)key << 32) | (uint64_t)(uint32_t)i;
 }
 
+// Lanes of the wave whose `bits`-bit digit equals this lane's, among the lanes in
+// `valid` (the wave64 stand-in for __match_any): one ballot per digit bit.  Per bit
+// 4 VALU: v_bfe_i32 (the bit as a 0 / -1 mask m), the ballot's v_cmp, and one
+// v_bitop3_b32 per mask half computing peers & ~(ballot ^ m) — truth table 0x90 for
+// (peers, ballot, m), index S0*4 + S1*2 + S2 (tools/microbench/bitop3_probe.hip) —
+// where the select-and-mask form compiles to 8.
+// (MAXB: compile-time bound on `bits`, so the loop unrolls; bits <= MAXB.)
+template <int MAXB>
+__device__ __forceinline__ uint64_t match_peers(uint32_t d, bool valid, int bits) {
+    const uint64_t v = __ballot(valid);
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#pragma unroll
+    for (int bit = 0; bit < MAXB; bit++) {
+        if (bit >= bits) break;
+        const int m = __builtin_amdgcn_sbfe((int)d, bit, 1);
+        const uint64_t bm = __ballot(m != 0);
+        lo = __builtin_amdgcn_bitop3_b32(lo, (uint32_t)bm, (uint32_t)m, 0x90);
+        hi = __builtin_amdgcn_bitop3_b32(hi, (uint32_t)(bm >> 32), (uint32_t)m, 0x90);
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // ------------------------------------------------------------------ radix sort
 //
 // Stable LSD pass, reduce-then-scan (no inter-workgroup spin waits, so no
@@ -688,12 +710,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
             const uint32_t el = wbase + k * 64 + lane;
             const bool valid = el < tn;
             const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
-            uint64_t peers = __ballot(valid);
-            for (int bit = 0; bit < bits; bit++) {
-                const bool on = (d >> bit) & 1u;
-                const uint64_t bm = __ballot(on);
-                peers &= on ? bm : ~bm;
-            }
+            const uint64_t peers = match_peers<8>(d, valid, bits);
             uint32_t r = 0;
             if (valid) {
                 const uint32_t before = s_wc[w][d];
@@ -852,12 +869,7 @@ __global__ __launch_bounds__(kSortThreads) void k_kv_downsweep(
             const uint32_t el = wbase + k * 64 + lane;
             const bool valid = el < tn;
             const uint32_t d = (kk[k] >> shift) & mask;
-            uint64_t peers = __ballot(valid);
-            for (int bit = 0; bit < bits; bit++) {
-                const bool on = (d >> bit) & 1u;
-                const uint64_t bm = __ballot(on);
-                peers &= on ? bm : ~bm;
-            }
+            const uint64_t peers = match_peers<8>(d, valid, bits);
             uint32_t r = 0;
             if (valid) {
                 const uint32_t before = s_wc[w][d];
@@ -1141,13 +1153,7 @@ __device__ __forceinline__ uint32_t bin_rank_tile(const uint32_t (&dig)[ITEMS], 
         const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
         const bool valid = el < tn;
         const uint32_t d = dig[k];
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int bit = 0; bit < BITS; bit++) {
-            const bool on = (d >> bit) & 1u;
-            const uint64_t bm = __ballot(on);
-            peers &= on ? bm : ~bm;
-        }
+        const uint64_t peers = match_peers<BITS>(d, valid, BITS);
         inslot[k] = (uint32_t)__popcll(peers & lt_mask);
         before[k] = s_wc[w][d];
         if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
