@@ -16,7 +16,9 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libgsr.so")
+# GSR_LIBRARY: another build of the same library (tools/ab_libs.sh A/B runs of two builds
+# on one box); the product default is the in-tree build.
+LIB_PATH = os.environ.get("GSR_LIBRARY") or os.path.join(_HERE, "lib", "libgsr.so")
 
 GSR_OK = 0
 GSR_E_ARG = -1

@@ -1518,13 +1518,19 @@ __global__ __launch_bounds__(256) void k_bin_cols_count(const uint64_t* __restri
         const uint32_t r = col_chunk_row(pl, c);
         const uint32_t ib = pl.rbase[r] + (c - pl.chbase[r]) * kColChunk;
         const uint32_t ie = min(ib + kColChunk, pl.rbase[r] + pl.rcnt[r]);
-        // difference arrays: +1 at the first column, -1 past the last
-        for (uint32_t i = ib + t; i < ie; i += 256) {
-            const uint64_t it = rows_in[i];
-            const uint32_t tx0 = (uint32_t)((it >> 32) & 0xffffu), tx1 = (uint32_t)(it >> 48);
-            atomicAdd(&h[w][tx0], 1u);
-            if (tx1 < 255u) atomicSub(&h[w][tx1 + 1], 1u);
-        }
+        // difference arrays: +1 at the first column, -1 past the last (all of a thread's
+        // loads issued before its first LDS update)
+        constexpr int PER = kColChunk / 256;
+        uint64_t its[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) its[k] = ib + t + 256 * k < ie ? rows_in[ib + t + 256 * k] : 0ull;
+#pragma unroll
+        for (int k = 0; k < PER; k++)
+            if (ib + t + 256 * k < ie) {
+                const uint32_t tx0 = (uint32_t)((its[k] >> 32) & 0xffffu), tx1 = (uint32_t)(its[k] >> 48);
+                atomicAdd(&h[w][tx0], 1u);
+                if (tx1 < 255u) atomicSub(&h[w][tx1 + 1], 1u);
+            }
         __syncthreads();
         const uint32_t dsum = h[0][t] + h[1][t] + h[2][t] + h[3][t];
         uint32_t tot;
@@ -1551,14 +1557,15 @@ __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restric
     if (r == 0 && t == 0) publish_pair_stats(P, cap, st, host_st);
     uint32_t run = 0;
     if (P <= cap && t < (uint32_t)tiles_x) {
-        // 8 chunks per step: the loads are issued together, not one round trip per chunk
+        // 32 chunks per step: the loads are issued together, not one round trip per chunk
+        // (a row of the 5M-Gaussian frame has ~75 chunks: 3 round trips instead of 10)
         const uint32_t c1 = pl.chbase[r + 1];
-        for (uint32_t c0 = pl.chbase[r]; c0 < c1; c0 += 8) {
-            uint32_t v[8];
+        for (uint32_t c0 = pl.chbase[r]; c0 < c1; c0 += 32) {
+            uint32_t v[32];
 #pragma unroll
-            for (int k = 0; k < 8; k++) v[k] = c0 + k < c1 ? cbins[(size_t)(c0 + k) * 256 + t] : 0u;
+            for (int k = 0; k < 32; k++) v[k] = c0 + k < c1 ? cbins[(size_t)(c0 + k) * 256 + t] : 0u;
 #pragma unroll
-            for (int k = 0; k < 8; k++)
+            for (int k = 0; k < 32; k++)
                 if (c0 + k < c1) {
                     cbins[(size_t)(c0 + k) * 256 + t] = run;
                     run += v[k];
