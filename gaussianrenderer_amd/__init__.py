@@ -420,6 +420,12 @@ class Renderer:
         """gsr_set_tuning: 0 blend schedule, 1 tile-sort items/thread, 2 depth-sort items/thread."""
         check(lib().gsr_set_tuning(self.ctx, int(knob), int(value)), "gsr_set_tuning")
 
+    def get_tuning(self, knob: int) -> int:
+        """gsr_get_tuning: the knob's current value (the default unless set)."""
+        v = ctypes.c_int(0)
+        check(lib().gsr_get_tuning(self.ctx, int(knob), ctypes.byref(v)), "gsr_get_tuning")
+        return int(v.value)
+
     def depth_passes(self) -> int:
         """Depth-sort digit passes the last frame ran (trailing identities are skipped)."""
         rc = lib().gsr_depth_passes(self.ctx)

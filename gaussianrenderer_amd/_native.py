@@ -127,6 +127,7 @@ SIGNATURES = [
     ("gsr_set_blend_variant", c_int, [c_void_p, c_int]),
     ("gsr_blend_stamps", c_int, [c_void_p, c_void_p, c_int64]),
     ("gsr_set_tuning", c_int, [c_void_p, c_int, c_int]),
+    ("gsr_get_tuning", c_int, [c_void_p, c_int, c_void_p]),
     ("gsr_set_timing_stride", c_int, [c_void_p, c_int, c_int]),
     ("gsr_depth_passes", c_int, [c_void_p]),
     ("gsr_scene_upload", c_void_p, [c_void_p, c_int64]),

@@ -2262,7 +2262,10 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
                              int rect_direct, uint32_t* pay0, uint32_t* pay1) {
     if ((rect == nullptr) != (pay0 == nullptr) || (pay0 == nullptr) != (pay1 == nullptr))
         return hipErrorInvalidValue;
-    if (items == 8)
+    if (items == 4)
+        radix_pass<4>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
+                      rect_direct, pay0, pay1, s);
+    else if (items == 8)
         radix_pass<8>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
                       rect_direct, pay0, pay1, s);
     else

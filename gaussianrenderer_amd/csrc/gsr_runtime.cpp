@@ -646,7 +646,9 @@ static uint32_t* pay_buf(gsr_context* c, int b) {
 // leaves them in depth order (pay_buf(c, passes run & 1)).  Result in items[passes run & 1].
 static int depth_sort_locked(gsr_context* c, bool with_rects) {
     const uint32_t n = (uint32_t)c->n;
-    // smaller tiles for the 1M-item depth sort: ~500 workgroups instead of ~250
+    // smaller tiles for the 1M-item depth sort: ~500 workgroups instead of ~250 (-2.6 %
+    // frame time one at a time; in flight 8 and 16 measure within 1.5 % of each other,
+    // either way round: profiles/r02_ab_depth_items.txt)
     const int di = c->depth_items ? c->depth_items : (c->n < (int64_t(4) << 20) ? 8 : 16);
     int gd = groups_for(c->n, 256 * di);
     if (c->depth_groups) gd = std::min(gd, c->depth_groups);
@@ -1193,6 +1195,29 @@ extern "C" int gsr_set_time(gsr_context* c, float t) {
     return GSR_OK;
 }
 
+extern "C" int gsr_get_tuning(gsr_context* c, int knob, int* value) {
+    if (!c || !value) return set_err(GSR_E_ARG, "gsr_get_tuning: null argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    switch (knob) {
+    case GSR_TUNE_BLEND_SCHEDULE: *value = c->blend_variant; break;
+    case GSR_TUNE_TILE_SORT_ITEMS: *value = c->tile_items; break;
+    case GSR_TUNE_DEPTH_SORT_ITEMS: *value = c->depth_items; break;
+    case GSR_TUNE_TILE_SORT_GROUPS: *value = c->tile_groups; break;
+    case GSR_TUNE_DEPTH_SORT_GROUPS: *value = c->depth_groups; break;
+    case GSR_TUNE_TILE_SORT_SPLIT: *value = c->tile_split_even ? 1 : 0; break;
+    case GSR_TUNE_DEPTH_SORT_SKIP: *value = c->depth_skip ? 1 : 0; break;
+    case GSR_TUNE_TILE_BINNING: *value = c->tile_binning; break;
+    case GSR_TUNE_BIN_ROW_ITEMS: *value = c->bin_row_items; break;
+    case GSR_TUNE_BIN_COL_ITEMS: *value = c->bin_col_items; break;
+    case GSR_TUNE_BIN_COL_GROUPS: *value = c->bin_col_groups; break;
+    case GSR_TUNE_COMPLETION_EVENTS: *value = c->completion_events ? 1 : 0; break;
+    case GSR_TUNE_BLEND_BAND_TILES: *value = c->blend_band_tiles; break;
+    case GSR_TUNE_DEPTH_COMPACT: *value = c->depth_compact; break;
+    default: return set_err(GSR_E_ARG, "gsr_get_tuning: unknown knob");
+    }
+    return GSR_OK;
+}
+
 extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     if (!c) return set_err(GSR_E_ARG, "null context");
     std::lock_guard<std::mutex> lk(c->mu);
@@ -1207,8 +1232,8 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         c->tile_items = value;
         return GSR_OK;
     case GSR_TUNE_DEPTH_SORT_ITEMS:
-        if (value != 0 && value != 8 && value != 16)
-            return set_err(GSR_E_ARG, "gsr_set_tuning: depth-sort items must be 0, 8 or 16");
+        if (value != 0 && value != 4 && value != 8 && value != 16)
+            return set_err(GSR_E_ARG, "gsr_set_tuning: depth-sort items must be 0, 4, 8 or 16");
         c->depth_items = value;
         return GSR_OK;
     case GSR_TUNE_TILE_BINNING:

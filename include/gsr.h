@@ -254,6 +254,8 @@ enum {
                                         2 (default) = partition for 4D scenes only; same order, same image */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
+/* Current value of a knob (what gsr_set_tuning last set, else the default). */
+int gsr_get_tuning(gsr_context* ctx, int knob, int* value);
 /* Depth-sort digit passes the last sorted frame ran (1..4; trailing identity
  * passes are skipped on the device), or a negative error code. */
 int gsr_depth_passes(gsr_context* ctx);

@@ -6,9 +6,12 @@ pair; prints fps per setting and checks every frame equals the sequential image.
     python tools/ab_path.py [--config 2] [--rounds 5] [--frames 200] [--inflight 2 3 4]
                             [--settings 0=0 0=1 14=2,13=4 ...]
 
-A setting is a comma-separated list of gsr_set_tuning knob=value pairs applied
-before its runs (knobs: include/gsr.h GSR_TUNE_*; the first setting is the
-baseline; every setting is reset to the baseline's knobs first).
+A setting is a comma-separated list of gsr_set_tuning knob=value pairs (knobs:
+include/gsr.h GSR_TUNE_*; "-" = library defaults; the first setting is the
+baseline).  Before each setting every knob that any setting names goes back to
+its default (gsr_get_tuning at start), so nothing carries over.  One Renderer
+for all settings: separate renderers would put their lane streams on different
+hardware-queue assignments and bias the comparison.
 """
 from __future__ import annotations
 
@@ -45,6 +48,9 @@ def main():
     cam = multi.orbit_camera(0, W, H)
     stream = torch.cuda.current_stream().cuda_stream
     r = gsr.Renderer()
+    parsed = {m: [tuple(int(x) for x in kv.split("=")) for kv in m.split(",") if kv and kv != "-"]
+              for m in a.settings}
+    defaults = {kn: r.get_tuning(kn) for kvs in parsed.values() for kn, _ in kvs}
     F = max(a.inflight)
     outs = [torch.empty(3 * W * H, dtype=torch.float32, device="cuda") for _ in range(F)]
     r.render(scene, cam, W, H, outs[0].data_ptr(), stream=stream)
@@ -56,10 +62,11 @@ def main():
     for rnd in range(a.rounds + 1):          # round 0 warms every setting up (lane buffers grow)
         for f in a.inflight:
             for m in a.settings:
+                for kn, v in defaults.items():
+                    r.set_tuning(kn, v)
+                for kn, v in parsed[m]:
+                    r.set_tuning(kn, v)
                 r.set_frames_in_flight(f)
-                for kv in (a.settings[0] + "," + m).split(","):
-                    kn, v = kv.split("=")
-                    r.set_tuning(int(kn), int(v))
                 for o in outs:
                     o.zero_()
                 torch.cuda.synchronize()
