@@ -7,7 +7,7 @@ JOBS ?= 8
 
 # -ffp-contract=off: no implicit FMA anywhere (bit parity with the oracle);
 # no fast-math: IEEE division/sqrt (HIP's default correctly rounded fp32 div/sqrt).
-HIPFLAGS = -O3 -std=c++17 --offload-arch=$(ARCH) -mcode-object-version=5 -ffp-contract=off -fno-fast-math -fPIC \
+HIPFLAGS = $(EXTRA_HIPFLAGS) -O3 -std=c++17 --offload-arch=$(ARCH) -mcode-object-version=5 -ffp-contract=off -fno-fast-math -fPIC \
            -Wall -Wno-unused-result -Iinclude -Igaussianrenderer_amd/csrc
 HOSTFLAGS = -O2 -std=c++17 -I$(ROCM)/include -ffp-contract=off -fno-fast-math -fPIC -Wall -Iinclude -Igaussianrenderer_amd/csrc
 

@@ -39,6 +39,19 @@ namespace {
 __constant__ float kShC0 = 0.28209479177387814f;      // render.cu:369-377
 __constant__ float kShC1 = 0.4886025119029199f;
 
+// Geometry kernels raise their waves' instruction-issue priority (s_setprio) above
+// the blend's: with frames in flight, a geometry wave that shares a SIMD with blend
+// waves would otherwise queue behind them for the VALU.  Issue priority only: no
+// preemption, no effect on a kernel running alone (+0.8 % frames/s in flight,
+// interleaved A/B of two builds: profiles/r02_ab_setprio.txt).
+#ifndef GSR_GEOM_PRIORITY
+#define GSR_GEOM_PRIORITY 3
+#endif
+#define GSR_GEOM_PRIO()                                                            \
+    do {                                                                           \
+        if (GSR_GEOM_PRIORITY > 0) __builtin_amdgcn_s_setprio(GSR_GEOM_PRIORITY); \
+    } while (0)
+
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
 // ------------------------------------------------------------------ helpers
@@ -254,6 +267,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
                                                     uint64_t* __restrict__ items, uint64_t* __restrict__ rect,
                                                     int packed,
                                                     float tnow) {
+    GSR_GEOM_PRIO();
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     float gx = arr[GSR_A_X * stride + i];
@@ -519,6 +533,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
                                                                 uint32_t n_host, int shift, uint32_t mask,
                                                                 int groups, uint32_t* __restrict__ hist,
                                                                 uint32_t* __restrict__ dstats, int pass) {
+    GSR_GEOM_PRIO();
     __shared__ uint32_t h[4][256];
     __shared__ uint32_t s_st[4];
     if (depth_pass_skipped(dstats, pass)) return;
@@ -586,6 +601,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
 __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist, int groups,
                                                      uint32_t* __restrict__ totals,
                                                      const uint32_t* __restrict__ dstats, int pass) {
+    GSR_GEOM_PRIO();
     __shared__ uint32_t scratch[4];
     if (dstats && pass == 0 && blockIdx.x == 0) {
         // reduce the upsweep's per-workgroup plan words into dstats[0..3]
@@ -649,6 +665,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const uint32_t* __restrict__ totals, uint2* __restrict__ ranges, const uint32_t* __restrict__ dstats,
     int pass, const uint32_t* __restrict__ rect, int rect_direct, const uint32_t* __restrict__ pay_in,
     uint32_t* __restrict__ pay_out) {
+    GSR_GEOM_PRIO();
     constexpr int kTile = kSortThreads * ITEMS;
     __shared__ uint64_t s_items[kTile];
     if (depth_pass_skipped(dstats, pass)) return;
@@ -799,6 +816,7 @@ __global__ __launch_bounds__(kSortThreads) void k_kv_upsweep(const K* __restrict
                                                              const uint32_t* __restrict__ n_dev, int shift,
                                                              uint32_t mask, int groups,
                                                              uint32_t* __restrict__ hist) {
+    GSR_GEOM_PRIO();
     __shared__ uint32_t h[4][256];
     const uint32_t t = threadIdx.x;
     const uint32_t w = t >> 6;
@@ -829,6 +847,7 @@ __global__ __launch_bounds__(kSortThreads) void k_kv_downsweep(
     const K* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, K* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, const uint32_t* __restrict__ n_dev, int shift, int bits, int groups,
     const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals, uint2* __restrict__ ranges) {
+    GSR_GEOM_PRIO();
     constexpr int kTile = kSortThreads * ITEMS;
     __shared__ K s_keys[kTile];
     __shared__ uint32_t s_vals[kTile];
@@ -946,6 +965,7 @@ __global__ __launch_bounds__(256) void k_emit_count(const uint64_t* __restrict__
                                                      const uint64_t* __restrict__ rect, int groups,
                                                      unsigned long long* __restrict__ wg_sum,
                                                      uint2* __restrict__ ranges, int ntiles) {
+    GSR_GEOM_PRIO();
     __shared__ unsigned long long scr[4];
     // zero the tile ranges for the tile sort's final pass (a slice per workgroup)
     for (int q = blockIdx.x * 256 + threadIdx.x; q < ntiles; q += groups * 256) ranges[q] = make_uint2(0u, 0u);
@@ -985,6 +1005,7 @@ __global__ __launch_bounds__(256) void k_emit_count(const uint64_t* __restrict__
 __global__ __launch_bounds__(256) void k_emit_scan(unsigned long long* __restrict__ wg, int groups,
                                                     uint32_t cap, Stats* __restrict__ st,
                                                     Stats* host_st) {
+    GSR_GEOM_PRIO();
     __shared__ unsigned long long scr[4];
     const int per = (groups + 255) / 256;
     const int b = threadIdx.x * per;
@@ -1034,6 +1055,7 @@ __global__ __launch_bounds__(256) void k_emit_pairs(const uint64_t* __restrict__
                                                      const unsigned long long* __restrict__ wg_base,
                                                      uint32_t cap, int tiles_x, K* __restrict__ keys,
                                                      uint32_t* __restrict__ vals) {
+    GSR_GEOM_PRIO();
     __shared__ unsigned long long scr[4];
     __shared__ uint32_t s_incl[4][64], s_idx[4][64];
     __shared__ uint64_t s_rect[4][64];
@@ -1277,6 +1299,7 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint32
                                                          const uint32_t* __restrict__ pay1,
                                                          const uint32_t* __restrict__ dstats, int groups,
                                                          int tiles_y, uint32_t* __restrict__ hist) {
+    GSR_GEOM_PRIO();
     __shared__ uint32_t h_items[4][256], h_pairs[4][256];
     const uint32_t t = threadIdx.x, w = t >> 6;
 #pragma unroll
@@ -1329,6 +1352,7 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint32
 __global__ __launch_bounds__(256) void k_bin_rows_scan(uint32_t* __restrict__ hist, int groups, int tiles_y,
                                                         uint32_t* __restrict__ row_items,
                                                         unsigned long long* __restrict__ row_pairs) {
+    GSR_GEOM_PRIO();
     __shared__ uint32_t scr[4];
     __shared__ unsigned long long scr64[4];
     const uint32_t r = blockIdx.x, t = threadIdx.x;
@@ -1381,6 +1405,7 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
                                                            const uint32_t* __restrict__ row_items,
                                                            const unsigned long long* __restrict__ row_pairs,
                                                            uint32_t cap, int tiles_y, uint64_t* __restrict__ rows_out) {
+    GSR_GEOM_PRIO();
     constexpr uint32_t kTile = 256u * ITEMS;
     __shared__ uint32_t s_pref[kRowSources], s_idx[kRowSources];
     __shared__ uint64_t s_rect[kRowSources];
@@ -1505,6 +1530,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_count(const uint64_t* __restri
                                                          const uint32_t* __restrict__ row_items,
                                                          const unsigned long long* __restrict__ row_pairs,
                                                          uint32_t cap, int tiles_x, uint32_t* __restrict__ cbins) {
+    GSR_GEOM_PRIO();
     __shared__ ColPlan<false> pl;
     __shared__ uint32_t h[4][256], s_scr[4];
     __shared__ unsigned long long s_scr64[4];
@@ -1549,6 +1575,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restric
                                                         uint32_t cap, int tiles_x, uint32_t* __restrict__ cbins,
                                                         uint2* __restrict__ ranges, Stats* __restrict__ st,
                                                         Stats* host_st) {
+    GSR_GEOM_PRIO();
     __shared__ ColPlan<true> pl;
     __shared__ uint32_t s_scr[4];
     __shared__ unsigned long long s_scr64[4];
@@ -1591,6 +1618,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
                                                            const uint32_t* __restrict__ cbins,
                                                            const uint2* __restrict__ ranges,
                                                            uint32_t* __restrict__ vals) {
+    GSR_GEOM_PRIO();
     constexpr uint32_t kTile = 256u * ITEMS;
     __shared__ ColPlan<false> pl;
     __shared__ uint32_t s_pref[kColChunk], s_idx[kColChunk];
@@ -1679,6 +1707,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
 // visible counts, their exclusive scan (+ total), the scatter.
 __global__ __launch_bounds__(256) void k_part_count(const uint64_t* __restrict__ in, uint32_t n, int groups,
                                                      uint32_t* __restrict__ counts) {
+    GSR_GEOM_PRIO();
     __shared__ uint32_t s_scr[4];
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, 256, b, e);
@@ -1691,6 +1720,7 @@ __global__ __launch_bounds__(256) void k_part_count(const uint64_t* __restrict__
 
 __global__ __launch_bounds__(256) void k_part_scan(uint32_t* __restrict__ counts, int groups,
                                                     uint32_t* __restrict__ n_live) {
+    GSR_GEOM_PRIO();
     __shared__ uint32_t s_scr[4];
     const int per = (groups + 255) / 256;
     const int b = (int)threadIdx.x * per;
@@ -1714,6 +1744,7 @@ __global__ __launch_bounds__(256) void k_part_scatter(const uint64_t* __restrict
                                                        uint64_t* __restrict__ out,
                                                        const uint32_t* __restrict__ rect,
                                                        uint32_t* __restrict__ pay0, uint32_t* __restrict__ pay1) {
+    GSR_GEOM_PRIO();
     __shared__ uint32_t s_w[4];
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, 256, b, e);
