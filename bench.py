@@ -81,19 +81,20 @@ def algorithmic_blend_bytes(ntiles: int, consumed: int, W: int, H: int) -> int:
 def algorithmic_stage_bytes(n: int, m: int, pairs: int, ntiles: int, consumed: int, W: int, H: int,
                             depth_passes: int = 4, tile_passes: int = 2, row_items: int = -1) -> dict:
     """Minimal bytes each stage of this design must move (per-stage table):
-    preprocess N*152 read (38 fp32 SoA arrays) + M*64 records + N*16 (item + tile rect);
+    preprocess N*152 read (38 fp32 SoA arrays) + M*64 records + N*8 item + the tile
+    rect (N*4 packed on the binning path, N*8 for the pair sort);
     blend as algorithmic_blend_bytes.
-    Tile binning (row_items R >= 0): depth sort passes*N*24 (upsweep read 8, downsweep
-    read 8 + write 8) + N*16 (last pass: rect gather + depth-ordered rect write);
-    row pass ("emit") N*24 (rects for the count, items + rects for the scatter) +
-    R*8 row items; column pass ("tile_sort") R*16 (count + scatter reads) + P*4
-    values + T*8 ranges.
+    Tile binning (row_items R >= 0): depth sort passes*N*32 (upsweep read 8, downsweep
+    read 8 + 4 and write 8 + 4: item and its packed rect payload);
+    row pass ("emit") N*16 (4-B rects for the count, items + 4-B rects for the
+    scatter) + R*8 row items; column pass ("tile_sort") R*16 (count + scatter reads)
+    + P*4 values + T*8 ranges.
     Per-tile depth order (depth_passes 0): the binning as above over Gaussians in index
     order, then "depth_sort" = P*16 (list read, key gather, list write).
     Pair sort (R < 0): depth sort passes*N*24; emit N*40 (sorted items twice, rect
     gather, srect write/read) + P*6 (u16 key + u32 value); tile sort P*14 per
     non-final pass, P*12 for the final one (keys 2 up, 6 read, 6|4 write) + T*8."""
-    out = {"preprocess": 152 * n + 64 * m + 16 * n,
+    out = {"preprocess": 152 * n + 64 * m + (12 if row_items >= 0 else 16) * n,
            "blend": algorithmic_blend_bytes(ntiles, consumed, W, H)}
     if row_items >= 0 and depth_passes == 0:
         # per-tile depth order: binning in index order (rects + items read as in the
@@ -103,8 +104,8 @@ def algorithmic_stage_bytes(n: int, m: int, pairs: int, ntiles: int, consumed: i
                     "emit": 24 * n + 8 * row_items,
                     "tile_sort": 16 * row_items + 4 * pairs + 8 * ntiles})
     elif row_items >= 0:
-        out.update({"depth_sort": depth_passes * 24 * n + 16 * n,
-                    "emit": 24 * n + 8 * row_items,
+        out.update({"depth_sort": depth_passes * 32 * n,
+                    "emit": 16 * n + 8 * row_items,
                     "tile_sort": 16 * row_items + 4 * pairs + 8 * ntiles})
     else:
         out.update({"depth_sort": depth_passes * 24 * n,
