@@ -1160,7 +1160,10 @@ __global__ __launch_bounds__(256) void k_emit_pairs(const uint64_t* __restrict__
 // the same stable order as the pair sort [render.cu:788-857].
 
 constexpr uint32_t kRowSources = 1024;              // Gaussians per row-pass sub-chunk
-constexpr uint32_t kColChunk = 2048;                // row items per column-pass chunk (inside one row)
+#ifndef GSR_COL_CHUNK
+#define GSR_COL_CHUNK 2048
+#endif
+constexpr uint32_t kColChunk = GSR_COL_CHUNK;       // row items per column-pass chunk (inside one row)
 
 __device__ __forceinline__ uint32_t rect_rows(uint64_t r) {
     return rect_count(r) ? (uint32_t)((r >> 48) - ((r >> 32) & 0xffffu) + 1u) : 0u;

@@ -264,6 +264,47 @@ def test_depth_pass_plan_exact(gpu, orc, torch, c1, pos, look):
     assert np.array_equal(orders[0], orders[1])
 
 
+@pytest.mark.parametrize("items", [4, 8, 16])
+def test_depth_sort_carries_rects(gpu, orc, torch, c1, items):
+    """The depth sort carries every Gaussian's packed 4-B tile rect through its passes
+    (read at the item's position on a fresh frame, gathered by index when the same
+    frame is sorted again, since its items are then in a pass's order).  Every tile
+    size (4, 8, 16 items per thread) and the repeated sort give the first sort's tile
+    lists and the oracle's image; gsr_get_tuning reads the knob back."""
+    path, soa = c1
+    W, H = 640, 480
+    cam = cam_for(gpu, W, H, **CAMS[1])
+    scene = gpu.Scene.from_soa(soa)
+    r = gpu.Renderer()
+    assert r.get_tuning(2) == 0
+    r.set_tuning(2, items)
+    assert r.get_tuning(2) == items
+    got, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
+    want = orc.render(soa, cam, W, H, 3.0)
+    assert_image_parity(got, want)
+    first = r.read_pairs()
+    assert first.shape[0] > 10_000
+    r.sort()
+    assert np.array_equal(r.read_pairs(), first)
+    out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    r.blend(out.data_ptr())
+    assert r.sync() == 0
+    assert_image_parity(out.view(3, H, W).cpu().numpy(), want)
+
+
+def test_tuning_defaults_read_back(gpu):
+    """gsr_get_tuning returns the documented defaults (include/gsr.h) and what
+    gsr_set_tuning set; unknown knobs are refused."""
+    r = gpu.Renderer()
+    defaults = {1: 16, 2: 0, 3: 1024, 4: 0, 5: 1, 6: 1, 7: 1, 8: 4, 9: 8, 10: 0, 11: 1, 13: 4, 18: 2}
+    for kn, v in defaults.items():
+        assert r.get_tuning(kn) == v, kn
+    r.set_tuning(9, 16)
+    assert r.get_tuning(9) == 16
+    with pytest.raises(gpu.GsrError):
+        r.get_tuning(12)
+
+
 def test_blend_slow_path_and_degenerate_records(gpu, orc, torch, c1):
     """Records without the blend's fast-path proof (cull word S = inf: needle-thin
     Gaussians whose conic is not robustly positive definite and has coefficients
