@@ -39,8 +39,9 @@ constexpr int kMaxSortGroups = 8192;                    // grid upper bound (his
 struct Stats {
     unsigned long long pairs_total;   // P before the capacity clamp
     uint32_t pairs_eff;               // min(P, capacity): what sort/ranges/blend consume
-    uint32_t overflow;                // 1 if P > capacity
-    uint32_t pad;
+    uint32_t overflow;                // bit 0: P > capacity; bit 1: the depth sort needed more
+                                      // passes than were launched (depth pass budget)
+    uint32_t depth_passes;            // passes the depth sort's device plan needed (binning path; 0: n/a)
 };
 
 // ---- launch wrappers (gsr_kernels.hip) ----
@@ -96,7 +97,7 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
 hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, const unsigned long long* row_pairs,
                            uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
                            uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,
-                           hipStream_t s);
+                           hipStream_t s, const uint32_t* dstats = nullptr, int passes_launched = 4);
 uint32_t bin_col_chunks_max(uint32_t pair_capacity, int tiles_y);
 // Standalone sort ABI helpers (oneSweepSort / oneSweep3DGaussianSort).
 hipError_t launch_items_from_keys(const int* keys, uint32_t n, uint64_t* items, hipStream_t s);

@@ -1291,22 +1291,29 @@ __device__ __forceinline__ void bin_tile_owners(const uint32_t (&cnt)[PER], cons
 
 // Frame pair statistics (st[0]) + the sticky copy (st[1], and the host-mapped
 // mirror) the non-blocking overflow check reads.
+// Binning path: `needed` = depth passes the device plan asked for, `launched` = passes
+// the host launched (its pass budget); needed > launched leaves the depth order
+// incomplete, so the frame is flagged (overflow bit 1) and re-rendered like a
+// pair-buffer overflow.  depth_passes is the latest frame's, not sticky.
 __device__ __forceinline__ void publish_pair_stats(unsigned long long total, uint32_t cap, Stats* st,
-                                                   Stats* host_st) {
+                                                   Stats* host_st, uint32_t needed = 0, uint32_t launched = 4) {
     Stats s{};
     s.pairs_total = total;
     s.pairs_eff = (uint32_t)(total < cap ? total : cap);
-    s.overflow = total > cap ? 1u : 0u;
+    s.overflow = (total > cap ? 1u : 0u) | (needed > launched ? 2u : 0u);
+    s.depth_passes = needed;
     st[0] = s;
     Stats k = st[1];
     if (s.pairs_total > k.pairs_total) k.pairs_total = s.pairs_total;
     k.pairs_eff = s.pairs_eff;
     k.overflow |= s.overflow;
+    k.depth_passes = s.depth_passes;
     st[1] = k;
     if (host_st) {
         host_st->pairs_total = k.pairs_total;
         host_st->pairs_eff = k.pairs_eff;
         host_st->overflow = k.overflow;
+        host_st->depth_passes = k.depth_passes;
         __threadfence_system();
     }
 }
@@ -1594,14 +1601,17 @@ __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restric
                                                         const unsigned long long* __restrict__ row_pairs,
                                                         uint32_t cap, int tiles_x, uint32_t* __restrict__ cbins,
                                                         uint2* __restrict__ ranges, Stats* __restrict__ st,
-                                                        Stats* host_st) {
+                                                        Stats* host_st, const uint32_t* __restrict__ dstats,
+                                                        int passes_launched) {
     GSR_GEOM_PRIO();
     __shared__ ColPlan<true> pl;
     __shared__ uint32_t s_scr[4];
     __shared__ unsigned long long s_scr64[4];
     const uint32_t t = threadIdx.x, r = blockIdx.x;
     const unsigned long long P = col_plan(row_items, row_pairs, pl, s_scr, s_scr64);
-    if (r == 0 && t == 0) publish_pair_stats(P, cap, st, host_st);
+    if (r == 0 && t == 0)
+        publish_pair_stats(P, cap, st, host_st, dstats ? (uint32_t)depth_passes_run(dstats) : 0u,
+                           (uint32_t)passes_launched);
     uint32_t run = 0;
     if (P <= cap && t < (uint32_t)tiles_x) {
         // 32 chunks per step: the loads are issued together, not one round trip per chunk
@@ -2375,14 +2385,14 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
 hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, const unsigned long long* row_pairs,
                            uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
                            uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,
-                           hipStream_t s) {
+                           hipStream_t s, const uint32_t* dstats, int passes_launched) {
     if (tiles_x < 1 || tiles_x > 256 || tiles_y < 1 || tiles_y > 256 || col_groups < 1 ||
         (items != 4 && items != 8 && items != 16))
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_bin_cols_count, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs,
                        pair_capacity, tiles_x, cbins);
     hipLaunchKernelGGL(k_bin_cols_scan, dim3(tiles_y), dim3(256), 0, s, row_items, row_pairs, pair_capacity, tiles_x,
-                       cbins, ranges, stats, host_mapped_stats);
+                       cbins, ranges, stats, host_mapped_stats, dstats, passes_launched);
     auto scatter = tiles_x <= 128 ? (items == 4 ? k_bin_cols_scatter<4, 7> : items == 8 ? k_bin_cols_scatter<8, 7>
                                                                                     : k_bin_cols_scatter<16, 7>)
                                   : (items == 4 ? k_bin_cols_scatter<4, 8> : items == 8 ? k_bin_cols_scatter<8, 8>

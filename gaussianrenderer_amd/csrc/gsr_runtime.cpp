@@ -333,6 +333,10 @@ struct gsr_context {
     int tile_groups = 1024;          // tile sort: workgroup cap (measured best: 2 tiles of items per group)
     int tile_split_even = 1;         // tile sort: digits split evenly over the passes
     int depth_skip = 1;              // depth sort: skip trailing identity passes (device-side plan)
+    int depth_budget = 4;            // binning path: depth passes launched (adapts to the plan's needs)
+    int depth_budget_streak = 0;     // consecutive checked frames that needed fewer passes than the budget
+    int depth_budget_seen = 0;       // most passes any of those frames needed
+    int passes_launched = 4;         // passes the last depth sort launched
     uint32_t* dstats = nullptr;      // depth-sort pass plan: 4 final words + 4 per upsweep workgroup
     uint32_t* nlive = nullptr;       // visible count of the live partition (device word)
     int depth_compact = 2;           // live partition before the depth sort: 0 off, 1 on, 2 4D scenes only
@@ -497,7 +501,39 @@ int check_overflow(gsr_context* c, bool blocking) {
     s.pairs_total = hv->pairs_total;
     s.pairs_eff = hv->pairs_eff;
     s.overflow = hv->overflow;
-    if (!s.overflow) return GSR_OK;
+    s.depth_passes = hv->depth_passes;
+    if (s.overflow == 2u) {
+        // the depth sort needed more passes than the budget launched: back to four,
+        // and the frame(s) since the last check re-render (GSR_E_OVERFLOW)
+        HIP_TRY(hipDeviceSynchronize());
+        c->depth_budget = 4;
+        c->depth_budget_streak = 0;
+        c->depth_budget_seen = 0;
+        HIP_TRY(hipMemset(c->stats + 1, 0, sizeof(Stats)));
+        std::memset(c->hstats, 0, sizeof(Stats));
+        return set_err(GSR_E_OVERFLOW, "depth sort needed %u passes, %d were launched; re-render",
+                       (unsigned)s.depth_passes, c->passes_launched);
+    }
+    if (!s.overflow) {
+        // lower the pass budget once 4 checked frames in a row needed fewer passes
+        if (s.depth_passes >= 1 && (int)s.depth_passes < c->depth_budget) {
+            c->depth_budget_seen = std::max(c->depth_budget_seen, (int)s.depth_passes);
+            if (++c->depth_budget_streak >= 4) {
+                c->depth_budget = c->depth_budget_seen;
+                c->depth_budget_streak = 0;
+                c->depth_budget_seen = 0;
+            }
+        } else {
+            c->depth_budget_streak = 0;
+            c->depth_budget_seen = 0;
+        }
+        return GSR_OK;
+    }
+    if (s.overflow & 2u) {
+        c->depth_budget = 4;
+        c->depth_budget_streak = 0;
+        c->depth_budget_seen = 0;
+    }
     // frames queued after the event may still be running: drain them so the
     // grown capacity covers their totals too (ensure_pairs syncs again; cheap)
     HIP_TRY(hipDeviceSynchronize());
@@ -664,7 +700,14 @@ static int depth_sort_locked(gsr_context* c, bool with_rects) {
     // items[1] is the sort's scratch from here on; a repeated sort of this frame sorts
     // the whole partitioned items[0] (same order: visible and culled keys never tie)
     if (part) c->compact_frame = false;
-    for (int p = 0; p < 4; p++)
+    // Trailing passes the device plan skips still cost a launch each (upsweep, scan and
+    // downsweep returning at once: ~12 us of the frame's dependent chain).  On the
+    // binning path the host launches only as many passes as recent frames needed
+    // (depth_budget, check_overflow); a frame that needs more is flagged by the
+    // column scan and re-rendered with all four, like a pair-buffer overflow.
+    const int launch = with_rects && c->depth_skip ? std::max(1, std::min(4, c->depth_budget)) : 4;
+    c->passes_launched = launch;
+    for (int p = 0; p < launch; p++)
         HIP_TRY(gsr::launch_radix_pass(c->items[p & 1], c->items[(p + 1) & 1], part ? c->nlive : nullptr, n, 32 + 8 * p, 8, gd, di,
                                        c->hist, c->totals, nullptr, c->stream, c->depth_skip ? c->dstats : nullptr,
                                        p, with_rects ? reinterpret_cast<const uint32_t*>(c->rect) : nullptr, rect_mode,
@@ -706,7 +749,8 @@ static int sort_locked(gsr_context* c) {
                                            : (int)std::min<int64_t>(4096, std::max<int64_t>(1024, c->n / 1024));
         HIP_TRY(gsr::launch_bin_cols(c->pairs[0], row_items, row_pairs, c->cbins, gcol, cap,
                                      c->fr.tiles_x, c->fr.tiles_y, pair_vals(c, 1), c->ranges, c->stats,
-                                     c->hstats_dev, c->bin_col_items, c->stream));
+                                     c->hstats_dev, c->bin_col_items, c->stream,
+                                     c->depth_skip ? c->dstats : nullptr, c->passes_launched));
         c->pair_buf = 1;
         mark(c, GSR_STAGE_RANGES);
         c->have_sort = true;

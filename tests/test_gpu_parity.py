@@ -305,6 +305,30 @@ def test_tuning_defaults_read_back(gpu):
         r.get_tuning(12)
 
 
+def test_depth_pass_budget_adapts_and_recovers(gpu, orc, torch, c1):
+    """The binning path launches only the depth passes recent frames needed (4 checked
+    frames needing 3 lower the budget to 3).  A frame whose keys then need 4 (camera
+    at 17.3: keys straddle 2^24) is flagged — gsr_sync reports an overflow — and its
+    re-render runs all four passes, bit-exact against the oracle."""
+    path, soa = c1
+    W, H = 640, 480
+    scene = gpu.Scene.from_soa(soa)
+    near = cam_for(gpu, W, H, pos=(0, 0, 4))
+    far = cam_for(gpu, W, H, pos=(0, 0, 17.3))
+    r = gpu.Renderer()
+    out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    for i in range(8):
+        r.render(scene, near, W, H, out.data_ptr())
+        assert r.sync() == 0 or i == 0
+        assert r.depth_passes() == 3
+    assert_image_parity(out.view(3, H, W).cpu().numpy(), orc.render(soa, near, W, H, 3.0))
+    r.render(scene, far, W, H, out.data_ptr())
+    assert r.sync() != 0                      # launched 3, needed 4: flagged
+    r.render(scene, far, W, H, out.data_ptr())
+    assert r.sync() == 0 and r.depth_passes() == 4
+    assert_image_parity(out.view(3, H, W).cpu().numpy(), orc.render(soa, far, W, H, 3.0))
+
+
 def test_blend_slow_path_and_degenerate_records(gpu, orc, torch, c1):
     """Records without the blend's fast-path proof (cull word S = inf: needle-thin
     Gaussians whose conic is not robustly positive definite and has coefficients
