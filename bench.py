@@ -225,18 +225,41 @@ def host_cpu() -> dict:
 
 
 def gpu_telemetry() -> dict | None:
-    """Clocks, power and temperature of the card(s) from rocm-smi (host-side child
-    process, read outside the timed region), or None when it is unavailable."""
-    import subprocess
-    try:
-        out = subprocess.run(["rocm-smi", "--showpower", "--showclocks", "--showtemp", "--json"],
-                             capture_output=True, text=True, timeout=30).stdout
-        d = json.loads(out[out.index("{"):])
-    except (OSError, ValueError, subprocess.SubprocessError):
-        return None
-    keep = ("power", "sclk", "mclk", "fclk", "socclk", "junction", "memory")
-    return {card: {k: v for k, v in vals.items() if any(w in k.lower() for w in keep)}
-            for card, vals in d.items() if isinstance(vals, dict)}
+    """Clocks, power and temperature of the card(s), read in-process from sysfs
+    (amdgpu's pp_dpm_* current levels and hwmon sensors) outside the timed region;
+    None when unavailable.  No child process: a process that has initialised the GPU
+    must not start programs that re-exec themselves (rocm-smi is a script)."""
+    import glob
+    cards = {}
+    for dev in sorted(glob.glob("/sys/class/drm/card[0-9]*/device")):
+        if not os.path.exists(os.path.join(dev, "pp_dpm_sclk")):
+            continue
+        card = os.path.basename(os.path.dirname(dev))
+        vals = {}
+        for clk in ("sclk", "mclk", "fclk", "socclk"):
+            try:
+                with open(os.path.join(dev, f"pp_dpm_{clk}")) as f:
+                    cur = [ln.split(":", 1)[1].strip().rstrip("*").strip() for ln in f if ln.rstrip().endswith("*")]
+                if cur:
+                    vals[f"{clk} (current dpm level)"] = cur[0]
+            except OSError:
+                pass
+        for hw in glob.glob(os.path.join(dev, "hwmon", "hwmon*")):
+            for inp in sorted(glob.glob(os.path.join(hw, "temp*_input"))):
+                try:
+                    lab = inp.replace("_input", "_label")
+                    name = open(lab).read().strip() if os.path.exists(lab) else os.path.basename(inp)
+                    vals[f"temperature {name} (C)"] = int(open(inp).read()) / 1000.0
+                except (OSError, ValueError):
+                    pass
+            for pw in ("power1_average", "power1_input"):
+                try:
+                    vals[f"{pw} (W)"] = int(open(os.path.join(hw, pw)).read()) / 1e6
+                except (OSError, ValueError):
+                    pass
+        if vals:
+            cards[card] = vals
+    return cards or None
 
 
 def frame_time(i: int) -> float:
