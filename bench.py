@@ -224,8 +224,9 @@ def host_cpu() -> dict:
     return {"model": model, "logical_cpus": os.cpu_count()}
 
 
-def gpu_telemetry() -> dict | None:
-    """Clocks, power and temperature of the card(s), read in-process from sysfs
+def gpu_telemetry(pci: str | None = None) -> dict | None:
+    """Clocks, power and temperature of this rank's card (PCI address `pci`, e.g.
+    "0000:75:00.0"; sysfs lists every card of the host), read in-process from sysfs
     (amdgpu's pp_dpm_* current levels and hwmon sensors) outside the timed region;
     None when unavailable.  No child process: a process that has initialised the GPU
     must not start programs that re-exec themselves (rocm-smi is a script)."""
@@ -233,6 +234,8 @@ def gpu_telemetry() -> dict | None:
     cards = {}
     for dev in sorted(glob.glob("/sys/class/drm/card[0-9]*/device")):
         if not os.path.exists(os.path.join(dev, "pp_dpm_sclk")):
+            continue
+        if pci is None or os.path.basename(os.path.realpath(dev)).lower() != pci.lower():
             continue
         card = os.path.basename(os.path.dirname(dev))
         vals = {}
@@ -393,7 +396,10 @@ def main():
 
     # clocks and power before the timed regions (a ~1 s host-side child process, so it
     # runs before the sustained warmup, never between warmup and timing)
-    telemetry_before = gpu_telemetry() if rank == 0 else None
+    props = torch.cuda.get_device_properties(device)
+    pci = (f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}.0"
+           if hasattr(props, "pci_bus_id") else None)
+    telemetry_before = gpu_telemetry(pci) if rank == 0 else None
     # sustained warmup: the card leaves its idle power state over tens of ms, so a
     # short K (the driver's --steps 20 is ~10 ms of frames) would otherwise be timed on
     # the ramp.  Frames in flight for at least --warm-ms of wall time, untimed.
@@ -426,7 +432,7 @@ def main():
     else:
         elapsed, blend_times_pipe, timed_frames_pipe = seq_elapsed, blend_times, timed_frames
     overflow = r.sync() or seq_overflow
-    telemetry_after = gpu_telemetry() if rank == 0 else None
+    telemetry_after = gpu_telemetry(pci) if rank == 0 else None
 
     max_elapsed = multi.max_over_ranks(dist, elapsed, "cpu" if gloo else "cuda")
     max_seq = multi.max_over_ranks(dist, seq_elapsed, "cpu" if gloo else "cuda")
