@@ -1,0 +1,105 @@
+// Streaming-bandwidth yardstick (gfx950): what a plain coalesced kernel reaches on
+// this HBM3E — read-only (sum), copy, write-only, and a 38-stream read shaped like
+// k_preprocess (one thread per element, one 4-B load from each of 38 arrays) — so
+// the geometry kernels' GB/s can be set against the practical rate, not only the
+// 8 TB/s spec.  Sizes: 1 GiB per array pass (larger than the 256 MB MALL).
+//   hipcc --offload-arch=gfx950 -O3 -o stream_rate stream_rate.hip && ./stream_rate
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+#define CHECK(x)                                                                      \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            return 1;                                                                 \
+        }                                                                             \
+    } while (0)
+
+__global__ __launch_bounds__(256) void k_read(const float4* __restrict__ a, size_t n, float* out) {
+    float s = 0.0f;
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const float4 v = a[i];
+        s += v.x + v.y + v.z + v.w;
+    }
+    if (s == 1.2345f) out[0] = s;
+}
+
+__global__ __launch_bounds__(256) void k_copy(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) b[i] = a[i];
+}
+
+__global__ __launch_bounds__(256) void k_write(float4* __restrict__ b, size_t n) {
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        b[i] = make_float4(1.0f, 2.0f, 3.0f, 4.0f);
+}
+
+// 38 arrays of n floats, one thread per element (the preprocess's access shape), all
+// loads issued before use; writes one 16-B word per element (its record's shape).
+__global__ __launch_bounds__(256) void k_soa38(const float* __restrict__ a, size_t stride, size_t n,
+                                               float4* __restrict__ rec) {
+    const size_t i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    float v[38];
+#pragma unroll
+    for (int k = 0; k < 38; k++) v[k] = a[k * stride + i];
+    float s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+    for (int k = 0; k < 38; k += 4) {
+        s0 += v[k];
+        if (k + 1 < 38) s1 += v[k + 1];
+        if (k + 2 < 38) s2 += v[k + 2];
+        if (k + 3 < 38) s3 += v[k + 3];
+    }
+    rec[i] = make_float4(s0, s1, s2, s3);
+}
+
+int main() {
+    const size_t bytes = 1ull << 30, n4 = bytes / 16;
+    float4 *a, *b;
+    float* out;
+    CHECK(hipMalloc(&a, bytes));
+    CHECK(hipMalloc(&b, bytes));
+    CHECK(hipMalloc(&out, 64));
+    CHECK(hipMemset(a, 0, bytes));
+    CHECK(hipMemset(b, 0, bytes));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    const int grids[] = {1024, 2048, 4096, 8192};
+    for (int g : grids) {
+        float best[3] = {1e9f, 1e9f, 1e9f};
+        for (int rep = 0; rep < 5; rep++) {
+            for (int k = 0; k < 3; k++) {
+                CHECK(hipEventRecord(e0));
+                if (k == 0) hipLaunchKernelGGL(k_read, dim3(g), dim3(256), 0, 0, a, n4, out);
+                if (k == 1) hipLaunchKernelGGL(k_copy, dim3(g), dim3(256), 0, 0, a, b, n4 / 2);
+                if (k == 2) hipLaunchKernelGGL(k_write, dim3(g), dim3(256), 0, 0, b, n4);
+                CHECK(hipEventRecord(e1));
+                CHECK(hipEventSynchronize(e1));
+                float ms;
+                CHECK(hipEventElapsedTime(&ms, e0, e1));
+                if (ms < best[k]) best[k] = ms;
+            }
+        }
+        printf("grid %5d x 256: read %.0f GB/s  copy (half read, half write) %.0f GB/s  write %.0f GB/s\n", g,
+               bytes / (best[0] * 1e6), bytes / (best[1] * 1e6), bytes / (best[2] * 1e6));
+    }
+    // preprocess shape at config 3 size: 5M elements x 38 arrays (760 MB) + 80 MB of 16-B writes
+    const size_t n = 5000000, stride = (n + 63) / 64 * 64;
+    float best = 1e9f;
+    for (int rep = 0; rep < 5; rep++) {
+        CHECK(hipEventRecord(e0));
+        hipLaunchKernelGGL(k_soa38, dim3((n + 255) / 256), dim3(256), 0, 0, reinterpret_cast<const float*>(a), stride,
+                           n, b);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < best) best = ms;
+    }
+    const double mb = (38.0 * 4 * n + 16.0 * n) / 1e6;
+    printf("38-array SoA read + 16-B write, 5M elements (%.0f MB): %.1f us, %.0f GB/s\n", mb, best * 1e3,
+           mb / (best * 1e3) * 1e3);
+    return 0;
+}
