@@ -6,7 +6,7 @@
 // blend-like: 32,640 one-wave workgroups (the config-2 blend's grid), 6 KB of LDS
 // each (~26 per CU resident, like the blend), 20-100 us of dependent FMAs each.
 // chain: 16 phases; each phase streams a 4 MB slice (read + write) over G
-// workgroups of 256 threads.  "kernels": one launch per phase on a second stream;
+// workgroups of 256 threads (or 4 G one-wave workgroups).  "kernels": one launch per phase on a second stream;
 // "resident": one launch of G workgroups, a grid barrier between phases (bounded
 // spin: a barrier that waits too long sets an error flag and the kernel exits).
 //   hipcc --offload-arch=gfx950 -O3 -o chain_probe chain_probe.hip && ./chain_probe
@@ -61,10 +61,16 @@ __device__ __forceinline__ void phase_work(const float* in, float* out, int phas
     for (size_t i = b + threadIdx.x; i < b + per; i += 256) dst[i] = src[i] * 1.5f + 1.0f;
 }
 
-__global__ __launch_bounds__(256) void k_phase(const float* in, float* out, int phase, unsigned long long* t) {
+template <int TPB>
+__global__ __launch_bounds__(TPB) void k_phase(const float* in, float* out, int phase, unsigned long long* t) {
     __builtin_amdgcn_s_setprio(3);
     if (phase == 0 && threadIdx.x == 0) atomicMin(&t[2], (unsigned long long)now());
-    phase_work(in, out, phase, blockIdx.x, gridDim.x);
+    // TPB threads per workgroup: the same slice per phase, split over gridDim.x workgroups
+    const size_t per = kSlice / gridDim.x;
+    const size_t b = (size_t)blockIdx.x * per;
+    const float* src = in + (size_t)phase * kSlice;
+    float* dst = out + (size_t)phase * kSlice;
+    for (size_t i = b + threadIdx.x; i < b + per; i += TPB) dst[i] = src[i] * 1.5f + 1.0f;
     if (phase == kPhases - 1 && threadIdx.x == 0) atomicMax(&t[3], (unsigned long long)now());
 }
 
@@ -114,21 +120,26 @@ int main() {
     printf("blend-like: %d one-wave workgroups, 20-100 us each; chain: %d phases of a 4 MB slice (read+write)\n"
            "times in us; 'chain' counts from the chain's first wave to its last\n", blend_groups, kPhases);
     const unsigned long long init[4] = {~0ull, 0ull, ~0ull, 0ull};
-    for (int rep = 0; rep < 3; rep++) {
-        // mode 0: blend-like alone; 1: kernels alone; 2: resident alone; 3: blend + kernels; 4: blend + resident
-        for (int G : {256, 512}) {
-            for (int mode = 0; mode < 5; mode++) {
-                if (mode == 0 && G == 512) continue;
+    for (int rep = 0; rep < 2; rep++) {
+        // mode 0: blend-like alone; 1: kernels alone; 2: resident alone; 3: blend + kernels; 4: blend + resident;
+        // 5: one-wave-workgroup kernels alone; 6: blend + one-wave-workgroup kernels
+        for (int G : {256, 512, 1024}) {
+            for (int mode = 0; mode < 7; mode++) {
+                if (mode == 0 && G != 256) continue;
+                if ((mode == 2 || mode == 4) && G > 512) continue;   // resident: at most 2 workgroups per CU
                 CHECK(hipMemcpy(t, init, 32, hipMemcpyHostToDevice));
                 CHECK(hipMemset(ctr, 0, 4));
                 CHECK(hipMemset(err, 0, 4));
                 CHECK(hipDeviceSynchronize());
-                const bool blend = mode == 0 || mode >= 3;
+                const bool blend = mode == 0 || mode == 3 || mode == 4 || mode == 6;
                 if (blend) hipLaunchKernelGGL(k_blendlike, dim3(blend_groups), dim3(64), 0, sa, t, sink);
                 if (blend && mode != 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
                 if (mode == 1 || mode == 3)
                     for (int p = 0; p < kPhases; p++)
-                        hipLaunchKernelGGL(k_phase, dim3(G), dim3(256), 0, sb, in, out, p, t);
+                        hipLaunchKernelGGL(k_phase<256>, dim3(G), dim3(256), 0, sb, in, out, p, t);
+                if (mode == 5 || mode == 6)   // one-wave workgroups, 4x as many (same threads)
+                    for (int p = 0; p < kPhases; p++)
+                        hipLaunchKernelGGL(k_phase<64>, dim3(4 * G), dim3(64), 0, sb, in, out, p, t);
                 if (mode == 2 || mode == 4) hipLaunchKernelGGL(k_resident, dim3(G), dim3(256), 0, sb, in, out, ctr, err, t);
                 CHECK(hipGetLastError());
                 CHECK(hipDeviceSynchronize());
@@ -137,8 +148,8 @@ int main() {
                 CHECK(hipMemcpy(h, t, 32, hipMemcpyDeviceToHost));
                 CHECK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
                 const char* names[] = {"blend alone", "kernels alone", "resident alone", "blend + kernels",
-                                       "blend + resident"};
-                printf("rep %d G %3d %-17s", rep, G, names[mode]);
+                                       "blend + resident", "64-thr kernels alone", "blend + 64-thr kernels"};
+                printf("rep %d G %4d %-22s", rep, G, names[mode]);
                 if (blend) printf("  blend %7.1f", (h[1] - h[0]) / 100.0);
                 if (mode) printf("  chain %7.1f", (h[3] - h[2]) / 100.0);
                 if (blend && mode) printf("  (chain start %+7.1f, end %+7.1f vs blend start)",
