@@ -12,6 +12,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -o chain_probe chain_probe.hip && ./chain_probe
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cstdio>
 #include <thread>
@@ -65,6 +66,7 @@ template <int TPB>
 __global__ __launch_bounds__(TPB) void k_phase(const float* in, float* out, int phase, unsigned long long* t) {
     __builtin_amdgcn_s_setprio(3);
     if (phase == 0 && threadIdx.x == 0) atomicMin(&t[2], (unsigned long long)now());
+    if (threadIdx.x == 0) atomicMin(&t[4 + 2 * phase], (unsigned long long)now());   // per-phase first start
     // TPB threads per workgroup: the same slice per phase, split over gridDim.x workgroups
     const size_t per = kSlice / gridDim.x;
     const size_t b = (size_t)blockIdx.x * per;
@@ -72,6 +74,7 @@ __global__ __launch_bounds__(TPB) void k_phase(const float* in, float* out, int 
     float* dst = out + (size_t)phase * kSlice;
     for (size_t i = b + threadIdx.x; i < b + per; i += TPB) dst[i] = src[i] * 1.5f + 1.0f;
     if (phase == kPhases - 1 && threadIdx.x == 0) atomicMax(&t[3], (unsigned long long)now());
+    if (threadIdx.x == 0) atomicMax(&t[5 + 2 * phase], (unsigned long long)now());   // per-phase last end
 }
 
 __global__ __launch_bounds__(256) void k_resident(const float* in, float* out, unsigned* ctr, unsigned* err,
@@ -103,13 +106,21 @@ __global__ __launch_bounds__(256) void k_resident(const float* in, float* out, u
 }
 
 int main() {
+    // CHAIN_FIRST=1: the chain's stream is created before the blend-like one (HIP hands
+    // out hardware queues in creation order; does the queue order decide who waits?)
     hipStream_t sa, sb;
-    CHECK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
-    CHECK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+    const char* cf = getenv("CHAIN_FIRST");
+    if (cf && cf[0] == '1') {
+        CHECK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+        CHECK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+    } else {
+        CHECK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+        CHECK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+    }
     unsigned long long* t;
     unsigned *ctr, *err;
     float *in, *out, *sink;
-    CHECK(hipMalloc(&t, 32));
+    CHECK(hipMalloc(&t, 8 * (4 + 2 * kPhases)));
     CHECK(hipMalloc(&ctr, 4));
     CHECK(hipMalloc(&err, 4));
     CHECK(hipMalloc(&in, kPhases * kSlice * 4));
@@ -119,7 +130,8 @@ int main() {
     const int blend_groups = 32640;
     printf("blend-like: %d one-wave workgroups, 20-100 us each; chain: %d phases of a 4 MB slice (read+write)\n"
            "times in us; 'chain' counts from the chain's first wave to its last\n", blend_groups, kPhases);
-    const unsigned long long init[4] = {~0ull, 0ull, ~0ull, 0ull};
+    unsigned long long init[4 + 2 * kPhases];
+    for (int i = 0; i < 4 + 2 * kPhases; i++) init[i] = (i % 2 == 0) ? ~0ull : 0ull;
     for (int rep = 0; rep < 2; rep++) {
         // mode 0: blend-like alone; 1: kernels alone; 2: resident alone; 3: blend + kernels; 4: blend + resident;
         // 5: one-wave-workgroup kernels alone; 6: blend + one-wave-workgroup kernels
@@ -127,7 +139,7 @@ int main() {
             for (int mode = 0; mode < 7; mode++) {
                 if (mode == 0 && G != 256) continue;
                 if ((mode == 2 || mode == 4) && G > 512) continue;   // resident: at most 2 workgroups per CU
-                CHECK(hipMemcpy(t, init, 32, hipMemcpyHostToDevice));
+                CHECK(hipMemcpy(t, init, sizeof init, hipMemcpyHostToDevice));
                 CHECK(hipMemset(ctr, 0, 4));
                 CHECK(hipMemset(err, 0, 4));
                 CHECK(hipDeviceSynchronize());
@@ -143,9 +155,9 @@ int main() {
                 if (mode == 2 || mode == 4) hipLaunchKernelGGL(k_resident, dim3(G), dim3(256), 0, sb, in, out, ctr, err, t);
                 CHECK(hipGetLastError());
                 CHECK(hipDeviceSynchronize());
-                unsigned long long h[4];
+                unsigned long long h[4 + 2 * kPhases];
                 unsigned herr;
-                CHECK(hipMemcpy(h, t, 32, hipMemcpyDeviceToHost));
+                CHECK(hipMemcpy(h, t, sizeof h, hipMemcpyDeviceToHost));
                 CHECK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
                 const char* names[] = {"blend alone", "kernels alone", "resident alone", "blend + kernels",
                                        "blend + resident", "64-thr kernels alone", "blend + 64-thr kernels"};
@@ -156,6 +168,13 @@ int main() {
                                           ((double)h[2] - (double)h[0]) / 100.0, ((double)h[3] - (double)h[0]) / 100.0);
                 if (herr) printf("  BARRIER TIMEOUT");
                 printf("\n");
+                if (blend && (mode == 3 || mode == 6) && G == 256) {   // per-phase [start, end] vs blend start
+                    printf("      phases:");
+                    for (int p = 0; p < kPhases; p++)
+                        printf(" [%.0f,%.0f]", ((double)h[4 + 2 * p] - (double)h[0]) / 100.0,
+                               ((double)h[5 + 2 * p] - (double)h[0]) / 100.0);
+                    printf("\n");
+                }
             }
         }
     }
