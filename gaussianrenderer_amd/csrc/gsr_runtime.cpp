@@ -1390,12 +1390,16 @@ int gsr::dropin_render_device(gsr_gaussian* d_gaussians, int num_gaussians, cons
     if (num_gaussians > 0 && d_gaussians) {
         gsr_scene_header h{};
         *what = "scene";
-        // the magic first (16 B fit inside any 240-B AoS record), the rest of the
-        // header only once it is known to be our block
-        HIP_TRY(hipMemcpy(&h.magic, d_gaussians, sizeof h.magic, hipMemcpyDeviceToHost));
+        // One synchronous read (~16 us each on the viewer's frame): the whole header
+        // when even an AoS buffer of num_gaussians records is at least that long (2+
+        // records), else the magic first (16 B fit inside any 240-B AoS record) and the
+        // rest of the header only once it is known to be our block.
+        const bool whole = (int64_t)num_gaussians * (int64_t)sizeof(gsr_gaussian) >= (int64_t)sizeof h;
+        HIP_TRY(hipMemcpy(whole ? static_cast<void*>(&h) : static_cast<void*>(&h.magic), d_gaussians,
+                          whole ? sizeof h : sizeof h.magic, hipMemcpyDeviceToHost));
         if (h.magic[0] == GSR_SCENE_MAGIC0 && h.magic[1] == GSR_SCENE_MAGIC1 && h.magic[2] == GSR_SCENE_MAGIC2 &&
             h.magic[3] == GSR_SCENE_MAGIC3) {
-            HIP_TRY(hipMemcpy(&h, d_gaussians, sizeof h, hipMemcpyDeviceToHost));
+            if (!whole) HIP_TRY(hipMemcpy(&h, d_gaussians, sizeof h, hipMemcpyDeviceToHost));
             // 4D blocks render at the drop-in context's time (gsr_set_time on it is not
             // reachable through this ABI, so t = 0: the sequence's first frame)
             layout = h.narrays == GSR_SCENE4D_NARRAYS    ? GSR_LAYOUT_SCENE_BLOCK_4D

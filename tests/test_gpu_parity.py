@@ -414,19 +414,35 @@ def aos_records(soa):
     return rec
 
 
-def test_dropin_aos_input(gpu, orc, torch, c1):
-    """A reference-layout Gaussian[] device array (e.g. from the reference's own loader)."""
+@pytest.mark.parametrize("n", [4000, 2, 1])
+def test_dropin_aos_input(gpu, orc, torch, c1, n):
+    """A reference-layout Gaussian[] device array (e.g. from the reference's own loader).
+    One and two records: the layout probe reads 16 B first when the whole 256-B header
+    would run past a 240-B array, one 256-B read otherwise."""
     path, soa = c1
     W, H = 320, 240
-    rec = aos_records(soa[:, :4000])
-    dev = torch.from_numpy(rec).cuda()
     cam = cam_for(gpu, W, H, pos=(0.3, 0.2, 3.5))
+    if n < 10:   # splats in view, so the tiny images are not trivially empty
+        spl = orc.preprocess(soa, cam, W, H, 3.0)
+        vis = np.nonzero(spl["status"] == 2)[0]
+        sub = soa[:, vis[:n]]
+    else:
+        sub = soa[:, :n]
+    rec = aos_records(sub)
+    dev = torch.from_numpy(rec).cuda()
     t = gpu.TilingInformation(40, 40, H, W)
-    got = gpu.preprocessCUDAGaussians(dev.data_ptr(), 4000, cam, t.num_tile_y, t.num_tile_x, t.width_stride,
+    got = gpu.preprocessCUDAGaussians(dev.data_ptr(), n, cam, t.num_tile_y, t.num_tile_x, t.width_stride,
                                       t.height_stride, W, H, 3.0)
     torch.cuda.synchronize()
-    want = orc.render(soa[:, :4000], cam, W, H, 3.0, tiling=(40, 40, t.width_stride, t.height_stride))
+    want = orc.render(sub, cam, W, H, 3.0, tiling=(40, 40, t.width_stride, t.height_stride))
+    assert (want != 0).any()
     assert_image_parity(got, want)
+    # the same splats as a one- or two-Gaussian scene block through the drop-in
+    if n < 10:
+        scene = gpu.Scene.from_soa(np.ascontiguousarray(sub))
+        got2 = gpu.preprocessCUDAGaussians(scene.ptr, n, cam, t.num_tile_y, t.num_tile_x, t.width_stride,
+                                           t.height_stride, W, H, 3.0)
+        assert_image_parity(got2, want)
 
 
 @pytest.mark.parametrize("tiling", [(8, 8, 40, 30), (7, 3, 92, 160), (3, 5, 100, 100)])
