@@ -4,10 +4,10 @@
 //   k_preprocess      one thread per Gaussian, SoA coalesced loads: cull + SH
 //                     colour + view/clip + 2D covariance + extent + AABB, writes a
 //                     64-B splat record, the (depth_key << 32 | index) item and
-//                     a compact 8-B tile rectangle [render.cu:472-786]
+//                     the tile rectangle (4 B packed on the binning path) [render.cu:472-786]
 //   radix passes      stable LSD sort of the N items by depth key (8-bit digits,
-//                     trailing identity passes skipped on the device); the last
-//                     pass also writes the rectangles in depth order
+//                     trailing identity passes skipped on the device); every pass
+//                     carries the packed rectangles, so they end in depth order
 //   k_bin_rows_*      tile binning, row pass: one item per covered tile row,
 //                     binned stably by row [render.cu:811-857, 788-809, 1099-1118]
 //   k_bin_cols_*      tile binning, column pass: one Gaussian index per covered
@@ -18,7 +18,6 @@
 //                     batches culled against the block, survivors compacted into
 //                     LDS pair slots, two splats per iteration with packed math;
 //                     exact per-pixel early termination [render.cu:266-367]
-//                     (k_blend: the same per 16x16 tile workgroup)
 //
 // Every float expression restates render.cu / math.cu in the same operation
 // order; the file is compiled with -ffp-contract=off so no FMA is formed
