@@ -105,6 +105,23 @@ __device__ __forceinline__ void chunk_range(uint64_t n, int groups, int g, uint6
     if (e > n) e = n;
 }
 
+// Chunk handled by workgroup b of G when the chunks are dealt so that each XCD
+// takes one contiguous run of them (a bijection on [0, G); hardware dispatch sends
+// workgroup b to XCD b mod 8).  The partial cache lines at the seams between
+// consecutive chunks' output runs are then written through one L2.  Used by the
+// depth sort's downsweep at 16 items per thread (scenes of 4M+ Gaussians: config
+// 3 depth sort 173 -> 163 us); not by the binning scatters, whose chunks carry
+// uneven work (near splats cover more rows and columns) that contiguous runs would
+// pile onto one XCD (config 3 rows 100 -> 143 us, columns 143 -> 199 us;
+// profiles/r02_ab_xcd_chunks.txt).
+#ifndef GSR_XCD_DEPTH
+#define GSR_XCD_DEPTH 1   // 0: round-robin chunks in the depth downsweep too (A/B builds)
+#endif
+__device__ __forceinline__ int xcd_chunk(int b, int G) {
+    const int xcd = b & 7, q = G >> 3, r = G & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
 // --------------------------------------------------------------- AoS -> SoA
 
 // Accepts the reference's Gaussian[] (gaussians.hpp:16-30) as input.
@@ -696,14 +713,15 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const uint32_t mask = (1u << bits) - 1u;
     const uint64_t n = n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
     uint64_t b, e;
-    chunk_range(n, groups, blockIdx.x, kTile, b, e);
+    const int chunk = GSR_XCD_DEPTH && ITEMS == 16 ? xcd_chunk((int)blockIdx.x, groups) : (int)blockIdx.x;
+    chunk_range(n, groups, chunk, kTile, b, e);
     if (b >= e) return;                          // uniform per workgroup
 
     // global base of each digit for this workgroup
     {
         uint32_t tot;
         const uint32_t dig_excl = block_exclusive_scan<uint32_t>(totals[t], s_scr, tot);
-        s_gbase[t] = dig_excl + hist[t * (uint32_t)groups + blockIdx.x];
+        s_gbase[t] = dig_excl + hist[t * (uint32_t)groups + chunk];
     }
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
@@ -1445,11 +1463,12 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
     __shared__ unsigned long long s_scr64[4];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     uint64_t b, e;
-    chunk_range(n, groups, blockIdx.x, kRowSources, b, e);
+    const int chunk = (int)blockIdx.x;
+    chunk_range(n, groups, chunk, kRowSources, b, e);
     {
         uint32_t tot;
         s_gbase[t] = block_exclusive_scan<uint32_t>(row_items[t], s_scr, tot) +
-                     (t < (uint32_t)tiles_y ? hist[t * (uint32_t)groups + blockIdx.x] : 0u);
+                     (t < (uint32_t)tiles_y ? hist[t * (uint32_t)groups + chunk] : 0u);
         unsigned long long ptot;
         block_exclusive_scan<unsigned long long>(row_pairs[t], s_scr64, ptot);
         if (ptot > cap || b >= e) return;   // uniform: overflow frames stop here
