@@ -718,6 +718,11 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     __shared__ uint32_t s_gbase[256];           // running global offset per digit
     __shared__ uint32_t s_lbase[256];           // tile-local exclusive base per digit
     __shared__ uint32_t s_scr[4];
+    // up to 8 items per thread the payloads get slots of their own (+8 KB of LDS, no
+    // occupancy change) and travel with the items; at 16 the LDS is the occupancy
+    // limit, so they reuse the items' slots in a second round (two more barriers)
+    constexpr bool kPaySlots = ITEMS <= 8;
+    __shared__ uint32_t s_payd[kPaySlots ? kTile : 1];
     const uint32_t t = threadIdx.x;
     const uint32_t lane = lane_id();
     const uint32_t w = t >> 6;
@@ -807,7 +812,9 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
             const uint32_t el = wbase + k * 64 + lane;
             if (el < tn) {
                 const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
-                s_items[s_lbase[d] + s_wc[w][d] + rk[k]] = it[k];
+                const uint32_t slot = s_lbase[d] + s_wc[w][d] + rk[k];
+                s_items[slot] = it[k];
+                if (kPaySlots && carry) s_payd[slot] = pv[k];
             }
         }
         __syncthreads();
@@ -820,6 +827,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
                 const uint32_t d = (uint32_t)(v >> shift) & mask;
                 const uint32_t dst = s_gbase[d] + (q - s_lbase[d]);
                 out[dst] = v;
+                if (kPaySlots && carry) pay_out[dst] = s_payd[q];
                 dq[k] = dst;
                 if (ranges) {
                     // final pass of the tile sort: the LDS tile is fully sorted, so each
@@ -832,7 +840,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
                 }
             }
         }
-        if (carry) {
+        if (!kPaySlots && carry) {
             // the payloads take the items' LDS slots once every item is read, so their
             // stores leave in the same digit runs as the items' (coalesced)
             uint32_t* s_pay = reinterpret_cast<uint32_t*>(s_items);
