@@ -49,7 +49,7 @@ hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, 
                              hipStream_t s);
 hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
                              uint4* rec, uint64_t* items, uint64_t* rect, bool packed, bool four_d, bool sh3,
-                             float t, hipStream_t s);
+                             float t, hipStream_t s, uint16_t* spans = nullptr);
 // One stable LSD pass over u64 items on bits [shift, shift + bits) (bits <= 8).
 // n = n_dev ? *n_dev : n_host.  hist: 256 * groups u32, totals: 256 u32.
 // ranges (nullable, final tile-sort pass): per-tile {~start, end} of key (item >> 32),
@@ -93,7 +93,7 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
                            const uint32_t* pay0, const uint32_t* pay1, int groups, uint32_t* hist,
                            uint32_t* row_items,
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
-                           int items, hipStream_t s);
+                           int items, hipStream_t s, const uint16_t* spans = nullptr);
 hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, const unsigned long long* row_pairs,
                            uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
                            uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,

@@ -273,6 +273,119 @@ __device__ __forceinline__ uint4 cull_word(float a, float b, float c, float e, f
                       __float_as_uint(fast ? S : inf));
 }
 
+// Can any pixel of an integer rectangle reach md2 <= cut?  dx0..dy1 bound the
+// (float)pixel - (float)centre offsets of the rectangle's pixels (monotone, so
+// every pixel's dx lies in [dx0, dx1]).  Returns false only when the exact
+// minimum of the quadratic form a dx^2 + (b+c) dx dy + e dy^2 over that
+// rectangle exceeds cut by more than a bound on the float rounding of md2
+// (<= ~6 ulp of |a|dx^2 + (|b|+|c|)|dx dy| + |e|dy^2, padded 10x) — so a culled
+// splat could never have composited onto this block.  cut, ih, iv and S come
+// from the record's cull word (cull_word): a conic that is not robustly
+// positive definite has cut = +inf, a record without the per-record fast proof
+// S = +inf (infinite margin); NaN anywhere: never culled.
+__device__ __forceinline__ bool block_may_reach(float a, float b, float c, float e, float ih, float iv, float S,
+                                                float dx0, float dx1, float dy0, float dy1, float M, float cut) {
+    if (dx0 <= 0.0f && dx1 >= 0.0f && dy0 <= 0.0f && dy1 >= 0.0f) return true;
+    const float h = 0.5f * (b + c);
+    auto q = [&](float x, float y) { return a * x * x + 2.0f * h * x * y + e * y * y; };
+    // The form is convex with its minimum at the splat centre (offset 0,0), which
+    // lies outside the rectangle here.  A far edge never holds the rectangle's
+    // minimum (from any of its points the segment toward the centre enters the
+    // interior, where the form is smaller), so only the near x-edge (when 0 is not
+    // in [dx0, dx1]) and the near y-edge (when 0 is not in [dy0, dy1]) are evaluated.
+    const float xe = dx0 > 0.0f ? dx0 : dx1, ye = dy0 > 0.0f ? dy0 : dy1;
+    const float qx = q(xe, fminf(fmaxf(ih * xe, dy0), dy1));
+    const float qy = q(fminf(fmaxf(iv * ye, dx0), dx1), ye);
+    const bool x_out = dx0 > 0.0f || dx1 < 0.0f, y_out = dy0 > 0.0f || dy1 < 0.0f;
+    const float qm = fminf(x_out ? qx : 3.0e38f, y_out ? qy : 3.0e38f);
+    const float err = 4e-6f * S * M * M + 1e-3f;
+    return !(qm - err > cut);
+}
+
+// Tile row spans (binning path, GSR_TUNE_TILE_SPANS).  A splat's tile rect is the
+// box of its AABB, and an elongated or tilted ellipse reaches alpha >= 1e-3 on only
+// part of it: config 2 lists 5.39M (tile, splat) pairs of which 4.12M can composite
+// at all.  For each of the first four tile rows of the rect, nibble r of the 16-bit
+// code counts the columns at the row's left end (bits 0-1) and right end (bits 2-3)
+// that hold no in-box pixel of the ellipse q <= C; the row pass lists only the
+// columns in between (none when left + right >= the row's width).  Rows past the
+// fourth (4.1M of the 4.12M reachable pairs sit in the first four) keep every
+// column; a count stops at 3, keeping the middle columns (conservative; counts up
+// to 15 drop no more pairs on config 2, and 2 B per Gaussian keep the row pass's
+// gather of the codes by index half the footprint of 4 B).
+//
+// Why a dropped pair changes no pixel.  q = a dx^2 + (b + c) dx dy + e dy^2 is the
+// exact md2 of the record's float conic; the blend's float md2 is within
+// 4e-6 S M^2 of it (block_may_reach's bound: S = |a|+|b|+|c|+|e|, M = largest
+// |offset| in the AABB), so with C = cut + 4e-6 S M^2 + 1e-3 every pixel outside
+// q <= C has float md2 > cut, alpha < 1e-3, and is never taken.  The x-extent of
+// q <= C over a strip of offsets [u0, u1] is [L, R]: R is the ellipse's rightmost
+// offset xr = sqrt(C e / det) when the strip holds its ordinate yr = -h xr / e,
+// else (-h u + sqrt(a C - det u^2)) / a at the strip end nearer yr (R(dy) is
+// concave); L mirrors it.  Float error: det = a e - h^2 is within 3e-7 k of itself
+// relative (k = a e / det <= 1e4 for a finite cut), which moves xr, ym and the
+// square root by at most sqrt(6e-7 (k + 1)) xr; the pads below cover that and the
+// approximate rcp / sqrt (~1 ulp) with room.  A numpy restatement of this function
+// (tools/sim/spans_check.py) keeps 78.7 % of config 2's pairs (the exact hull: 76.5 %)
+// and every pair it drops peaks at alpha <= 0.9976e-3 on its tile.
+__device__ __forceinline__ uint16_t tile_row_spans(float cx, float cy, float a, float b, float c, float e,
+                                                   uint4 cw, int xmin_px, int xmax_px, int ymin_px, int ymax_px,
+                                                   int tx0, int tx1, int ty0, int ty1) {
+    const float cut = __uint_as_float(cw.x), S = __uint_as_float(cw.w);
+    // not robustly positive definite (cut = inf) or without the fast proof (S = inf): keep all
+    if (!(cut < 3.0e38f) || !(S < 3.0e38f)) return 0u;
+    const float h = 0.5f * (b + c);
+    const float det = a * e - h * h;   // > 1e-4 a e here (cull_word's pd test)
+    const float M = fmaxf(fmaxf(fabsf((float)xmin_px - cx), fabsf((float)xmax_px - cx)),
+                          fmaxf(fabsf((float)ymin_px - cy), fabsf((float)ymax_px - cy)));
+    const float C = cut + (4e-6f * S * M * M + 1e-3f);
+    const float rdet = __builtin_amdgcn_rcpf(det), ra = __builtin_amdgcn_rcpf(a);
+    const float xr = __builtin_amdgcn_sqrtf(C * e * rdet);   // rightmost offset (leftmost: -xr)
+    const float ym = __builtin_amdgcn_sqrtf(C * a * rdet);   // largest |dy| of the ellipse
+    const float yr = -h * xr * __builtin_amdgcn_rcpf(e);     // its ordinate (leftmost: -yr)
+    const float k = a * e * rdet;
+    const float rel = __builtin_amdgcn_sqrtf(6e-7f * (k + 1.0f)) + 1e-4f;
+    // offsets are exact (integer pixel minus integer-valued centre); cx + L rounds by
+    // < 5e-4 px below 4096, hence the 1/64 px (a 2-px pad kept 6 % more pairs)
+    const float padx = 0.015625f + rel * xr, ymp = ym * (1.0f + rel) + 0.015625f;
+    const float aC = a * C;
+    const int w = tx1 - tx0 + 1;
+    const int rows = min(ty1 - ty0 + 1, 4);
+    uint32_t code = 0;
+    for (int r = 0; r < rows; r++) {
+        const int ty = ty0 + r;
+        const int y0 = max(ty * GSR_TILE_PX, ymin_px), y1 = min(ty * GSR_TILE_PX + (GSR_TILE_PX - 1), ymax_px);
+        const float dy0 = (float)y0 - cy, dy1 = (float)y1 - cy;
+        int c0 = tx1 + 1, c1 = tx0 - 1;   // empty
+        if (!(dy0 > ymp || dy1 < -ymp)) {
+            const float u0 = fminf(fmaxf(dy0, -ym), ym), u1 = fminf(fmaxf(dy1, -ym), ym);
+            float R = xr, L = -xr;
+            if (!(yr >= u0 && yr <= u1)) {
+                const float u = yr < u0 ? u0 : u1;
+                R = (-h * u + __builtin_amdgcn_sqrtf(fmaxf(aC - det * u * u, 0.0f))) * ra;
+            }
+            if (!(-yr >= u0 && -yr <= u1)) {
+                const float u = -yr < u0 ? u0 : u1;
+                L = (-h * u - __builtin_amdgcn_sqrtf(fmaxf(aC - det * u * u, 0.0f))) * ra;
+            }
+            const float xl = fmaxf(cx + L - padx, (float)xmin_px), xh = fminf(cx + R + padx, (float)xmax_px);
+            if (xl <= xh) {
+                c0 = max(tx0, (int)floorf(xl * (1.0f / GSR_TILE_PX)));
+                c1 = min(tx1, (int)floorf(xh * (1.0f / GSR_TILE_PX)));
+            }
+        }
+        int sl, sr;
+        if (c0 > c1) {
+            sl = sr = min(w, 3);   // no column reachable (w > 6: the middle ones stay)
+        } else {
+            sl = min(c0 - tx0, 3);
+            sr = min(tx1 - c1, 3);
+        }
+        code |= (uint32_t)(sl | (sr << 2)) << (4 * r);
+    }
+    return (uint16_t)code;
+}
+
 // Temporal state of a 4D (Spacetime-Gaussian style) Gaussian at time t, in
 // this exact operation order (the oracle restates it, oracle/gsr_oracle.c):
 // dt = t - c; x_t = ((x + m0 dt) + m3 dt^2) + m6 dt^3 (dt^2 = dt dt, dt^3 =
@@ -281,7 +394,7 @@ template <bool T4D, bool SH3>
 __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ arr, int64_t stride,
                                                     int64_t n, Frame fr, uint4* __restrict__ rec,
                                                     uint64_t* __restrict__ items, uint64_t* __restrict__ rect,
-                                                    int packed,
+                                                    int packed, uint16_t* __restrict__ spans,
                                                     float tnow) {
     GSR_GEOM_PRIO();
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -503,7 +616,11 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     // centre pixel stored as the float the blend computes with ((float)px, render.cu:329)
     R[2] = make_uint4(__float_as_uint((float)px_x), __float_as_uint((float)px_y), (uint32_t)xmin_px | ((uint32_t)xmax_px << 16),
                       (uint32_t)ymin_px | ((uint32_t)ymax_px << 16));
-    R[3] = cull_word(ic0, ic1, ic2, ic3, opacity, col[0], col[1], col[2]);
+    const uint4 cw = cull_word(ic0, ic1, ic2, ic3, opacity, col[0], col[1], col[2]);
+    R[3] = cw;
+    if (spans)
+        spans[i] = tile_row_spans((float)px_x, (float)px_y, ic0, ic1, ic2, ic3, cw, xmin_px, xmax_px, ymin_px,
+                                  ymax_px, tx0, tx1, ty0, ty1);
     put_rect(rect, i,
              (uint64_t)((uint32_t)tx0 | ((uint32_t)tx1 << 16)) | ((uint64_t)((uint32_t)ty0 | ((uint32_t)ty1 << 16)) << 32),
              packed);
@@ -1473,7 +1590,7 @@ __global__ __launch_bounds__(256) void k_bin_rows_scan(uint32_t* __restrict__ hi
 // and the column pass emits nothing).  The sorted tile holds only each item's
 // source slot: the payload (index | tx0 << 32 | tx1 << 48) is rebuilt at the write.
 template <int ITEMS, int BITS>
-__global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __restrict__ items0,
+__global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(const uint64_t* __restrict__ items0,
                                                            const uint64_t* __restrict__ items1,
                                                            const uint32_t* __restrict__ dstats,
                                                            const uint32_t* __restrict__ pay0,
@@ -1481,10 +1598,13 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
                                                            int groups, const uint32_t* __restrict__ hist,
                                                            const uint32_t* __restrict__ row_items,
                                                            const unsigned long long* __restrict__ row_pairs,
-                                                           uint32_t cap, int tiles_y, uint64_t* __restrict__ rows_out) {
+                                                           uint32_t cap, int tiles_y, uint64_t* __restrict__ rows_out,
+                                                           const uint16_t* __restrict__ spans) {
     GSR_GEOM_PRIO();
     constexpr uint32_t kTile = 256u * ITEMS;
     __shared__ uint32_t s_pref[kRowSources], s_idx[kRowSources];
+    // per source: packed rect (pack_rect) | tile row spans << 32 (no LDS beyond the
+    // 8 B per source it always had: 6 workgroups per CU)
     __shared__ uint64_t s_rect[kRowSources];
     // s_own (source owners, read by the generation) and s_l (source slots of the
     // ranked tile, written after the ranking) share storage: their lives do not overlap
@@ -1498,6 +1618,24 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
     uint64_t b, e;
     const int chunk = (int)blockIdx.x;
     chunk_range(n, groups, chunk, kRowSources, b, e);
+    const uint64_t* sorted = depth_sorted(items0, items1, dstats);
+    const uint32_t* srect = depth_sorted_rects(pay0, pay1, dstats);
+    // thread t owns sources 4t .. 4t+3 of a sub-chunk (source order): packed rect, index
+    // and (by index) tile row spans; the first sub-chunk's (usually the only one) are
+    // loaded before the base scan, so the dependent spans gather overlaps it (loading
+    // every next sub-chunk ahead too holds 86 VGPRs: one wave per SIMD fewer)
+    uint32_t prc[4], gix[4], spv[4];
+    auto load_sources = [&](uint64_t c0) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint64_t j = c0 + 4 * t + i;
+            prc[i] = j < e ? srect[j] : pack_rect(kDeadRect);
+            gix[i] = j < e ? (uint32_t)sorted[j] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) spv[i] = spans && rect_rows(unpack_rect(prc[i])) ? spans[gix[i]] : 0u;
+    };
+    load_sources(b);
     {
         uint32_t tot;
         s_gbase[t] = block_exclusive_scan<uint32_t>(row_items[t], s_scr, tot) +
@@ -1506,22 +1644,20 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
         block_exclusive_scan<unsigned long long>(row_pairs[t], s_scr64, ptot);
         if (ptot > cap || b >= e) return;   // uniform: overflow frames stop here
     }
-    const uint64_t* sorted = depth_sorted(items0, items1, dstats);
-    const uint32_t* srect = depth_sorted_rects(pay0, pay1, dstats);
     for (uint64_t c0 = b; c0 < e; c0 += kRowSources) {
-        // thread t owns sources 4t .. 4t+3 of this sub-chunk (source order)
+        if (c0 != b) load_sources(c0);
         uint32_t cnt[4], start[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const uint64_t j = c0 + 4 * t + i;
-            const uint64_t r = j < e ? unpack_rect(srect[j]) : kDeadRect;
-            s_idx[4 * t + i] = j < e ? (uint32_t)sorted[j] : 0u;
-            s_rect[4 * t + i] = r;
-            cnt[i] = rect_rows(r);
+            s_idx[4 * t + i] = gix[i];
+            cnt[i] = rect_rows(unpack_rect(prc[i]));
         }
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) s_own[t * ITEMS + i] = 0;
         const uint32_t total = bin_source_prefix<4>(cnt, start, s_pref, s_scr);
+#pragma unroll
+        for (int i = 0; i < 4; i++)   // read after bin_tile_owners' barriers
+            s_rect[4 * t + i] = (uint64_t)prc[i] | ((uint64_t)spv[i] << 32);
         uint32_t carry = 0;
         for (uint32_t tb = 0; tb < total; tb += kTile) {
             const uint32_t tn = min(kTile, total - tb);
@@ -1533,7 +1669,7 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
                 const uint32_t l = (uint32_t)s_own[el] - 1u;
                 src[k] = l;
                 const uint32_t first = l ? s_pref[l - 1] : 0u;
-                dig[k] = (uint32_t)((s_rect[l] >> 32) & 0xffffu) + (tb + el - first);
+                dig[k] = (uint32_t)((s_rect[l] >> 16) & 0xffu) + (tb + el - first);   // ty0 + row
             }
             const uint32_t tcount = bin_rank_tile<ITEMS, BITS>(dig, tn, pos, s_wc, s_lbase, s_scr);
 #pragma unroll
@@ -1552,8 +1688,17 @@ __global__ __launch_bounds__(256) void k_bin_rows_scatter(const uint64_t* __rest
                 const uint32_t d = s_dig[qc], l = s_l[qc];
                 const uint32_t dst = s_gbase[d] + (qc - s_lbase[d]);
                 const uint64_t r = s_rect[l];
-                if (q < tn && dst < cap)
-                    rows_out[dst] = (uint64_t)s_idx[l] | ((r & 0xffffu) << 32) | (((r >> 16) & 0xffffu) << 48);
+                uint32_t x0 = (uint32_t)(r & 0xffu), x1 = (uint32_t)((r >> 8) & 0xffu);
+                const uint32_t ro = d - (uint32_t)((r >> 16) & 0xffu);   // row within the rect
+                if (ro < 4u) {
+                    // tile row spans: columns [x0 + left, x1 - right]; an empty row gets the
+                    // empty range (1, 0), which the column pass counts and expands to nothing
+                    const uint32_t sp = (uint32_t)(r >> (32u + 4u * ro)) & 15u;
+                    const int c0 = (int)(x0 + (sp & 3u)), c1 = (int)x1 - (int)(sp >> 2);
+                    x0 = c0 <= c1 ? (uint32_t)c0 : 1u;
+                    x1 = c0 <= c1 ? (uint32_t)c1 : 0u;
+                }
+                if (q < tn && dst < cap) rows_out[dst] = (uint64_t)s_idx[l] | ((uint64_t)x0 << 32) | ((uint64_t)x1 << 48);
             }
             __syncthreads();
             s_gbase[t] += tcount;
@@ -1879,35 +2024,6 @@ __global__ __launch_bounds__(256) void k_part_scatter(const uint64_t* __restrict
 __device__ __forceinline__ int xcd_remap(int b, int nb) {
     const int xcd = b & 7, q = nb >> 3, r = nb & 7;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-}
-
-// Can any pixel of an integer rectangle reach md2 <= cut?  dx0..dy1 bound the
-// (float)pixel - (float)centre offsets of the rectangle's pixels (monotone, so
-// every pixel's dx lies in [dx0, dx1]).  Returns false only when the exact
-// minimum of the quadratic form a dx^2 + (b+c) dx dy + e dy^2 over that
-// rectangle exceeds cut by more than a bound on the float rounding of md2
-// (<= ~6 ulp of |a|dx^2 + (|b|+|c|)|dx dy| + |e|dy^2, padded 10x) — so a culled
-// splat could never have composited onto this block.  cut, ih, iv and S come
-// from the record's cull word (cull_word): a conic that is not robustly
-// positive definite has cut = +inf, a record without the per-record fast proof
-// S = +inf (infinite margin); NaN anywhere: never culled.
-__device__ __forceinline__ bool block_may_reach(float a, float b, float c, float e, float ih, float iv, float S,
-                                                float dx0, float dx1, float dy0, float dy1, float M, float cut) {
-    if (dx0 <= 0.0f && dx1 >= 0.0f && dy0 <= 0.0f && dy1 >= 0.0f) return true;
-    const float h = 0.5f * (b + c);
-    auto q = [&](float x, float y) { return a * x * x + 2.0f * h * x * y + e * y * y; };
-    // The form is convex with its minimum at the splat centre (offset 0,0), which
-    // lies outside the rectangle here.  A far edge never holds the rectangle's
-    // minimum (from any of its points the segment toward the centre enters the
-    // interior, where the form is smaller), so only the near x-edge (when 0 is not
-    // in [dx0, dx1]) and the near y-edge (when 0 is not in [dy0, dy1]) are evaluated.
-    const float xe = dx0 > 0.0f ? dx0 : dx1, ye = dy0 > 0.0f ? dy0 : dy1;
-    const float qx = q(xe, fminf(fmaxf(ih * xe, dy0), dy1));
-    const float qy = q(fminf(fmaxf(iv * ye, dx0), dx1), ye);
-    const bool x_out = dx0 > 0.0f || dx1 < 0.0f, y_out = dy0 > 0.0f || dy1 < 0.0f;
-    const float qm = fminf(x_out ? qx : 3.0e38f, y_out ? qy : 3.0e38f);
-    const float err = 4e-6f * S * M * M + 1e-3f;
-    return !(qm - err > cut);
 }
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -2333,19 +2449,19 @@ hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, 
 
 hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
                              uint4* rec, uint64_t* items, uint64_t* rect, bool packed, bool four_d, bool sh3,
-                             float t, hipStream_t s) {
+                             float t, hipStream_t s, uint16_t* spans) {
     if (n <= 0) return hipSuccess;
     const dim3 g(grid_for(n, 256));
     const int pk = packed ? 1 : 0;
     if (four_d)
         hipLaunchKernelGGL((k_preprocess<true, false>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect,
-                           pk, t);
+                           pk, packed ? spans : nullptr, t);
     else if (sh3)
         hipLaunchKernelGGL((k_preprocess<false, true>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect,
-                           pk, t);
+                           pk, packed ? spans : nullptr, t);
     else
         hipLaunchKernelGGL((k_preprocess<false, false>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect,
-                           pk, t);
+                           pk, packed ? spans : nullptr, t);
     return hipGetLastError();
 }
 
@@ -2417,7 +2533,7 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
                            const uint32_t* pay0, const uint32_t* pay1, int groups, uint32_t* hist,
                            uint32_t* row_items,
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
-                           int items, hipStream_t s) {
+                           int items, hipStream_t s, const uint16_t* spans) {
     if (tiles_y < 1 || tiles_y > 256 || groups < 1 || groups > kMaxSortGroups / 2 ||
         (items != 4 && items != 8 && items != 16))
         return hipErrorInvalidValue;
@@ -2429,7 +2545,7 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
                                   : (items == 4 ? k_bin_rows_scatter<4, 8> : items == 8 ? k_bin_rows_scatter<8, 8>
                                                                                     : k_bin_rows_scatter<16, 8>);
     hipLaunchKernelGGL(scatter, dim3(groups), dim3(256), 0, s, items0, items1, dstats, pay0, pay1, n, groups, hist,
-                       row_items, row_pairs, pair_capacity, tiles_y, rows_buf);
+                       row_items, row_pairs, pair_capacity, tiles_y, rows_buf, spans);
     return hipGetLastError();
 }
 

@@ -315,6 +315,8 @@ struct gsr_context {
     bool rect_packed = false;        // this frame's rects are packed (binning path, set by gsr_preprocess)
     uint64_t* srect = nullptr;       // binning path: two u32 rect-payload buffers the depth sort carries
                                      // (pack_rect), one of them depth-ordered at its end
+    uint16_t* spans = nullptr;       // binning path: per-Gaussian tile row spans (tile_row_spans)
+    bool spans_frame = false;        // this frame's preprocess wrote them (the row pass reads them)
     uint32_t* hist = nullptr;
     uint32_t* totals = nullptr;
     unsigned long long* wg = nullptr;
@@ -346,6 +348,9 @@ struct gsr_context {
     int tile_binning = 1;            // row + column binning instead of emit + tile sort (grids <= 256 x 256)
     int bin_row_items = 4;           // binning: items per thread of a row-pass tile (4 | 8 | 16)
     int bin_col_items = 8;           // binning: items per thread of a column-pass tile (4 | 8 | 16)
+    int tile_spans = 2;              // binning: drop the tiles of a splat's first four tile rows that
+                                     // it provably cannot composite on (GSR_TUNE_TILE_SPANS): 0 off,
+                                     // 1 on, 2 on up to kSpansAutoMax Gaussians
     int bin_col_groups = 0;          // binning: column-pass workgroups (chunks are strided over them);
                                      // 0 = by scene size (n / 1024 clamped to 1024..4096)
     uint64_t* binmeta = nullptr;     // binning: row pair totals (u64 x 256) then row item totals (u32 x 256)
@@ -428,6 +433,7 @@ int ensure_n(gsr_context* c, int64_t n) {
     if (int rc = realloc_dev(&c->items[1], (size_t)cap)) return rc;
     if (int rc = realloc_dev(&c->rect, (size_t)cap)) return rc;
     if (int rc = realloc_dev(&c->srect, (size_t)cap)) return rc;
+    if (int rc = realloc_dev(&c->spans, (size_t)cap)) return rc;
     c->n_cap = cap;
     if (c->p_cap < 4 * cap) {
         const int64_t pc = std::min<int64_t>(std::max<int64_t>(4 * cap, 1 << 20), 0xffffffffLL);
@@ -591,7 +597,7 @@ extern "C" void gsr_destroy(gsr_context* c) {
     for (auto* p : {(void*)c->rec, (void*)c->items[0], (void*)c->items[1], (void*)c->rect, (void*)c->pairs[0],
                     (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->dstats,
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
-                    (void*)c->cbins, (void*)c->srect, (void*)c->nlive})
+                    (void*)c->cbins, (void*)c->srect, (void*)c->spans, (void*)c->nlive})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -648,9 +654,16 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     // the binning path takes the tile rects packed to 4 B (pack_rect), the pair path 8 B;
     // the sort follows the path chosen here (rect_packed)
     c->rect_packed = c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
+    // tile row spans: the row pass gathers each source's 2-B code by index; up to 1.5M
+    // Gaussians the codes (<= 3 MB) stay in an XCD's 4-MB L2 and the gather is cheap:
+    // config 2 (1M) +0.8 % one frame at a time, +1.2 % in flight; config 5 (2M) -1 % in
+    // flight, config 3 (5M) -3 / -6 % (profiles/r02_ab_tile_spans.txt)
+    constexpr int64_t kSpansAutoMax = 3 << 19;
+    c->spans_frame = c->rect_packed && (c->tile_spans == 1 || (c->tile_spans == 2 && n <= kSpansAutoMax));
     HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[c->compact_frame ? 1 : 0], c->rect,
                                    c->rect_packed, layout == GSR_LAYOUT_SCENE_BLOCK_4D,
-                                   layout == GSR_LAYOUT_SCENE_BLOCK_SH3, c->time, c->stream));
+                                   layout == GSR_LAYOUT_SCENE_BLOCK_SH3, c->time, c->stream,
+                                   c->spans_frame ? c->spans : nullptr));
     c->have_pre = true;
     c->have_sort = false;
     return rc_over;
@@ -741,7 +754,7 @@ static int sort_locked(gsr_context* c) {
         HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n, pay_buf(c, 0),
                                      pay_buf(c, 1), gb,
                                      c->hist, row_items, row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items,
-                                     c->stream));
+                                     c->stream, c->spans_frame ? c->spans : nullptr));
         mark(c, GSR_STAGE_TILE_SORT);
         // column-pass workgroups: ~one 2048-item chunk each (config 3: 2048-4096 groups 12 us
         // faster than 1024; config 2: 1024 best, profiles/r02_ab_col_groups.txt)
@@ -866,6 +879,7 @@ void copy_settings(gsr_context* d, const gsr_context* s) {
     d->tile_binning = s->tile_binning;
     d->bin_row_items = s->bin_row_items;
     d->bin_col_items = s->bin_col_items;
+    d->tile_spans = s->tile_spans;
     d->bin_col_groups = s->bin_col_groups;
     d->blend_band_tiles = s->blend_band_tiles;
     d->completion_events = s->completion_events;
@@ -1143,18 +1157,21 @@ extern "C" int64_t gsr_read_pairs(gsr_context* c, uint64_t* host, int64_t cap) {
     HIP_TRY(hipMemcpy(&s, c->stats, sizeof s, hipMemcpyDeviceToHost));
     const int64_t m = std::min<int64_t>(cap, s.pairs_eff);
     if (!m) return 0;
-    // the sorted pairs live as values + tile ranges; rebuild (tile << 32 | index)
+    // the sorted pairs live as values + tile ranges; rebuild (tile << 32 | index) tile by
+    // tile.  Ranges ascend with the tile; with tile row spans the binning leaves unused
+    // slots between rows (pairs_total counts every tile of every rect), so the listed
+    // pairs are packed here and their count returned.
     std::vector<uint32_t> vals((size_t)m);
     std::vector<uint2> rg((size_t)c->ntiles);
     HIP_TRY(hipMemcpy(vals.data(), pair_vals(c, c->pair_buf), (size_t)m * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(rg.data(), c->ranges, sizeof(uint2) * rg.size(), hipMemcpyDeviceToHost));
-    for (int64_t j = 0; j < m; j++) host[j] = ~0ull;
+    int64_t k = 0;
     for (int t = 0; t < c->ntiles; t++) {
         if (!rg[t].y) continue;
         for (int64_t j = ~rg[t].x; j < (int64_t)rg[t].y && j < m; j++)
-            host[j] = ((uint64_t)(uint32_t)t << 32) | vals[(size_t)j];
+            host[k++] = ((uint64_t)(uint32_t)t << 32) | vals[(size_t)j];
     }
-    return m;
+    return k;
 }
 
 extern "C" int gsr_tile_grid(gsr_context* c, int* tx, int* ty) {
@@ -1257,6 +1274,7 @@ extern "C" int gsr_get_tuning(gsr_context* c, int knob, int* value) {
     case GSR_TUNE_COMPLETION_EVENTS: *value = c->completion_events ? 1 : 0; break;
     case GSR_TUNE_BLEND_BAND_TILES: *value = c->blend_band_tiles; break;
     case GSR_TUNE_DEPTH_COMPACT: *value = c->depth_compact; break;
+    case GSR_TUNE_TILE_SPANS: *value = c->tile_spans; break;
     default: return set_err(GSR_E_ARG, "gsr_get_tuning: unknown knob");
     }
     return GSR_OK;
@@ -1306,6 +1324,10 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         return GSR_OK;
     case GSR_TUNE_DEPTH_SORT_SKIP:
         c->depth_skip = value != 0;
+        return GSR_OK;
+    case GSR_TUNE_TILE_SPANS:
+        if (value < 0 || value > 2) return set_err(GSR_E_ARG, "gsr_set_tuning: tile spans must be 0, 1 or 2");
+        c->tile_spans = value;
         return GSR_OK;
     case GSR_TUNE_TILE_SORT_SPLIT:
         c->tile_split_even = value != 0;

@@ -175,7 +175,8 @@ int gsr_sync(gsr_context* ctx);
 
 /* ---- readback (synchronous; for tests and tooling) ---- */
 
-/* Number of (tile, Gaussian) pairs of the last frame (before capacity clamp). */
+/* Number of (tile, Gaussian) pairs of the last frame's tile rects (before the capacity
+ * clamp; an upper bound of the pairs listed when GSR_TUNE_TILE_SPANS drops some). */
 int64_t gsr_pair_count(gsr_context* ctx);
 /* Number of (tile row, Gaussian) items the last frame's row pass produced (tile
  * binning), or -1 if that frame used pair emission + the key-value tile sort. */
@@ -191,7 +192,7 @@ int gsr_read_splats(gsr_context* ctx, void* host_records, int64_t n);
  * that used the per-tile depth order has no global one: it is computed here
  * (stable sort of that frame's keys, the same kernels as the global path). */
 int gsr_read_depth_order(gsr_context* ctx, uint64_t* host_items, int64_t n);
-/* (tile << 32 | index) pairs after the tile sort; returns the count copied. */
+/* (tile << 32 | index) pairs the tile lists hold, in tile order; returns the count copied. */
 int64_t gsr_read_pairs(gsr_context* ctx, uint64_t* host_pairs, int64_t cap);
 /* Internal tile grid of the last frame and its [start, end) ranges. */
 int gsr_tile_grid(gsr_context* ctx, int* tiles_x, int* tiles_y);
@@ -249,9 +250,13 @@ enum {
     /* 14-17 reserved (removed, all measured slower: two blocks per workgroup, per-tile depth
        order after index-order binning (config 3: 1.53 ms vs 0.24 ms), several blocks per wave,
        LDS-capped blend occupancy) */
-    GSR_TUNE_DEPTH_COMPACT = 18      /* global depth sort on the binning path: 1 = stable partition of the
+    GSR_TUNE_DEPTH_COMPACT = 18,     /* global depth sort on the binning path: 1 = stable partition of the
                                         visible Gaussians first, the passes sort only those; 0 = sort all;
                                         2 (default) = partition for 4D scenes only; same order, same image */
+    GSR_TUNE_TILE_SPANS = 19         /* binning path: 1 = list a splat in only the tiles of its first four
+                                        tile rows it can composite on (conservative ellipse-vs-tile test);
+                                        0 = every tile of its rect; 2 (default) = 1 up to 1.5M Gaussians;
+                                        same image */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Current value of a knob (what gsr_set_tuning last set, else the default). */

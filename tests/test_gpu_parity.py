@@ -77,6 +77,52 @@ def test_math_probe_bitwise(gpu, orc):
         assert bad.size == 0, f"{name}: {bad.size} mismatches, e.g. x={xs[bad[:3]]} y={ys[bad[:3]]} got={got[bad[:3], col]} ref={ref[bad[:3], col]}"
 
 
+KNOB_TILE_SPANS = 19
+
+
+def rect_pairs(want, order, W, H):
+    """(tile << 32 | index) for every tile of every visible splat's tile rect, stable
+    by tile over the depth order (the lists without tile row spans)."""
+    tx, ty = (W + 15) // 16, (H + 15) // 16
+    idx_sorted = (order & 0xFFFFFFFF).astype(np.int64)
+    idx_sorted = idx_sorted[want["status"][idx_sorted] == 2]
+    a = want["aabb"]
+    ex_tiles = []
+    for i in idx_sorted:
+        x0, x1 = a[i, 0] // 16, min(tx - 1, a[i, 2] // 16)
+        y0, y1 = a[i, 1] // 16, min(ty - 1, a[i, 3] // 16)
+        for yy in range(y0, y1 + 1):
+            for xx in range(x0, x1 + 1):
+                ex_tiles.append((yy * tx + xx, i))
+    ex = np.array(ex_tiles, dtype=np.uint64).reshape(-1, 2)
+    ex_pairs = (ex[:, 0] << np.uint64(32)) | ex[:, 1]
+    return ex_pairs[np.argsort(ex[:, 0], kind="stable")]
+
+
+def max_alpha_on_tiles(want, pairs, W):
+    """Largest alpha = op * exp(-md2 / 2) (float32, render.cu:329-332 operation order)
+    of each (tile, splat) pair over the tile's pixels inside the splat's AABB."""
+    tx = (W + 15) // 16
+    tile = (pairs >> np.uint64(32)).astype(np.int64)
+    idx = (pairs & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    a = want["aabb"][idx].astype(np.int64)
+    best = np.full(pairs.size, -np.inf, np.float32)
+    cx, cy = want["px_x"][idx].astype(np.float32), want["px_y"][idx].astype(np.float32)
+    ic = want["inv_covar"][idx].astype(np.float32)
+    op = want["opacity"][idx].astype(np.float32)
+    for oy in range(16):
+        for ox in range(16):
+            px = (tile % tx) * 16 + ox
+            py = (tile // tx) * 16 + oy
+            ok = (px >= a[:, 0]) & (px <= a[:, 2]) & (py >= a[:, 1]) & (py <= a[:, 3])
+            dx = px.astype(np.float32) - cx
+            dy = py.astype(np.float32) - cy
+            md = dx * (ic[:, 0] * dx + ic[:, 1] * dy) + dy * (ic[:, 2] * dx + ic[:, 3] * dy)
+            al = np.minimum(op * np.exp(np.float32(-0.5) * md), np.float32(0.99))
+            best = np.where(ok, np.maximum(best, al), best)
+    return best
+
+
 CAMS = [dict(pos=(0, 0, 4)), dict(pos=(1.0, 0.5, 3.0), look=(0.2, 0, 0), fov=70), dict(pos=(0, 0, 1.5), fov=90),
         dict(pos=(-2.5, -1.0, -3.0))]
 
@@ -88,6 +134,7 @@ def test_preprocess_records_bit_exact(gpu, orc, torch, c1, ci):
     cam = cam_for(gpu, W, H, **CAMS[ci])
     scene = gpu.Scene.from_soa(soa)
     r = gpu.Renderer()
+    r.set_tuning(KNOB_TILE_SPANS, 0)   # every tile of every rect (the spans test covers 1)
     r.preprocess(scene, cam, W, H, k=3.0)
     r.sort()
     got = r.read_splats(soa.shape[1])
@@ -114,20 +161,7 @@ def test_preprocess_records_bit_exact(gpu, orc, torch, c1, ci):
     order = r.read_depth_order(soa.shape[1])
     assert np.array_equal(order, orc.expected_depth_order(want))
 
-    # pairs: (tile << 32 | index), stable by tile over the depth order
-    idx_sorted = (order & 0xFFFFFFFF).astype(np.int64)
-    idx_sorted = idx_sorted[want["status"][idx_sorted] == 2]
-    a = want["aabb"]
-    ex_tiles = []
-    for i in idx_sorted:
-        x0, x1 = a[i, 0] // 16, min(tx - 1, a[i, 2] // 16)
-        y0, y1 = a[i, 1] // 16, min(ty - 1, a[i, 3] // 16)
-        for yy in range(y0, y1 + 1):
-            for xx in range(x0, x1 + 1):
-                ex_tiles.append((yy * tx + xx, i))
-    ex = np.array(ex_tiles, dtype=np.uint64).reshape(-1, 2)
-    ex_pairs = (ex[:, 0] << np.uint64(32)) | ex[:, 1]
-    ex_pairs = ex_pairs[np.argsort(ex[:, 0], kind="stable")]
+    ex_pairs = rect_pairs(want, order, W, H)
     pairs = r.read_pairs()
     assert r.pair_count() == ex_pairs.size
     assert np.array_equal(pairs, ex_pairs)
@@ -137,6 +171,42 @@ def test_preprocess_records_bit_exact(gpu, orc, torch, c1, ci):
     nz = counts > 0
     assert np.array_equal((ranges[nz, 1] - ranges[nz, 0]).astype(np.int64), counts[nz])
     assert (ranges[~nz, 1] == ranges[~nz, 0]).all()
+
+
+@pytest.mark.parametrize("ci", range(len(CAMS)))
+def test_tile_spans_drop_only_unreachable_pairs(gpu, orc, torch, c1, ci):
+    """Tile row spans (GSR_TUNE_TILE_SPANS; the default 2 turns them on for this size): the tile lists are the full
+    rect lists with some pairs left out, in the same order; every left-out pair is one
+    whose splat reaches alpha < 1e-3 on every in-box pixel of that tile; the image is
+    bit-identical to the one without spans and to the oracle's."""
+    path, soa = c1
+    W, H = 640, 480
+    cam = cam_for(gpu, W, H, **CAMS[ci])
+    scene = gpu.Scene.from_soa(soa)
+    r_on, r_off = gpu.Renderer(), gpu.Renderer()
+    assert r_on.get_tuning(KNOB_TILE_SPANS) == 2   # default: on up to 1.5M Gaussians
+    r_on.set_tuning(KNOB_TILE_SPANS, 1)
+    r_off.set_tuning(KNOB_TILE_SPANS, 0)
+    with pytest.raises(gpu.GsrError):
+        r_off.set_tuning(KNOB_TILE_SPANS, 3)
+    got_on, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_on)
+    got_off, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_off)
+    assert np.array_equal(got_on.view(np.uint32), got_off.view(np.uint32))
+    assert_image_parity(got_on, orc.render(soa, cam, W, H, 3.0))
+    want = orc.preprocess(soa, cam, W, H, 3.0)
+    full = rect_pairs(want, r_on.read_depth_order(soa.shape[1]), W, H)
+    assert np.array_equal(r_off.read_pairs(), full)
+    on = r_on.read_pairs()
+    assert r_on.pair_count() == full.size          # pair_count: every tile of every rect
+    kept = np.isin(full, on)
+    assert np.array_equal(on, full[kept])          # a subsequence: same order, nothing new
+    dropped = full[~kept]
+    assert dropped.size > 0.05 * full.size         # ~24 % on config 2
+    assert (max_alpha_on_tiles(want, dropped, W) < np.float32(1e-3)).all()
+    # the row pass still makes one item per covered tile row
+    spl = r_on.read_splats(soa.shape[1])
+    ty = spl["tile_y_range"][spl["tile_count"] > 0]
+    assert r_on.row_item_count() == int(((ty >> 16) - (ty & 0xFFFF) + 1).sum())
 
 
 @pytest.mark.parametrize("ci", range(len(CAMS)))
@@ -188,6 +258,7 @@ def test_tile_binning_matches_pair_sort(gpu, orc, torch, c1, knobs):
     r_bin, r_sort = gpu.Renderer(), gpu.Renderer()
     for kn, v in knobs.items():
         r_bin.set_tuning(kn, v)
+    r_bin.set_tuning(KNOB_TILE_SPANS, 0)   # the pair path lists every tile of every rect
     r_sort.set_tuning(7, 0)
     got_bin, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_bin)
     got_sort, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_sort)
@@ -211,14 +282,18 @@ def test_tile_binning_8bit_digits(gpu, orc, torch, c1):
     W, H = 2100, 2060
     scene = gpu.Scene.from_soa(soa)
     cam = cam_for(gpu, W, H, pos=(0.3, -0.2, 3.2), fov=60)
-    r_bin, r_sort = gpu.Renderer(), gpu.Renderer()
+    r_bin, r_sort, r_span = gpu.Renderer(), gpu.Renderer(), gpu.Renderer()
+    r_bin.set_tuning(KNOB_TILE_SPANS, 0)
     r_sort.set_tuning(7, 0)
     got, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_bin)
     ref, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_sort)
+    spanned, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_span)
     tx, ty = r_bin.tile_grid()
     assert tx > 128 and ty > 128 and r_bin.row_item_count() > 0
     assert np.array_equal(r_bin.read_pairs(), r_sort.read_pairs())
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(spanned.view(np.uint32), ref.view(np.uint32))
+    assert r_span.read_pairs().size < r_bin.read_pairs().size
     assert_image_parity(got, orc.render(soa, cam, W, H, 3.0))
 
 
@@ -296,7 +371,7 @@ def test_tuning_defaults_read_back(gpu):
     """gsr_get_tuning returns the documented defaults (include/gsr.h) and what
     gsr_set_tuning set; unknown knobs are refused."""
     r = gpu.Renderer()
-    defaults = {1: 16, 2: 0, 3: 1024, 4: 0, 5: 1, 6: 1, 7: 1, 8: 4, 9: 8, 10: 0, 11: 1, 13: 4, 18: 2}
+    defaults = {1: 16, 2: 0, 3: 1024, 4: 0, 5: 1, 6: 1, 7: 1, 8: 4, 9: 8, 10: 0, 11: 1, 13: 4, 18: 2, 19: 2}
     for kn, v in defaults.items():
         assert r.get_tuning(kn) == v, kn
     r.set_tuning(9, 16)
