@@ -294,8 +294,11 @@ __device__ __forceinline__ bool block_may_reach(float a, float b, float c, float
     // interior, where the form is smaller), so only the near x-edge (when 0 is not
     // in [dx0, dx1]) and the near y-edge (when 0 is not in [dy0, dy1]) are evaluated.
     const float xe = dx0 > 0.0f ? dx0 : dx1, ye = dy0 > 0.0f ? dy0 : dy1;
-    const float qx = q(xe, fminf(fmaxf(ih * xe, dy0), dy1));
-    const float qy = q(fminf(fmaxf(iv * ye, dx0), dx1), ye);
+    // clamps as v_med3_f32: equal to fminf(fmaxf(v, lo), hi) here (lo <= hi; lo and hi
+    // both NaN or neither; quiet NaN v gives lo either way), without the two
+    // canonicalising v_max each fminf / fmaxf operand costs in IEEE mode
+    const float qx = q(xe, __builtin_amdgcn_fmed3f(ih * xe, dy0, dy1));
+    const float qy = q(__builtin_amdgcn_fmed3f(iv * ye, dx0, dx1), ye);
     const bool x_out = dx0 > 0.0f || dx1 < 0.0f, y_out = dy0 > 0.0f || dy1 < 0.0f;
     const float qm = fminf(x_out ? qx : 3.0e38f, y_out ? qy : 3.0e38f);
     const float err = 4e-6f * S * M * M + 1e-3f;
