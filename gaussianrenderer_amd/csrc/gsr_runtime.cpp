@@ -940,7 +940,16 @@ extern "C" int gsr_frames_in_flight(gsr_context* c) {
 extern "C" int gsr_render_path(gsr_context* c, const void* scene, int layout, int64_t n, const gsr_camera* cams,
                                const float* times, int nframes, int W, int H, int nx, int ny, int ws, int hs,
                                float k, float* const* d_outs, void* stream) {
+    return gsr_render_path_ex(c, scene, layout, n, cams, times, nframes, W, H, nx, ny, ws, hs, k, d_outs, stream,
+                              nullptr, 0);
+}
+
+extern "C" int gsr_render_path_ex(gsr_context* c, const void* scene, int layout, int64_t n, const gsr_camera* cams,
+                                  const float* times, int nframes, int W, int H, int nx, int ny, int ws, int hs,
+                                  float k, float* const* d_outs, void* stream, void* const* frame_events,
+                                  int flags) {
     if (!c) return set_err(GSR_E_ARG, "null context");
+    if (flags & ~GSR_PATH_NO_JOIN) return set_err(GSR_E_ARG, "gsr_render_path_ex: unknown flags 0x%x", flags);
     if (nframes < 0 || (nframes > 0 && (!cams || !d_outs)))
         return set_err(GSR_E_ARG, "gsr_render_path: bad frame arrays");
     for (int i = 0; i < nframes; i++)
@@ -998,10 +1007,11 @@ extern "C" int gsr_render_path(gsr_context* c, const void* scene, int layout, in
         if (rc == GSR_E_OVERFLOW) result = GSR_E_OVERFLOW;
         else if (rc != GSR_OK) return rc;
         if (record[i]) HIP_TRY(hipEventRecord(c->alias_evs[lane], ls));
+        if (frame_events && frame_events[i]) HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(frame_events[i]), ls));
     }
     c->time = t_saved;
     // join: work queued on the caller's stream afterwards sees every frame
-    for (int l = 0; l < F - 1 && l + 1 < nframes; l++) {
+    for (int l = 0; l < F - 1 && l + 1 < nframes && !(flags & GSR_PATH_NO_JOIN); l++) {
         HIP_TRY(hipEventRecord(c->join_evs[l], c->lane_streams[l]));
         HIP_TRY(hipStreamWaitEvent(S, c->join_evs[l], 0));
     }

@@ -77,7 +77,7 @@ class FrameShard:
 
     def __init__(self, dist, renderer, scene, cam, W: int, H: int, k: float = 3.0, steps: int = 1,
                  gather: str = "step", inflight: int = 1, chunk: int = 8, gloo: bool = False,
-                 frame_time=None, stream: int = 0):
+                 frame_time=None, stream: int = 0, overlap: bool = True):
         import torch
         self.dist, self.r, self.scene, self.cam = dist, renderer, scene, cam
         self.W, self.H, self.k, self.stream = W, H, k, stream
@@ -96,6 +96,12 @@ class FrameShard:
                        for _ in range(world)] for _ in range(len(self.outs))]
                      if (self.step_gather and rank == 0) else None)
         self.pending = [None] * len(self.outs)
+        # RCCL: each gather waits for its own frame's completion event (gsr_render_path_ex)
+        # on a side stream, and render_path runs without the exit join, so the lanes keep
+        # frames in flight across chunks instead of draining at every chunk boundary
+        self.frame_events = (None if (gloo or not self.step_gather or not overlap)
+                             else [torch.cuda.Event() for _ in range(len(self.outs))])
+        self.gather_stream = torch.cuda.Stream() if self.frame_events else None
 
     def _times(self, i0: int, m: int):
         return [self.frame_time(i0 + j) for j in range(m)] if self.frame_time else None
@@ -110,6 +116,15 @@ class FrameShard:
             self.wait_pending(b)
 
     def gather(self, b: int):
+        if self.frame_events:
+            import torch
+            # RCCL's stream waits on the current stream: the side stream, which waits
+            # on buffer b's frame only
+            with torch.cuda.stream(self.gather_stream):
+                self.gather_stream.wait_event(self.frame_events[b])
+                self.pending[b] = self.dist.gather(self.outs[b], self.recv[b] if self.recv else None, dst=0,
+                                                   async_op=True)
+            return
         src = self.outs[b].cpu() if self.gloo else self.outs[b]
         self.pending[b] = self.dist.gather(src, self.recv[b] if self.recv else None, dst=0,
                                            async_op=not self.gloo)
@@ -119,11 +134,14 @@ class FrameShard:
         self.r.render(self.scene, self.cam, self.W, self.H, self.outs[b].data_ptr(), k=self.k,
                       stream=self.stream, time=self.frame_time(i) if self.frame_time else None)
 
-    def path(self, i0: int, m: int, bufs):
+    def path(self, i0: int, m: int, bufs, overlap: bool = False):
         """Frames i0 .. i0+m-1 through gsr_render_path into outs[bufs[j]]; returns its code
-        (GSR_E_OVERFLOW: some frame of the call overflowed and must be re-rendered)."""
+        (GSR_E_OVERFLOW: some frame of the call overflowed and must be re-rendered).
+        overlap: record each buffer's frame event and skip the exit join (run())."""
+        ov = overlap and self.frame_events is not None
         return self.r.render_path(self.scene, [self.cam] * m, self.W, self.H, [self.outs[b].data_ptr() for b in bufs],
-                           k=self.k, stream=self.stream, times=self._times(i0, m))
+                                  k=self.k, stream=self.stream, times=self._times(i0, m),
+                                  events=[self.frame_events[b] for b in bufs] if ov else None, join=not ov)
 
     def run(self, steps: int):
         """K frames in flight, gathered per step when enabled (not drained: call drain())."""
@@ -136,6 +154,6 @@ class FrameShard:
             bufs = [base + j for j in range(m)]
             for b in bufs:
                 self.wait_pending(b)
-            self.path(c0, m, bufs)
+            self.path(c0, m, bufs, overlap=True)
             for b in bufs:
                 self.gather(b)

@@ -149,6 +149,20 @@ int gsr_render(gsr_context* ctx, const void* d_scene, int layout, int64_t n,
 int gsr_render_path(gsr_context* ctx, const void* d_scene, int layout, int64_t n, const gsr_camera* cams,
                     const float* times, int nframes, int W, int H, int num_tile_x, int num_tile_y,
                     int width_stride, int height_stride, float k, float* const* d_outs, void* stream);
+/* gsr_render_path with per-frame completion events, for consumers that hand each
+ * finished frame on (the multi-GPU gather) while later frames still render.
+ * frame_events (may be NULL; entries may be NULL): hipEvent_t frame_events[i] is
+ * recorded on frame i's lane right after its blend.  flags & GSR_PATH_NO_JOIN:
+ * skip the join, so `stream` orders after lane 0's frames only and the lanes keep
+ * running into the next call without a pipeline drain (a later call's lanes still
+ * start after the work queued on `stream` before it).  Without the join the caller
+ * orders everything else through the events: reading frame i, and re-using one of
+ * this call's output buffers in a later call (wait for the buffer's last frame). */
+#define GSR_PATH_NO_JOIN 1
+int gsr_render_path_ex(gsr_context* ctx, const void* d_scene, int layout, int64_t n, const gsr_camera* cams,
+                       const float* times, int nframes, int W, int H, int num_tile_x, int num_tile_y,
+                       int width_stride, int height_stride, float k, float* const* d_outs, void* stream,
+                       void* const* frame_events, int flags);
 /* Frames in flight for gsr_render_path: 1..GSR_MAX_FRAMES_IN_FLIGHT (default 3;
  * 1 = strictly sequential on `stream`).  Each extra lane holds its own workspace. */
 int gsr_set_frames_in_flight(gsr_context* ctx, int frames);

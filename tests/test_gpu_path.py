@@ -115,6 +115,55 @@ def test_path_is_stream_ordered(gpu, orc, torch, c1):
         assert sm == pytest.approx(float(want.astype(np.float64).sum()), rel=1e-12)
 
 
+def test_path_frame_events_without_join(gpu, orc, torch, c1):
+    """gsr_render_path_ex as the multi-GPU frame loop drives it: per-frame completion
+    events, no exit join, three chained calls over the same five buffers.  A consumer
+    stream waits on each frame's event and copies the image out; the caller's stream
+    waits on the consumer before the next call reuses the buffers.  Every copy equals
+    its frame's oracle image (a copy taken before its frame finished, or a buffer
+    overwritten before its copy, would not)."""
+    path, soa = c1
+    W, H = 320, 240
+    F, chunk, calls = 4, 5, 3
+    cams = orbit_cams(gpu, W, H, chunk * calls)
+    scene = gpu.Scene.from_soa(soa)
+    r = gpu.Renderer()
+    r.set_frames_in_flight(F)
+    bufs = [torch.empty(3 * W * H, device="cuda") for _ in range(chunk)]
+    ptrs = [b.data_ptr() for b in bufs]
+    # every lane renders every orbit camera once first (pair buffers at their high-water mark)
+    warm = [torch.empty(3 * W * H, device="cuda") for _ in range(4 * 8)]
+    render_path_checked(r, scene, [orbit_cams(gpu, W, H, 8)[(i // F) % 8] for i in range(4 * 8)], W, H,
+                        [w.data_ptr() for w in warm])
+    torch.cuda.synchronize()
+    evs = [torch.cuda.Event() for _ in range(chunk)]
+    S = torch.cuda.current_stream()
+    cons = torch.cuda.Stream()
+    snaps = []
+    for c in range(calls):
+        S.wait_stream(cons)                       # the buffers' previous copies are done
+        rc = r.render_path(scene, cams[c * chunk:(c + 1) * chunk], W, H, ptrs, events=evs, join=False,
+                           stream=S.cuda_stream)
+        assert rc == 0
+        with torch.cuda.stream(cons):
+            for j in range(chunk):
+                cons.wait_event(evs[j])
+                snaps.append(bufs[j].clone())
+    torch.cuda.synchronize()
+    assert r.sync() == 0
+    for cam, snap in zip(cams, snaps):
+        assert_image_parity(snap.view(3, H, W).cpu().numpy(), orc.render(soa, cam, W, H, 3.0))
+
+
+def test_path_ex_rejects_unknown_flags(gpu, torch, c1):
+    import ctypes
+    from gaussianrenderer_amd import _native
+    r = gpu.Renderer()
+    rc = _native.lib().gsr_render_path_ex(r.ctx, None, 0, 0, None, None, 0, 64, 64, 1, 1, 64, 64, 3.0, None,
+                                          None, None, ctypes.c_int(2))
+    assert rc == _native.GSR_E_ARG
+
+
 def test_path_4d_times(gpu, orc, torch, tmp_path_factory):
     p = tmp_path_factory.mktemp("p4d") / "scene4d.ply"
     gpu.write_synthetic_ply4d(str(p), 20_000, 5)

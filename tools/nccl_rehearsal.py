@@ -28,9 +28,16 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--n", type=int, default=200_000)
+    ap.add_argument("--gaussians", dest="n", type=int, default=200_000)
     ap.add_argument("--W", type=int, default=1280)
     ap.add_argument("--H", type=int, default=720)
+    ap.add_argument("--chunk", type=int, default=8)
+    ap.add_argument("--inflight", type=int, default=4)
+    ap.add_argument("--gather", choices=("step", "none"), default="step",
+                    help="none: the same frames with no gathers (one render_path call, the N=1 bench loop)")
+    ap.add_argument("--warm-ms", type=float, default=0.0, help="untimed sustained frames before the timed ones")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="render_path joins at every chunk (the drain the per-frame events remove)")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -48,10 +55,10 @@ def main():
     W, H = a.W, a.H
     cam = multi.orbit_camera(info.rank, W, H)
     r = gsr.Renderer()
-    r.set_frames_in_flight(4)
+    r.set_frames_in_flight(a.inflight)
     stream = torch.cuda.current_stream().cuda_stream
-    shard = multi.FrameShard(dist, r, scene, cam, W, H, steps=a.steps, gather="step", inflight=4, chunk=8,
-                             stream=stream)
+    shard = multi.FrameShard(dist, r, scene, cam, W, H, steps=a.steps, gather=a.gather, inflight=a.inflight, chunk=a.chunk,
+                             stream=stream, overlap=not a.no_overlap)
     # reference image of this rank's camera (grows the pair buffers too)
     ref = torch.empty(3 * W * H, device="cuda")
     for _ in range(3):
@@ -59,10 +66,15 @@ def main():
         if r.sync() == 0:
             break
     for _ in range(3):            # warm the lanes (their pair buffers grow on overflow)
-        rc = shard.path(0, 8, list(range(8)))
+        rc = shard.path(0, 8, [j % len(shard.outs) for j in range(8)])
         if r.sync() == 0 and rc == 0:
             break
     torch.cuda.synchronize()
+    w0 = time.perf_counter()
+    while (time.perf_counter() - w0) * 1e3 < a.warm_ms:
+        shard.run(a.steps)
+        shard.drain()
+        torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
     shard.run(a.steps)
@@ -74,7 +86,11 @@ def main():
     # every rank's reference to rank 0, compared with what the per-step gathers delivered
     refs = multi.gather_frames(dist, ref)
     ok = True
-    if info.rank == 0:
+    if info.rank == 0 and shard.recv is None:
+        print(f"nccl rehearsal: world {info.world}, {a.steps} frames per rank, no gathers; "
+              f"{info.world * a.steps / mx:.1f} frames/s aggregate ({a.inflight} lanes, warm {a.warm_ms:.0f} ms)",
+              flush=True)
+    elif info.rank == 0:
         used = sorted({(c0 // shard.chunk % shard.nsets) * shard.per_set + j
                        for c0 in range(0, a.steps, shard.chunk) for j in range(min(shard.chunk, a.steps - c0))})
         for b in used:
@@ -85,7 +101,9 @@ def main():
                     print(f"MISMATCH buffer {b} rank {src}", flush=True)
         print(f"nccl rehearsal: world {info.world}, {a.steps} frames per rank, {len(used)} buffers checked, "
               f"{'bit-exact' if ok else 'FAILED'}; {info.world * a.steps / mx:.1f} frames/s aggregate "
-              f"(max elapsed {mx * 1e3:.2f} ms)", flush=True)
+              f"(max elapsed {mx * 1e3:.2f} ms, {'join per chunk' if a.no_overlap else 'frame events, no join'}, "
+              f"chunk {a.chunk}, {a.inflight} lanes, "
+              f"HW queues {os.environ.get('GPU_MAX_HW_QUEUES', 'default')}, warm {a.warm_ms:.0f} ms, {W}x{H}, n {a.n})", flush=True)
     dist.barrier()
     dist.destroy_process_group()
     sys.exit(0 if ok else 1)
