@@ -78,6 +78,7 @@ def main():
     dist.barrier()
     t0 = time.perf_counter()
     shard.run(a.steps)
+    t_enq = time.perf_counter() - t0          # host time to enqueue the frames and gathers
     shard.drain()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -88,7 +89,8 @@ def main():
     ok = True
     if info.rank == 0 and shard.recv is None:
         print(f"nccl rehearsal: world {info.world}, {a.steps} frames per rank, no gathers; "
-              f"{info.world * a.steps / mx:.1f} frames/s aggregate ({a.inflight} lanes, warm {a.warm_ms:.0f} ms)",
+              f"{info.world * a.steps / mx:.1f} frames/s aggregate ({a.inflight} lanes, warm {a.warm_ms:.0f} ms, "
+              f"host enqueue {t_enq * 1e3:.2f} ms)",
               flush=True)
     elif info.rank == 0:
         used = sorted({(c0 // shard.chunk % shard.nsets) * shard.per_set + j
@@ -101,7 +103,7 @@ def main():
                     print(f"MISMATCH buffer {b} rank {src}", flush=True)
         print(f"nccl rehearsal: world {info.world}, {a.steps} frames per rank, {len(used)} buffers checked, "
               f"{'bit-exact' if ok else 'FAILED'}; {info.world * a.steps / mx:.1f} frames/s aggregate "
-              f"(max elapsed {mx * 1e3:.2f} ms, {'join per chunk' if a.no_overlap else 'frame events, no join'}, "
+              f"(max elapsed {mx * 1e3:.2f} ms, host enqueue {t_enq * 1e3:.2f} ms, {'join per chunk' if a.no_overlap else 'frame events, no join'}, "
               f"chunk {a.chunk}, {a.inflight} lanes, "
               f"HW queues {os.environ.get('GPU_MAX_HW_QUEUES', 'default')}, warm {a.warm_ms:.0f} ms, {W}x{H}, n {a.n})", flush=True)
     dist.barrier()
