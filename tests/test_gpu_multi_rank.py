@@ -4,7 +4,8 @@ its orbit camera (azimuth 45 deg * rank, camera.cpp:130-158) through
 Renderer.render_path with frames in flight, hands every frame to rank 0 per step
 (double-buffered chunks, pending-gather reuse), and max-reduces the elapsed time.
 Rank 0's gathered frames must equal the oracle's renders of cameras 0 and 1 bit for
-bit.  Also: bench.py --gpus 2 launches two real ranks and prints n_gpus 2."""
+bit.  Also: the RCCL branch at world 1, and bench.py --gpus 2 launches two real ranks
+and prints n_gpus 2."""
 import json
 import os
 import socket
@@ -79,6 +80,65 @@ def test_two_rank_hip_frames_gathered(gpu, orc, tmp_path):
     for b in range(steps):
         for r in range(world):
             assert np.array_equal(recv[b][r], wants[r]), f"buffer {b}, rank {r}"
+
+
+def _nccl_worker(port, ply, W, H, steps, chunk, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    import gaussianrenderer_amd as gsr
+    from gaussianrenderer_amd import multi
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    scene = gsr.Scene.from_ply(ply)
+    r = gsr.Renderer()
+    r.set_frames_in_flight(3)
+    cam = multi.orbit_camera(0, W, H)
+    shard = multi.FrameShard(dist, r, scene, cam, W, H, steps=steps, gather="step", inflight=3, chunk=chunk,
+                             stream=torch.cuda.current_stream().cuda_stream)
+    assert shard.frame_events is not None          # RCCL: per-frame events, no join
+    for _ in range(3):                             # grow the lanes' pair buffers first
+        if shard.path(0, 3, [0, 1, 2]) == 0 and r.sync() == 0:
+            break
+    torch.cuda.synchronize()
+    for b in range(len(shard.outs)):
+        shard.outs[b].fill_(-1.0)
+    torch.cuda.synchronize()
+    shard.run(steps)
+    shard.drain()
+    torch.cuda.synchronize()
+    ok = r.sync() == 0
+    elapsed = multi.max_over_ranks(dist, 0.5, "cuda")
+    q.put((ok, elapsed, [shard.recv[b][0].cpu().numpy().copy() for b in range(len(shard.recv))]))
+    dist.destroy_process_group()
+
+
+def test_rccl_world1_frame_events(gpu, orc, tmp_path):
+    """The RCCL branch of FrameShard (what bench.py --gpus N runs on a node): each frame's
+    gather waits on that frame's completion event (gsr_render_path_ex) and the lanes do
+    not join between chunks.  World 1 (RCCL cannot put two ranks on one GPU): 7 frames in
+    chunks of 3 over two buffer sets, so a set is re-used behind its pending gathers;
+    every gathered buffer must equal the oracle's render bit for bit."""
+    W, H, steps, chunk = 320, 240, 7, 3
+    ply = str(tmp_path / "s.ply")
+    gpu.write_synthetic_ply(ply, 10_000, 4)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), ply, W, H, steps, chunk, q))
+    p.start()
+    try:
+        ok, elapsed, recv = q.get(timeout=100)
+    finally:
+        p.join(timeout=60)
+    assert p.exitcode == 0 and ok
+    assert elapsed == pytest.approx(0.5)
+    soa = gpu.read_ply(ply)
+    from gaussianrenderer_amd import multi
+    want = orc.render(soa, multi.orbit_camera(0, W, H), W, H, 3.0).reshape(-1)
+    assert len(recv) == 2 * chunk
+    for b, got in enumerate(recv):
+        assert np.array_equal(got, want), f"buffer {b}"
 
 
 def test_bench_launches_ranks(gpu, tmp_path):
