@@ -95,6 +95,14 @@ class FrameShard:
         self.recv = ([[torch.empty_like(self.outs[0], device="cpu" if gloo else self.outs[0].device)
                        for _ in range(world)] for _ in range(len(self.outs))]
                      if (self.step_gather and rank == 0) else None)
+        if self.recv is not None and not gloo:
+            # rank 0's own slot IS its output buffer: the gather's local copy of the
+            # root's frame (torch copies input -> gather_list[root]) becomes a no-op,
+            # which at world 1 was the whole gather cost (a 24.9-MB device copy per
+            # frame competing with the blends).  Same lifetime as the other slots: a
+            # buffer is rendered again only after its pending gather completed.
+            for b in range(len(self.outs)):
+                self.recv[b][0] = self.outs[b]
         self.pending = [None] * len(self.outs)
         # RCCL: each gather waits for its own frame's completion event (gsr_render_path_ex)
         # on a side stream, and render_path runs without the exit join, so the lanes keep

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--gather", choices=("step", "none"), default="step",
                     help="none: the same frames with no gathers (one render_path call, the N=1 bench loop)")
     ap.add_argument("--warm-ms", type=float, default=0.0, help="untimed sustained frames before the timed ones")
+    ap.add_argument("--no-gather-calls", action="store_true",
+                    help="diagnostic: the chunked per-step loop without issuing the gathers (no buffer check)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="render_path joins at every chunk (the drain the per-frame events remove)")
     a = ap.parse_args()
@@ -59,6 +61,8 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     shard = multi.FrameShard(dist, r, scene, cam, W, H, steps=a.steps, gather=a.gather, inflight=a.inflight, chunk=a.chunk,
                              stream=stream, overlap=not a.no_overlap)
+    if a.no_gather_calls:
+        shard.gather = lambda b: None
     # reference image of this rank's camera (grows the pair buffers too)
     ref = torch.empty(3 * W * H, device="cuda")
     for _ in range(3):
@@ -87,9 +91,10 @@ def main():
     # every rank's reference to rank 0, compared with what the per-step gathers delivered
     refs = multi.gather_frames(dist, ref)
     ok = True
-    if info.rank == 0 and shard.recv is None:
+    if info.rank == 0 and (shard.recv is None or a.no_gather_calls):
         print(f"nccl rehearsal: world {info.world}, {a.steps} frames per rank, no gathers; "
               f"{info.world * a.steps / mx:.1f} frames/s aggregate ({a.inflight} lanes, warm {a.warm_ms:.0f} ms, "
+              f"{'chunked step loop without gather calls, ' if a.no_gather_calls else ''}"
               f"host enqueue {t_enq * 1e3:.2f} ms)",
               flush=True)
     elif info.rank == 0:
