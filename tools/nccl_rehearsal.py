@@ -36,6 +36,10 @@ def main():
     ap.add_argument("--gather", choices=("step", "none"), default="step",
                     help="none: the same frames with no gathers (one render_path call, the N=1 bench loop)")
     ap.add_argument("--warm-ms", type=float, default=0.0, help="untimed sustained frames before the timed ones")
+    ap.add_argument("--events-only", action="store_true",
+                    help="diagnostic (--gather none): the one render_path call, plus a completion event per frame")
+    ap.add_argument("--ring", type=int, default=0,
+                    help="diagnostic (--gather none): output ring of this many buffers instead of one per lane")
     ap.add_argument("--no-gather-calls", action="store_true",
                     help="diagnostic: the chunked per-step loop without issuing the gathers (no buffer check)")
     ap.add_argument("--no-overlap", action="store_true",
@@ -63,6 +67,16 @@ def main():
                              stream=stream, overlap=not a.no_overlap)
     if a.no_gather_calls:
         shard.gather = lambda b: None
+    if a.ring and a.gather == "none":
+        shard.outs = [torch.empty(3 * W * H, device="cuda") for _ in range(a.ring)]
+        shard.F = a.ring        # run(): frame j -> outs[j % ring]
+        shard.pending = [None] * a.ring
+    if a.events_only and a.gather == "none":
+        evs = [torch.cuda.Event() for _ in range(len(shard.outs))]
+        nb = len(shard.outs)
+        shard.run = lambda steps: r.render_path(scene, [cam] * steps, W, H,
+                                                [shard.outs[j % nb].data_ptr() for j in range(steps)],
+                                                stream=stream, events=[evs[j % nb] for j in range(steps)])
     # reference image of this rank's camera (grows the pair buffers too)
     ref = torch.empty(3 * W * H, device="cuda")
     for _ in range(3):
@@ -95,6 +109,8 @@ def main():
         print(f"nccl rehearsal: world {info.world}, {a.steps} frames per rank, no gathers; "
               f"{info.world * a.steps / mx:.1f} frames/s aggregate ({a.inflight} lanes, warm {a.warm_ms:.0f} ms, "
               f"{'chunked step loop without gather calls, ' if a.no_gather_calls else ''}"
+              f"{'one call with per-frame events, ' if a.events_only else ''}"
+              f"{f'ring of {a.ring} outputs, ' if a.ring else ''}"
               f"host enqueue {t_enq * 1e3:.2f} ms)",
               flush=True)
     elif info.rank == 0:
