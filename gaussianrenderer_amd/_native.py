@@ -26,7 +26,8 @@ GSR_E_HIP = -2
 GSR_E_IO = -3
 GSR_E_FORMAT = -4
 GSR_E_OVERFLOW = -5
-GSR_PATH_NO_JOIN = 1   # gsr_render_path_ex flag (include/gsr.h)
+GSR_PATH_NO_JOIN = 1   # gsr_render_path_ex flags (include/gsr.h)
+GSR_PATH_NO_FORK = 2
 GSR_E_DISPLAY = -6
 
 LAYOUT_SCENE_BLOCK = 0
@@ -107,7 +108,8 @@ SIGNATURES = [
     ("gsr_render_path", c_int, [c_void_p, c_void_p, c_int, c_int64, POINTER(Camera), c_void_p, c_int, c_int,
                                 c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p]),
     ("gsr_render_path_ex", c_int, [c_void_p, c_void_p, c_int, c_int64, POINTER(Camera), c_void_p, c_int, c_int,
-                                   c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_int]),
+                                   c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_int]),
     ("gsr_set_frames_in_flight", c_int, [c_void_p, c_int]),
     ("gsr_frames_in_flight", c_int, [c_void_p]),
     ("gsr_preprocess", c_int, [c_void_p, c_void_p, c_int, c_int64, POINTER(Camera), c_int, c_int, c_int, c_int,

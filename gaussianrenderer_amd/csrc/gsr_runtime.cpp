@@ -941,15 +941,16 @@ extern "C" int gsr_render_path(gsr_context* c, const void* scene, int layout, in
                                const float* times, int nframes, int W, int H, int nx, int ny, int ws, int hs,
                                float k, float* const* d_outs, void* stream) {
     return gsr_render_path_ex(c, scene, layout, n, cams, times, nframes, W, H, nx, ny, ws, hs, k, d_outs, stream,
-                              nullptr, 0);
+                              nullptr, nullptr, 0);
 }
 
 extern "C" int gsr_render_path_ex(gsr_context* c, const void* scene, int layout, int64_t n, const gsr_camera* cams,
                                   const float* times, int nframes, int W, int H, int nx, int ny, int ws, int hs,
                                   float k, float* const* d_outs, void* stream, void* const* frame_events,
-                                  int flags) {
+                                  void* const* wait_events, int flags) {
     if (!c) return set_err(GSR_E_ARG, "null context");
-    if (flags & ~GSR_PATH_NO_JOIN) return set_err(GSR_E_ARG, "gsr_render_path_ex: unknown flags 0x%x", flags);
+    if (flags & ~(GSR_PATH_NO_JOIN | GSR_PATH_NO_FORK))
+        return set_err(GSR_E_ARG, "gsr_render_path_ex: unknown flags 0x%x", flags);
     if (nframes < 0 || (nframes > 0 && (!cams || !d_outs)))
         return set_err(GSR_E_ARG, "gsr_render_path: bad frame arrays");
     for (int i = 0; i < nframes; i++)
@@ -970,7 +971,7 @@ extern "C" int gsr_render_path_ex(gsr_context* c, const void* scene, int layout,
         }
     }
     // fork: every lane starts after the work already queued on the caller's stream
-    if (F > 1) {
+    if (F > 1 && !(flags & GSR_PATH_NO_FORK)) {
         HIP_TRY(hipEventRecord(c->fork_ev, S));
         for (int l = 0; l < F - 1; l++) HIP_TRY(hipStreamWaitEvent(c->lane_streams[l], c->fork_ev, 0));
     }
@@ -1001,6 +1002,7 @@ extern "C" int gsr_render_path_ex(gsr_context* c, const void* scene, int layout,
         gsr_context* lc = lane == 0 ? c : c->lanes[lane - 1];
         const hipStream_t ls = lane == 0 ? S : c->lane_streams[lane - 1];
         if (prev[i] >= 0 && prev[i] % F != lane) HIP_TRY(hipStreamWaitEvent(ls, c->alias_evs[prev[i] % F], 0));
+        if (wait_events && wait_events[i]) HIP_TRY(hipStreamWaitEvent(ls, static_cast<hipEvent_t>(wait_events[i]), 0));
         if (times) lc->time = times[i];
         else lc->time = t_saved;
         const int rc = render_one_locked(lc, scene, layout, n, &cams[i], W, H, nx, ny, ws, hs, k, d_outs[i], ls);

@@ -110,6 +110,12 @@ class FrameShard:
         self.frame_events = (None if (gloo or not self.step_gather or not overlap)
                              else [torch.cuda.Event() for _ in range(len(self.outs))])
         self.gather_stream = torch.cuda.Stream() if self.frame_events else None
+        # ... and buffer b's next frame waits on the completion of b's last gather
+        # (recorded on the side stream) instead of the whole path waiting on the caller's
+        # stream: the chunked calls skip the fork, which otherwise holds lanes 1.. behind
+        # lane 0's frames of the previous call (~4 % of the rate)
+        self.gathered = [torch.cuda.Event() for _ in range(len(self.outs))] if self.frame_events else None
+        self.gathered_valid = [False] * len(self.outs)
 
     def _times(self, i0: int, m: int):
         return [self.frame_time(i0 + j) for j in range(m)] if self.frame_time else None
@@ -132,6 +138,9 @@ class FrameShard:
                 self.gather_stream.wait_event(self.frame_events[b])
                 self.pending[b] = self.dist.gather(self.outs[b], self.recv[b] if self.recv else None, dst=0,
                                                    async_op=True)
+                self.pending[b].wait()                       # side stream: after the gather
+                self.gathered[b].record(self.gather_stream)
+                self.gathered_valid[b] = True
             return
         src = self.outs[b].cpu() if self.gloo else self.outs[b]
         self.pending[b] = self.dist.gather(src, self.recv[b] if self.recv else None, dst=0,
@@ -142,14 +151,18 @@ class FrameShard:
         self.r.render(self.scene, self.cam, self.W, self.H, self.outs[b].data_ptr(), k=self.k,
                       stream=self.stream, time=self.frame_time(i) if self.frame_time else None)
 
-    def path(self, i0: int, m: int, bufs, overlap: bool = False):
+    def path(self, i0: int, m: int, bufs, overlap: bool = False, first: bool = True):
         """Frames i0 .. i0+m-1 through gsr_render_path into outs[bufs[j]]; returns its code
         (GSR_E_OVERFLOW: some frame of the call overflowed and must be re-rendered).
-        overlap: record each buffer's frame event and skip the exit join (run())."""
+        overlap (run()): record each buffer's frame event, skip the exit join, wait per
+        frame on the buffer's last gather, and fork from the caller's stream only on the
+        first call of a run."""
         ov = overlap and self.frame_events is not None
+        waits = [self.gathered[b] if self.gathered_valid[b] else None for b in bufs] if ov else None
         return self.r.render_path(self.scene, [self.cam] * m, self.W, self.H, [self.outs[b].data_ptr() for b in bufs],
                                   k=self.k, stream=self.stream, times=self._times(i0, m),
-                                  events=[self.frame_events[b] for b in bufs] if ov else None, join=not ov)
+                                  events=[self.frame_events[b] for b in bufs] if ov else None, join=not ov,
+                                  fork=not ov or first, wait_events=waits)
 
     def run(self, steps: int):
         """K frames in flight, gathered per step when enabled (not drained: call drain())."""
@@ -160,8 +173,9 @@ class FrameShard:
             m = min(self.chunk, steps - c0)
             base = ((c0 // self.chunk) % self.nsets) * self.per_set
             bufs = [base + j for j in range(m)]
-            for b in bufs:
-                self.wait_pending(b)
-            self.path(c0, m, bufs, overlap=True)
+            if not self.frame_events:                # gloo: the caller's stream orders reuse
+                for b in bufs:
+                    self.wait_pending(b)
+            self.path(c0, m, bufs, overlap=True, first=c0 == 0)
             for b in bufs:
                 self.gather(b)

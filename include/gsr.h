@@ -159,10 +159,18 @@ int gsr_render_path(gsr_context* ctx, const void* d_scene, int layout, int64_t n
  * orders everything else through the events: reading frame i, and re-using one of
  * this call's output buffers in a later call (wait for the buffer's last frame). */
 #define GSR_PATH_NO_JOIN 1
+/* flags & GSR_PATH_NO_FORK: lanes 1..F-1 do not wait for `stream` (lane 0 still runs
+ * on it), so they are never held behind lane 0's frames of an earlier call (with the
+ * fork, chunked calls cost ~4 % of the in-flight rate); the caller orders the frames
+ * after its own work through wait_events instead. */
+#define GSR_PATH_NO_FORK 2
+/* wait_events (may be NULL; entries may be NULL): frame i's lane waits for
+ * hipEvent_t wait_events[i] before rendering frame i (e.g. the hand-off of the frame
+ * that last used d_outs[i]). */
 int gsr_render_path_ex(gsr_context* ctx, const void* d_scene, int layout, int64_t n, const gsr_camera* cams,
                        const float* times, int nframes, int W, int H, int num_tile_x, int num_tile_y,
                        int width_stride, int height_stride, float k, float* const* d_outs, void* stream,
-                       void* const* frame_events, int flags);
+                       void* const* frame_events, void* const* wait_events, int flags);
 /* Frames in flight for gsr_render_path: 1..GSR_MAX_FRAMES_IN_FLIGHT (default 3;
  * 1 = strictly sequential on `stream`).  Each extra lane holds its own workspace. */
 int gsr_set_frames_in_flight(gsr_context* ctx, int frames);

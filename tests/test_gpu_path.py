@@ -160,7 +160,7 @@ def test_path_ex_rejects_unknown_flags(gpu, torch, c1):
     from gaussianrenderer_amd import _native
     r = gpu.Renderer()
     rc = _native.lib().gsr_render_path_ex(r.ctx, None, 0, 0, None, None, 0, 64, 64, 1, 1, 64, 64, 3.0, None,
-                                          None, None, ctypes.c_int(2))
+                                          None, None, None, ctypes.c_int(4))
     assert rc == _native.GSR_E_ARG
 
 

@@ -40,6 +40,8 @@ def main():
                     help="diagnostic (--gather none): the one render_path call, plus a completion event per frame")
     ap.add_argument("--ring", type=int, default=0,
                     help="diagnostic (--gather none): output ring of this many buffers instead of one per lane")
+    ap.add_argument("--no-fork", action="store_true",
+                    help="diagnostic (with --no-gather-calls): render_path calls without the fork (GSR_PATH_NO_FORK)")
     ap.add_argument("--no-gather-calls", action="store_true",
                     help="diagnostic: the chunked per-step loop without issuing the gathers (no buffer check)")
     ap.add_argument("--no-overlap", action="store_true",
@@ -67,6 +69,11 @@ def main():
                              stream=stream, overlap=not a.no_overlap)
     if a.no_gather_calls:
         shard.gather = lambda b: None
+        if a.no_fork:
+            def path_nofork(i0, m, bufs, overlap=False):
+                return r.render_path(scene, [cam] * m, W, H, [shard.outs[b].data_ptr() for b in bufs],
+                                     stream=stream, join=False, fork=False)
+            shard.path = path_nofork
     if a.ring and a.gather == "none":
         shard.outs = [torch.empty(3 * W * H, device="cuda") for _ in range(a.ring)]
         shard.F = a.ring        # run(): frame j -> outs[j % ring]
@@ -109,6 +116,7 @@ def main():
         print(f"nccl rehearsal: world {info.world}, {a.steps} frames per rank, no gathers; "
               f"{info.world * a.steps / mx:.1f} frames/s aggregate ({a.inflight} lanes, warm {a.warm_ms:.0f} ms, "
               f"{'chunked step loop without gather calls, ' if a.no_gather_calls else ''}"
+              f"{'no fork, ' if a.no_fork else ''}"
               f"{'one call with per-frame events, ' if a.events_only else ''}"
               f"{f'ring of {a.ring} outputs, ' if a.ring else ''}"
               f"host enqueue {t_enq * 1e3:.2f} ms)",
