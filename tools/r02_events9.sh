@@ -17,6 +17,7 @@ run() {
 }
 for rep in 1 2; do
   run step$rep ""
+  run step3_$rep "--inflight 3"
   run step16_$rep "--chunk 16"
   run none$rep "--gather none"
 done
