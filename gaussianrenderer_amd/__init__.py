@@ -242,15 +242,20 @@ def preprocessCUDAGaussiansGL(d_gaussians: int, gl_buffer: int, num_gaussians: i
                                     width_stride, height_stride, tile_W, tile_H, k)
 
 
-def _event_handle(ev):
-    """hipEvent_t of a torch.cuda.Event (created on first use: the library records into
-    it), or of a raw integer handle; None -> NULL."""
+def _event_handle(ev, wait: bool = False):
+    """hipEvent_t of a torch.cuda.Event, or of a raw integer handle; None -> NULL.
+    An event the library records into (wait=False) is created on first use (torch
+    creates the HIP event lazily, at its first record).  A wait event that was never
+    recorded has nothing to wait for: NULL (recording it here would make the lane wait
+    on all work queued on torch's current stream, an implicit fork)."""
     if ev is None:
         return None
     if isinstance(ev, int):
         return ev
     if not ev.cuda_event:
-        ev.record()          # torch creates the HIP event lazily, at its first record
+        if wait:
+            return None
+        ev.record()
     return ev.cuda_event
 
 
@@ -331,7 +336,7 @@ class Renderer:
             if (events is not None and len(events) != nf) or (wait_events is not None and len(wait_events) != nf):
                 raise ValueError("render_path: events and wait_events must have one entry per frame")
             ev_arr = (c_void_p * max(1, nf))(*[_event_handle(e) for e in (events or [None] * nf)])
-            wt_arr = (c_void_p * max(1, nf))(*[_event_handle(e) for e in (wait_events or [None] * nf)])
+            wt_arr = (c_void_p * max(1, nf))(*[_event_handle(e, wait=True) for e in (wait_events or [None] * nf)])
             rc = lib().gsr_render_path_ex(self.ctx, ptr, layout, n, cam_arr, t_arr, nf, W, H, t.num_tile_x,
                                           t.num_tile_y, t.width_stride, t.height_stride, k, out_arr,
                                           stream or None, ev_arr, wt_arr,
@@ -478,6 +483,21 @@ class Renderer:
 
 def device_available() -> bool:
     return bool(lib().gsr_device_available())
+
+
+# gsr_set_tuning knobs used by the tests and tools (include/gsr.h lists them all)
+TUNE_TILE_BINNING = 7
+TUNE_TILE_SPANS = 19
+TUNE_RANK_ATOMIC = 20
+TUNE_RANK_ATOMIC_ACTIVE = 21
+
+
+def rank_order_check() -> tuple[int, int]:
+    """gsr_rank_order_check: (lane-operations checked, lanes out of lane order) of the
+    device self-check behind the atomic rank path (include/gsr.h)."""
+    ops, bad = c_int64(0), c_int64(0)
+    check(lib().gsr_rank_order_check(byref(ops), byref(bad)), "gsr_rank_order_check")
+    return int(ops.value), int(bad.value)
 
 
 def math_probe(xy: np.ndarray) -> np.ndarray:

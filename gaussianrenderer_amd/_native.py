@@ -154,6 +154,7 @@ SIGNATURES = [
     ("gsr_version", c_char_p, []),
     ("gsr_device_available", c_int, []),
     ("gsr_math_probe", c_int, [c_void_p, c_int, c_void_p]),
+    ("gsr_rank_order_check", c_int, [POINTER(c_int64), POINTER(c_int64)]),
 ]
 
 # C++-linkage drop-in loader (misc.cuh:4): mangled name of

@@ -61,7 +61,7 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
                              int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
                              uint2* ranges, hipStream_t s, uint32_t* dstats = nullptr, int pass = 0,
                              const uint32_t* rect = nullptr, int rect_direct = 0, uint32_t* pay0 = nullptr,
-                             uint32_t* pay1 = nullptr);
+                             uint32_t* pay1 = nullptr, bool rank_atomic = false);
 // Pair emission in depth order: tile counts (gathering each Gaussian's rect
 // once into srect, and zeroing the tile ranges), scan, then keys (uint16_t if
 // key16 else uint32_t) + values.
@@ -93,11 +93,12 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
                            const uint32_t* pay0, const uint32_t* pay1, int groups, uint32_t* hist,
                            uint32_t* row_items,
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
-                           int items, hipStream_t s, const uint16_t* spans = nullptr);
+                           int items, hipStream_t s, const uint16_t* spans = nullptr, bool rank_atomic = false);
 hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, const unsigned long long* row_pairs,
                            uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
                            uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,
-                           hipStream_t s, const uint32_t* dstats = nullptr, int passes_launched = 4);
+                           hipStream_t s, const uint32_t* dstats = nullptr, int passes_launched = 4,
+                           bool rank_atomic = false);
 uint32_t bin_col_chunks_max(uint32_t pair_capacity, int tiles_y);
 // Standalone sort ABI helpers (oneSweepSort / oneSweep3DGaussianSort).
 hipError_t launch_items_from_keys(const int* keys, uint32_t n, uint64_t* items, hipStream_t s);
@@ -106,6 +107,11 @@ hipError_t launch_items_from_lwg(const gsr_lwg* rec, const uint64_t* src_perm, u
                                  uint32_t mask, uint64_t* items, hipStream_t s);
 hipError_t launch_gather_lwg(const gsr_lwg* in, const uint64_t* stage1, const uint64_t* stage2, uint32_t n,
                              gsr_lwg* out, hipStream_t s);
+
+// Device self-check of the lane order of same-address returning LDS atomics (the
+// RA rank path): runs k_rank_order_check synchronously on the current device and
+// returns the lane-operations checked and how many returned a value out of lane order.
+hipError_t rank_order_check(unsigned long long* lane_ops, unsigned long long* mismatches);
 
 // Device math probe for the detmath GPU parity test.
 hipError_t launch_math_probe(const float* in, int n, float* out, hipStream_t s);

@@ -652,16 +652,16 @@ __device__ __forceinline__ uint64_t match_peers(uint32_t d, bool valid, int bits
     return ((uint64_t)hi << 32) | lo;
 }
 
-// Stable in-wave ranks from returning LDS atomics (GSR_RANK_ATOMIC, default):
-// atomicAdd(&count[digit], 1) from one wave64 instruction returns the old values in
-// LANE order when several lanes hit one address — measured on gfx950 with no
-// exception in 1.5e10 lane-operations over uniform, skewed, run and interleaved digit
-// patterns (tools/microbench/lds_atomic_order.hip) — so the returned value is the
-// element's stable rank among the wave's earlier elements of its digit: one LDS op
-// instead of ballot matching (4 VALU per digit bit, match_peers).  0: ballot matching.
-#ifndef GSR_RANK_ATOMIC
-#define GSR_RANK_ATOMIC 1
-#endif
+// Stable in-wave ranks from returning LDS atomics (template flag RA, runtime knob
+// GSR_TUNE_RANK_ATOMIC): atomicAdd(&count[digit], 1) from one wave64 instruction
+// returns the old values in LANE order when several lanes hit one address — measured
+// on gfx950 with no exception in 1.5e10 lane-operations over uniform, skewed, run and
+// interleaved digit patterns (tools/microbench/lds_atomic_order.hip) — so the returned
+// value is the element's stable rank among the wave's earlier elements of its digit:
+// one LDS op instead of ballot matching (4 VALU per digit bit, match_peers).  The ISA
+// does not document that order, so the runtime only takes RA = true after
+// k_rank_order_check (below) has found it on the device in this process; otherwise,
+// or with the knob at 0, every kernel ranks with ballots (RA = false).
 
 // ------------------------------------------------------------------ radix sort
 //
@@ -822,7 +822,7 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
 // Payloads leave through the items' LDS slots, in the same digit runs.
 // (The rects used to be gathered in the last pass only: a random 8-B read per item
 // that cost the 5M-Gaussian frame 76 us of its 110-us pass, profiles/r02_geom_pmc.txt.)
-template <int ITEMS>
+template <int ITEMS, bool RA>
 __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const uint64_t* __restrict__ in, uint64_t* __restrict__ out, const uint32_t* __restrict__ n_dev,
     uint32_t n_host, int shift, int bits, int groups, const uint32_t* __restrict__ hist,
@@ -900,7 +900,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
             uint32_t r = 0;
             // returning atomics at 4-8 items per thread; at 16 (4M+ items) ballot matching
             // measured faster (config 3 depth sort 163 vs 171 us)
-            if (GSR_RANK_ATOMIC && ITEMS < 16) {
+            if (RA && ITEMS < 16) {
                 if (valid) r = atomicAdd(&s_wc[w][d], 1u);
             } else {
                 const uint64_t peers = match_peers<8>(d, valid, bits);
@@ -1342,7 +1342,7 @@ __device__ __forceinline__ uint32_t rect_cols(uint64_t r) {
 // leader of each digit ADDS the slot's count (ds_add, no return): LDS ops of a
 // wave execute in issue order, so slot k's read sees slots < k and nothing waits
 // on a read before the next slot is issued.
-template <int ITEMS, int BITS>
+template <int ITEMS, int BITS, bool RA>
 __device__ __forceinline__ uint32_t bin_rank_tile(const uint32_t (&dig)[ITEMS], uint32_t tn,
                                                   uint32_t (&pos)[ITEMS], uint32_t (*s_wc)[256],
                                                   uint32_t* s_lbase, uint32_t* s_scr) {
@@ -1351,7 +1351,7 @@ __device__ __forceinline__ uint32_t bin_rank_tile(const uint32_t (&dig)[ITEMS], 
 #pragma unroll
     for (int k = 0; k < 4; k++) s_wc[k][t] = 0;
     __syncthreads();
-    if (GSR_RANK_ATOMIC) {
+    if (RA) {
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
             const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
@@ -1592,7 +1592,7 @@ __global__ __launch_bounds__(256) void k_bin_rows_scan(uint32_t* __restrict__ hi
 // row runs to rows_out (positions >= cap are dropped; the frame then overflows
 // and the column pass emits nothing).  The sorted tile holds only each item's
 // source slot: the payload (index | tx0 << 32 | tx1 << 48) is rebuilt at the write.
-template <int ITEMS, int BITS>
+template <int ITEMS, int BITS, bool RA>
 __global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(const uint64_t* __restrict__ items0,
                                                            const uint64_t* __restrict__ items1,
                                                            const uint32_t* __restrict__ dstats,
@@ -1674,7 +1674,7 @@ __global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(co
                 const uint32_t first = l ? s_pref[l - 1] : 0u;
                 dig[k] = (uint32_t)((s_rect[l] >> 16) & 0xffu) + (tb + el - first);   // ty0 + row
             }
-            const uint32_t tcount = bin_rank_tile<ITEMS, BITS>(dig, tn, pos, s_wc, s_lbase, s_scr);
+            const uint32_t tcount = bin_rank_tile<ITEMS, BITS, RA>(dig, tn, pos, s_wc, s_lbase, s_scr);
 #pragma unroll
             for (int k = 0; k < ITEMS; k++) {
                 const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
@@ -1839,7 +1839,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restric
 // Column pass, scatter: per chunk, its row items expand into one value per
 // covered column; tiles of 256*ITEMS values are ranked by column and written in
 // column runs at tile start + chunk offset.
-template <int ITEMS, int BITS>
+template <int ITEMS, int BITS, bool RA>
 __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __restrict__ rows_in,
                                                            const uint32_t* __restrict__ row_items,
                                                            const unsigned long long* __restrict__ row_pairs,
@@ -1893,7 +1893,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
                 const uint32_t first = l ? s_pref[l - 1] : 0u;
                 dig[k] = (uint32_t)s_tx0[l] + (tb + el - first);
             }
-            const uint32_t tcount = bin_rank_tile<ITEMS, BITS>(dig, tn, pos, s_wc, s_lbase, s_scr);
+            const uint32_t tcount = bin_rank_tile<ITEMS, BITS, RA>(dig, tn, pos, s_wc, s_lbase, s_scr);
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) s_own[t * ITEMS + i] = 0;   // for the next tile (rank barriers passed)
 #pragma unroll
@@ -2420,6 +2420,69 @@ __global__ void k_gather_lwg(const gsr_lwg* __restrict__ in, const uint64_t* __r
     out[i] = in[r];
 }
 
+// ------------------------------------------------------------------ rank-order self-check
+//
+// The RA rank path (match_peers' comment) relies on same-address ds_add_rtn_u32 lanes
+// of one wave64 instruction returning the old values in lane order.  The runtime runs
+// this check once per process and device before it uses that path: every wave of
+// 256-thread workgroups (per-wave counters, as in the sort and binning kernels) ranks
+// digits from 24 patterns — 1 to 256 distinct digits; uniform, a third of the lanes on
+// one digit, runs of 16 lanes, interleaved; ~1/8 of the lanes idle — by returning
+// atomics and by ballot matching, and counts the lanes where the two differ.
+__device__ __forceinline__ uint32_t rank_check_hash(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+__global__ __launch_bounds__(256) void k_rank_order_check(uint32_t seed, int iters,
+                                                           unsigned long long* __restrict__ out) {
+    __shared__ uint32_t cnt[4][256];
+    const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
+#pragma unroll
+    for (int k = 0; k < 4; k++) cnt[k][t] = 0;
+    __syncthreads();
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    unsigned long long bad = 0, ops = 0;
+    for (int pat = 0; pat < 24; pat++) {
+        const int skew = pat / 6;
+        constexpr uint32_t kDigits[6] = {1u, 2u, 4u, 16u, 128u, 256u};
+        const uint32_t ndig = kDigits[pat % 6];
+        for (int it = 0; it < iters; it++) {
+            const uint32_t h = rank_check_hash(seed ^ (blockIdx.x * 7919u + (uint32_t)(pat * iters + it) * 104729u +
+                                                       lane * 31u + w * 1000003u));
+            uint32_t d = h % ndig;
+            if (skew == 1) d = (h >> 8) % 3u == 0u ? 0u : d;
+            if (skew == 2) d = (lane >> 4) % ndig;
+            if (skew == 3) d = ((h >> 4) & 1u) ? (lane * 5u) % ndig : 1u % ndig;
+            const bool valid = ((h >> 20) & 7u) != 0u;
+            const uint64_t peers = match_peers<8>(d, valid, 8);
+            uint32_t before = 0;
+            if (valid) before = cnt[w][d];
+            __builtin_amdgcn_wave_barrier();
+            uint32_t got = 0;
+            if (valid) got = atomicAdd(&cnt[w][d], 1u);
+            __builtin_amdgcn_wave_barrier();
+            if (valid) {
+                bad += got != before + (uint32_t)__popcll(peers & lt);
+                ops++;
+            }
+        }
+    }
+    // wave sums, one device atomic per wave
+    for (int o = 32; o >= 1; o >>= 1) {
+        bad += __shfl_xor(bad, o, 64);
+        ops += __shfl_xor(ops, o, 64);
+    }
+    if (lane == 0) {
+        atomicAdd(&out[0], ops);
+        atomicAdd(&out[1], bad);
+    }
+}
+
 // ------------------------------------------------------------------ math probe
 
 __global__ void k_math_probe(const float* __restrict__ in, int n, float* __restrict__ out) {
@@ -2468,7 +2531,7 @@ hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, con
     return hipGetLastError();
 }
 
-template <int ITEMS>
+template <int ITEMS, bool RA>
 static void radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host, int shift,
                        int bits, int groups, uint32_t* hist, uint32_t* totals, uint2* ranges, uint32_t* dstats,
                        int pass, const uint32_t* rect, int rect_direct, uint32_t* pay0, uint32_t* pay1,
@@ -2482,7 +2545,7 @@ static void radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev,
     // rect_direct < 0 — the live partition wrote it) and writes pay[(p + 1) & 1]
     const uint32_t* pay_in = pay0 && (pass > 0 || rect_direct < 0) ? ((pass & 1) ? pay1 : pay0) : nullptr;
     uint32_t* pay_out = pay0 ? ((pass & 1) ? pay0 : pay1) : nullptr;
-    hipLaunchKernelGGL(k_radix_downsweep<ITEMS>, dim3(groups), dim3(kSortThreads), 0, s, in, out, n_dev, n_host,
+    hipLaunchKernelGGL((k_radix_downsweep<ITEMS, RA>), dim3(groups), dim3(kSortThreads), 0, s, in, out, n_dev, n_host,
                        shift, bits, groups, hist, totals, ranges, static_cast<const uint32_t*>(dstats), pass, rect,
                        rect_direct > 0 ? 1 : 0, pay_in, pay_out);
 }
@@ -2490,18 +2553,25 @@ static void radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev,
 hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
                              int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
                              uint2* ranges, hipStream_t s, uint32_t* dstats, int pass, const uint32_t* rect,
-                             int rect_direct, uint32_t* pay0, uint32_t* pay1) {
+                             int rect_direct, uint32_t* pay0, uint32_t* pay1, bool rank_atomic) {
     if ((rect == nullptr) != (pay0 == nullptr) || (pay0 == nullptr) != (pay1 == nullptr))
         return hipErrorInvalidValue;
-    if (items == 4)
-        radix_pass<4>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
-                      rect_direct, pay0, pay1, s);
+    // 16 items per thread always rank with ballots (k_radix_downsweep)
+    if (items == 4 && rank_atomic)
+        radix_pass<4, true>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
+                            rect_direct, pay0, pay1, s);
+    else if (items == 4)
+        radix_pass<4, false>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
+                             rect_direct, pay0, pay1, s);
+    else if (items == 8 && rank_atomic)
+        radix_pass<8, true>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
+                            rect_direct, pay0, pay1, s);
     else if (items == 8)
-        radix_pass<8>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
-                      rect_direct, pay0, pay1, s);
+        radix_pass<8, false>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
+                             rect_direct, pay0, pay1, s);
     else
-        radix_pass<16>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
-                       rect_direct, pay0, pay1, s);
+        radix_pass<16, false>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
+                              rect_direct, pay0, pay1, s);
     return hipGetLastError();
 }
 
@@ -2536,17 +2606,21 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
                            const uint32_t* pay0, const uint32_t* pay1, int groups, uint32_t* hist,
                            uint32_t* row_items,
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
-                           int items, hipStream_t s, const uint16_t* spans) {
+                           int items, hipStream_t s, const uint16_t* spans, bool rank_atomic) {
     if (tiles_y < 1 || tiles_y > 256 || groups < 1 || groups > kMaxSortGroups / 2 ||
         (items != 4 && items != 8 && items != 16))
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_bin_rows_count, dim3(groups), dim3(256), 0, s, n, pay0, pay1, dstats, groups, tiles_y,
                        hist);
     hipLaunchKernelGGL(k_bin_rows_scan, dim3(256), dim3(256), 0, s, hist, groups, tiles_y, row_items, row_pairs);
-    auto scatter = tiles_y <= 128 ? (items == 4 ? k_bin_rows_scatter<4, 7> : items == 8 ? k_bin_rows_scatter<8, 7>
-                                                                                    : k_bin_rows_scatter<16, 7>)
-                                  : (items == 4 ? k_bin_rows_scatter<4, 8> : items == 8 ? k_bin_rows_scatter<8, 8>
-                                                                                    : k_bin_rows_scatter<16, 8>);
+    auto pick = [&](auto ra) {
+        constexpr bool RA = decltype(ra)::value;
+        return tiles_y <= 128 ? (items == 4 ? k_bin_rows_scatter<4, 7, RA> : items == 8 ? k_bin_rows_scatter<8, 7, RA>
+                                                                                     : k_bin_rows_scatter<16, 7, RA>)
+                              : (items == 4 ? k_bin_rows_scatter<4, 8, RA> : items == 8 ? k_bin_rows_scatter<8, 8, RA>
+                                                                                     : k_bin_rows_scatter<16, 8, RA>);
+    };
+    auto scatter = rank_atomic ? pick(std::true_type{}) : pick(std::false_type{});
     hipLaunchKernelGGL(scatter, dim3(groups), dim3(256), 0, s, items0, items1, dstats, pay0, pay1, n, groups, hist,
                        row_items, row_pairs, pair_capacity, tiles_y, rows_buf, spans);
     return hipGetLastError();
@@ -2555,7 +2629,7 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
 hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, const unsigned long long* row_pairs,
                            uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
                            uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,
-                           hipStream_t s, const uint32_t* dstats, int passes_launched) {
+                           hipStream_t s, const uint32_t* dstats, int passes_launched, bool rank_atomic) {
     if (tiles_x < 1 || tiles_x > 256 || tiles_y < 1 || tiles_y > 256 || col_groups < 1 ||
         (items != 4 && items != 8 && items != 16))
         return hipErrorInvalidValue;
@@ -2563,10 +2637,14 @@ hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, 
                        pair_capacity, tiles_x, cbins);
     hipLaunchKernelGGL(k_bin_cols_scan, dim3(tiles_y), dim3(256), 0, s, row_items, row_pairs, pair_capacity, tiles_x,
                        cbins, ranges, stats, host_mapped_stats, dstats, passes_launched);
-    auto scatter = tiles_x <= 128 ? (items == 4 ? k_bin_cols_scatter<4, 7> : items == 8 ? k_bin_cols_scatter<8, 7>
-                                                                                    : k_bin_cols_scatter<16, 7>)
-                                  : (items == 4 ? k_bin_cols_scatter<4, 8> : items == 8 ? k_bin_cols_scatter<8, 8>
-                                                                                    : k_bin_cols_scatter<16, 8>);
+    auto pick = [&](auto ra) {
+        constexpr bool RA = decltype(ra)::value;
+        return tiles_x <= 128 ? (items == 4 ? k_bin_cols_scatter<4, 7, RA> : items == 8 ? k_bin_cols_scatter<8, 7, RA>
+                                                                                     : k_bin_cols_scatter<16, 7, RA>)
+                              : (items == 4 ? k_bin_cols_scatter<4, 8, RA> : items == 8 ? k_bin_cols_scatter<8, 8, RA>
+                                                                                     : k_bin_cols_scatter<16, 8, RA>);
+    };
+    auto scatter = rank_atomic ? pick(std::true_type{}) : pick(std::false_type{});
     hipLaunchKernelGGL(scatter, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs, pair_capacity,
                        tiles_x, cbins, ranges, vals);
     return hipGetLastError();
@@ -2654,6 +2732,24 @@ hipError_t launch_gather_lwg(const gsr_lwg* in, const uint64_t* stage1, const ui
                              gsr_lwg* out, hipStream_t s) {
     if (n) hipLaunchKernelGGL(k_gather_lwg, dim3((n + 255) / 256), dim3(256), 0, s, in, stage1, stage2, n, out);
     return hipGetLastError();
+}
+
+hipError_t rank_order_check(unsigned long long* lane_ops, unsigned long long* mismatches) {
+    unsigned long long* d = nullptr;
+    unsigned long long h[2] = {0, 0};
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&d), sizeof h);
+    if (e != hipSuccess) return e;
+    e = hipMemset(d, 0, sizeof h);
+    // 1,024 workgroups (4 per CU) x 24 patterns x 8 iterations: ~44M lane-operations, well under 1 ms
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_rank_order_check, dim3(1024), dim3(256), 0, nullptr, 0x9E3779B9u, 8, d);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    *lane_ops = h[0];
+    *mismatches = h[1];
+    return e;
 }
 
 hipError_t launch_math_probe(const float* in, int n, float* out, hipStream_t s) {

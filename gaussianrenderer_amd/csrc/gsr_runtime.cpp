@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <mutex>
@@ -360,6 +361,11 @@ struct gsr_context {
     int blend_band_tiles = 4;        // blend: tiles per spatial band, bands dealt round-robin to the
                                      // XCDs (0: one contiguous band per XCD)
     int completion_events = 1;       // 0: no completion event / overflow query (stream capture)
+    int rank_atomic = -1;            // GSR_TUNE_RANK_ATOMIC: 1 = ranks from returning LDS atomics when the
+                                     // device self-check passed, 0 = ballot matching; -1 = not yet set
+                                     // (the environment's GSR_RANK_ATOMIC=0 selects 0, else 1)
+    bool rank_ok = false;            // the device passed the rank-order self-check (ensure_static)
+    bool overflow_seen = false;      // an overflow was reported since the last gsr_sync (which reports it again)
     // frame state
     Frame fr{};
     int64_t n = 0;
@@ -407,8 +413,48 @@ int realloc_dev(T** p, size_t count) {
     return GSR_OK;
 }
 
+// ---- rank-order self-check, once per process and device (gsr_kernels.hip
+// k_rank_order_check).  The sort and binning kernels rank with returning LDS atomics
+// only on a gfx950 device that returned every same-address lane in lane order.
+struct RankCheck {
+    int state = -1;                  // -1 not run, 0 failed / not gfx950, 1 passed
+    unsigned long long ops = 0, bad = 0;
+};
+std::mutex g_rank_mu;
+std::unordered_map<int, RankCheck> g_rank;
+
+int rank_check_device(RankCheck* out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_rank_mu);
+    RankCheck& rc = g_rank[dev];
+    if (rc.state < 0) {
+        hipDeviceProp_t prop{};
+        HIP_TRY(hipGetDeviceProperties(&prop, dev));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            rc.state = 0;
+        } else {
+            HIP_TRY(gsr::rank_order_check(&rc.ops, &rc.bad));
+            rc.state = rc.ops > 0 && rc.bad == 0 ? 1 : 0;
+        }
+    }
+    if (out) *out = rc;
+    return GSR_OK;
+}
+
+int default_rank_atomic() {
+    const char* e = std::getenv("GSR_RANK_ATOMIC");
+    return e && e[0] == '0' ? 0 : 1;
+}
+
 int ensure_static(gsr_context* c) {
+    if (c->rank_atomic < 0) c->rank_atomic = default_rank_atomic();
     if (c->hist) return GSR_OK;
+    {
+        RankCheck rk;
+        if (int rc = rank_check_device(&rk)) return rc;
+        c->rank_ok = rk.state == 1;
+    }
     if (int rc = realloc_dev(&c->hist, 256 * (size_t)gsr::kMaxSortGroups)) return rc;
     if (int rc = realloc_dev(&c->totals, 256)) return rc;
     if (int rc = realloc_dev(&c->wg, (size_t)gsr::kMaxSortGroups)) return rc;
@@ -494,6 +540,9 @@ void mark(gsr_context* c, int stage) {
 }
 
 // Read the sticky stats of finished work; grow the pair buffer after an overflow.
+// An overflow (pairs over capacity, or a depth sort short of passes) is reported
+// once here and remembered in overflow_seen until gsr_sync, so a blocking sync also
+// reports what a non-blocking check inside a render call already consumed.
 int check_overflow(gsr_context* c, bool blocking) {
     if (!c->pending) return GSR_OK;
     if (blocking) {
@@ -508,18 +557,6 @@ int check_overflow(gsr_context* c, bool blocking) {
     s.pairs_eff = hv->pairs_eff;
     s.overflow = hv->overflow;
     s.depth_passes = hv->depth_passes;
-    if (s.overflow == 2u) {
-        // the depth sort needed more passes than the budget launched: back to four,
-        // and the frame(s) since the last check re-render (GSR_E_OVERFLOW)
-        HIP_TRY(hipDeviceSynchronize());
-        c->depth_budget = 4;
-        c->depth_budget_streak = 0;
-        c->depth_budget_seen = 0;
-        HIP_TRY(hipMemset(c->stats + 1, 0, sizeof(Stats)));
-        std::memset(c->hstats, 0, sizeof(Stats));
-        return set_err(GSR_E_OVERFLOW, "depth sort needed %u passes, %d were launched; re-render",
-                       (unsigned)s.depth_passes, c->passes_launched);
-    }
     if (!s.overflow) {
         // lower the pass budget once 4 checked frames in a row needed fewer passes
         if (s.depth_passes >= 1 && (int)s.depth_passes < c->depth_budget) {
@@ -535,21 +572,29 @@ int check_overflow(gsr_context* c, bool blocking) {
         }
         return GSR_OK;
     }
-    if (s.overflow & 2u) {
+    // frames queued after the event may still be running: drain them, then read the
+    // sticky stats again, so that a pair overflow of one of them (bit 0) is seen and
+    // the grown capacity covers its total too (ensure_pairs syncs again; cheap)
+    HIP_TRY(hipDeviceSynchronize());
+    s.overflow |= hv->overflow;
+    if (hv->pairs_total > s.pairs_total) s.pairs_total = hv->pairs_total;
+    c->overflow_seen = true;
+    if (s.overflow & 2u) {   // back to four launched passes
         c->depth_budget = 4;
         c->depth_budget_streak = 0;
         c->depth_budget_seen = 0;
     }
-    // frames queued after the event may still be running: drain them so the
-    // grown capacity covers their totals too (ensure_pairs syncs again; cheap)
-    HIP_TRY(hipDeviceSynchronize());
-    if (hv->pairs_total > s.pairs_total) s.pairs_total = hv->pairs_total;
-    const int64_t want = (int64_t)(s.pairs_total + s.pairs_total / 4 + 4096);
-    if (int rc = ensure_pairs(c, want)) return rc;
+    if (s.overflow & 1u) {
+        const int64_t want = (int64_t)(s.pairs_total + s.pairs_total / 4 + 4096);
+        if (int rc = ensure_pairs(c, want)) return rc;
+    }
     HIP_TRY(hipMemset(c->stats + 1, 0, sizeof(Stats)));
     std::memset(c->hstats, 0, sizeof(Stats));
-    return set_err(GSR_E_OVERFLOW, "pair buffer overflowed (%llu pairs); grown to %lld",
-                   (unsigned long long)s.pairs_total, (long long)c->p_cap);
+    if (s.overflow & 1u)
+        return set_err(GSR_E_OVERFLOW, "pair buffer overflowed (%llu pairs); grown to %lld; re-render",
+                       (unsigned long long)s.pairs_total, (long long)c->p_cap);
+    return set_err(GSR_E_OVERFLOW, "depth sort needed %u passes, %d were launched; re-render",
+                   (unsigned)s.depth_passes, c->passes_launched);
 }
 
 int fill_frame(gsr_context* c, const gsr_camera* cam, int W, int H, int nx, int ny, int ws, int hs, float k) {
@@ -685,6 +730,9 @@ static int ensure_cbins(gsr_context* c) {
     return GSR_OK;
 }
 
+// Ranks from returning LDS atomics: asked for (GSR_TUNE_RANK_ATOMIC) and verified on the device.
+static bool rank_atomic_on(const gsr_context* c) { return c->rank_atomic > 0 && c->rank_ok; }
+
 // Rect payload buffer b (0 or 1) of the binning's depth sort: the two u32 halves of srect.
 static uint32_t* pay_buf(gsr_context* c, int b) {
     return reinterpret_cast<uint32_t*>(c->srect) + (b ? c->n_cap : 0);
@@ -725,7 +773,7 @@ static int depth_sort_locked(gsr_context* c, bool with_rects) {
                                        c->hist, c->totals, nullptr, c->stream, c->depth_skip ? c->dstats : nullptr,
                                        p, with_rects ? reinterpret_cast<const uint32_t*>(c->rect) : nullptr, rect_mode,
                                        with_rects ? pay_buf(c, 0) : nullptr,
-                                       with_rects ? pay_buf(c, 1) : nullptr));
+                                       with_rects ? pay_buf(c, 1) : nullptr, rank_atomic_on(c)));
     return GSR_OK;
 }
 
@@ -754,7 +802,7 @@ static int sort_locked(gsr_context* c) {
         HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n, pay_buf(c, 0),
                                      pay_buf(c, 1), gb,
                                      c->hist, row_items, row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items,
-                                     c->stream, c->spans_frame ? c->spans : nullptr));
+                                     c->stream, c->spans_frame ? c->spans : nullptr, rank_atomic_on(c)));
         mark(c, GSR_STAGE_TILE_SORT);
         // column-pass workgroups: ~one 2048-item chunk each (config 3: 2048-4096 groups 12 us
         // faster than 1024; config 2: 1024 best, profiles/r02_ab_col_groups.txt)
@@ -763,7 +811,7 @@ static int sort_locked(gsr_context* c) {
         HIP_TRY(gsr::launch_bin_cols(c->pairs[0], row_items, row_pairs, c->cbins, gcol, cap,
                                      c->fr.tiles_x, c->fr.tiles_y, pair_vals(c, 1), c->ranges, c->stats,
                                      c->hstats_dev, c->bin_col_items, c->stream,
-                                     c->depth_skip ? c->dstats : nullptr, c->passes_launched));
+                                     c->depth_skip ? c->dstats : nullptr, c->passes_launched, rank_atomic_on(c)));
         c->pair_buf = 1;
         mark(c, GSR_STAGE_RANGES);
         c->have_sort = true;
@@ -884,6 +932,7 @@ void copy_settings(gsr_context* d, const gsr_context* s) {
     d->blend_band_tiles = s->blend_band_tiles;
     d->completion_events = s->completion_events;
     d->depth_compact = s->depth_compact;
+    d->rank_atomic = s->rank_atomic;
 }
 
 // Lanes 1..F-1: child contexts, streams and events, created once and kept.
@@ -1026,14 +1075,21 @@ extern "C" int gsr_sync(gsr_context* c) {
     std::lock_guard<std::mutex> lk(c->mu);
     int result = GSR_OK;
     for (size_t l = 0; l < c->lanes.size(); l++) {
+        gsr_context* lc = c->lanes[l];
         HIP_TRY(hipStreamSynchronize(c->lane_streams[l]));
-        const int rc = check_overflow(c->lanes[l], true);
-        if (rc == GSR_E_OVERFLOW) result = GSR_E_OVERFLOW;
-        else if (rc != GSR_OK) return rc;
+        const int rc = check_overflow(lc, true);
+        if (rc != GSR_OK && rc != GSR_E_OVERFLOW) return rc;
+        if (lc->overflow_seen) result = GSR_E_OVERFLOW;
+        lc->overflow_seen = false;
     }
     if (c->stream || c->pending) HIP_TRY(hipStreamSynchronize(c->stream));
     const int rc = check_overflow(c, true);
-    return rc != GSR_OK ? rc : result;
+    if (rc != GSR_OK && rc != GSR_E_OVERFLOW) return rc;
+    if (c->overflow_seen) result = GSR_E_OVERFLOW;
+    c->overflow_seen = false;
+    if (result == GSR_E_OVERFLOW && rc == GSR_OK)
+        set_err(GSR_E_OVERFLOW, "a frame since the last gsr_sync was incomplete (reported earlier); re-render");
+    return result;
 }
 
 // ------------------------------------------------------------------ readback
@@ -1287,6 +1343,14 @@ extern "C" int gsr_get_tuning(gsr_context* c, int knob, int* value) {
     case GSR_TUNE_BLEND_BAND_TILES: *value = c->blend_band_tiles; break;
     case GSR_TUNE_DEPTH_COMPACT: *value = c->depth_compact; break;
     case GSR_TUNE_TILE_SPANS: *value = c->tile_spans; break;
+    case GSR_TUNE_RANK_ATOMIC: *value = c->rank_atomic < 0 ? default_rank_atomic() : c->rank_atomic; break;
+    case GSR_TUNE_RANK_ATOMIC_ACTIVE: {
+        RankCheck rk;
+        if (int rc = rank_check_device(&rk)) return rc;
+        const int asked = c->rank_atomic < 0 ? default_rank_atomic() : c->rank_atomic;
+        *value = asked > 0 && rk.state == 1 ? 1 : 0;
+        break;
+    }
     default: return set_err(GSR_E_ARG, "gsr_get_tuning: unknown knob");
     }
     return GSR_OK;
@@ -1344,6 +1408,12 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     case GSR_TUNE_TILE_SORT_SPLIT:
         c->tile_split_even = value != 0;
         return GSR_OK;
+    case GSR_TUNE_RANK_ATOMIC:
+        if (value != 0 && value != 1) return set_err(GSR_E_ARG, "gsr_set_tuning: rank path must be 0 or 1");
+        c->rank_atomic = value;
+        return GSR_OK;
+    case GSR_TUNE_RANK_ATOMIC_ACTIVE:
+        return set_err(GSR_E_ARG, "gsr_set_tuning: GSR_TUNE_RANK_ATOMIC_ACTIVE is read-only");
     case GSR_TUNE_TILE_SORT_GROUPS:
     case GSR_TUNE_DEPTH_SORT_GROUPS:
         if (value < 0 || value > gsr::kMaxSortGroups) return set_err(GSR_E_ARG, "gsr_set_tuning: bad group cap");
@@ -1352,6 +1422,15 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     default:
         return set_err(GSR_E_ARG, "gsr_set_tuning: unknown knob");
     }
+}
+
+extern "C" int gsr_rank_order_check(int64_t* lane_ops, int64_t* mismatches) {
+    if (!lane_ops || !mismatches) return set_err(GSR_E_ARG, "gsr_rank_order_check: null argument");
+    unsigned long long ops = 0, bad = 0;
+    HIP_TRY(gsr::rank_order_check(&ops, &bad));
+    *lane_ops = (int64_t)ops;
+    *mismatches = (int64_t)bad;
+    return GSR_OK;
 }
 
 extern "C" int gsr_set_blend_variant(gsr_context* c, int variant) {

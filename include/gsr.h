@@ -42,7 +42,13 @@ enum {
     GSR_E_HIP = -2,        /* HIP runtime error (no device, OOM, launch failure) */
     GSR_E_IO = -3,         /* file missing / unreadable / truncated */
     GSR_E_FORMAT = -4,     /* unsupported PLY format */
-    GSR_E_OVERFLOW = -5,   /* pair buffer overflowed in the previous frame (grown; re-render) */
+    GSR_E_OVERFLOW = -5,   /* an earlier frame is incomplete and must be re-rendered: its pairs
+                              overflowed the pair buffer (grown now), or its depth sort needed more
+                              digit passes than the adaptive pass budget launched (budget reset to
+                              four).  Either can happen at any frame, not only during warm-up.  The
+                              code can arrive on a later call than the frame it refers to: every
+                              frame rendered since the last call that returned GSR_OK (or since the
+                              last gsr_sync) must be re-rendered. */
     GSR_E_DISPLAY = -6     /* display interop: no current GL context / GL registration failed (gsr_gl.h) */
 };
 
@@ -124,8 +130,9 @@ int gsr_reserve(gsr_context* ctx, int64_t n, int64_t pairs);
  * stream).  d_out: DEVICE buffer of 3*W*H floats (planar, row 0 = bottom).
  * Reference tiling arguments as in preprocessCUDAGaussians; pass
  * num_tile_x = num_tile_y = 1 and strides = W, H for "cover the image".
- * Returns GSR_E_OVERFLOW if an earlier frame overflowed the pair buffer
- * (the buffer has been grown; that earlier frame's image was incomplete). */
+ * Returns GSR_E_OVERFLOW if an earlier frame was incomplete (pair buffer
+ * overflow, grown; or a depth sort short of passes, budget reset): re-render
+ * every frame since the last clean return, see GSR_E_OVERFLOW. */
 int gsr_render(gsr_context* ctx, const void* d_scene, int layout, int64_t n,
                const gsr_camera* cam, int W, int H, int num_tile_x, int num_tile_y,
                int width_stride, int height_stride, float k, float* d_out, void* stream);
@@ -143,8 +150,8 @@ int gsr_render(gsr_context* ctx, const void* d_scene, int layout, int64_t n,
  * images (join events).  Outputs may repeat (e.g. a ring of buffers); a frame
  * whose output an in-flight frame of another lane also writes waits for it.
  * Readbacks, timing and diagnostics refer to lane 0's last frame.  Returns
- * GSR_E_OVERFLOW when an earlier frame of any lane overflowed its pair buffer
- * (grown; re-render), as gsr_render. */
+ * GSR_E_OVERFLOW when an earlier frame of any lane was incomplete (see
+ * GSR_E_OVERFLOW; every frame since the last clean return re-renders). */
 #define GSR_MAX_FRAMES_IN_FLIGHT 8
 int gsr_render_path(gsr_context* ctx, const void* d_scene, int layout, int64_t n, const gsr_camera* cams,
                     const float* times, int nframes, int W, int H, int num_tile_x, int num_tile_y,
@@ -191,8 +198,10 @@ int gsr_blend(gsr_context* ctx, float* d_out, void* stream);
  * so the image equals the uncut render. */
 int gsr_set_time(gsr_context* ctx, float t);
 
-/* Wait for all work of the context; returns GSR_E_OVERFLOW if the last frame
- * overflowed (and grows the buffer). */
+/* Wait for all work of the context (every lane); returns GSR_E_OVERFLOW if any
+ * frame since the last clean check was incomplete — including one that a
+ * non-blocking check inside a render call already reported — and grows the
+ * buffer / resets the pass budget. */
 int gsr_sync(gsr_context* ctx);
 
 /* ---- readback (synchronous; for tests and tooling) ---- */
@@ -275,14 +284,30 @@ enum {
     GSR_TUNE_DEPTH_COMPACT = 18,     /* global depth sort on the binning path: 1 = stable partition of the
                                         visible Gaussians first, the passes sort only those; 0 = sort all;
                                         2 (default) = partition for 4D scenes only; same order, same image */
-    GSR_TUNE_TILE_SPANS = 19         /* binning path: 1 = list a splat in only the tiles of its first four
+    GSR_TUNE_TILE_SPANS = 19,        /* binning path: 1 = list a splat in only the tiles of its first four
                                         tile rows it can composite on (conservative ellipse-vs-tile test);
                                         0 = every tile of its rect; 2 (default) = 1 up to 1.5M Gaussians;
                                         same image */
+    GSR_TUNE_RANK_ATOMIC = 20,       /* stable digit ranks in the depth sort and both binning scatters:
+                                        1 (default) = from returning LDS atomics, taken only on a gfx950
+                                        device that passed the one-shot rank-order self-check
+                                        (gsr_rank_order_check) when the context first ran; 0 = ballot
+                                        matching.  The environment variable GSR_RANK_ATOMIC=0 makes 0
+                                        the default.  Same order, same image */
+    GSR_TUNE_RANK_ATOMIC_ACTIVE = 21 /* read-only: 1 if the atomic ranks are in use (knob 20 at 1 and the
+                                        self-check passed), 0 if the kernels rank with ballots */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Current value of a knob (what gsr_set_tuning last set, else the default). */
 int gsr_get_tuning(gsr_context* ctx, int knob, int* value);
+/* Device self-check behind GSR_TUNE_RANK_ATOMIC: wave64 instructions whose lanes
+ * add to the same LDS address with a returning atomic (ds_add_rtn_u32) on the
+ * current device, over 24 digit patterns, compared lane by lane with the stable
+ * ranks ballot matching gives.  *lane_ops = lanes checked, *mismatches = lanes
+ * whose returned value was out of lane order.  The ISA does not document that
+ * order; contexts run this once per process and device and rank with ballots if
+ * any lane mismatches or the device is not gfx950.  Synchronous, < 1 ms. */
+int gsr_rank_order_check(int64_t* lane_ops, int64_t* mismatches);
 /* Depth-sort digit passes the last sorted frame ran (1..4; trailing identity
  * passes are skipped on the device), or a negative error code. */
 int gsr_depth_passes(gsr_context* ctx);
