@@ -312,13 +312,19 @@ def main():
     os.makedirs(scene_dir, exist_ok=True)
     four_d = args.config == 5
     ply = os.path.join(scene_dir, f"config{args.config}_n{n}_s{seed}{'_4d' if four_d else ''}.ply")
-    if local_rank == 0 and not os.path.exists(ply):
-        tmp = ply + f".tmp{os.getpid()}"
-        (gsr.write_synthetic_ply4d if four_d else gsr.write_synthetic_ply)(tmp, n, seed)
-        os.replace(tmp, ply)
-    if dist:
-        dist.barrier()
-    scene = gsr.Scene.from_ply(ply)           # the drop-in loader path (misc.cu:13-134)
+    gloo = dist is not None and args.dist_backend == "gloo"
+    scene = None
+    if rank == 0:
+        if not os.path.exists(ply):
+            tmp = ply + f".tmp{os.getpid()}"
+            (gsr.write_synthetic_ply4d if four_d else gsr.write_synthetic_ply)(tmp, n, seed)
+            os.replace(tmp, ply)
+        scene = gsr.Scene.from_ply(ply)       # the drop-in loader path (misc.cu:13-134)
+    # N > 1: rank 0's device scene block reaches the other ranks in one broadcast
+    # (over xGMI with RCCL), no rank but 0 reads the file
+    load_s = time.perf_counter()
+    scene = multi.broadcast_scene(dist, scene, gloo=gloo) if dist else scene
+    broadcast_ms = (time.perf_counter() - load_s) * 1e3 if dist else None
     cam = multi.orbit_camera(rank, W, H)      # rank 0: camera (0,0,4); config 4: orbit 45 deg * rank
 
     r = gsr.Renderer()
@@ -327,7 +333,6 @@ def main():
         r.set_tuning(int(knob), int(val))
     F = max(1, min(8, args.inflight))
     r.set_frames_in_flight(F)
-    gloo = dist is not None and args.dist_backend == "gloo"
     stream = torch.cuda.current_stream().cuda_stream
     shard = multi.FrameShard(dist, r, scene, cam, W, H, k=args.k, steps=args.steps, gather=args.gather,
                              inflight=F, chunk=args.chunk, gloo=gloo, frame_time=frame_time if four_d else None,
@@ -424,11 +429,21 @@ def main():
     # pipelined timed region (the reported value): the same K frames through
     # gsr_render_path with F frames in flight; blend events on lane 0's launches
     # measure the kernel while it shares the GPU with the other lanes
+    # Every rank checks its frames for GSR_E_OVERFLOW (an incomplete frame: pair buffer
+    # grown, or a depth sort short of passes) and all ranks agree (shard.finish, a
+    # collective); a region with one is timed again, once, on the grown buffers.
+    dev_kind = "cpu" if gloo else "cuda"
+    reruns = 0
     if F > 1 or shard.step_gather:
-        r.set_timing(1, TIMING_STRIDE)
-        elapsed = timed(lambda: shard.run(args.steps))
-        blend_times_pipe, timed_frames_pipe = r.stage_times()
-        r.set_timing(0)
+        for attempt in range(2):
+            shard.overflowed, shard.gathers = False, 0
+            r.set_timing(1, TIMING_STRIDE)
+            elapsed = timed(lambda: shard.run(args.steps))
+            blend_times_pipe, timed_frames_pipe = r.stage_times()
+            r.set_timing(0)
+            if not shard.finish(dev_kind):
+                break
+            reruns += 1
     else:
         elapsed, blend_times_pipe, timed_frames_pipe = seq_elapsed, blend_times, timed_frames
     overflow = r.sync() or seq_overflow
@@ -499,11 +514,15 @@ def main():
         "blend_lane_efficiency": round(counters["active_lanes"] / max(1, counters["lane_slots"]), 4),
         "image_mean": float(img.mean().item()),
         "overflow_after_timed": overflow,
+        "overflow_reruns": reruns,
     }
     result["gpu_telemetry"] = {"before_warmup": telemetry_before, "after_timed": telemetry_after}
     result["sustained_warmup"] = {"frames": warm_frames, "min_ms": args.warm_ms}
     if gather_ms is not None:
         result["gather_ms"] = round(gather_ms, 3)
+    if dist:
+        result["scene_broadcast_ms"] = round(broadcast_ms, 2)
+        result["gathers_per_rank_timed"] = shard.gathers
     sb = algorithmic_stage_bytes(n, visible, pairs, ntiles, consumed, W, H, depth_passes=depth_passes,
                                  row_items=row_items)
     result["stages_gbs"] = {k: round(sb[k] / (stages[k] * 1e-3) / 1e9, 1) for k in sb if stages.get(k)}

@@ -140,6 +140,8 @@ SIGNATURES = [
     ("gsr_set_time", c_int, [c_void_p, c_float]),
     ("gsr_scene_free", None, [c_void_p]),
     ("gsr_scene_download", c_int, [c_void_p, c_void_p, c_int64]),
+    ("gsr_scene_bytes", c_int64, [c_int, c_int64]),
+    ("gsr_scene_copy", c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p]),
     ("gsr_ply_read_host", c_int, [c_char_p, c_void_p, c_int64, POINTER(c_int64)]),
     ("gsr_ply_read_host_ex", c_int, [c_char_p, c_void_p, c_int, c_int64, POINTER(c_int64), c_int, POINTER(c_int)]),
     ("gsr_synth_write_ply", c_int, [c_char_p, c_int64, c_uint64]),

@@ -2031,18 +2031,25 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-// Packed products with the HIGH half of one operand broadcast to both lanes, in
-// one v_pk_mul_f32 through op_sel (the compiler otherwise copies that half into
+// Packed product with the HIGH half of the second operand broadcast to both lanes,
+// in one v_pk_mul_f32 through op_sel (the compiler otherwise copies that half into
 // a fresh register pair first: one v_mov per use in the compositing loop).
 // Same IEEE products as the plain expressions (multiplication commutes exactly).
-__device__ __forceinline__ f2 pk_mul_a_hi(f2 a, f2 b) {   // (a.y * b.x, a.y * b.y)
-    f2 r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
 __device__ __forceinline__ f2 pk_mul_b_hi(f2 a, f2 b) {   // (a.x * b.y, a.y * b.y)
     f2 r;
     asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// Packed fused multiply-adds with the second factor's LOW / HIGH half broadcast:
+// (fma(a.x, b.x, c.x), fma(a.y, b.x, c.y)) and (fma(a.x, b.y, c.x), fma(a.y, b.y, c.y)).
+__device__ __forceinline__ f2 pk_fma_b_lo(f2 a, f2 b, f2 c) {
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ f2 pk_fma_b_hi(f2 a, f2 b, f2 c) {
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
 
@@ -2057,6 +2064,12 @@ __device__ __forceinline__ f2 gsr_expf_x2(f2 xc) {
     // fma rounding on ~6e3) and ldexp(y, n) rounds to +0 for every x < -104 —
     // gsr_expf's clamped result.  Out-of-box lanes are discarded by the caller.
     const f2 t = xc * 1.44269504088896341f;
+#ifdef GSR_AB_FASTEXP   // throw-away measurement build (hardware v_exp_f32; not bit-exact)
+    f2 q;
+    q.x = __builtin_amdgcn_exp2f(t.x);
+    q.y = __builtin_amdgcn_exp2f(t.y);
+    return q;
+#endif
     f2 n;
     n.x = rintf(t.x);
     n.y = rintf(t.y);
@@ -2229,12 +2242,14 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                                       (has1 ? ~0ull : 0ull);
                 const float4 q0 = wP4[j * 5 + 0], q1 = wP4[j * 5 + 1], q2 = wP4[j * 5 + 2];
                 const float4 q3 = wP4[j * 5 + 3], q4 = wP4[j * 5 + 4];
-                // render.cu:329-332, same operation order, both splats at once; the
-                // conic is stored pre-scaled by -0.5, so this is -0.5f * md2 exactly
+                // render.cu:329-332, same operation order and fused multiply-adds
+                // (gsr_blend_md2), both splats at once; the conic is stored pre-scaled
+                // by -0.5, so this is -0.5f * md2 exactly
                 const f2 dx = (f2)fpx - (f2){q0.x, q0.y};
                 const f2 dy = (f2)fpy - (f2){q0.z, q0.w};
-                const f2 mdh = dx * ((f2){q1.x, q1.y} * dx + (f2){q1.z, q1.w} * dy) +
-                               dy * ((f2){q2.x, q2.y} * dx + (f2){q2.z, q2.w} * dy);
+                const f2 u = __builtin_elementwise_fma((f2){q1.x, q1.y}, dx, (f2){q1.z, q1.w} * dy);
+                const f2 v = __builtin_elementwise_fma((f2){q2.x, q2.y}, dx, (f2){q2.z, q2.w} * dy);
+                const f2 mdh = __builtin_elementwise_fma(dx, u, dy * v);
                 const f2 ee = gsr_expf_x2(mdh);
                 const f2 al = (f2){q3.x, q3.y} * ee;
                 const float al0 = fminf(al.x, 0.99f), al1 = fminf(al.y, 0.99f);
@@ -2249,18 +2264,15 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 TT.y = TT.x * (1.0f - AA.x);
                 const bool take1 = in1 & !(TT.y < 1e-3f) & !(al1 < 1e-3f);
                 AA.y = take1 ? al1 : 0.0f;
-                // the three colour products first, then the three transmittance
-                // products, then the sums in list order (independent packed ops
-                // adjacent: no wait states between dependent v_pk_* instructions)
+                // the three colour products, then rgb += (col * alpha) * T as fused
+                // multiply-adds in list order (render.cu:337, the contraction
+                // gsr_blend_md2 documents)
                 const f2 p0 = (f2){q3.z, q3.w} * AA.x;
                 const f2 p1 = pk_mul_b_hi((f2){q4.x, q4.y}, AA);     // col1 * AA.y
                 const f2 pb = (f2){q4.z, q4.w} * AA;
-                const f2 w0 = p0 * TT.x;
-                const f2 w1 = pk_mul_a_hi(TT, p1);                   // (col1 * AA.y) * TT.y
-                const f2 wb = pb * TT;
-                crg = crg + w0;
-                crg = crg + w1;
-                cb = (cb + wb.x) + wb.y;
+                crg = pk_fma_b_lo(p0, TT, crg);                      // + (col0 * AA.x) * TT.x
+                crg = pk_fma_b_hi(p1, TT, crg);                      // + (col1 * AA.y) * TT.y
+                cb = __builtin_fmaf(pb.y, TT.y, __builtin_fmaf(pb.x, TT.x, cb));
                 if (DIAG) {
                     // splat-iterations with no taken lane; pair-iterations in which no live
                     // in-box lane of either splat passes md2 <= cut (a pre-exp skip test)
@@ -2290,15 +2302,15 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 const float* S = wP + (k >> 1) * kSlot;
                 const int h = (int)(k & 1u);
                 const float dx = fpx - S[0 + h], dy = fpy - S[2 + h];
-                const float md = dx * (S[4 + h] * dx + S[6 + h] * dy) + dy * (S[8 + h] * dx + S[10 + h] * dy);
+                const float md = gsr_blend_md2(dx, dy, S[4 + h], S[6 + h], S[8 + h], S[10 + h]);
                 const float ee = gsr_expf(-0.5f * md);
                 float alpha = S[12 + h] * ee;
                 alpha = fminf(alpha, 0.99f);
                 const bool in = __builtin_amdgcn_inverse_ballot_w64(box);
                 const bool take = in & !(T < 1e-3f) & !(alpha < 1e-3f);
-                const float wr = S[14 + 2 * h] * alpha * T;
-                const float wg = S[15 + 2 * h] * alpha * T;
-                const float wb = S[18 + h] * alpha * T;
+                const float wr = __builtin_fmaf(S[14 + 2 * h] * alpha, T, crg.x);
+                const float wg = __builtin_fmaf(S[15 + 2 * h] * alpha, T, crg.y);
+                const float wb = __builtin_fmaf(S[18 + h] * alpha, T, cb);
                 const float Tn = T * (1.0f - alpha);
                 if (DIAG) {
                     dg.iter += 1;
@@ -2306,9 +2318,9 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                     dg.active += (uint64_t)__popcll(__ballot(in & !(T < 1e-3f)));
                     dg.taken += (uint64_t)__popcll(__ballot(take));
                 }
-                crg.x = take ? crg.x + wr : crg.x;
-                crg.y = take ? crg.y + wg : crg.y;
-                cb = take ? cb + wb : cb;
+                crg.x = take ? wr : crg.x;
+                crg.y = take ? wg : crg.y;
+                cb = take ? wb : cb;
                 T = take ? Tn : T;
                 alive = __ballot(!(T < 1e-3f)) != 0ull;
             }

@@ -242,6 +242,26 @@ extern "C" void* gsr_scene_upload_ex(const float* host_soa, int narrays, int64_t
     return d;
 }
 
+extern "C" int64_t gsr_scene_bytes(int narrays, int64_t n) {
+    if (n < 0 || n > INT32_MAX ||
+        (narrays != GSR_SCENE_NARRAYS && narrays != GSR_SCENE4D_NARRAYS && narrays != GSR_SCENE_SH3_NARRAYS))
+        return set_err(GSR_E_ARG, "gsr_scene_bytes: bad argument");
+    return (int64_t)GSR_SCENE_HEADER_BYTES + (int64_t)sizeof(float) * narrays * scene_stride(n);
+}
+
+extern "C" int gsr_scene_copy(void* d_dst, const void* d_scene, int narrays, int64_t n, void* stream) {
+    const int64_t bytes = gsr_scene_bytes(narrays, n);
+    if (bytes < 0) return (int)bytes;
+    if (!d_dst || !d_scene) return set_err(GSR_E_ARG, "gsr_scene_copy: null pointer");
+    gsr_scene_header h{};
+    HIP_TRY(hipMemcpy(&h, d_scene, sizeof h, hipMemcpyDeviceToHost));
+    if (h.count != (uint64_t)n || h.narrays != (uint64_t)narrays)
+        return set_err(GSR_E_ARG, "gsr_scene_copy: block holds %llu Gaussians x %llu arrays, not %lld x %d",
+                       (unsigned long long)h.count, (unsigned long long)h.narrays, (long long)n, narrays);
+    HIP_TRY(hipMemcpyAsync(d_dst, d_scene, (size_t)bytes, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+    return GSR_OK;
+}
+
 extern "C" void* gsr_scene_upload(const float* host_soa, int64_t n) {
     return gsr_scene_upload_ex(host_soa, GSR_SCENE_NARRAYS, n);
 }

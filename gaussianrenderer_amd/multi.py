@@ -2,8 +2,9 @@
 camera per rank, finished frames gathered to rank 0 over torch.distributed
 (backend "nccl" = RCCL over xGMI on the MI355X node, "gloo" in CPU tests).
 
-Frames are independent, so the render path has no collective; the only
-exchange is the hand-off of finished images to rank 0 (the offline-render
+Frames are independent, so the render path has no collective; the exchanges are
+the scene's replication at load (one broadcast of the device scene block from
+rank 0) and the hand-off of finished images to rank 0 (the offline-render
 consumer).  SURVEY.md section 8e.
 """
 from __future__ import annotations
@@ -51,6 +52,11 @@ def max_over_ranks(dist, value: float, device) -> float:
     return float(t.item())
 
 
+def any_over_ranks(dist, flag: bool, device) -> bool:
+    """True on every rank if `flag` is true on any rank (a collective: every rank calls it)."""
+    return max_over_ranks(dist, 1.0 if flag else 0.0, device) > 0.0
+
+
 def gather_frames(dist, frame, root: int = 0):
     """Gather every rank's finished frame (same shape) to `root`; returns the
     list of frames on root (index = rank) and None elsewhere."""
@@ -63,17 +69,59 @@ def gather_frames(dist, frame, root: int = 0):
     return out
 
 
+def broadcast_scene(dist, scene, gloo: bool = False):
+    """Replicate rank 0's device scene block on every rank (one
+    broadcast at load instead of N ranks parsing the .ply).  `scene` is rank 0's
+    loaded Scene (ignored elsewhere).  The block (header + SoA arrays, one
+    allocation) travels whole; each rank gets a Scene over a torch-owned copy.
+    gloo stages the block through host memory."""
+    import torch
+    from . import Scene, check, lib
+    rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return scene
+    dev = "cpu" if gloo else "cuda"
+    meta = torch.tensor([scene.n, scene.narrays] if rank == 0 else [0, 0], dtype=torch.int64, device=dev)
+    dist.broadcast(meta, 0)
+    n, narrays = (int(v) for v in meta.tolist())
+    nbytes = int(lib().gsr_scene_bytes(narrays, n))
+    if nbytes <= 0:
+        raise RuntimeError(f"broadcast_scene: bad scene size ({narrays} arrays, {n} Gaussians)")
+    block = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    if rank == 0:
+        check(lib().gsr_scene_copy(block.data_ptr(), scene.ptr, narrays, n,
+                                   torch.cuda.current_stream().cuda_stream), "gsr_scene_copy")
+    if gloo:
+        host = block.cpu()
+        dist.broadcast(host, 0)
+        block.copy_(host)
+    else:
+        dist.broadcast(block, 0)
+    torch.cuda.synchronize()
+    out = Scene(block.data_ptr(), n, owned=False, narrays=narrays)
+    out.storage = block          # the torch allocation backs the scene's pointer
+    return out
+
+
 class FrameShard:
     """One rank's frame loop for bench.py --gpus N (config 4): K frames of this rank's
     camera through Renderer.render_path (F lanes in flight), and with gather="step"
-    every finished frame handed to rank 0 — issued asynchronously (RCCL) right after
-    its chunk is enqueued and overlapped with the next chunk's render.
+    the finished frames handed to rank 0 — one gather per CHUNK of frames, issued
+    asynchronously right after the chunk is enqueued and overlapped with the next
+    chunk's render.
 
-    Buffers: with per-step gathers, two sets of `chunk` output buffers (one set
-    renders while the other's gathers drain; a buffer is reused only after its
-    pending gather completes); otherwise a ring of F.  On rank 0, `recv[b]` holds
-    the last frame gathered from every rank into buffer b.  gloo (the CPU / shared-GPU
-    rehearsal) gathers host copies synchronously."""
+    Buffers: with per-step gathers, two SETS of `chunk` frames, each set one
+    contiguous [chunk, 3*H*W] tensor (one set renders while the other's gather
+    drains; a set is rendered again only after its gather completed); otherwise a
+    ring of F frames.  On rank 0, `recv[s][r]` is rank r's copy of set s
+    (`gathered(b)` lists buffer b's frame from every rank).  gloo (the CPU /
+    shared-GPU rehearsal) gathers host copies synchronously.
+
+    Overflow: render_path reports GSR_E_OVERFLOW when a frame came out incomplete
+    (pair buffer grown, or a depth sort short of passes); the shard records it, and
+    finish() — a collective — tells every rank whether any rank saw one, so that all
+    ranks agree to re-run (a rank cannot re-send frames on its own: the gathers
+    are collectives)."""
 
     def __init__(self, dist, renderer, scene, cam, W: int, H: int, k: float = 3.0, steps: int = 1,
                  gather: str = "step", inflight: int = 1, chunk: int = 8, gloo: bool = False,
@@ -88,94 +136,121 @@ class FrameShard:
         self.chunk = max(1, chunk) if self.step_gather else max(1, steps)
         self.nsets = 2 if self.step_gather else 1
         self.per_set = self.chunk if self.step_gather else self.F
-        self.outs = [torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
-                     for _ in range(self.nsets * self.per_set)]
-        rank = dist.get_rank() if dist is not None else 0
-        world = dist.get_world_size() if dist is not None else 1
-        self.recv = ([[torch.empty_like(self.outs[0], device="cpu" if gloo else self.outs[0].device)
-                       for _ in range(world)] for _ in range(len(self.outs))]
-                     if (self.step_gather and rank == 0) else None)
-        if self.recv is not None and not gloo:
-            # rank 0's own slot IS its output buffer: the gather's local copy of the
-            # root's frame (torch copies input -> gather_list[root]) becomes a no-op,
-            # which at world 1 was the whole gather cost (a 24.9-MB device copy per
-            # frame competing with the blends).  Same lifetime as the other slots: a
-            # buffer is rendered again only after its pending gather completed.
-            for b in range(len(self.outs)):
-                self.recv[b][0] = self.outs[b]
-        self.pending = [None] * len(self.outs)
-        # RCCL: each gather waits for its own frame's completion event (gsr_render_path_ex)
-        # on a side stream, and render_path runs without the exit join, so the lanes keep
-        # frames in flight across chunks instead of draining at every chunk boundary
+        npx = 3 * W * H
+        self.sets = [torch.empty((self.per_set, npx), dtype=torch.float32, device="cuda")
+                     for _ in range(self.nsets)]
+        self.outs = [self.sets[s][j] for s in range(self.nsets) for j in range(self.per_set)]
+        self.rank = dist.get_rank() if dist is not None else 0
+        self.world = dist.get_world_size() if dist is not None else 1
+        self.recv = None
+        if self.step_gather and self.rank == 0:
+            # rank 0's own slot IS its set: torch's gather copies input -> gather_list[root],
+            # a no-op when they alias (at world 1 that copy was the whole gather cost)
+            self.recv = [[self.sets[s] if (r == 0 and not gloo) else
+                          torch.empty_like(self.sets[s], device="cpu" if gloo else "cuda")
+                          for r in range(self.world)] for s in range(self.nsets)]
+        self.pending = [None] * self.nsets
+        # RCCL: a chunk's gather waits, on a side stream, for the completion events of the
+        # chunk's frames (gsr_render_path_ex), and render_path runs without the exit
+        # join, so the lanes keep frames in flight across chunks
         self.frame_events = (None if (gloo or not self.step_gather or not overlap)
                              else [torch.cuda.Event() for _ in range(len(self.outs))])
         self.gather_stream = torch.cuda.Stream() if self.frame_events else None
-        # ... and buffer b's next frame waits on the completion of b's last gather
+        # ... and a set's next frames wait on the completion of the set's last gather
         # (recorded on the side stream) instead of the whole path waiting on the caller's
         # stream: the chunked calls skip the fork, which otherwise holds lanes 1.. behind
         # lane 0's frames of the previous call (~4 % of the rate)
-        self.gathered = [torch.cuda.Event() for _ in range(len(self.outs))] if self.frame_events else None
-        self.gathered_valid = [False] * len(self.outs)
+        self.gathered_ev = [torch.cuda.Event() for _ in range(self.nsets)] if self.frame_events else None
+        self.gathered_valid = [False] * self.nsets
+        self.overflowed = False
+        self.gathers = 0
 
     def _times(self, i0: int, m: int):
         return [self.frame_time(i0 + j) for j in range(m)] if self.frame_time else None
 
-    def wait_pending(self, b: int):
-        if self.pending[b] is not None:
-            self.pending[b].wait()          # nccl: stream-wait until the gather of buffer b is done
-            self.pending[b] = None
+    def gathered(self, b: int):
+        """Rank 0: buffer b's frame from every rank (index = rank), as device/host views."""
+        s, j = divmod(b, self.per_set)
+        return [self.recv[s][r][j] for r in range(self.world)]
+
+    def wait_pending(self, s: int):
+        if self.pending[s] is not None:
+            self.pending[s].wait()          # nccl: stream-wait until the gather of set s is done
+            self.pending[s] = None
 
     def drain(self):
-        for b in range(len(self.outs)):
-            self.wait_pending(b)
+        for s in range(self.nsets):
+            self.wait_pending(s)
 
-    def gather(self, b: int):
+    def gather(self, s: int, m: int):
+        """One gather of frames 0..m-1 of set s to rank 0."""
+        self.gathers += 1
+        src = self.sets[s][:m]
+        dst = None
+        if self.recv:
+            # rank 0's slot is the very tensor object it sends (torch then skips the copy)
+            dst = [src if t is self.sets[s] else t[:m] for t in self.recv[s]]
         if self.frame_events:
             import torch
-            # RCCL's stream waits on the current stream: the side stream, which waits
-            # on buffer b's frame only
+            # RCCL's stream waits on the current stream: the side stream, which waits on
+            # the chunk's frames only (the last frame of each lane covers its lane)
             with torch.cuda.stream(self.gather_stream):
-                self.gather_stream.wait_event(self.frame_events[b])
-                self.pending[b] = self.dist.gather(self.outs[b], self.recv[b] if self.recv else None, dst=0,
-                                                   async_op=True)
-                self.pending[b].wait()                       # side stream: after the gather
-                self.gathered[b].record(self.gather_stream)
-                self.gathered_valid[b] = True
+                for j in range(max(0, m - self.F), m):
+                    self.gather_stream.wait_event(self.frame_events[s * self.per_set + j])
+                self.pending[s] = self.dist.gather(src, dst, dst=0, async_op=True)
+                self.pending[s].wait()                       # side stream: after the gather
+                self.gathered_ev[s].record(self.gather_stream)
+                self.gathered_valid[s] = True
             return
-        src = self.outs[b].cpu() if self.gloo else self.outs[b]
-        self.pending[b] = self.dist.gather(src, self.recv[b] if self.recv else None, dst=0,
-                                           async_op=not self.gloo)
+        if self.gloo:
+            self.pending[s] = self.dist.gather(src.cpu(), dst, dst=0)
+        else:
+            self.pending[s] = self.dist.gather(src, dst, dst=0, async_op=True)
 
     def frame(self, i: int = 0, b: int = 0):
         """One frame on the caller's stream (sequential: the viewer's one-at-a-time use)."""
-        self.r.render(self.scene, self.cam, self.W, self.H, self.outs[b].data_ptr(), k=self.k,
-                      stream=self.stream, time=self.frame_time(i) if self.frame_time else None)
+        rc = self.r.render(self.scene, self.cam, self.W, self.H, self.outs[b].data_ptr(), k=self.k,
+                           stream=self.stream, time=self.frame_time(i) if self.frame_time else None)
+        self.overflowed |= rc != 0
+        return rc
 
-    def path(self, i0: int, m: int, bufs, overlap: bool = False, first: bool = True):
+    def path(self, i0: int, m: int, bufs, overlap: bool = False, first: bool = True, wait_set=None):
         """Frames i0 .. i0+m-1 through gsr_render_path into outs[bufs[j]]; returns its code
-        (GSR_E_OVERFLOW: some frame of the call overflowed and must be re-rendered).
-        overlap (run()): record each buffer's frame event, skip the exit join, wait per
-        frame on the buffer's last gather, and fork from the caller's stream only on the
+        (GSR_E_OVERFLOW: some frame since the last clean check came out incomplete).
+        overlap (run()): record each buffer's frame event, skip the exit join, wait on
+        the last gather of set `wait_set`, and fork from the caller's stream only on the
         first call of a run."""
         ov = overlap and self.frame_events is not None
-        waits = [self.gathered[b] if self.gathered_valid[b] else None for b in bufs] if ov else None
-        return self.r.render_path(self.scene, [self.cam] * m, self.W, self.H, [self.outs[b].data_ptr() for b in bufs],
-                                  k=self.k, stream=self.stream, times=self._times(i0, m),
-                                  events=[self.frame_events[b] for b in bufs] if ov else None, join=not ov,
-                                  fork=not ov or first, wait_events=waits)
+        waits = None
+        if ov and wait_set is not None and self.gathered_valid[wait_set]:
+            waits = [self.gathered_ev[wait_set]] * m
+        rc = self.r.render_path(self.scene, [self.cam] * m, self.W, self.H, [self.outs[b].data_ptr() for b in bufs],
+                                k=self.k, stream=self.stream, times=self._times(i0, m),
+                                events=[self.frame_events[b] for b in bufs] if ov else None, join=not ov,
+                                fork=not ov or first, wait_events=waits)
+        self.overflowed |= rc != 0
+        return rc
 
     def run(self, steps: int):
-        """K frames in flight, gathered per step when enabled (not drained: call drain())."""
+        """K frames in flight, gathered per chunk when enabled (not drained: call drain())."""
         if not self.step_gather:
             self.path(0, steps, [j % self.F for j in range(steps)])
             return
         for c0 in range(0, steps, self.chunk):
             m = min(self.chunk, steps - c0)
-            base = ((c0 // self.chunk) % self.nsets) * self.per_set
-            bufs = [base + j for j in range(m)]
-            if not self.frame_events:                # gloo: the caller's stream orders reuse
-                for b in bufs:
-                    self.wait_pending(b)
-            self.path(c0, m, bufs, overlap=True, first=c0 == 0)
-            for b in bufs:
-                self.gather(b)
+            s = (c0 // self.chunk) % self.nsets
+            if not self.frame_events:                # gloo / no overlap: the caller's stream orders reuse
+                self.wait_pending(s)
+            self.path(c0, m, [s * self.per_set + j for j in range(m)], overlap=True, first=c0 == 0, wait_set=s)
+            self.gather(s, m)
+
+    def finish(self, device) -> bool:
+        """Drain the gathers and the renderer, then agree over ranks (a collective)
+        whether any rank's frames since the last finish() were incomplete
+        (GSR_E_OVERFLOW); clears the flag."""
+        import torch
+        self.drain()
+        torch.cuda.synchronize()
+        bad = self.overflowed or self.r.sync() != 0
+        self.overflowed = False
+        return any_over_ranks(self.dist, bad, device)

@@ -324,6 +324,14 @@ void* gsr_scene_upload(const float* host_soa, int64_t n);
 /* narrays = GSR_SCENE_NARRAYS (3D), GSR_SCENE4D_NARRAYS (4D) or GSR_SCENE_SH3_NARRAYS. */
 void* gsr_scene_upload_ex(const float* host_soa, int narrays, int64_t n);
 void gsr_scene_free(void* d_scene);
+/* Bytes of a scene block (header + narrays arrays of n floats, padded), or a
+ * negative error code. */
+int64_t gsr_scene_bytes(int narrays, int64_t n);
+/* Copy a whole device scene block (n Gaussians, narrays arrays: checked against its
+ * header) into d_dst, a device buffer of gsr_scene_bytes(narrays, n) bytes, on
+ * `stream` — e.g. into a buffer that a collective then broadcasts to the other
+ * ranks (the multi-GPU scene replication; the copy is a valid scene block). */
+int gsr_scene_copy(void* d_dst, const void* d_scene, int narrays, int64_t n, void* stream);
 /* Copy a device scene block back into host SoA form (38 * n floats). */
 /* Copies every array of the block (38, 49 for 4D, 59 for SH-3) into host_soa. */
 int gsr_scene_download(const void* d_scene, float* host_soa, int64_t n);

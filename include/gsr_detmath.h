@@ -115,6 +115,19 @@ GSR_HD float gsr_expf(float x) {
     return (x != x) ? x + x : res;                        /* NaN */
 }
 
+/* md2 of renderGaussians (render.cu:331),
+ *   dx * (ic0 * dx + ic1 * dy) + dy * (ic2 * dx + ic3 * dy),
+ * with the fused multiply-adds the reference's compiler forms: nvcc contracts
+ * a * b + c into an FMA by default (--fmad=true) and, like LLVM's combiner, fuses
+ * the product that is the sum's FIRST operand.  The blend's accumulation
+ * rgb += color * alpha * T (render.cu:337) contracts the same way, to
+ * fmaf(color * alpha, T, rgb).  Which product nvcc fuses cannot be observed here
+ * (the CUDA path cannot be built); the oracle and the kernels make this one choice
+ * together, so they agree bit for bit. */
+GSR_HD float gsr_blend_md2(float dx, float dy, float ic0, float ic1, float ic2, float ic3) {
+    return __builtin_fmaf(dx, __builtin_fmaf(ic0, dx, ic1 * dy), dy * __builtin_fmaf(ic2, dx, ic3 * dy));
+}
+
 /* Polynomial cores on |r| <= pi/4 (Cephes sinf / cosf). */
 GSR_HD float gsr_sin_core(float r) {
     const float z = r * r;

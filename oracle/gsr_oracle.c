@@ -459,11 +459,12 @@ static inline void blend_step(const orc_splat* g, int gx, int gy, float* T, floa
     const float dx = ((float)gx - (float)g->px_x);
     const float dy = ((float)gy - (float)g->px_y);
     const float* ic = g->inv_covar;
-    const float md2 = dx * (ic[0] * dx + ic[1] * dy) + dy * (ic[2] * dx + ic[3] * dy);
+    /* render.cu:331 and 337 with nvcc's default FMA contraction (gsr_blend_md2) */
+    const float md2 = gsr_blend_md2(dx, dy, ic[0], ic[1], ic[2], ic[3]);
     float opacity = g->opacity * gsr_expf(-0.5f * md2);
     opacity = fminf(opacity, 0.99f);
     if (opacity < 1e-3f) return;
-    for (int c = 0; c < 3; ++c) rgb[c] += g->color[c] * opacity * *T;
+    for (int c = 0; c < 3; ++c) rgb[c] = __builtin_fmaf(g->color[c] * opacity, *T, rgb[c]);
     *T *= (1.0f - opacity);
 }
 

@@ -39,19 +39,19 @@ def _worker(rank, world, port, ply, W, H, steps, q):
     from gaussianrenderer_amd import multi
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    scene = gsr.Scene.from_ply(ply)
+    # rank 0 loads the scene; rank 1 gets the device block by broadcast
+    scene = multi.broadcast_scene(dist, gsr.Scene.from_ply(ply) if rank == 0 else None, gloo=True)
     r = gsr.Renderer()
     r.set_frames_in_flight(2)
     cam = multi.orbit_camera(rank, W, H)
     shard = multi.FrameShard(dist, r, scene, cam, W, H, steps=steps, gather="step", inflight=2, chunk=2,
                              gloo=True, stream=torch.cuda.current_stream().cuda_stream)
     shard.run(steps)
-    shard.drain()
-    torch.cuda.synchronize()
-    assert r.sync() == 0
+    assert not shard.finish("cpu")                 # no rank saw an incomplete frame
+    assert shard.gathers == 2                      # one gather per chunk (2 + 1 frames)
     elapsed = multi.max_over_ranks(dist, 0.25 + rank, "cpu")
     if rank == 0:
-        q.put((elapsed, [[f.numpy().copy() for f in shard.recv[b]] for b in range(len(shard.recv))]))
+        q.put((elapsed, [[f.numpy().copy() for f in shard.gathered(b)] for b in range(len(shard.outs))]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -77,7 +77,7 @@ def test_two_rank_hip_frames_gathered(gpu, orc, tmp_path):
     from gaussianrenderer_amd import multi
     wants = [orc.render(soa, multi.orbit_camera(r, W, H), W, H, 3.0).reshape(-1) for r in range(world)]
     assert not np.array_equal(wants[0], wants[1])
-    for b in range(steps):
+    for b in range(steps):                         # buffers 0, 1 (set 0) and 2 (set 1)
         for r in range(world):
             assert np.array_equal(recv[b][r], wants[r]), f"buffer {b}, rank {r}"
 
@@ -105,21 +105,21 @@ def _nccl_worker(port, ply, W, H, steps, chunk, q):
     for b in range(len(shard.outs)):
         shard.outs[b].fill_(-1.0)
     torch.cuda.synchronize()
+    shard.overflowed = False
     shard.run(steps)
-    shard.drain()
-    torch.cuda.synchronize()
-    ok = r.sync() == 0
+    ok = not shard.finish("cuda") and shard.gathers == (steps + chunk - 1) // chunk
     elapsed = multi.max_over_ranks(dist, 0.5, "cuda")
-    q.put((ok, elapsed, [shard.recv[b][0].cpu().numpy().copy() for b in range(len(shard.recv))]))
+    q.put((ok, elapsed, [shard.gathered(b)[0].cpu().numpy().copy() for b in range(len(shard.outs))]))
     dist.destroy_process_group()
 
 
 def test_rccl_world1_frame_events(gpu, orc, tmp_path):
-    """The RCCL branch of FrameShard (what bench.py --gpus N runs on a node): each frame's
-    gather waits on that frame's completion event (gsr_render_path_ex) and the lanes do
-    not join between chunks.  World 1 (RCCL cannot put two ranks on one GPU): 7 frames in
-    chunks of 3 over two buffer sets, so a set is re-used behind its pending gathers;
-    every gathered buffer must equal the oracle's render bit for bit."""
+    """The RCCL branch of FrameShard (what bench.py --gpus N runs on a node): one gather
+    per chunk, waiting on the completion events of the chunk's frames
+    (gsr_render_path_ex), and the lanes do not join between chunks.  World 1 (RCCL
+    cannot put two ranks on one GPU): 7 frames in chunks of 3 over two buffer sets, so
+    a set is re-used behind its pending gather; every gathered buffer must equal the
+    oracle's render bit for bit."""
     W, H, steps, chunk = 320, 240, 7, 3
     ply = str(tmp_path / "s.ply")
     gpu.write_synthetic_ply(ply, 10_000, 4)

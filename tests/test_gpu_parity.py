@@ -117,7 +117,11 @@ def max_alpha_on_tiles(want, pairs, W):
             ok = (px >= a[:, 0]) & (px <= a[:, 2]) & (py >= a[:, 1]) & (py <= a[:, 3])
             dx = px.astype(np.float32) - cx
             dy = py.astype(np.float32) - cy
-            md = dx * (ic[:, 0] * dx + ic[:, 1] * dy) + dy * (ic[:, 2] * dx + ic[:, 3] * dy)
+            # gsr_blend_md2's fused multiply-adds: float32 products are exact in float64
+            f64 = np.float64
+            u = (ic[:, 0].astype(f64) * dx + (ic[:, 1] * dy)).astype(np.float32)
+            v = (ic[:, 2].astype(f64) * dx + (ic[:, 3] * dy)).astype(np.float32)
+            md = (dx.astype(f64) * u + (dy * v)).astype(np.float32)
             al = np.minimum(op * np.exp(np.float32(-0.5) * md), np.float32(0.99))
             best = np.where(ok, np.maximum(best, al), best)
     return best

@@ -214,3 +214,35 @@ def test_path_bad_arguments(gpu, torch, c1):
     with pytest.raises(gpu.GsrError):
         r.set_frames_in_flight(9)
     assert r.render_path(gpu.Scene.from_soa(c1[1]), [], 64, 64, []) == 0
+
+
+def test_frameshard_reports_depth_budget_overflow(gpu, orc, torch, c1):
+    """the adaptive depth-pass budget makes GSR_E_OVERFLOW a steady-state
+    event.  Lower every lane's budget to 3 passes on a scene whose keys fit 3 digits,
+    then render a scene whose depth keys need all 4 through FrameShard.run: finish()
+    must report the incomplete frames (even when a non-blocking check inside a render
+    call consumed the flag first), and the re-run must match the oracle."""
+    from gaussianrenderer_amd import multi
+    path, soa = c1
+    W, H, F = 320, 240, 2
+    near = gpu.Scene.from_soa(soa)                       # view depth 3..5: keys < 2^24
+    far_soa = soa.copy()
+    far_soa[2] = np.linspace(-90.0, 1.0, soa.shape[1], dtype=np.float32)   # keys up to ~9.4e7 > 2^24
+    far = gpu.Scene.from_soa(far_soa)
+    r = gpu.Renderer()
+    r.set_frames_in_flight(F)
+    cam = cam_for(gpu, W, H)
+    shard = multi.FrameShard(None, r, near, cam, W, H, steps=4, gather="none", inflight=F)
+    for _ in range(8):                                   # >= 4 clean checked frames per lane
+        shard.run(4)
+        assert not shard.finish("cuda")
+    assert r.depth_passes() == 3
+    shard.scene = far
+    shard.run(4)
+    assert shard.finish("cuda"), "frames sorted with too few passes were not reported"
+    shard.run(4)                                         # budget back at four passes
+    assert not shard.finish("cuda")
+    assert r.depth_passes() == 4
+    want = orc.render(far_soa, cam, W, H, 3.0)
+    for o in shard.outs:
+        assert_image_parity(o.view(3, H, W).cpu().numpy(), want)

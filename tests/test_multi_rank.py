@@ -38,6 +38,9 @@ def _worker(rank, world, port, ply, W, H, q):
     cam = multi.orbit_camera(info.rank, W, H)
     frame = torch.from_numpy(_oracle.render(soa, cam, W, H, 3.0, threads=1)).reshape(-1)
     elapsed = multi.max_over_ranks(dist, 0.5 + rank, "cpu")
+    # the overflow agreement behind FrameShard.finish: any rank's flag reaches every rank
+    assert multi.any_over_ranks(dist, rank == 1, "cpu") is True
+    assert multi.any_over_ranks(dist, False, "cpu") is False
     frames = multi.gather_frames(dist, frame)
     if info.is_root:
         q.put((elapsed, [f.numpy().copy() for f in frames]))

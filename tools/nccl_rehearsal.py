@@ -3,8 +3,8 @@
 
 bench.py --gpus N uses the nccl (= RCCL) backend only when N > 1, and RCCL cannot
 put two ranks on one GPU, so on a one-GPU box the RCCL code path of
-multi.FrameShard (async per-frame gathers on RCCL's stream, pending-gather waits
-before buffer reuse, the max-reduce of the elapsed time on a device tensor) would
+multi.FrameShard (one async gather per chunk on RCCL's stream, gather-done waits
+before a buffer set is reused, the max-reduce of the elapsed time on a device tensor) would
 first run in the driver's 8-GPU scaling run.  This script runs that path with
 however many ranks the launcher starts (one per GPU; world 1 is enough to exercise
 every call) and checks the gathered frames bit for bit against a plain render of
@@ -36,12 +36,6 @@ def main():
     ap.add_argument("--gather", choices=("step", "none"), default="step",
                     help="none: the same frames with no gathers (one render_path call, the N=1 bench loop)")
     ap.add_argument("--warm-ms", type=float, default=0.0, help="untimed sustained frames before the timed ones")
-    ap.add_argument("--events-only", action="store_true",
-                    help="diagnostic (--gather none): the one render_path call, plus a completion event per frame")
-    ap.add_argument("--ring", type=int, default=0,
-                    help="diagnostic (--gather none): output ring of this many buffers instead of one per lane")
-    ap.add_argument("--no-fork", action="store_true",
-                    help="diagnostic (with --no-gather-calls): render_path calls without the fork (GSR_PATH_NO_FORK)")
     ap.add_argument("--no-gather-calls", action="store_true",
                     help="diagnostic: the chunked per-step loop without issuing the gathers (no buffer check)")
     ap.add_argument("--no-overlap", action="store_true",
@@ -68,22 +62,7 @@ def main():
     shard = multi.FrameShard(dist, r, scene, cam, W, H, steps=a.steps, gather=a.gather, inflight=a.inflight, chunk=a.chunk,
                              stream=stream, overlap=not a.no_overlap)
     if a.no_gather_calls:
-        shard.gather = lambda b: None
-        if a.no_fork:
-            def path_nofork(i0, m, bufs, overlap=False):
-                return r.render_path(scene, [cam] * m, W, H, [shard.outs[b].data_ptr() for b in bufs],
-                                     stream=stream, join=False, fork=False)
-            shard.path = path_nofork
-    if a.ring and a.gather == "none":
-        shard.outs = [torch.empty(3 * W * H, device="cuda") for _ in range(a.ring)]
-        shard.F = a.ring        # run(): frame j -> outs[j % ring]
-        shard.pending = [None] * a.ring
-    if a.events_only and a.gather == "none":
-        evs = [torch.cuda.Event() for _ in range(len(shard.outs))]
-        nb = len(shard.outs)
-        shard.run = lambda steps: r.render_path(scene, [cam] * steps, W, H,
-                                                [shard.outs[j % nb].data_ptr() for j in range(steps)],
-                                                stream=stream, events=[evs[j % nb] for j in range(steps)])
+        shard.gather = lambda s, m: None
     # reference image of this rank's camera (grows the pair buffers too)
     ref = torch.empty(3 * W * H, device="cuda")
     for _ in range(3):
@@ -107,7 +86,7 @@ def main():
     shard.drain()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    assert r.sync() == 0, "overflow in the timed frames"
+    assert not shard.finish("cuda"), "overflow in the timed frames"
     mx = multi.max_over_ranks(dist, elapsed, "cuda")
     # every rank's reference to rank 0, compared with what the per-step gathers delivered
     refs = multi.gather_frames(dist, ref)
@@ -116,9 +95,6 @@ def main():
         print(f"nccl rehearsal: world {info.world}, {a.steps} frames per rank, no gathers; "
               f"{info.world * a.steps / mx:.1f} frames/s aggregate ({a.inflight} lanes, warm {a.warm_ms:.0f} ms, "
               f"{'chunked step loop without gather calls, ' if a.no_gather_calls else ''}"
-              f"{'no fork, ' if a.no_fork else ''}"
-              f"{'one call with per-frame events, ' if a.events_only else ''}"
-              f"{f'ring of {a.ring} outputs, ' if a.ring else ''}"
               f"host enqueue {t_enq * 1e3:.2f} ms)",
               flush=True)
     elif info.rank == 0:
@@ -126,7 +102,7 @@ def main():
                        for c0 in range(0, a.steps, shard.chunk) for j in range(min(shard.chunk, a.steps - c0))})
         for b in used:
             for src in range(info.world):
-                same = torch.equal(shard.recv[b][src], refs[src])
+                same = torch.equal(shard.gathered(b)[src], refs[src])
                 ok = ok and same
                 if not same:
                     print(f"MISMATCH buffer {b} rank {src}", flush=True)

@@ -11,6 +11,7 @@ B="bench.py --steps ${STEPS:-50} --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-}"
 [ "${SKIP_KT:-0}" = 1 ] || timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 $B > "$OUT/kt.log" 2>&1
 rc=$?; echo "kernel-trace rc=$rc"; fatal $rc kt
 # counter groups separated by ';' (each group = one pass)
+[ "${SKIP_PMC:-0}" = 1 ] && exit 0
 IFS=';' read -ra GROUPS_ <<< "${PMC_GROUPS:-FETCH_SIZE;WRITE_SIZE}"
 for G in "${GROUPS_[@]}"; do
   TAG=$(echo $G | awk '{print $1}')
