@@ -10,6 +10,8 @@
 #   pmc        the PMC passes of the same command              (tools/profile.sh, PMC only)
 #   rehearsal  RCCL rehearsal of the multi-GPU loop at world 1 (tools/nccl_rehearsal.py),
 #              with per-chunk gathers and without gathers (REH_ARGS)
+#   ktab       kernel trace of the one-frame-at-a-time bench per knob setting (TUNES,
+#              e.g. TUNES="19=0 19=1"; CONFIGS) -> gpurun_out/kt_ab_<tag>/summary.txt
 #   abtune     interleaved knob A/B in one process (tools/ab_path.py, AB_ARGS)
 #   ablibs     interleaved A/B of two library builds            (tools/ab_libs.sh)
 #
@@ -54,6 +56,13 @@ for step in ${STEPS:-suite smoke bench}; do
         --master-port $((29500 + RANDOM % 400)) tools/nccl_rehearsal.py --gather $g ${REH_ARGS:---steps 400 --gaussians 1000000 --W 1920 --H 1080 --warm-ms 1000} \
         > gpurun_out/rehearsal_${TAG}_$g.log 2>&1
       rc=$?; fatal $rc rehearsal; grep "nccl rehearsal" gpurun_out/rehearsal_${TAG}_$g.log; [ $rc = 0 ] || { tail -5 gpurun_out/rehearsal_${TAG}_$g.log; exit $rc; }
+    done ;;
+  ktab)
+    for t in ${TUNES:-19=0 19=1}; do
+      tg=$(echo "$t" | tr '=,' '__'); O=gpurun_out/kt_ab_$tg; mkdir -p $O
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 bench.py --config ${CONFIGS:-2} --steps 60 --warmup 5 --no-cpu-baseline --inflight 1 --warm-ms 200 --tune "$t" > $O/kt.log 2>&1
+      rc=$?; echo "tune $t kt rc=$rc"; fatal $rc ktab; [ $rc = 0 ] || exit $rc
+      python3 tools/summarize_prof.py $O > $O/summary.txt 2>&1; echo "== $t"; head -16 $O/summary.txt
     done ;;
   abtune)
     timeout -k 10 600 python tools/ab_path.py ${AB_ARGS:-} > gpurun_out/abtune_$TAG.log 2>&1
