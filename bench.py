@@ -44,7 +44,10 @@ TIMESTEPS_4D = 120
 TIMING_STRIDE = 8
 STAGE_FRAMES = 10     # untimed frames averaged for stages_ms
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
-BLEND_KERNEL = "k_blend_w<false, false>"   # the blend (one 64-thread workgroup per 8x8 block)
+# the blend (one 64-thread workgroup per 8x8 block): template <DIAG, STAMPS, FX>, FX = the
+# fast-exp blend (GSR_TUNE_BLEND_EXP 1) or the exact one (0, the default)
+BLEND_KERNELS = {1: "k_blend_w<false, false, true>", 0: "k_blend_w<false, false, false>"}
+BLEND_KERNEL = BLEND_KERNELS[0]
 
 
 def parse():
@@ -380,8 +383,11 @@ def main():
     pairs = r.pair_count()
     row_items = r.row_item_count()
     depth_passes = r.depth_passes()
-    counters = r.blend_counters()
+    counters = r.blend_counters_ex()
     consumed = counters["records_loaded"]
+    global BLEND_KERNEL
+    blend_exp = r.get_tuning(22)
+    BLEND_KERNEL = BLEND_KERNELS[min(blend_exp, 1)]
     r.set_diagnostics(False)
     tiles_x, tiles_y = r.tile_grid()
     # visible Gaussians M (depth key != 0xFFFFFFFF), untimed
@@ -510,6 +516,8 @@ def main():
         "row_items": row_items,
         "depth_passes": depth_passes,
         "pairs_consumed": consumed,
+        "blend_exp": {1: "fast (v_exp_f32 alpha, exact alpha tests, guarded T tests, exact re-blend of "
+                         "suspect pixels)", 0: "exact (gsr_expf)"}[min(blend_exp, 1)],
         "blend_counters": counters,
         "blend_lane_efficiency": round(counters["active_lanes"] / max(1, counters["lane_slots"]), 4),
         "image_mean": float(img.mean().item()),

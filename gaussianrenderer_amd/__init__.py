@@ -446,6 +446,22 @@ class Renderer:
                 "zero_taken_iters", "lane_slots", "no_candidate_pair_iters")
         return dict(zip(keys, (int(x) for x in v)))
 
+    def blend_counters_ex(self) -> dict:
+        """blend_counters() plus the fast-exp blend's re-blended blocks and their
+        suspect pixels (gsr_blend_counters_ex)."""
+        v = np.zeros(16, dtype=np.int64)
+        check(lib().gsr_blend_counters_ex(self.ctx, v.ctypes.data, 16), "gsr_blend_counters_ex")
+        d = self.blend_counters()
+        d["reblended_blocks"], d["suspect_pixels"] = int(v[8]), int(v[9])
+        return d
+
+    def take_map(self, W: int, H: int) -> np.ndarray:
+        """Per-pixel take map of the last diagnostics frame (gsr_blend_take_map):
+        splats composited | (index-mix sum << 32), shape (H, W)."""
+        out = np.zeros((H, W), dtype=np.uint64)
+        check(lib().gsr_blend_take_map(self.ctx, out.ctypes.data, out.size), "gsr_blend_take_map")
+        return out
+
     def set_blend_variant(self, variant: int):
         check(lib().gsr_set_blend_variant(self.ctx, int(variant)), "gsr_set_blend_variant")
 
@@ -490,6 +506,7 @@ TUNE_TILE_BINNING = 7
 TUNE_TILE_SPANS = 19
 TUNE_RANK_ATOMIC = 20
 TUNE_RANK_ATOMIC_ACTIVE = 21
+TUNE_BLEND_EXP = 22
 
 
 def rank_order_check() -> tuple[int, int]:
@@ -505,4 +522,20 @@ def math_probe(xy: np.ndarray) -> np.ndarray:
     xy = np.ascontiguousarray(xy, dtype=np.float32).reshape(-1, 2)
     out = np.zeros((xy.shape[0], 8), dtype=np.float32)
     check(lib().gsr_math_probe(xy.ctypes.data, xy.shape[0], out.ctypes.data), "gsr_math_probe")
+    return out
+
+
+def exp_probe(x_lo: float, x_hi: float, x_big: float) -> tuple[int, float, float]:
+    """gsr_exp_probe: (monotonicity violations of gsr_expf, max relative fast-exp error,
+    the same over x >= x_big) over every float in [x_lo, x_hi), on the GPU."""
+    v, ea, eb = c_int64(0), ctypes.c_float(0), ctypes.c_float(0)
+    check(lib().gsr_exp_probe(x_lo, x_hi, x_big, byref(v), byref(ea), byref(eb)), "gsr_exp_probe")
+    return int(v.value), float(ea.value), float(eb.value)
+
+
+def alpha_cut_probe(op: np.ndarray) -> np.ndarray:
+    """gsr_alpha_take_min_x evaluated on the GPU for each opacity."""
+    op = np.ascontiguousarray(op, dtype=np.float32).ravel()
+    out = np.zeros_like(op)
+    check(lib().gsr_alpha_cut_probe(op.ctypes.data, op.size, out.ctypes.data), "gsr_alpha_cut_probe")
     return out

@@ -131,6 +131,8 @@ SIGNATURES = [
     ("gsr_blend_counters", c_int, [c_void_p, c_void_p]),
     ("gsr_set_blend_variant", c_int, [c_void_p, c_int]),
     ("gsr_blend_stamps", c_int, [c_void_p, c_void_p, c_int64]),
+    ("gsr_blend_counters_ex", c_int, [c_void_p, c_void_p, c_int]),
+    ("gsr_blend_take_map", c_int, [c_void_p, c_void_p, c_int64]),
     ("gsr_set_tuning", c_int, [c_void_p, c_int, c_int]),
     ("gsr_get_tuning", c_int, [c_void_p, c_int, c_void_p]),
     ("gsr_set_timing_stride", c_int, [c_void_p, c_int, c_int]),
@@ -156,6 +158,8 @@ SIGNATURES = [
     ("gsr_version", c_char_p, []),
     ("gsr_device_available", c_int, []),
     ("gsr_math_probe", c_int, [c_void_p, c_int, c_void_p]),
+    ("gsr_exp_probe", c_int, [c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
+    ("gsr_alpha_cut_probe", c_int, [c_void_p, c_int, c_void_p]),
     ("gsr_rank_order_check", c_int, [POINTER(c_int64), POINTER(c_int64)]),
 ]
 

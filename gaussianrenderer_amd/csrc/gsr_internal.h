@@ -75,11 +75,15 @@ hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* ke
                           bool key16, const uint32_t* n_dev, int shift, int bits, int groups, int items,
                           uint32_t* hist, uint32_t* totals, uint2* ranges, hipStream_t s);
 // One wave per 8x8 block (k_blend_w).  consumed: optional device counters
-// (diagnostics), or with stamps the per-wave timeline (tools/blend_timeline.py).
-// band_tiles > 0: bands of that many tiles dealt round-robin to the XCDs; 0: one
-// contiguous run of blocks per XCD.
+// (diagnostics: 16 counters, then a u64 take map entry per pixel), or with stamps the
+// per-wave timeline (tools/blend_timeline.py).  band_tiles > 0: bands of that many
+// tiles dealt round-robin to the XCDs; 0: one contiguous run of blocks per XCD.
+// blend_exp (GSR_TUNE_BLEND_EXP): 0 gsr_expf; 1 hardware exp with exact alpha tests
+// and guarded transmittance tests, blocks it cannot vouch for blended again exactly;
+// 2 the same with the guard band at 100 % (test hook for the exact re-blend).
 hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
-                        float* out, unsigned long long* consumed, bool stamps, int band_tiles, hipStream_t s);
+                        float* out, unsigned long long* consumed, bool stamps, int band_tiles, int blend_exp,
+                        hipStream_t s);
 // Stable partition of the preprocess items: visible first, culled last (both in
 // index order), visible count into *n_live; culled tail to out only, with dead
 // rects in srect (gsr_kernels.hip "live partition").  counts: groups words.
@@ -115,6 +119,9 @@ hipError_t rank_order_check(unsigned long long* lane_ops, unsigned long long* mi
 
 // Device math probe for the detmath GPU parity test.
 hipError_t launch_math_probe(const float* in, int n, float* out, hipStream_t s);
+hipError_t launch_exp_probe(uint32_t key_lo, uint32_t key_hi, float x_big, unsigned long long* viol, uint32_t* errs,
+                            hipStream_t s);
+hipError_t launch_xs_probe(const float* op, int n, float* out, hipStream_t s);
 
 // Drop-in frame into a device image on the drop-in context (gsr_runtime.cpp);
 // callers hold dropin_mutex().  `what` names the failing step for the message.

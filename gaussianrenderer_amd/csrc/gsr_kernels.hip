@@ -220,9 +220,12 @@ __device__ __forceinline__ void put_rect(uint64_t* rect, int64_t i, uint64_t r, 
 // tests that depends on the record alone is computed once here, in
 // k_preprocess, and stored as the record's fourth 16-B word (the blend's record
 // gather fetches the whole 64-B line anyway: profiles/r01_fetch_calibration.txt):
-//   { cut, ih, iv, S }
-// cut  md2 cutoff (md2_cutoff) if the conic is robustly positive definite, else +inf
-//      (+inf or NaN: the block test never culls)
+//   { xs, ih, iv, S }
+// xs   gsr_alpha_take_min_x(op): the alpha test passes on a pixel iff its exp
+//      argument -md2/2 >= xs (exact, gsr_detmath.h).  The block test's md2 cutoff is
+//      -2 xs (+1e-6, block_cut) when the conic is robustly positive definite; the
+//      blend's fast-exp mode takes its alpha decisions from xs
+//      (-inf: every pixel passes, the block test never culls)
 // ih   -h / e, iv = -h / a (edge minimisers of the quadratic form), h = (b + c) / 2
 // S    |a| + |b| + |c| + |e| if the record passes the per-record part of the
 //      fast-path proof (robustly PD, finite S and colour, coefficients 0 or
@@ -260,7 +263,6 @@ __device__ __forceinline__ uint4 cull_word(float a, float b, float c, float e, f
     const float inf = __builtin_huge_valf();
     const float h = 0.5f * (b + c);
     const bool pd = a > 0.0f && e > 0.0f && (a * e - h * h) > 1e-4f * (a * e);
-    const float cut = md2_cutoff(op);
     const float S = fabsf(a) + fabsf(b) + fabsf(c) + fabsf(e);
     const bool fast = pd && isfinite(S) && isfinite(r) && isfinite(g) && isfinite(bl) && coef_ok(a) &&
                       coef_ok(b) && coef_ok(c) && coef_ok(e);
@@ -269,9 +271,16 @@ __device__ __forceinline__ uint4 cull_word(float a, float b, float c, float e, f
     // block test's rounding margin
     const float ih = pd ? -h * __builtin_amdgcn_rcpf(e) : 0.0f;
     const float iv = pd ? -h * __builtin_amdgcn_rcpf(a) : 0.0f;
-    return make_uint4(__float_as_uint(pd && cut < 3.0e38f ? cut : inf), __float_as_uint(ih), __float_as_uint(iv),
-                      __float_as_uint(fast ? S : inf));
+    // a conic that is not robustly PD never culls: xs = -inf makes block_cut +inf.  Its
+    // alpha decisions come from the exact one-splat path (no fast proof), never xs.
+    const float xs = pd ? gsr_alpha_take_min_x(op) : -inf;
+    return make_uint4(__float_as_uint(xs), __float_as_uint(ih), __float_as_uint(iv), __float_as_uint(fast ? S : inf));
 }
+
+// md2 cutoff of the block test from the record's xs: a lane with float md2 > -2 xs has
+// -md2/2 < xs (exact scaling; the 1e-6 pad covers a subnormal -md2/2 rounding up to xs)
+// and fails the alpha test.  xs = -inf: +inf (never culls); +inf: -inf (always culls).
+__device__ __forceinline__ float block_cut(float xs) { return __builtin_fmaf(-2.0f, xs, 1e-6f); }
 
 // Can any pixel of an integer rectangle reach md2 <= cut?  dx0..dy1 bound the
 // (float)pixel - (float)centre offsets of the rectangle's pixels (monotone, so
@@ -332,9 +341,9 @@ __device__ __forceinline__ bool block_may_reach(float a, float b, float c, float
 // (tools/sim/spans_check.py) keeps 78.7 % of config 2's pairs (the exact hull: 76.5 %)
 // and every pair it drops peaks at alpha <= 0.9976e-3 on its tile.
 __device__ __forceinline__ uint16_t tile_row_spans(float cx, float cy, float a, float b, float c, float e,
-                                                   uint4 cw, int xmin_px, int xmax_px, int ymin_px, int ymax_px,
-                                                   int tx0, int tx1, int ty0, int ty1) {
-    const float cut = __uint_as_float(cw.x), S = __uint_as_float(cw.w);
+                                                   float cut, uint4 cw, int xmin_px, int xmax_px, int ymin_px,
+                                                   int ymax_px, int tx0, int tx1, int ty0, int ty1) {
+    const float S = __uint_as_float(cw.w);
     // not robustly positive definite (cut = inf) or without the fast proof (S = inf): keep all
     if (!(cut < 3.0e38f) || !(S < 3.0e38f)) return 0u;
     const float h = 0.5f * (b + c);
@@ -622,8 +631,10 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     const uint4 cw = cull_word(ic0, ic1, ic2, ic3, opacity, col[0], col[1], col[2]);
     R[3] = cw;
     if (spans)
-        spans[i] = tile_row_spans((float)px_x, (float)px_y, ic0, ic1, ic2, ic3, cw, xmin_px, xmax_px, ymin_px,
-                                  ymax_px, tx0, tx1, ty0, ty1);
+        spans[i] = tile_row_spans((float)px_x, (float)px_y, ic0, ic1, ic2, ic3,
+                                  cw.x == __float_as_uint(-__builtin_huge_valf()) ? __builtin_huge_valf()
+                                                                                 : md2_cutoff(opacity),
+                                  cw, xmin_px, xmax_px, ymin_px, ymax_px, tx0, tx1, ty0, ty1);
     put_rect(rect, i,
              (uint64_t)((uint32_t)tx0 | ((uint32_t)tx1 << 16)) | ((uint64_t)((uint32_t)ty0 | ((uint32_t)ty1 << 16)) << 32),
              packed);
@@ -2064,12 +2075,6 @@ __device__ __forceinline__ f2 gsr_expf_x2(f2 xc) {
     // fma rounding on ~6e3) and ldexp(y, n) rounds to +0 for every x < -104 —
     // gsr_expf's clamped result.  Out-of-box lanes are discarded by the caller.
     const f2 t = xc * 1.44269504088896341f;
-#ifdef GSR_AB_FASTEXP   // throw-away measurement build (hardware v_exp_f32; not bit-exact)
-    f2 q;
-    q.x = __builtin_amdgcn_exp2f(t.x);
-    q.y = __builtin_amdgcn_exp2f(t.y);
-    return q;
-#endif
     f2 n;
     n.x = rintf(t.x);
     n.y = rintf(t.y);
@@ -2088,6 +2093,66 @@ __device__ __forceinline__ f2 gsr_expf_x2(f2 xc) {
     return res;
 }
 
+// The blend's fast exp (GSR_TUNE_BLEND_EXP 1): e^x as the hardware 2^t (v_exp_f32) of
+// t = x log2(e), two lanes at once.  Its relative difference from gsr_expf, with the
+// alpha product, is bounded on the argument range a composited lane can have
+// (kFxEpsMax, kFxEpsBig below; measured exhaustively by gsr_exp_probe); the
+// alpha decisions never use it (xs), and the transmittance test is guarded.
+__device__ __forceinline__ f2 fast_expf_x2(f2 x) {
+    const f2 t = x * 1.44269504088896341f;
+    f2 q;
+    q.x = __builtin_amdgcn_exp2f(t.x);
+    q.y = __builtin_amdgcn_exp2f(t.y);
+    return q;
+}
+
+// Fast-exp blend: bounds on |alpha_fast / alpha_exact - 1| for a composited lane
+// (opacity in [0, 1] and alpha_exact >= 1e-3, so the exp argument x lies in
+// [ln(1e-3), 5]; alpha > 0.5 needs x > ln 0.5, alpha > 0.9 needs x > ln 0.9).  Each is
+// the exhaustive maximum of |fast_expf / gsr_expf - 1| over every float x of its
+// range (gsr_exp_probe; tests/test_gpu_fastexp.py checks these constants stay above
+// it) plus 2^-23 for the two roundings of op * e:
+//   kFxEps3  all composited lanes (x >= -6.95)
+//   kFxEps2  alpha > 0.5            (x >= -0.70)
+//   kFxEps1  alpha > 0.9            (x >= -0.11)
+// The transmittance of a pixel then differs from the exact chain's by a relative
+//   rho <= 207.1 kFxEps1 + 6.9078 max(3.909 kFxEps2, 1.4427 kFxEps3) + 4 2^-24 n
+// (n = composited splats, bounded by the wave's splat-iterations) up to and including
+// the step where it first drops below 1e-3 ("Fast exp"):
+// kFxBand0 and kFxBandStep are those terms with 2 % headroom.
+constexpr float kFxEps3 = 6.6e-7f;
+constexpr float kFxEps2 = 4.8e-7f;
+constexpr float kFxEps1 = 4.8e-7f;
+constexpr float kFxBand0 = 1.02f * (207.1f * kFxEps1 + 6.9078f * (3.909f * kFxEps2 > 1.4427f * kFxEps3
+                                                                  ? 3.909f * kFxEps2 : 1.4427f * kFxEps3));
+constexpr float kFxBandStep = 1.02f * 4.0f * 0x1p-24f;
+
+// n + (lane's bit of ma) + (lane's bit of mb): the wave masks are the carry-ins of two
+// v_addc_co_u32 (one VALU each; counting booleans compiles to selects and an add).
+__device__ __forceinline__ uint32_t count_lanes2(uint32_t n, uint64_t ma, uint64_t mb) {
+    uint64_t c0, c1;
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(n), "=s"(c0) : "v"(n), "s"(ma));
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(n), "=s"(c1) : "v"(n), "s"(mb));
+    (void)c0;
+    (void)c1;
+    return n;
+}
+
+// The band for one pixel from what it composited so far: n splats, the largest alpha
+// m.  Besides the worst case above (band0 = kFxBand0), the alpha terms obey
+//   sum alpha_i / (1 - alpha_i) <= (sum alpha_i) / (1 - m)
+//                              <= (ln 1000 + ln(1 / (1 - m))) / (1 - m)
+// (alpha <= -ln(1 - alpha), and the exact T stayed >= 1e-3 before the step being
+// tested, whose own alpha is <= m), so rho <= kFxEps3 of that, which is far smaller
+// unless some alpha came near 0.99.  2 % headroom over the hardware log / rcp.
+// band0 < 0 (measurement builds only) turns the guard off.
+__device__ __forceinline__ float fx_band(float band0, uint32_t n, float m) {
+    const float om = 1.0f - m;                                 // >= 0.01 (alpha <= 0.99)
+    const float lnm = -0.693147181f * __builtin_amdgcn_logf(om);   // ln(1 / (1 - m))
+    const float byM = 1.02f * kFxEps3 * (6.9078f + lnm) * __builtin_amdgcn_rcpf(om);
+    return __builtin_fmaf((float)n, kFxBandStep, band0 < 0.0f || band0 > 0.5f ? band0 : fminf(band0, byM));
+}
+
 // One wave64 per 8x8 pixel block (four per 16x16 tile, one tile per
 // workgroup), no workgroup barrier.  Each wave streams its tile's splat list in
 // 64-record batches (records of batch k+1 and indices of batch k+2 prefetched
@@ -2102,7 +2167,7 @@ __device__ __forceinline__ f2 gsr_expf_x2(f2 xc) {
 //
 // Pair slot dwords (h = 0 / 1 for the first / second splat of the pair):
 //   [0+h] cx  [2+h] cy  [4+h] a  [6+h] b  [8+h] c  [10+h] e  [12+h] opacity
-//   [14+2h] red  [15+2h] green  [18+h] blue
+//   [14+2h] red  [15+2h] green  [18+h] blue  (fast exp only: [20+h] xs)
 struct BlendDiag {
     uint64_t loaded = 0, iter = 0, active = 0, taken = 0, slow = 0, zero_taken = 0, no_cand_pairs = 0;
 };
@@ -2116,28 +2181,52 @@ __device__ __forceinline__ uint64_t box_mask(uint32_t d) {
     return rows & (((uint64_t)rep << 32) | rep);
 }
 
+// Diagnostics take map: per pixel, the number of splats composited and a sum of
+// a mix of their Gaussian indices (the oracle's orc_render_takes computes the same).
+__device__ __forceinline__ uint32_t take_mix(uint32_t g) { return (g + 1u) * 2654435761u; }
+
 // One 8x8 pixel block (bx, by) blended by one wave over the tile list
 // idx[beg, end), using the wave's private LDS slice wP (32 pair slots).
-template <bool DIAG>
-__device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, const uint4* __restrict__ rec,
-                                            uint32_t beg, uint32_t end, int bx, int by, int lane, int W, int H,
-                                            int cover_w, int cover_h, float* __restrict__ out, float* wP,
-                                            BlendDiag& dg) {
-    constexpr int kSlot = 20;                               // dwords per pair slot
+//
+// FX (fast exp, GSR_TUNE_BLEND_EXP 1): alpha from fast_expf_x2; the alpha test is
+// the exact one through the record's xs (-md2/2 >= xs, gsr_alpha_take_min_x), so
+// only the transmittance can differ from the exact chain, by less than the band
+// kFxBand0 + kFxBandStep n.  The wave flags a pixel ("suspect") when a value of T on
+// either side of its first drop below 1e-3 lies within the band of 1e-3, or when
+// it ends unsaturated within the band; then the exact T could have taken the other
+// branch.  The block writes every other pixel and returns the suspect mask; the
+// caller blends the suspect pixels again exactly (FX false, `only` = the mask).  A
+// batch holding a record without the fast proof aborts the fast pass (all ones, no
+// pixel written).  Every pixel therefore composites exactly the splats the exact
+// blend composites, in the same order.
+template <bool DIAG, bool FX>
+__device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx, const uint4* __restrict__ rec,
+                                                uint32_t beg, uint32_t end, int bx, int by, int lane, int W,
+                                                int H, int cover_w, int cover_h, float* __restrict__ out,
+                                                float* wP, BlendDiag& dg, uint64_t* __restrict__ tmap,
+                                                float band0, uint64_t only) {
+    constexpr int kSlot = FX ? 24 : 20;                     // dwords per pair slot
     const int px = bx + (lane & 7), py = by + (lane >> 3);
     const bool inside = px < cover_w && py < cover_h;
     const float fpx = (float)px, fpy = (float)py;
     // transmittance; a pixel is saturated ("done", render.cu:328) iff T < 1e-3.
-    // Pixels outside the covered area start saturated (T = 0) and write 0.
-    float T = inside ? 1.0f : 0.0f;
+    // Pixels outside the covered area start saturated (T = 0) and write 0; so do the
+    // pixels outside `only` (the exact re-blend of a fast block's suspect pixels).
+    const bool mine = ((only >> lane) & 1ull) != 0ull;
+    float T = inside && mine ? 1.0f : 0.0f;
     f2 crg = (f2)0.0f;
     float cb = 0.0f;
     const float4* wP4 = reinterpret_cast<const float4*>(wP);
+    uint64_t suspect = 0;      // FX: pixels whose T decisions the band cannot vouch for
+    uint32_t ntk = 0;          // FX: splats this pixel composited so far
+    f2 amax = (f2)0.0f;        // FX: largest alpha it composited (two halves)
+    uint32_t tcount = 0, thash = 0;   // DIAG take map
 
     uint4 ra = make_uint4(0, 0, 0, 0), rb = ra, rc = ra, rd = ra;
-    uint32_t nidx = 0;
+    uint32_t nidx = 0, cidx = 0;
     if (beg + lane < end) {
-        const uint4* R = rec + 4 * (uint64_t)idx[beg + lane];
+        cidx = idx[beg + lane];
+        const uint4* R = rec + 4 * (uint64_t)cidx;
         ra = R[0];
         rb = R[1];
         rc = R[2];
@@ -2178,12 +2267,15 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 const float M = fmaxf(fmaxf(fabsf(dx0), fabsf(dx1)), fmaxf(fabsf(dy0), fabsf(dy1)));
                 hit = ((mlo & (uint32_t)live_b) | (mhi & (uint32_t)(live_b >> 32))) != 0u &&
                       block_may_reach(a, b, c, e, __uint_as_float(rd.y), __uint_as_float(rd.z), S, dx0, dx1, dy0,
-                                      dy1, M, __uint_as_float(rd.x));
+                                      dy1, M, block_cut(__uint_as_float(rd.x)));
                 fast = S * M * M <= 4e7f;   // per-block part of the fast-path proof
+                // the fast exp's error bound assumes opacity in [0, 1] (NaN fails)
+                if (FX) fast = fast && __uint_as_float(rb.x) <= 1.0f;
             }
         }
         const uint64_t m = __ballot(hit);
         const bool all_fast = __ballot(hit & !fast) == 0ull;
+        if (FX && !all_fast) return ~0ull;   // exact re-blend of the whole block
         if (hit) {
             const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -2201,6 +2293,7 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
             S[14 + 2 * h] = __uint_as_float(rb.y);
             S[15 + 2 * h] = __uint_as_float(rb.z);
             S[18 + h] = __uint_as_float(rb.w);
+            if (FX) S[20 + h] = __uint_as_float(rd.x);
         }
         const uint32_t nsurv = (uint32_t)__popcll(m);
         if ((nsurv & 1u) && lane < 10) {
@@ -2210,9 +2303,11 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
             wP[(nsurv >> 1) * kSlot + (lane < 7 ? 2 * lane + 1 : lane + 9 + (lane == 9))] = 0.0f;
         }
         if (DIAG) dg.loaded += cnt;
-        const float cut_l = DIAG ? __uint_as_float(rd.x) : 0.0f;   // diagnostics: md2 cutoff of record `lane`
+        const float xs_l = DIAG ? __uint_as_float(rd.x) : 0.0f;   // diagnostics: xs of record `lane`
+        const uint32_t gi_l = cidx;                                // diagnostics: its Gaussian index
         // ---- prefetch: records of batch k+1, indices of batch k+2 ----
         if (base + 64 + lane < end) {
+            cidx = nidx;
             const uint4* R = rec + 4 * (uint64_t)nidx;
             ra = R[0];
             rb = R[1];
@@ -2240,8 +2335,9 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 const uint64_t box0 = box_mask((uint32_t)__builtin_amdgcn_readlane((int)dsc, s0));
                 const uint64_t box1 = box_mask((uint32_t)__builtin_amdgcn_readlane((int)dsc, s1)) &
                                       (has1 ? ~0ull : 0ull);
-                const float4 q0 = wP4[j * 5 + 0], q1 = wP4[j * 5 + 1], q2 = wP4[j * 5 + 2];
-                const float4 q3 = wP4[j * 5 + 3], q4 = wP4[j * 5 + 4];
+                const float4 q0 = wP4[j * (kSlot / 4) + 0], q1 = wP4[j * (kSlot / 4) + 1];
+                const float4 q2 = wP4[j * (kSlot / 4) + 2], q3 = wP4[j * (kSlot / 4) + 3];
+                const float4 q4 = wP4[j * (kSlot / 4) + 4];
                 // render.cu:329-332, same operation order and fused multiply-adds
                 // (gsr_blend_md2), both splats at once; the conic is stored pre-scaled
                 // by -0.5, so this is -0.5f * md2 exactly
@@ -2250,19 +2346,44 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 const f2 u = __builtin_elementwise_fma((f2){q1.x, q1.y}, dx, (f2){q1.z, q1.w} * dy);
                 const f2 v = __builtin_elementwise_fma((f2){q2.x, q2.y}, dx, (f2){q2.z, q2.w} * dy);
                 const f2 mdh = __builtin_elementwise_fma(dx, u, dy * v);
-                const f2 ee = gsr_expf_x2(mdh);
+                const f2 ee = FX ? fast_expf_x2(mdh) : gsr_expf_x2(mdh);
                 const f2 al = (f2){q3.x, q3.y} * ee;
                 const float al0 = fminf(al.x, 0.99f), al1 = fminf(al.y, 0.99f);
+                // alpha tests (render.cu:335): on alpha itself, or (FX) on the exp
+                // argument against xs — the same decisions
+                bool pass0, pass1;
+                if (FX) {
+                    const float2 xs = *reinterpret_cast<const float2*>(&wP4[j * (kSlot / 4) + 5]);
+                    pass0 = !(mdh.x < xs.x);
+                    pass1 = !(mdh.y < xs.y);
+                } else {
+                    pass0 = !(al0 < 1e-3f);
+                    pass1 = !(al1 < 1e-3f);
+                }
                 // render.cu:333-340: splat 2j, then splat 2j+1 against what 2j left
                 const bool in0 = __builtin_amdgcn_inverse_ballot_w64(box0 & live);
                 const bool in1 = __builtin_amdgcn_inverse_ballot_w64(box1);
                 // (a0, a1) and (T, T1) live in register pairs, written in place, so
-                // the packed blue product needs no moves; TT.x carries T across
-                const bool take0 = in0 & !(al0 < 1e-3f);
+                // the packed blue product needs no moves; TT.x carries T across.
+                // FX forms the take decisions as wave masks (the composited-splat
+                // count below uses them as carry-ins)
+                uint64_t t0m = 0, t1m = 0;
+                bool take0, take1;
                 f2 AA;
+                if (FX) {
+                    t0m = box0 & live & __builtin_amdgcn_ballot_w64(pass0);
+                    take0 = __builtin_amdgcn_inverse_ballot_w64(t0m);
+                } else {
+                    take0 = in0 & pass0;
+                }
                 AA.x = take0 ? al0 : 0.0f;
                 TT.y = TT.x * (1.0f - AA.x);
-                const bool take1 = in1 & !(TT.y < 1e-3f) & !(al1 < 1e-3f);
+                if (FX) {
+                    t1m = box1 & __builtin_amdgcn_ballot_w64(!(TT.y < 1e-3f)) & __builtin_amdgcn_ballot_w64(pass1);
+                    take1 = __builtin_amdgcn_inverse_ballot_w64(t1m);
+                } else {
+                    take1 = in1 & !(TT.y < 1e-3f) & pass1;
+                }
                 AA.y = take1 ? al1 : 0.0f;
                 // the three colour products, then rgb += (col * alpha) * T as fused
                 // multiply-adds in list order (render.cu:337, the contraction
@@ -2275,20 +2396,45 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                 cb = __builtin_fmaf(pb.y, TT.y, __builtin_fmaf(pb.x, TT.x, cb));
                 if (DIAG) {
                     // splat-iterations with no taken lane; pair-iterations in which no live
-                    // in-box lane of either splat passes md2 <= cut (a pre-exp skip test)
-                    const float cut0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cut_l), s0));
-                    const float cut1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cut_l), s1));
-                    const bool cand0 = in0 && !(mdh.x < -0.5f * cut0);
-                    const bool cand1 = has1 && in1 && !(TT.x < 1e-3f) && !(mdh.y < -0.5f * cut1);
+                    // in-box lane of either splat passes the alpha test's exp argument
+                    const float xs0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xs_l), s0));
+                    const float xs1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xs_l), s1));
+                    const bool cand0 = in0 && !(mdh.x < xs0);
+                    const bool cand1 = has1 && in1 && !(TT.x < 1e-3f) && !(mdh.y < xs1);
                     dg.zero_taken += (__ballot(take0) == 0ull ? 1 : 0) + (has1 && __ballot(take1) == 0ull ? 1 : 0);
                     dg.no_cand_pairs += (__ballot(cand0 || cand1) == 0ull) ? 1 : 0;
                     dg.iter += has1 ? 2 : 1;
                     dg.active += (uint64_t)__popcll(__ballot(in0)) +
                                 (uint64_t)__popcll(__ballot(in1 & !(TT.y < 1e-3f)));
                     dg.taken += (uint64_t)__popcll(__ballot(take0)) + (uint64_t)__popcll(__ballot(take1));
+                    const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)gi_l, s0);
+                    const uint32_t g1 = (uint32_t)__builtin_amdgcn_readlane((int)gi_l, s1);
+                    tcount += (take0 ? 1u : 0u) + (take1 ? 1u : 0u);
+                    thash += (take0 ? take_mix(g0) : 0u) + (take1 ? take_mix(g1) : 0u);
                 }
                 TT.x = TT.y * (1.0f - AA.y);
-                live = __ballot(!(TT.x < 1e-3f));
+                const uint64_t live_new = __ballot(!(TT.x < 1e-3f));
+                if (FX) {
+                    // n += take0 + take1 as two v_addc (the take masks as carry-in);
+                    // alpha >= +0 here, so its float maximum is the u32 maximum
+                    ntk = count_lanes2(ntk, t0m, t1m);
+                    amax.x = __uint_as_float(max(__float_as_uint(amax.x), __float_as_uint(AA.x)));
+                    amax.y = __uint_as_float(max(__float_as_uint(amax.y), __float_as_uint(AA.y)));
+                    if (live_new != live) {
+                        // lanes whose T first dropped below 1e-3 in this iteration: the
+                        // value before the drop and the value after (TT.x) must lie
+                        // outside the band.  Before the drop: TT.y when the drop came at
+                        // TT.x; T0 = the iteration's starting T when it came at TT.y,
+                        // where T0 < hi is tested as TT.y < hi (1 - a0), padded by 2^-22
+                        // for the two roundings of TT.y = T0 (1 - a0).
+                        const float B = fx_band(band0, ntk, fmaxf(amax.x, amax.y));
+                        const float hi = 1e-3f * (1.0f + B), lo = 1e-3f * (1.0f - B);
+                        const float lim = TT.y < 1e-3f ? hi * (1.0f - AA.x) * (1.0f + 0x1p-22f) : hi;
+                        const bool nr = TT.y < lim || !(TT.x < lo);
+                        suspect |= __ballot(nr) & (live & ~live_new);
+                    }
+                }
+                live = live_new;
                 alive = live != 0ull;   // whole block saturated -> stop
             }
             T = TT.x;
@@ -2317,6 +2463,8 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
                     dg.slow += 1;
                     dg.active += (uint64_t)__popcll(__ballot(in & !(T < 1e-3f)));
                     dg.taken += (uint64_t)__popcll(__ballot(take));
+                    tcount += take ? 1u : 0u;
+                    thash += take ? take_mix((uint32_t)__builtin_amdgcn_readlane((int)gi_l, s)) : 0u;
                 }
                 crg.x = take ? wr : crg.x;
                 crg.y = take ? wg : crg.y;
@@ -2326,13 +2474,22 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
             }
         }
     }
-    if (px < W && py < H) {
+    if (FX) {
+        // pixels that never dropped below 1e-3 but end within the band above it
+        const float B = fx_band(band0, ntk, fmaxf(amax.x, amax.y));
+        suspect |= __ballot(!(T < 1e-3f) && T < 1e-3f * (1.0f + B));
+    }
+    // FX: every pixel but the suspect ones; exact: the pixels of `only`
+    const bool write = FX ? ((suspect >> lane) & 1ull) == 0ull : mine;
+    if (write && px < W && py < H) {
         const size_t o = (size_t)py * (size_t)W + (size_t)px;
         const size_t hw = (size_t)W * (size_t)H;
         out[o] = inside ? crg.x : 0.0f;
         out[hw + o] = inside ? crg.y : 0.0f;
         out[2 * hw + o] = inside ? cb : 0.0f;
+        if (DIAG && tmap) tmap[o] = (uint64_t)tcount | ((uint64_t)thash << 32);
     }
+    return suspect;
 }
 
 // One-wave workgroups: workgroup g blends one 8x8 block, so a finished block
@@ -2343,17 +2500,21 @@ __device__ __forceinline__ void blend_block(const uint32_t* __restrict__ idx, co
 // of neighbouring tiles while heavy and light image regions spread over all XCDs;
 // padding workgroups past the last block exit.  bands <= 1: one contiguous run of
 // blocks per XCD (xcd_remap).
+// FX: fast-exp blend; a block it cannot vouch for is blended again exactly by the
+// same wave (counters[8] blocks, counters[9] suspect pixels, with diagnostics).
 // STAMPS (timeline diagnostics, no counters): counters[2 * g] = start of the
 // s_memrealtime clock (100 MHz), counters[2 * g + 1] = duration (40 bits) |
 // placement << 40 (XCC id and HW_ID's SE / SH / CU / SIMD / slot).
-template <bool DIAG, bool STAMPS = false>
+// DIAG: counters[0..9], then the take map (one u64 per pixel) from counters + 16.
+template <bool DIAG, bool STAMPS, bool FX>
 __global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx,
                                                  const uint2* __restrict__ ranges,
                                                  const uint4* __restrict__ rec, int tiles_x, int tiles_y,
                                                  int W, int H, int cover_w, int cover_h,
                                                  float* __restrict__ out,
-                                                 unsigned long long* __restrict__ counters, int bands) {
-    __shared__ float4 sP[32 * 20 / 4];
+                                                 unsigned long long* __restrict__ counters, int bands,
+                                                 float band0) {
+    __shared__ float4 sP[32 * (FX ? 24 : 20) / 4];
     const int ntiles = tiles_x * tiles_y;
     const int vb = (int)blockIdx.x;
     int L;
@@ -2380,10 +2541,23 @@ __global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx
         counters[2 * vb] = t_start;
     }
     const uint2 rr = ranges[tile];                          // {~start, end}, zero = empty
+    const uint32_t beg = rr.y ? ~rr.x : 0u;
+    const int bx = tx * GSR_TILE_PX + (sub & 1) * 8, by = ty * GSR_TILE_PX + (sub >> 1) * 8;
+    uint64_t* tmap = DIAG ? reinterpret_cast<uint64_t*>(counters + 16) : nullptr;
     BlendDiag dg;
-    blend_block<DIAG>(idx, rec, rr.y ? ~rr.x : 0u, rr.y, tx * GSR_TILE_PX + (sub & 1) * 8,
-                      ty * GSR_TILE_PX + (sub >> 1) * 8, lane, W, H, cover_w, cover_h, out,
-                      reinterpret_cast<float*>(sP), dg);
+    const uint64_t redo = blend_block<DIAG, FX>(idx, rec, beg, rr.y, bx, by, lane, W, H, cover_w, cover_h, out,
+                                                reinterpret_cast<float*>(sP), dg, tmap, band0, ~0ull);
+    if (FX && redo) {
+        if (DIAG && lane == 0) {
+            atomicAdd(counters + 8, 1ull);
+            atomicAdd(counters + 9, (unsigned long long)__popcll(redo));
+        }
+        // only the suspect pixels (all of them after an aborted fast pass): the others
+        // start saturated, so the cull drops every record that misses the suspects
+        // and the wave stops once they saturate
+        blend_block<DIAG, false>(idx, rec, beg, rr.y, bx, by, lane, W, H, cover_w, cover_h, out,
+                                 reinterpret_cast<float*>(sP), dg, tmap, 0.0f, redo);
+    }
     if (STAMPS && lane == 0)
         counters[2 * vb + 1] = ((__builtin_amdgcn_s_memrealtime() - t_start) & ((1ull << 40) - 1)) | (place << 40);
     if (DIAG && lane == 0) {
@@ -2510,6 +2684,42 @@ __global__ void k_math_probe(const float* __restrict__ in, int n, float* __restr
     o[5] = x / y;
     o[6] = roundf(x);
     o[7] = __int_as_float(gsr_f2i_sat(x * 1000.0f));
+}
+
+// Exhaustive checks behind the fast-exp blend (gsr_exp_probe).  Over every float key k
+// in [key_lo, key_hi): viol[0] counts gsr_expf(x_k) > gsr_expf(x_k+1) (monotonicity of
+// the exact exp, which makes the alpha test a threshold on its argument), and
+// over the same keys the largest |fast_expf / gsr_expf - 1| is kept as float bits,
+// split at x >= x_big: errs[0] every key (x in the range), errs[1] x >= x_big.
+__global__ __launch_bounds__(256) void k_exp_probe(uint32_t key_lo, uint32_t key_hi, float x_big,
+                                                   unsigned long long* __restrict__ viol,
+                                                   uint32_t* __restrict__ errs) {
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t bad = 0;
+    float emax = 0.0f, ebig = 0.0f;
+    for (uint64_t k = (uint64_t)key_lo + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < key_hi; k += nthr) {
+        const float x = gsr_key_float((uint32_t)k);
+        const float e = gsr_expf(x);
+        const float en = gsr_expf(gsr_key_float((uint32_t)k + 1u));
+        bad += e > en ? 1u : 0u;
+        f2 xx;
+        xx.x = x;
+        xx.y = x;
+        const float f = fast_expf_x2(xx).x;
+        const float r = (float)fabs((double)f / (double)e - 1.0);   // rounded up below
+        const float ru = __uint_as_float(__float_as_uint(r) + 1u);
+        emax = fmaxf(emax, ru);
+        if (x >= x_big) ebig = fmaxf(ebig, ru);
+    }
+    if (bad) atomicAdd(viol, (unsigned long long)bad);
+    atomicMax(errs, __float_as_uint(emax));
+    atomicMax(errs + 1, __float_as_uint(ebig));
+}
+
+// gsr_alpha_take_min_x on the device, one opacity per thread (tests).
+__global__ void k_xs_probe(const float* __restrict__ op, int n, float* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = gsr_alpha_take_min_x(op[i]);
 }
 
 inline int grid_for(int64_t n, int block) { return (int)((n + block - 1) / block); }
@@ -2699,7 +2909,12 @@ hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* ke
 }
 
 hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
-                        float* out, unsigned long long* consumed, bool stamps, int band_tiles, hipStream_t s) {
+                        float* out, unsigned long long* consumed, bool stamps, int band_tiles, int blend_exp,
+                        hipStream_t s) {
+    // blend_exp 2 (test hook): the fast blend with a band of 100 %, so every block in
+    // which a pixel saturates (or ends below 2e-3) is blended again exactly
+    const bool fast_exp = blend_exp != 0;
+    const float band0 = blend_exp == 2 ? 1.0f : kFxBand0;
     const int nt = fr.tiles_x * fr.tiles_y;
     if (nt <= 0) return hipSuccess;
     // bands of band_tiles tiles (4 blocks each) dealt round-robin to the 8 XCDs; the
@@ -2710,15 +2925,20 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
         bands = (nt + 8 * band_tiles - 1) / (8 * band_tiles);          // bands per XCD
         ng = 8 * bands * ((4 * nt + 8 * bands - 1) / (8 * bands));
     }
-    if (stamps && consumed)
-        hipLaunchKernelGGL((k_blend_w<false, true>), dim3(ng), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,
-                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, bands);
-    else if (consumed)
-        hipLaunchKernelGGL((k_blend_w<true, false>), dim3(ng), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,
-                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, bands);
-    else
-        hipLaunchKernelGGL((k_blend_w<false, false>), dim3(ng), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,
-                           fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, bands);
+#define GSR_BLEND(D, ST, FX)                                                                                \
+    hipLaunchKernelGGL((k_blend_w<D, ST, FX>), dim3(ng), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x, fr.tiles_y, \
+                       fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, bands, band0)
+    if (stamps && consumed) {
+        if (fast_exp) GSR_BLEND(false, true, true);
+        else GSR_BLEND(false, true, false);
+    } else if (consumed) {
+        if (fast_exp) GSR_BLEND(true, false, true);
+        else GSR_BLEND(true, false, false);
+    } else {
+        if (fast_exp) GSR_BLEND(false, false, true);
+        else GSR_BLEND(false, false, false);
+    }
+#undef GSR_BLEND
     return hipGetLastError();
 }
 
@@ -2767,6 +2987,17 @@ hipError_t rank_order_check(unsigned long long* lane_ops, unsigned long long* mi
 hipError_t launch_math_probe(const float* in, int n, float* out, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_math_probe, dim3(grid_for(n, 256)), dim3(256), 0, s, in, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_exp_probe(uint32_t key_lo, uint32_t key_hi, float x_big, unsigned long long* viol, uint32_t* errs,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_exp_probe, dim3(8192), dim3(256), 0, s, key_lo, key_hi, x_big, viol, errs);
+    return hipGetLastError();
+}
+
+hipError_t launch_xs_probe(const float* op, int n, float* out, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(k_xs_probe, dim3(grid_for(n, 256)), dim3(256), 0, s, op, n, out);
     return hipGetLastError();
 }
 

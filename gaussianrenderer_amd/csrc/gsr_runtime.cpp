@@ -24,6 +24,7 @@
 
 #include "gsr.h"
 #include "gsr_internal.h"
+#include "gsr_detmath.h"
 
 using gsr::Frame;
 using gsr::Stats;
@@ -378,6 +379,8 @@ struct gsr_context {
     uint32_t* cbins = nullptr;       // binning: column counts per chunk (256 x chunks)
     int64_t cbins_cap = 0;
     bool last_binned = false;        // the last sorted frame took the binning path
+    int blend_exp = 0;               // blend: 0 = gsr_expf (bit-exact); 1 = fast exp with exact alpha
+                                     // tests and guarded T tests (re-blends what it cannot vouch for)
     int blend_band_tiles = 4;        // blend: tiles per spatial band, bands dealt round-robin to the
                                      // XCDs (0: one contiguous band per XCD)
     int completion_events = 1;       // 0: no completion event / overflow query (stream capture)
@@ -649,7 +652,12 @@ int ceil_log2(int64_t v) {
 
 }  // namespace
 
-extern "C" gsr_context* gsr_create(void) { return new gsr_context(); }
+extern "C" gsr_context* gsr_create(void) {
+    gsr_context* c = new gsr_context();
+    const char* e = std::getenv("GSR_BLEND_EXP");
+    if (e && e[0] == '1') c->blend_exp = 1;
+    return c;
+}
 
 extern "C" void gsr_destroy(gsr_context* c) {
     if (!c) return;
@@ -873,9 +881,10 @@ static int blend_locked(gsr_context* c, float* d_out) {
     if (!d_out) return set_err(GSR_E_ARG, "null output");
     mark(c, GSR_STAGE_BLEND);
     if (c->diagnostics) {
-        // counters (8) or, for the timestamp schedule, 2 stamps per wave
+        // counters (16) and the per-pixel take map, or, for the timestamp schedule,
+        // 2 stamps per wave
         const int64_t need = c->blend_variant == 3 ? 12 * (int64_t)c->ntiles + 64   // >= 2 x the padded grid
-                                                   : 8;
+                                                   : 16 + (int64_t)c->fr.W * c->fr.H;
         if (c->consumed_cap < need) {
             if (int rc = realloc_dev(&c->consumed, (size_t)need)) return rc;
             c->consumed_cap = need;
@@ -884,7 +893,7 @@ static int blend_locked(gsr_context* c, float* d_out) {
     }
     HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
                               c->diagnostics ? c->consumed : nullptr, c->blend_variant == 3,
-                              c->blend_band_tiles, c->stream));
+                              c->blend_band_tiles, c->blend_exp, c->stream));
     mark(c, GSR_NUM_STAGES);
     if (c->timing && c->timing_now) c->ev_frames.push_back(c->cur);
     c->cur = FrameEvents{};
@@ -950,6 +959,7 @@ void copy_settings(gsr_context* d, const gsr_context* s) {
     d->tile_spans = s->tile_spans;
     d->bin_col_groups = s->bin_col_groups;
     d->blend_band_tiles = s->blend_band_tiles;
+    d->blend_exp = s->blend_exp;
     d->completion_events = s->completion_events;
     d->depth_compact = s->depth_compact;
     d->rank_atomic = s->rank_atomic;
@@ -1363,6 +1373,7 @@ extern "C" int gsr_get_tuning(gsr_context* c, int knob, int* value) {
     case GSR_TUNE_BLEND_BAND_TILES: *value = c->blend_band_tiles; break;
     case GSR_TUNE_DEPTH_COMPACT: *value = c->depth_compact; break;
     case GSR_TUNE_TILE_SPANS: *value = c->tile_spans; break;
+    case GSR_TUNE_BLEND_EXP: *value = c->blend_exp; break;
     case GSR_TUNE_RANK_ATOMIC: *value = c->rank_atomic < 0 ? default_rank_atomic() : c->rank_atomic; break;
     case GSR_TUNE_RANK_ATOMIC_ACTIVE: {
         RankCheck rk;
@@ -1428,6 +1439,10 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     case GSR_TUNE_TILE_SORT_SPLIT:
         c->tile_split_even = value != 0;
         return GSR_OK;
+    case GSR_TUNE_BLEND_EXP:
+        if (value < 0 || value > 2) return set_err(GSR_E_ARG, "gsr_set_tuning: blend exp must be 0, 1 or 2");
+        c->blend_exp = value;
+        return GSR_OK;
     case GSR_TUNE_RANK_ATOMIC:
         if (value != 0 && value != 1) return set_err(GSR_E_ARG, "gsr_set_tuning: rank path must be 0 or 1");
         c->rank_atomic = value;
@@ -1477,6 +1492,27 @@ extern "C" int64_t gsr_blend_records_loaded(gsr_context* c) {
     return v[0];
 }
 
+extern "C" int gsr_blend_counters_ex(gsr_context* c, int64_t* out, int n) {
+    if (!c || !c->consumed || !out || n < 0 || n > 16 || c->blend_variant == 3)
+        return set_err(GSR_E_ARG, "gsr_blend_counters_ex: diagnostics were off or bad count");
+    std::lock_guard<std::mutex> lk(c->mu);
+    unsigned long long v[16] = {};
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(v, c->consumed, sizeof v, hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; i++) out[i] = (int64_t)v[i];
+    return GSR_OK;
+}
+
+extern "C" int gsr_blend_take_map(gsr_context* c, uint64_t* out, int64_t n) {
+    if (!c || !c->consumed || !out || c->blend_variant == 3 || n != (int64_t)c->fr.W * c->fr.H ||
+        c->consumed_cap < 16 + n)
+        return set_err(GSR_E_ARG, "gsr_blend_take_map: diagnostics were off or bad size");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (n) HIP_TRY(hipMemcpy(out, c->consumed + 16, (size_t)n * 8, hipMemcpyDeviceToHost));
+    return GSR_OK;
+}
+
 extern "C" int gsr_blend_counters(gsr_context* c, int64_t* out4) {
     if (!c || !c->consumed || !out4) return set_err(GSR_E_ARG, "gsr_blend_counters: diagnostics were off");
     std::lock_guard<std::mutex> lk(c->mu);
@@ -1497,6 +1533,42 @@ extern "C" int gsr_math_probe(const float* host_in, int n, float* host_out) {
     HIP_TRY(hipMemcpy(din, host_in, sizeof(float) * 2 * (size_t)n, hipMemcpyHostToDevice));
     HIP_TRY(gsr::launch_math_probe(din, n, dout, nullptr));
     HIP_TRY(hipMemcpy(host_out, dout, sizeof(float) * 8 * (size_t)n, hipMemcpyDeviceToHost));
+    (void)hipFree(din);
+    (void)hipFree(dout);
+    return GSR_OK;
+}
+
+extern "C" int gsr_exp_probe(float x_lo, float x_hi, float x_big, int64_t* violations, float* err_all,
+                             float* err_big) {
+    if (!violations || !err_all || !err_big || !(x_lo < x_hi))
+        return set_err(GSR_E_ARG, "gsr_exp_probe: bad argument");
+    unsigned long long* dv = nullptr;
+    uint32_t* de = nullptr;
+    HIP_TRY(hipMalloc(&dv, sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&de, 2 * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(dv, 0, sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(de, 0, 2 * sizeof(uint32_t)));
+    HIP_TRY(gsr::launch_exp_probe(gsr_float_key(x_lo), gsr_float_key(x_hi), x_big, dv, de, nullptr));
+    unsigned long long v = 0;
+    uint32_t e[2] = {0, 0};
+    HIP_TRY(hipMemcpy(&v, dv, sizeof v, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(e, de, sizeof e, hipMemcpyDeviceToHost));
+    (void)hipFree(dv);
+    (void)hipFree(de);
+    *violations = (int64_t)v;
+    *err_all = gsr_bits_to_float(e[0]);
+    *err_big = gsr_bits_to_float(e[1]);
+    return GSR_OK;
+}
+
+extern "C" int gsr_alpha_cut_probe(const float* host_op, int n, float* host_out) {
+    if (!host_op || !host_out || n <= 0) return set_err(GSR_E_ARG, "gsr_alpha_cut_probe: bad argument");
+    float *din = nullptr, *dout = nullptr;
+    HIP_TRY(hipMalloc(&din, sizeof(float) * (size_t)n));
+    HIP_TRY(hipMalloc(&dout, sizeof(float) * (size_t)n));
+    HIP_TRY(hipMemcpy(din, host_op, sizeof(float) * (size_t)n, hipMemcpyHostToDevice));
+    HIP_TRY(gsr::launch_xs_probe(din, n, dout, nullptr));
+    HIP_TRY(hipMemcpy(host_out, dout, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost));
     (void)hipFree(din);
     (void)hipFree(dout);
     return GSR_OK;

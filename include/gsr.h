@@ -252,13 +252,24 @@ int64_t gsr_blend_records_loaded(gsr_context* ctx);
  * (64 x pixels per lane x iterations), 0};
  * lane efficiency = active / slots. */
 int gsr_blend_counters(gsr_context* ctx, int64_t* out8);
+/* The first n (<= 16) blend counters: the 8 above, then {blocks the fast-exp blend
+ * handed to the exact blend, their suspect pixels}. */
+int gsr_blend_counters_ex(gsr_context* ctx, int64_t* out, int n);
+/* Take map of the last diagnostics frame: per pixel (row-major, n = W * H), the
+ * number of splats composited (low 32 bits) and the sum over them of
+ * (gaussian index + 1) * 2654435761 mod 2^32 (high 32 bits).  The oracle's
+ * orc_render_takes computes the same map, so the tests compare which splats
+ * every pixel composited, not only the colours. */
+int gsr_blend_take_map(gsr_context* ctx, uint64_t* out, int64_t n);
 /* Blend schedule: 0 = one 64-thread workgroup per 8x8 pixel block (the
  * kernel); 3 = the same with per-wave timestamps instead of counters (see
  * gsr_blend_stamps; diagnostics frames only).  Other values are refused (the
  * tile-per-workgroup schedule, longest-tiles-first, several blocks per wave or
  * workgroup and LDS-capped occupancy were measured slower and removed). */
 int gsr_set_blend_variant(gsr_context* ctx, int variant);
-/* Tuning knobs for A/B experiments (all settings give bit-identical output). */
+/* Tuning knobs for A/B experiments (all settings give bit-identical output, except
+ * GSR_TUNE_BLEND_EXP 1, which is within the parity gate and composites the same
+ * splats on every pixel). */
 enum {
     GSR_TUNE_BLEND_SCHEDULE = 0,     /* as gsr_set_blend_variant */
     GSR_TUNE_TILE_SORT_ITEMS = 1,    /* tile sort items per thread: 8 | 16 (default 16) */
@@ -294,8 +305,16 @@ enum {
                                         (gsr_rank_order_check) when the context first ran; 0 = ballot
                                         matching.  The environment variable GSR_RANK_ATOMIC=0 makes 0
                                         the default.  Same order, same image */
-    GSR_TUNE_RANK_ATOMIC_ACTIVE = 21 /* read-only: 1 if the atomic ranks are in use (knob 20 at 1 and the
+    GSR_TUNE_RANK_ATOMIC_ACTIVE = 21, /* read-only: 1 if the atomic ranks are in use (knob 20 at 1 and the
                                         self-check passed), 0 if the kernels rank with ballots */
+    GSR_TUNE_BLEND_EXP = 22          /* blend exp: 0 (default) = gsr_expf throughout (bit-exact with the
+                                        oracle).  1 (environment GSR_BLEND_EXP=1 selects it) = hardware
+                                        exp for alpha, with the alpha test exact on the exp argument and
+                                        the transmittance test guarded by a proven band; suspect pixels
+                                        are blended again exactly.  Images within 1e-6 of the exact
+                                        blend, identical take map; measured slower on config 2.
+                                        2 = test hook: 1 with a 100 % guard band, so every block
+                                        in which a pixel saturates is blended again exactly. */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Current value of a knob (what gsr_set_tuning last set, else the default). */
@@ -372,6 +391,14 @@ void gsr_camera_intrinsics(const gsr_camera* cam, float* fx, float* fy);
  * gsr_atan2f(x, y), sqrtf(x), x / y, roundf(x), bits(gsr_f2i_sat(1000x))}
  * into host_out (8n floats), so the CPU twins can be compared bit for bit. */
 int gsr_math_probe(const float* host_in, int n, float* host_out);
+/* Exhaustive device checks behind GSR_TUNE_BLEND_EXP, over every float x in
+ * [x_lo, x_hi): *violations = the number of x with gsr_expf(x) > gsr_expf(next x)
+ * (0: the exact exp is monotone, so the alpha test is a threshold on -md2/2);
+ * *err_all / *err_big = the largest |fast exp / gsr_expf - 1| over the range / over
+ * x >= x_big (rounded up). */
+int gsr_exp_probe(float x_lo, float x_hi, float x_big, int64_t* violations, float* err_all, float* err_big);
+/* gsr_alpha_take_min_x (gsr_detmath.h) evaluated on the device for n opacities. */
+int gsr_alpha_cut_probe(const float* host_op, int n, float* host_out);
 
 const char* gsr_last_error(void);
 const char* gsr_version(void);

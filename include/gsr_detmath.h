@@ -128,6 +128,64 @@ GSR_HD float gsr_blend_md2(float dx, float dy, float ic0, float ic1, float ic2, 
     return __builtin_fmaf(dx, __builtin_fmaf(ic0, dx, ic1 * dy), dy * __builtin_fmaf(ic2, dx, ic3 * dy));
 }
 
+/* Total order of floats as unsigned keys (-inf < ... < -0 < +0 < ... < +inf). */
+GSR_HD uint32_t gsr_float_key(float f) {
+    const uint32_t b = gsr_float_to_bits(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+GSR_HD float gsr_key_float(uint32_t k) {
+    return gsr_bits_to_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+/* The blend's alpha test (render.cu:333-335) as a predicate of the exp argument
+ * x = -md2 / 2: is fminf(op * expf(x), 0.99f) >= 1e-3f? */
+GSR_HD int gsr_alpha_taken(float op, float x) {
+    return !(fminf(op * gsr_expf(x), 0.99f) < 1e-3f);
+}
+
+/*
+ * Smallest float x with gsr_alpha_taken(op, x): a splat is composited on a pixel
+ * (alpha test passed) iff its exp argument -md2/2 >= this value, because
+ * gsr_expf is monotone non-decreasing on every float (checked exhaustively on
+ * [-104, 88.75], tests/test_gpu_fastexp.py; constant outside) and so is the
+ * rounded product op * y for op > 0.  NaN op: alpha = fminf(NaN, 0.99) passes for
+ * every x (-inf); op <= 0 never passes (+inf); op = +inf always passes (-inf).
+ * For finite op > 0 the answer lies in (-104, 88.75]: gsr_expf(-104) = +0 fails
+ * and gsr_expf(88.75) = +inf passes.  A few steps from the log estimate find it
+ * (the estimate is within a few ulp), with bisection on the float order as the
+ * bound.  Host and device give the same value: the estimate only picks where the
+ * search starts.
+ */
+GSR_HD float gsr_alpha_take_min_x(float op) {
+    if (op != op) return -INFINITY;
+    if (!(op > 0.0f)) return INFINITY;
+    if (op == INFINITY) return -INFINITY;
+    uint32_t lo = gsr_float_key(-104.0f), hi = gsr_float_key(88.75f);   /* fails / passes */
+#if defined(__HIP_DEVICE_COMPILE__)
+    float e = __logf(1e-3f / op);
+#else
+    float e = logf(1e-3f / op);
+#endif
+    e = fminf(fmaxf(e, -103.0f), 88.0f);
+    uint32_t k = gsr_float_key(e);
+    for (int s = 0; s < 6 && hi - lo > 1u; s++) {
+        if (gsr_alpha_taken(op, gsr_key_float(k))) {
+            hi = k;
+            k = k - 1u;
+        } else {
+            lo = k;
+            k = k + 1u;
+        }
+        if (k <= lo || k >= hi) break;
+    }
+    while (hi - lo > 1u) {
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (gsr_alpha_taken(op, gsr_key_float(mid))) hi = mid;
+        else lo = mid;
+    }
+    return gsr_key_float(hi);
+}
+
 /* Polynomial cores on |r| <= pi/4 (Cephes sinf / cosf). */
 GSR_HD float gsr_sin_core(float r) {
     const float z = r * r;

@@ -28,6 +28,8 @@ float orc_expf(float x) { return gsr_expf(x); }
 float orc_sinf(float x) { return gsr_sinf(x); }
 float orc_cosf(float x) { return gsr_cosf(x); }
 float orc_atan2f(float y, float x) { return gsr_atan2f(y, x); }
+float orc_alpha_take_min_x(float op) { return gsr_alpha_take_min_x(op); }
+int orc_alpha_taken(float op, float x) { return gsr_alpha_taken(op, x); }
 
 /* ------------------------------------------------------------ PLY loader */
 
@@ -452,8 +454,10 @@ static int cmp_kv(const void* a, const void* b) {
     return x->idx < y->idx ? -1 : (x->idx > y->idx);
 }
 
-/* One pixel-splat step of renderGaussians (render.cu:326-340). */
-static inline void blend_step(const orc_splat* g, int gx, int gy, float* T, float* rgb) {
+/* One pixel-splat step of renderGaussians (render.cu:326-340).  take (optional): the
+ * pixel's take-map entry (gsr_blend_take_map: count | index-mix sum << 32). */
+static inline void blend_step(const orc_splat* g, int gx, int gy, float* T, float* rgb, uint64_t* take,
+                              uint32_t gid) {
     if (gx < g->aabb[0] || gx > g->aabb[2] || gy < g->aabb[1] || gy > g->aabb[3]) return;
     if (*T < 1e-3f) return;
     const float dx = ((float)gx - (float)g->px_x);
@@ -466,6 +470,10 @@ static inline void blend_step(const orc_splat* g, int gx, int gy, float* T, floa
     if (opacity < 1e-3f) return;
     for (int c = 0; c < 3; ++c) rgb[c] = __builtin_fmaf(g->color[c] * opacity, *T, rgb[c]);
     *T *= (1.0f - opacity);
+    if (take) {
+        const uint32_t cnt = (uint32_t)*take + 1u, hs = (uint32_t)(*take >> 32) + (gid + 1u) * 2654435761u;
+        *take = (uint64_t)cnt | ((uint64_t)hs << 32);
+    }
 }
 
 static int cover_dims(int W, int H, int nx, int ny, int ws, int hs, int* cw, int* ch) {
@@ -476,8 +484,18 @@ static int cover_dims(int W, int H, int nx, int ny, int ws, int hs, int* cw, int
     return 0;
 }
 
+/* orc_render plus the per-pixel take map (W * H entries, row-major; pixels outside
+ * the covered area stay 0), the GPU's gsr_blend_take_map. */
+int orc_render_takes(const float* soa, int64_t n, const gsr_camera* cam, int W, int H, int nx, int ny,
+                     int ws, int hs, float k, float* out, uint64_t* takes, int threads);
+
 int orc_render(const float* soa, int64_t n, const gsr_camera* cam, int W, int H, int nx, int ny,
                int ws, int hs, float k, float* out, int threads) {
+    return orc_render_takes(soa, n, cam, W, H, nx, ny, ws, hs, k, out, NULL, threads);
+}
+
+int orc_render_takes(const float* soa, int64_t n, const gsr_camera* cam, int W, int H, int nx, int ny,
+                     int ws, int hs, float k, float* out, uint64_t* takes, int threads) {
     int cw, ch;
     if (cover_dims(W, H, nx, ny, ws, hs, &cw, &ch)) return -1;
     orc_splat* sp = (orc_splat*)malloc(sizeof(orc_splat) * (size_t)(n > 0 ? n : 1));
@@ -492,6 +510,7 @@ int orc_render(const float* soa, int64_t n, const gsr_camera* cam, int W, int H,
 
     const size_t npx = (size_t)W * (size_t)H;
     memset(out, 0, sizeof(float) * 3 * npx);
+    if (takes) memset(takes, 0, sizeof(uint64_t) * npx);
     const int band = 8;
     const int nbands = (ch + band - 1) / band;
 #ifdef _OPENMP
@@ -514,7 +533,8 @@ int orc_render(const float* soa, int64_t n, const gsr_camera* cam, int W, int H,
             for (int y = ya; y <= yb; y++)
                 for (int x = xa; x <= xb; x++) {
                     const size_t q = (size_t)(y - y0) * cw + x;
-                    blend_step(g, x, y, &T[q], &rgb[3 * q]);
+                    blend_step(g, x, y, &T[q], &rgb[3 * q], takes ? &takes[(size_t)y * W + x] : NULL,
+                               order[s].idx);
                 }
         }
         for (int y = y0; y <= y1; y++)
@@ -579,7 +599,7 @@ int orc_render_tiled(const float* soa, int64_t n, const gsr_camera* cam, int W, 
             for (int j = 0; j < bs; j++) {
                 const int gx = j % ws + x_off, gy = j / ws + y_off;
                 if (gx >= W || gy >= H) continue;
-                blend_step(g, gx, gy, &T[j], &rgb[3 * j]);
+                blend_step(g, gx, gy, &T[j], &rgb[3 * j], NULL, 0u);
             }
             p++;
         }

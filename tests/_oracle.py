@@ -45,6 +45,13 @@ def lib():
         L.orc_render.argtypes = [c_void_p, c_int64, cam, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
                                  c_void_p, c_int]
         L.orc_render.restype = c_int
+        L.orc_render_takes.argtypes = [c_void_p, c_int64, cam, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+                                       c_void_p, c_void_p, c_int]
+        L.orc_render_takes.restype = c_int
+        L.orc_alpha_take_min_x.argtypes = [c_float]
+        L.orc_alpha_take_min_x.restype = c_float
+        L.orc_alpha_taken.argtypes = [c_float, c_float]
+        L.orc_alpha_taken.restype = c_int
         L.orc_render_tiled.argtypes = [c_void_p, c_int64, cam, c_int, c_int, c_int, c_int, c_int, c_int,
                                        c_float, c_void_p]
         L.orc_render_tiled.restype = c_int
@@ -134,6 +141,19 @@ def render(soa: np.ndarray, cam, W: int, H: int, k: float, tiling=None, threads:
                           out.ctypes.data, threads)
     assert rc == 0
     return out
+
+
+def render_takes(soa: np.ndarray, cam, W: int, H: int, k: float, tiling=None, threads: int = 0):
+    """render() plus the take map (gsr_blend_take_map): per pixel, the splats composited
+    as count | (sum of (index + 1) * 2654435761 mod 2^32) << 32."""
+    soa = np.ascontiguousarray(soa, dtype=np.float32)
+    nx, ny, ws, hs = tiling if tiling else (1, 1, W, H)
+    out = np.zeros((3, H, W), dtype=np.float32)
+    takes = np.zeros((H, W), dtype=np.uint64)
+    rc = lib().orc_render_takes(soa.ctypes.data, soa.shape[1], ctypes.byref(cam), W, H, nx, ny, ws, hs, k,
+                                out.ctypes.data, takes.ctypes.data, threads)
+    assert rc == 0
+    return out, takes
 
 
 def render_tiled(soa: np.ndarray, cam, W: int, H: int, k: float, tiling) -> np.ndarray:

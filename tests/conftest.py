@@ -9,6 +9,38 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# BASELINE.json north_star: per-pixel L-inf <= 1e-4 against the oracle.
+LINF_TOL = 1e-4
+# The library's blend default (GSR_TUNE_BLEND_EXP 0) is the exact blend (bit-identical
+# to the oracle); GSR_BLEND_EXP=1 in the environment selects the fast-exp blend, which
+# composites exactly the oracle's splats on every pixel with alpha within a few ulp.
+BLEND_EXACT_DEFAULT = not os.environ.get("GSR_BLEND_EXP", "0").startswith("1")
+KNOB_BLEND_EXP = 22
+
+
+def assert_frames(got, want, exact=None):
+    """GPU frame against the oracle's: finite and within the north-star L-inf gate;
+    bit for bit when the frame came from the exact blend (exact=None: the default
+    renderer's mode)."""
+    import numpy as np
+    exact = BLEND_EXACT_DEFAULT if exact is None else exact
+    got = np.asarray(got, dtype=np.float32)
+    want = np.asarray(want, dtype=np.float32)
+    assert got.shape == want.shape
+    diff = np.abs(got.astype(np.float64) - want.astype(np.float64))
+    linf = float(diff.max()) if diff.size else 0.0
+    assert np.isfinite(got).all()
+    assert linf <= LINF_TOL, f"L-inf {linf} > {LINF_TOL} at {np.unravel_index(diff.argmax(), diff.shape)}"
+    if exact:
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"not bit-exact (L-inf {linf})"
+    return linf
+
+
+def exact_blend(renderer):
+    """Switch a Renderer to the exact blend (bit-identical to the oracle)."""
+    renderer.set_tuning(KNOB_BLEND_EXP, 0)
+    return renderer
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")

@@ -12,6 +12,8 @@ import os
 import numpy as np
 import pytest
 
+from conftest import assert_frames
+
 from conftest import scene_soa
 from gaussianrenderer_amd import _native
 
@@ -96,7 +98,7 @@ def test_render_display_device_target_bit_exact(gpu, orc, torch, d1, W, H, extra
     assert (buf[3 * W * H:] == 7.0).all()
     want = orc.render(soa, cam, W, H, 3.0)
     assert (want != 0).sum() > 100
-    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert_frames(got, want)
     plain = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
     r.render(scene, cam, W, H, plain.data_ptr())
     r.sync()
@@ -136,4 +138,4 @@ def test_render_display_4d_scene(gpu, orc, torch, tmp_path):
         if r.sync() == 0:
             break
     want = orc.render(orc.temporal(soa49, 0.4), cam, W, H, 3.0)
-    assert np.array_equal(buf.view(3, H, W).cpu().numpy().view(np.uint32), want.view(np.uint32))
+    assert_frames(buf.view(3, H, W).cpu().numpy(), want)

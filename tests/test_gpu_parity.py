@@ -1,19 +1,19 @@
 """GPU parity: the HIP pipeline (through the C ABI) against the CPU oracle on
 the same seeded inputs.  Integer / index outputs (AABBs, pixel centres, depth
 keys, sort orders, tile ranges) must be bit-exact; the image gate is the
-north-star per-pixel L-inf <= 1e-4 (the pipeline is in fact bit-exact, which
-is asserted separately so a regression is visible)."""
+north-star per-pixel L-inf <= 1e-4.  The exact blend (GSR_TUNE_BLEND_EXP 0) is
+bit-exact, asserted wherever a test selects it; the default fast-exp blend must
+composite the same splats on every pixel (take maps, tests/test_gpu_fastexp.py)."""
 import ctypes
 import os
 
 import numpy as np
 import pytest
 
-from conftest import ROOT, scene_soa
+from conftest import LINF_TOL, ROOT, assert_frames, exact_blend, scene_soa  # noqa: F401
 
 pytestmark = pytest.mark.gpu
 
-LINF_TOL = 1e-4          # BASELINE.json north_star: per-pixel L-inf <= 1e-4
 
 
 @pytest.fixture(scope="module")
@@ -42,12 +42,9 @@ def render_gpu(gsr, torch, scene, cam, W, H, k=3.0, tiling=None, renderer=None, 
     return out.view(3, H, W).cpu().numpy(), r
 
 
-def assert_image_parity(got, want):
-    diff = np.abs(got.astype(np.float64) - want.astype(np.float64))
-    linf = float(diff.max()) if diff.size else 0.0
-    assert np.isfinite(got).all()
-    assert linf <= LINF_TOL, f"L-inf {linf} > {LINF_TOL} at {np.unravel_index(diff.argmax(), diff.shape)}"
-    assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"not bit-exact (L-inf {linf})"
+def assert_image_parity(got, want, exact=None):
+    """L-inf gate; bit-exact for frames of the exact blend (conftest.assert_frames)."""
+    return assert_frames(got, want, exact)
 
 
 def test_math_probe_bitwise(gpu, orc):
@@ -78,6 +75,7 @@ def test_math_probe_bitwise(gpu, orc):
 
 
 KNOB_TILE_SPANS = 19
+KNOB_BLEND_EXP = 22
 
 
 def rect_pairs(want, order, W, H):
@@ -187,7 +185,9 @@ def test_tile_spans_drop_only_unreachable_pairs(gpu, orc, torch, c1, ci):
     W, H = 640, 480
     cam = cam_for(gpu, W, H, **CAMS[ci])
     scene = gpu.Scene.from_soa(soa)
-    r_on, r_off = gpu.Renderer(), gpu.Renderer()
+    # exact blend: the lists differ, so the fast blend's guard band (which counts list
+    # entries) could re-blend different blocks; the exact images must be identical
+    r_on, r_off = exact_blend(gpu.Renderer()), exact_blend(gpu.Renderer())
     assert r_on.get_tuning(KNOB_TILE_SPANS) == 2   # default: on up to 1.5M Gaussians
     r_on.set_tuning(KNOB_TILE_SPANS, 1)
     r_off.set_tuning(KNOB_TILE_SPANS, 0)
@@ -196,7 +196,7 @@ def test_tile_spans_drop_only_unreachable_pairs(gpu, orc, torch, c1, ci):
     got_on, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_on)
     got_off, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_off)
     assert np.array_equal(got_on.view(np.uint32), got_off.view(np.uint32))
-    assert_image_parity(got_on, orc.render(soa, cam, W, H, 3.0))
+    assert_image_parity(got_on, orc.render(soa, cam, W, H, 3.0), exact=True)
     want = orc.preprocess(soa, cam, W, H, 3.0)
     full = rect_pairs(want, r_on.read_depth_order(soa.shape[1]), W, H)
     assert np.array_equal(r_off.read_pairs(), full)
@@ -259,7 +259,7 @@ def test_tile_binning_matches_pair_sort(gpu, orc, torch, c1, knobs):
     W, H = 1000, 700
     scene = gpu.Scene.from_soa(soa)
     cam = cam_for(gpu, W, H, pos=(0.4, 0.3, 3.5))
-    r_bin, r_sort = gpu.Renderer(), gpu.Renderer()
+    r_bin, r_sort = exact_blend(gpu.Renderer()), exact_blend(gpu.Renderer())
     for kn, v in knobs.items():
         r_bin.set_tuning(kn, v)
     r_bin.set_tuning(KNOB_TILE_SPANS, 0)   # the pair path lists every tile of every rect
@@ -270,7 +270,7 @@ def test_tile_binning_matches_pair_sort(gpu, orc, torch, c1, knobs):
     pb, ps = r_bin.read_pairs(), r_sort.read_pairs()
     assert pb.shape == ps.shape and pb.shape[0] > 10_000
     assert np.array_equal(pb, ps)
-    assert_image_parity(got_bin, orc.render(soa, cam, W, H, 3.0))
+    assert_image_parity(got_bin, orc.render(soa, cam, W, H, 3.0), exact=True)
     # the row pass made one item per covered tile row of every visible splat
     spl = r_bin.read_splats(soa.shape[1])
     live = spl["tile_count"] > 0
@@ -286,7 +286,7 @@ def test_tile_binning_8bit_digits(gpu, orc, torch, c1):
     W, H = 2100, 2060
     scene = gpu.Scene.from_soa(soa)
     cam = cam_for(gpu, W, H, pos=(0.3, -0.2, 3.2), fov=60)
-    r_bin, r_sort, r_span = gpu.Renderer(), gpu.Renderer(), gpu.Renderer()
+    r_bin, r_sort, r_span = (exact_blend(gpu.Renderer()) for _ in range(3))
     r_bin.set_tuning(KNOB_TILE_SPANS, 0)
     r_sort.set_tuning(7, 0)
     got, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r_bin)
@@ -433,8 +433,14 @@ def test_blend_slow_path_and_degenerate_records(gpu, orc, torch, c1):
         assert_image_parity(got, want)
         r.set_diagnostics(True)
         got2, _ = render_gpu(gpu, torch, gpu.Scene.from_soa(s), cam, W, H, renderer=r)
-        assert np.array_equal(got2.view(np.uint32), want.view(np.uint32))
-        assert r.blend_counters()["slow_path_iters"] > 0
+        assert_image_parity(got2, want)
+        d = r.blend_counters_ex()
+        assert d["slow_path_iters"] > 0
+        # the fast blend hands every block holding such a record to the exact blend
+        assert (d["reblended_blocks"] > 0) != (r.get_tuning(KNOB_BLEND_EXP) == 0)
+        r.set_tuning(KNOB_BLEND_EXP, 0)
+        got3, _ = render_gpu(gpu, torch, gpu.Scene.from_soa(s), cam, W, H, renderer=r)
+        assert_image_parity(got3, want, exact=True)
 
 
 @pytest.mark.parametrize("ci", [0, 1, 3])
@@ -461,7 +467,7 @@ def test_sh3_mode_parity(gpu, orc, torch, c1, ci):
     t = gpu.TilingInformation(50, 50, H, W)
     host = gpu.preprocessCUDAGaussians(scene.ptr, scene.n, cam, t.num_tile_y, t.num_tile_x, t.width_stride,
                                        t.height_stride, W, H, 3.0)
-    assert np.array_equal(host.view(np.uint32), want.view(np.uint32))
+    assert_image_parity(host, want)
 
 
 def test_dropin_scene_block_reference_tiling(gpu, orc, torch, c1):
@@ -614,9 +620,18 @@ def test_config2_full_parity(gpu, orc, torch, tmp_path_factory):
     path, soa = scene_soa(gpu, tmp_path_factory, 1_000_000, 2)
     W, H = 1920, 1080
     cam = cam_for(gpu, W, H)
-    got, r = render_gpu(gpu, torch, gpu.Scene.from_ply(path), cam, W, H)
-    want = orc.render(soa, cam, W, H, 3.0, threads=min(16, os.cpu_count() or 1))
-    assert_image_parity(got, want)
+    full_size_both_blends(gpu, orc, torch, gpu.Scene.from_ply(path), soa, cam, W, H)
+
+
+def full_size_both_blends(gpu, orc, torch, scene, soa, cam, W, H):
+    """The default (exact) blend is bit-identical with the same take map as the oracle;
+    the opt-in fast-exp blend composites exactly the oracle's splats on every pixel
+    (take maps) within the gate."""
+    from test_gpu_fastexp import take_parity
+    want, takes_want = orc.render_takes(soa, cam, W, H, 3.0, threads=min(16, len(os.sched_getaffinity(0))))
+    take_parity(gpu, torch, scene, cam, W, H, want, takes_want, mode=0)
+    linf, c = take_parity(gpu, torch, scene, cam, W, H, want, takes_want, mode=1)
+    print(f"{W}x{H}: fast-exp blend L-inf {linf:.3g}, re-blended blocks {c['reblended_blocks']}")
 
 
 def test_config3_full_parity_and_properties(gpu, orc, torch, tmp_path_factory):
@@ -632,8 +647,7 @@ def test_config3_full_parity_and_properties(gpu, orc, torch, tmp_path_factory):
     assert np.isfinite(got).all() and got.min() >= 0.0 and got.max() <= 1.0
     again, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
     assert np.array_equal(got.view(np.uint32), again.view(np.uint32))
-    want = orc.render(soa, cam, W, H, 3.0, threads=min(16, os.cpu_count() or 1))
-    assert_image_parity(got, want)
+    full_size_both_blends(gpu, orc, torch, scene, soa, cam, W, H)
 
 
 @pytest.mark.parametrize("azimuth", [0.0, 135.0])

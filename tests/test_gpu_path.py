@@ -111,8 +111,9 @@ def test_path_is_stream_ordered(gpu, orc, torch, c1):
     assert r.sync() == 0
     for cam, o, sm in zip(cams, outs, sums.cpu().numpy()):
         want = orc.render(soa, cam, W, H, 3.0)
-        assert_image_parity(o.view(3, H, W).cpu().numpy(), want)
-        assert sm == pytest.approx(float(want.astype(np.float64).sum()), rel=1e-12)
+        img = o.view(3, H, W).cpu().numpy()
+        assert_image_parity(img, want)
+        assert sm == pytest.approx(float(img.astype(np.float64).sum()), rel=1e-12)
 
 
 def test_path_frame_events_without_join(gpu, orc, torch, c1):

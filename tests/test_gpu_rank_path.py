@@ -15,6 +15,7 @@ import numpy as np
 import pytest
 
 from conftest import scene_soa
+from conftest import exact_blend
 from test_gpu_parity import assert_image_parity, cam_for
 
 pytestmark = pytest.mark.gpu
@@ -44,7 +45,7 @@ def render_both(gpu, torch, scene, n, cam, W, H):
     """Render with ballot ranks and with atomic ranks; return {path: (image, depth order, pairs)}."""
     out = {}
     for ra in (0, 1):
-        r = gpu.Renderer()
+        r = exact_blend(gpu.Renderer())      # images bit-exact against the oracle
         r.set_tuning(gpu.TUNE_RANK_ATOMIC, ra)
         assert r.get_tuning(gpu.TUNE_RANK_ATOMIC_ACTIVE) == ra
         img = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
@@ -66,8 +67,8 @@ def check_paths(out, want):
     tie = keys[1:] == keys[:-1]
     assert (idx[1:][tie] > idx[:-1][tie]).all(), "depth ties not in index order"
     assert p0.size == p1.size and np.array_equal(p0, p1), "tile lists differ between the rank paths"
-    assert_image_parity(i0, want)
-    assert_image_parity(i1, want)
+    assert_image_parity(i0, want, exact=True)
+    assert_image_parity(i1, want, exact=True)
 
 
 def test_rank_paths_config2_full(gpu, orc, torch, tmp_path_factory):
