@@ -48,8 +48,11 @@ def _worker(rank, world, port, ply, W, H, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_orbit_gather(gsr, orc, tmp_path):
-    W, H, world = 96, 64, 2
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_two_rank_orbit_gather(gsr, orc, tmp_path, world):
+    """World 2 as before, and 4 and 8 ranks (the driver's scaling run): every rank's
+    orbit frame reaches rank 0 in rank order, the elapsed time is the max over ranks."""
+    W, H = 96, 64
     ply = str(tmp_path / "s.ply")
     gsr.write_synthetic_ply(ply, 3000, 4)
     ctx = mp.get_context("spawn")
@@ -62,10 +65,11 @@ def test_two_rank_orbit_gather(gsr, orc, tmp_path):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert elapsed == pytest.approx(1.5)          # MAX over ranks
+    assert elapsed == pytest.approx(0.5 + world - 1)   # MAX over ranks
     soa = gsr.read_ply(ply)
     from gaussianrenderer_amd import multi
     for r in range(world):
         want = orc.render(soa, multi.orbit_camera(r, W, H), W, H, 3.0, threads=1).reshape(-1)
         assert np.array_equal(frames[r], want)
-    assert not np.array_equal(frames[0], frames[1])   # different orbit cameras
+    for r in range(1, world):
+        assert not np.array_equal(frames[0], frames[r])   # different orbit cameras

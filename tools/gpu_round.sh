@@ -10,6 +10,8 @@
 #   pmc        the PMC passes of the same command              (tools/profile.sh, PMC only)
 #   rehearsal  RCCL rehearsal of the multi-GPU loop at world 1 (tools/nccl_rehearsal.py),
 #              with per-chunk gathers and without gathers (REH_ARGS)
+#   rehkt      kernel + memory-copy trace of the world-1 RCCL rehearsal, with per-chunk gathers
+#              and without (rank env set directly: no launcher under the profiler)
 #   ktab       kernel trace of the one-frame-at-a-time bench per knob setting (TUNES,
 #              e.g. TUNES="19=0 19=1"; CONFIGS) -> gpurun_out/kt_ab_<tag>/summary.txt
 #   abtune     interleaved knob A/B in one process (tools/ab_path.py, AB_ARGS)
@@ -22,6 +24,10 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${TAG:-run}
 fatal() { case $1 in 124|134|137|139) echo "FATAL rc=$1 in $2; stopping"; exit "$1";; esac; }
+slim() {   # drop the raw per-dispatch traces (gpurun brings back at most 64 MiB); keep stats + summaries
+  find "$1" \( -name "*kernel_trace.csv" -o -name "*memory_copy_trace.csv" -o -name "*counter_collection.csv" \) -delete 2>/dev/null
+  true
+}
 line() {   # summary of a bench JSON line
   tail -1 "$1" | python3 -c "import json,sys; d=json.load(sys.stdin); print('$2', d['value'], 'seq', d['sequential']['value'], 'blend', d['roofline']['avg_launch_ms'], 'inflight blend', d['roofline']['avg_launch_ms_inflight'], 'stages', d['stages_ms'], 'cpu', d.get('cpu_baseline', {}).get('value'))"
 }
@@ -46,16 +52,38 @@ for step in ${STEPS:-suite smoke bench}; do
   kt)
     OUT=gpurun_out/prof_$TAG SKIP_PMC=1 bash tools/profile.sh
     rc=$?; fatal $rc kt; [ $rc = 0 ] || exit $rc
-    python3 tools/summarize_prof.py gpurun_out/prof_$TAG > gpurun_out/prof_$TAG/summary.txt 2>&1; head -30 gpurun_out/prof_$TAG/summary.txt ;;
+    python3 tools/summarize_prof.py gpurun_out/prof_$TAG > gpurun_out/prof_$TAG/summary.txt 2>&1; head -30 gpurun_out/prof_$TAG/summary.txt
+    slim gpurun_out/prof_$TAG ;;
   pmc)
-    OUT=gpurun_out/prof_$TAG SKIP_KT=1 bash tools/profile.sh
-    rc=$?; fatal $rc pmc; [ $rc = 0 ] || exit $rc ;;
+    # PMC passes of the one-frame-at-a-time bench (BENCH_ARGS default --inflight 1), the
+    # per-kernel means written as gpurun_out/pmc_$TAG.json (bench.py reads profiles/pmc_latest.json)
+    OUT=gpurun_out/prof_$TAG BENCH_ARGS=${BENCH_ARGS:---inflight 1} SKIP_KT=1 \
+      PMC_GROUPS=${PMC_GROUPS:-"FETCH_SIZE;WRITE_SIZE;SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_INSTS_SALU"} \
+      bash tools/profile.sh
+    rc=$?; fatal $rc pmc; [ $rc = 0 ] || exit $rc
+    python3 tools/summarize_prof.py gpurun_out/prof_$TAG --json gpurun_out/pmc_$TAG.json ${CONFIGS:-2} \
+      "rocprofv3 --pmc, separate passes, bench.py --steps 50 ${BENCH_ARGS:---inflight 1}, $TAG"
+    python3 tools/pmc_agg.py gpurun_out/prof_$TAG k_ > gpurun_out/prof_$TAG/pmc_means.txt 2>&1
+    # with a kernel trace of the same TAG already there: the table with the PMC columns
+    [ -f gpurun_out/prof_$TAG/kt/kt_kernel_stats.csv ] && \
+      python3 tools/summarize_prof.py gpurun_out/prof_$TAG > gpurun_out/prof_$TAG/summary.txt 2>&1
+    slim gpurun_out/prof_$TAG ;;
   rehearsal)
     for g in step none; do
       timeout -k 10 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 \
         --master-port $((29500 + RANDOM % 400)) tools/nccl_rehearsal.py --gather $g ${REH_ARGS:---steps 400 --gaussians 1000000 --W 1920 --H 1080 --warm-ms 1000} \
         > gpurun_out/rehearsal_${TAG}_$g.log 2>&1
       rc=$?; fatal $rc rehearsal; grep "nccl rehearsal" gpurun_out/rehearsal_${TAG}_$g.log; [ $rc = 0 ] || { tail -5 gpurun_out/rehearsal_${TAG}_$g.log; exit $rc; }
+    done ;;
+  rehkt)
+    for g in step none; do
+      O=gpurun_out/prof_reh_${TAG}_$g; mkdir -p $O
+      RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=$((29500 + RANDOM % 400)) \
+        timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/kt -o kt --output-format csv -- \
+        python3 tools/nccl_rehearsal.py --gather $g ${REH_ARGS:---steps 400 --gaussians 1000000 --W 1920 --H 1080 --warm-ms 1000} > $O/kt.log 2>&1
+      rc=$?; echo "rehearsal trace $g rc=$rc"; fatal $rc rehkt; grep "nccl rehearsal" $O/kt.log; [ $rc = 0 ] || { tail -5 $O/kt.log; exit $rc; }
+      python3 tools/summarize_prof.py $O > $O/summary.txt 2>&1; head -24 $O/summary.txt
+      slim $O
     done ;;
   ktab)
     for t in ${TUNES:-19=0 19=1}; do

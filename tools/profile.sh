@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/prof}
 mkdir -p "$OUT"
 fatal() { case $1 in 124|134|137|139) echo "FATAL rc=$1 in $2; stopping"; exit "$1";; esac; }
-B="bench.py --steps ${STEPS:-50} --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-}"
+B="bench.py --steps ${BENCH_STEPS:-50} --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-}"
 [ "${SKIP_KT:-0}" = 1 ] || timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 $B > "$OUT/kt.log" 2>&1
 rc=$?; echo "kernel-trace rc=$rc"; fatal $rc kt
 # counter groups separated by ';' (each group = one pass)
