@@ -44,9 +44,13 @@ TIMESTEPS_4D = 120
 TIMING_STRIDE = 8
 STAGE_FRAMES = 10     # untimed frames averaged for stages_ms
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
-# the blend (one 64-thread workgroup per 8x8 block): template <DIAG, STAMPS, FX>, FX = the
-# fast-exp blend (GSR_TUNE_BLEND_EXP 1) or the exact one (0, the default)
-BLEND_KERNELS = {1: "k_blend_w<false, false, true>", 0: "k_blend_w<false, false, false>"}
+# the blend (one 64-thread workgroup per 8x8 block): template <DIAG, STAMPS, FX, SPLIT>, FX = the
+# fast-exp blend (GSR_TUNE_BLEND_EXP 1) or the exact one (0, the default); SPLIT 1 = the depth
+# split's phase A (GSR_TUNE_DEPTH_SPLIT, on by default above 1.5M Gaussians), whose launch is
+# the frame's blend; phase B (binning the rest of the depth order, resuming the blocks phase A
+# left unsaturated) is the "resume" stage
+BLEND_KERNELS = {1: "k_blend_w<false, false, true, 0>", 0: "k_blend_w<false, false, false, 0>",
+                 "split": "k_blend_w<false, false, false, 1>"}
 BLEND_KERNEL = BLEND_KERNELS[0]
 
 
@@ -387,7 +391,8 @@ def main():
     consumed = counters["records_loaded"]
     global BLEND_KERNEL
     blend_exp = r.get_tuning(22)
-    BLEND_KERNEL = BLEND_KERNELS[min(blend_exp, 1)]
+    split = stages.get("resume", 0.0) > 0.0          # the stage frames ran the depth split
+    BLEND_KERNEL = BLEND_KERNELS["split" if split else min(blend_exp, 1)]
     r.set_diagnostics(False)
     tiles_x, tiles_y = r.tile_grid()
     # visible Gaussians M (depth key != 0xFFFFFFFF), untimed
@@ -512,6 +517,10 @@ def main():
                        "ms_per_frame": round(max_seq / args.steps * 1e3, 4),
                        "note": "same K frames one at a time on one stream (gsr_render; the viewer's use)"},
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+        "depth_split": ({"split_permille": r.get_tuning(24), "unsaturated_blocks_after_phase_a": r.get_tuning(25),
+                         "note": "pairs / row_items / stages emit+tile_sort are phase A's (the nearest "
+                                 "split_permille/1000 of the depth order); stage resume = phase B"}
+                        if split else None),
         "pairs": pairs,
         "row_items": row_items,
         "depth_passes": depth_passes,

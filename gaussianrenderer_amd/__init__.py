@@ -507,6 +507,9 @@ TUNE_TILE_SPANS = 19
 TUNE_RANK_ATOMIC = 20
 TUNE_RANK_ATOMIC_ACTIVE = 21
 TUNE_BLEND_EXP = 22
+TUNE_DEPTH_SPLIT = 23
+TUNE_DEPTH_SPLIT_PERMILLE = 24
+TUNE_DEPTH_SPLIT_UNSAT = 25
 
 
 def rank_order_check() -> tuple[int, int]:

@@ -37,7 +37,7 @@ LAYOUT_SCENE_BLOCK_SH3 = 3
 PLY_TYPED = 1
 PLY_SH3 = 2
 
-STAGES = ("preprocess", "depth_sort", "emit", "tile_sort", "ranges", "blend")
+STAGES = ("preprocess", "depth_sort", "emit", "tile_sort", "ranges", "blend", "resume")
 NUM_STAGES = len(STAGES)
 TILE_PX = 16
 SPLAT_RECORD_BYTES = 64

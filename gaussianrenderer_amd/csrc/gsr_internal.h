@@ -42,6 +42,20 @@ struct Stats {
     uint32_t overflow;                // bit 0: P > capacity; bit 1: the depth sort needed more
                                       // passes than were launched (depth pass budget)
     uint32_t depth_passes;            // passes the depth sort's device plan needed (binning path; 0: n/a)
+    uint32_t split_unsat;             // depth split: blocks the last phase-A blend left unsaturated
+                                      // (written to the host-mapped copy by the phase-B blend)
+};
+
+// Depth split (GSR_TUNE_DEPTH_SPLIT): the frame's tiles are binned over the nearest
+// part of the depth order first (phase A); its blend saves the transmittance of
+// every block it leaves unsaturated, and phase B bins the rest of the depth order
+// and resumes those blocks.  phase: 1 = A (save), 2 = B (resume).
+struct BlendSplit {
+    int phase;
+    float* tbuf;                      // 64 floats per 8x8 block (4 blocks per tile)
+    uint8_t* bflag;                   // per block: 1 = left unsaturated by phase A (tbuf valid)
+    uint32_t* gate;                   // count of such blocks (cleared by phase A's row scan)
+    Stats* host_st;                   // phase B publishes the count here (nullable)
 };
 
 // ---- launch wrappers (gsr_kernels.hip) ----
@@ -83,7 +97,7 @@ hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* ke
 // 2 the same with the guard band at 100 % (test hook for the exact re-blend).
 hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
                         float* out, unsigned long long* consumed, bool stamps, int band_tiles, int blend_exp,
-                        hipStream_t s);
+                        hipStream_t s, const BlendSplit* split = nullptr);
 // Stable partition of the preprocess items: visible first, culled last (both in
 // index order), visible count into *n_live; culled tail to out only, with dead
 // rects in srect (gsr_kernels.hip "live partition").  counts: groups words.
@@ -97,12 +111,13 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
                            const uint32_t* pay0, const uint32_t* pay1, int groups, uint32_t* hist,
                            uint32_t* row_items,
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
-                           int items, hipStream_t s, const uint16_t* spans = nullptr, bool rank_atomic = false);
+                           int items, hipStream_t s, const uint16_t* spans = nullptr, bool rank_atomic = false,
+                           uint32_t base = 0, uint32_t* gate = nullptr, int gate_mode = 0);
 hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, const unsigned long long* row_pairs,
                            uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
                            uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,
                            hipStream_t s, const uint32_t* dstats = nullptr, int passes_launched = 4,
-                           bool rank_atomic = false);
+                           bool rank_atomic = false, const uint32_t* gate = nullptr);
 uint32_t bin_col_chunks_max(uint32_t pair_capacity, int tiles_y);
 // Standalone sort ABI helpers (oneSweepSort / oneSweep3DGaussianSort).
 hipError_t launch_items_from_keys(const int* keys, uint32_t n, uint64_t* items, hipStream_t s);

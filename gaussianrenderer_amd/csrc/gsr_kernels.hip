@@ -1506,8 +1506,10 @@ __device__ __forceinline__ void publish_pair_stats(unsigned long long total, uin
 __global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint32_t* __restrict__ pay0,
                                                          const uint32_t* __restrict__ pay1,
                                                          const uint32_t* __restrict__ dstats, int groups,
-                                                         int tiles_y, uint32_t* __restrict__ hist) {
+                                                         int tiles_y, uint32_t* __restrict__ hist, uint32_t base,
+                                                         const uint32_t* __restrict__ gate) {
     GSR_GEOM_PRIO();
+    if (gate && *gate == 0u) return;   // depth split, phase B: every block saturated in phase A
     __shared__ uint32_t h_items[4][256], h_pairs[4][256];
     const uint32_t t = threadIdx.x, w = t >> 6;
 #pragma unroll
@@ -1516,7 +1518,7 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint32
         h_pairs[k][t] = 0;
     }
     __syncthreads();
-    const uint32_t* srect = depth_sorted_rects(pay0, pay1, dstats);
+    const uint32_t* srect = depth_sorted_rects(pay0, pay1, dstats) + base;
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, kRowSources, b, e);
     for (uint64_t c0 = b; c0 < e; c0 += 1024) {
@@ -1559,8 +1561,13 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint32
 // counts over the workgroups (in place) and the row's totals.
 __global__ __launch_bounds__(256) void k_bin_rows_scan(uint32_t* __restrict__ hist, int groups, int tiles_y,
                                                         uint32_t* __restrict__ row_items,
-                                                        unsigned long long* __restrict__ row_pairs) {
+                                                        unsigned long long* __restrict__ row_pairs,
+                                                        uint32_t* __restrict__ gate, int gate_mode) {
     GSR_GEOM_PRIO();
+    // depth split: phase A clears the count of unsaturated blocks its blend raises;
+    // phase B runs only when that count is not zero
+    if (gate_mode == 1 && blockIdx.x == 0 && threadIdx.x == 0) *gate = 0u;
+    if (gate_mode == 2 && *gate == 0u) return;
     __shared__ uint32_t scr[4];
     __shared__ unsigned long long scr64[4];
     const uint32_t r = blockIdx.x, t = threadIdx.x;
@@ -1613,8 +1620,10 @@ __global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(co
                                                            const uint32_t* __restrict__ row_items,
                                                            const unsigned long long* __restrict__ row_pairs,
                                                            uint32_t cap, int tiles_y, uint64_t* __restrict__ rows_out,
-                                                           const uint16_t* __restrict__ spans) {
+                                                           const uint16_t* __restrict__ spans, uint32_t base,
+                                                           const uint32_t* __restrict__ gate) {
     GSR_GEOM_PRIO();
+    if (gate && *gate == 0u) return;
     constexpr uint32_t kTile = 256u * ITEMS;
     __shared__ uint32_t s_pref[kRowSources], s_idx[kRowSources];
     // per source: packed rect (pack_rect) | tile row spans << 32 (no LDS beyond the
@@ -1632,8 +1641,8 @@ __global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(co
     uint64_t b, e;
     const int chunk = (int)blockIdx.x;
     chunk_range(n, groups, chunk, kRowSources, b, e);
-    const uint64_t* sorted = depth_sorted(items0, items1, dstats);
-    const uint32_t* srect = depth_sorted_rects(pay0, pay1, dstats);
+    const uint64_t* sorted = depth_sorted(items0, items1, dstats) + base;
+    const uint32_t* srect = depth_sorted_rects(pay0, pay1, dstats) + base;
     // thread t owns sources 4t .. 4t+3 of a sub-chunk (source order): packed rect, index
     // and (by index) tile row spans; the first sub-chunk's (usually the only one) are
     // loaded before the base scan, so the dependent spans gather overlaps it (loading
@@ -1766,8 +1775,10 @@ __device__ __forceinline__ uint32_t col_chunk_row(const ColPlan<PB>& pl, uint32_
 __global__ __launch_bounds__(256) void k_bin_cols_count(const uint64_t* __restrict__ rows_in,
                                                          const uint32_t* __restrict__ row_items,
                                                          const unsigned long long* __restrict__ row_pairs,
-                                                         uint32_t cap, int tiles_x, uint32_t* __restrict__ cbins) {
+                                                         uint32_t cap, int tiles_x, uint32_t* __restrict__ cbins,
+                                                         const uint32_t* __restrict__ gate) {
     GSR_GEOM_PRIO();
+    if (gate && *gate == 0u) return;
     __shared__ ColPlan<false> pl;
     __shared__ uint32_t h[4][256], s_scr[4];
     __shared__ unsigned long long s_scr64[4];
@@ -1812,8 +1823,9 @@ __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restric
                                                         uint32_t cap, int tiles_x, uint32_t* __restrict__ cbins,
                                                         uint2* __restrict__ ranges, Stats* __restrict__ st,
                                                         Stats* host_st, const uint32_t* __restrict__ dstats,
-                                                        int passes_launched) {
+                                                        int passes_launched, const uint32_t* __restrict__ gate) {
     GSR_GEOM_PRIO();
+    if (gate && *gate == 0u) return;
     __shared__ ColPlan<true> pl;
     __shared__ uint32_t s_scr[4];
     __shared__ unsigned long long s_scr64[4];
@@ -1857,8 +1869,10 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
                                                            uint32_t cap, int tiles_x,
                                                            const uint32_t* __restrict__ cbins,
                                                            const uint2* __restrict__ ranges,
-                                                           uint32_t* __restrict__ vals) {
+                                                           uint32_t* __restrict__ vals,
+                                                           const uint32_t* __restrict__ gate) {
     GSR_GEOM_PRIO();
+    if (gate && *gate == 0u) return;
     constexpr uint32_t kTile = 256u * ITEMS;
     __shared__ ColPlan<false> pl;
     __shared__ uint32_t s_pref[kColChunk], s_idx[kColChunk];
@@ -2199,12 +2213,23 @@ __device__ __forceinline__ uint32_t take_mix(uint32_t g) { return (g + 1u) * 265
 // batch holding a record without the fast proof aborts the fast pass (all ones, no
 // pixel written).  Every pixel therefore composites exactly the splats the exact
 // blend composites, in the same order.
-template <bool DIAG, bool FX>
+//
+// SPLIT (depth split, exact blend only): 1 = phase A, which composites the block's
+// phase-A list and, when some pixel is still unsaturated at its end, saves every
+// pixel's T in tsave (64 floats), sets *flag and counts the block in *gate (else
+// clears *flag); 2 = phase B, which resumes such a block from the saved T and the
+// colours phase A wrote (and, with DIAG, the take map).  Each pixel composites the
+// same splats in the same order as over the whole list (the phase-A list is the
+// nearest part of it, the phase-B list the rest), with the same operations.
+template <bool DIAG, bool FX, int SPLIT>
 __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx, const uint4* __restrict__ rec,
                                                 uint32_t beg, uint32_t end, int bx, int by, int lane, int W,
                                                 int H, int cover_w, int cover_h, float* __restrict__ out,
                                                 float* wP, BlendDiag& dg, uint64_t* __restrict__ tmap,
-                                                float band0, uint64_t only) {
+                                                float band0, uint64_t only, float* __restrict__ tsave = nullptr,
+                                                uint8_t* __restrict__ flag = nullptr,
+                                                uint32_t* __restrict__ gate = nullptr) {
+    static_assert(SPLIT == 0 || !FX, "the depth split runs the exact blend");
     constexpr int kSlot = FX ? 24 : 20;                     // dwords per pair slot
     const int px = bx + (lane & 7), py = by + (lane >> 3);
     const bool inside = px < cover_w && py < cover_h;
@@ -2221,6 +2246,19 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
     uint32_t ntk = 0;          // FX: splats this pixel composited so far
     f2 amax = (f2)0.0f;        // FX: largest alpha it composited (two halves)
     uint32_t tcount = 0, thash = 0;   // DIAG take map
+    if (SPLIT == 2 && inside) {
+        // inside => px < W and py < H (cover_w <= W, cover_h <= H)
+        const size_t o = (size_t)py * (size_t)W + (size_t)px, hw = (size_t)W * (size_t)H;
+        T = tsave[lane];
+        crg.x = out[o];
+        crg.y = out[hw + o];
+        cb = out[2 * hw + o];
+        if (DIAG && tmap) {
+            const uint64_t tm = tmap[o];
+            tcount = (uint32_t)tm;
+            thash = (uint32_t)(tm >> 32);
+        }
+    }
 
     uint4 ra = make_uint4(0, 0, 0, 0), rb = ra, rc = ra, rd = ra;
     uint32_t nidx = 0, cidx = 0;
@@ -2479,6 +2517,14 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
         const float B = fx_band(band0, ntk, fmaxf(amax.x, amax.y));
         suspect |= __ballot(!(T < 1e-3f) && T < 1e-3f * (1.0f + B));
     }
+    if (SPLIT == 1) {
+        const bool unsat = __ballot(!(T < 1e-3f)) != 0ull;
+        if (unsat) tsave[lane] = T;
+        if (lane == 0) {
+            *flag = unsat ? 1u : 0u;
+            if (unsat) atomicAdd(gate, 1u);
+        }
+    }
     // FX: every pixel but the suspect ones; exact: the pixels of `only`
     const bool write = FX ? ((suspect >> lane) & 1ull) == 0ull : mine;
     if (write && px < W && py < H) {
@@ -2506,17 +2552,28 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
 // s_memrealtime clock (100 MHz), counters[2 * g + 1] = duration (40 bits) |
 // placement << 40 (XCC id and HW_ID's SE / SH / CU / SIMD / slot).
 // DIAG: counters[0..9], then the take map (one u64 per pixel) from counters + 16.
-template <bool DIAG, bool STAMPS, bool FX>
+// SPLIT: the depth split's phase A (1) or B (2), blend_block; phase B's workgroup 0
+// publishes the count of blocks phase A left unsaturated (sp.host_st), and every
+// workgroup returns at once when that count is 0 or its own block is saturated.
+template <bool DIAG, bool STAMPS, bool FX, int SPLIT>
 __global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx,
                                                  const uint2* __restrict__ ranges,
                                                  const uint4* __restrict__ rec, int tiles_x, int tiles_y,
                                                  int W, int H, int cover_w, int cover_h,
                                                  float* __restrict__ out,
                                                  unsigned long long* __restrict__ counters, int bands,
-                                                 float band0) {
+                                                 float band0, BlendSplit sp) {
     __shared__ float4 sP[32 * (FX ? 24 : 20) / 4];
     const int ntiles = tiles_x * tiles_y;
     const int vb = (int)blockIdx.x;
+    if (SPLIT == 2) {
+        const uint32_t g = *sp.gate;   // uniform
+        if (vb == 0 && threadIdx.x == 0 && sp.host_st) {
+            sp.host_st->split_unsat = g;
+            __threadfence_system();
+        }
+        if (g == 0u) return;
+    }
     int L;
     if (bands > 1) {
         const int nu = 4 * ntiles;
@@ -2528,6 +2585,7 @@ __global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx
         if (vb >= ntiles * 4) return;
         L = xcd_remap(vb, ntiles * 4);
     }
+    if (SPLIT == 2 && sp.bflag[L] == 0u) return;   // saturated in phase A: its pixels are final
     const int tile = L >> 2, sub = L & 3;
     const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int lane = (int)(threadIdx.x & 63u);
@@ -2545,8 +2603,10 @@ __global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx
     const int bx = tx * GSR_TILE_PX + (sub & 1) * 8, by = ty * GSR_TILE_PX + (sub >> 1) * 8;
     uint64_t* tmap = DIAG ? reinterpret_cast<uint64_t*>(counters + 16) : nullptr;
     BlendDiag dg;
-    const uint64_t redo = blend_block<DIAG, FX>(idx, rec, beg, rr.y, bx, by, lane, W, H, cover_w, cover_h, out,
-                                                reinterpret_cast<float*>(sP), dg, tmap, band0, ~0ull);
+    const uint64_t redo = blend_block<DIAG, FX, SPLIT>(idx, rec, beg, rr.y, bx, by, lane, W, H, cover_w, cover_h,
+                                                       out, reinterpret_cast<float*>(sP), dg, tmap, band0, ~0ull,
+                                                       SPLIT ? sp.tbuf + 64 * (size_t)L : nullptr,
+                                                       SPLIT ? sp.bflag + L : nullptr, sp.gate);
     if (FX && redo) {
         if (DIAG && lane == 0) {
             atomicAdd(counters + 8, 1ull);
@@ -2555,7 +2615,7 @@ __global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx
         // only the suspect pixels (all of them after an aborted fast pass): the others
         // start saturated, so the cull drops every record that misses the suspects
         // and the wave stops once they saturate
-        blend_block<DIAG, false>(idx, rec, beg, rr.y, bx, by, lane, W, H, cover_w, cover_h, out,
+        blend_block<DIAG, false, 0>(idx, rec, beg, rr.y, bx, by, lane, W, H, cover_w, cover_h, out,
                                  reinterpret_cast<float*>(sP), dg, tmap, 0.0f, redo);
     }
     if (STAMPS && lane == 0)
@@ -2828,13 +2888,16 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
                            const uint32_t* pay0, const uint32_t* pay1, int groups, uint32_t* hist,
                            uint32_t* row_items,
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
-                           int items, hipStream_t s, const uint16_t* spans, bool rank_atomic) {
+                           int items, hipStream_t s, const uint16_t* spans, bool rank_atomic, uint32_t base,
+                           uint32_t* gate, int gate_mode) {
     if (tiles_y < 1 || tiles_y > 256 || groups < 1 || groups > kMaxSortGroups / 2 ||
-        (items != 4 && items != 8 && items != 16))
+        (items != 4 && items != 8 && items != 16) || (gate_mode != 0 && !gate) || gate_mode < 0 || gate_mode > 2)
         return hipErrorInvalidValue;
+    const uint32_t* g = gate_mode == 2 ? gate : nullptr;
     hipLaunchKernelGGL(k_bin_rows_count, dim3(groups), dim3(256), 0, s, n, pay0, pay1, dstats, groups, tiles_y,
-                       hist);
-    hipLaunchKernelGGL(k_bin_rows_scan, dim3(256), dim3(256), 0, s, hist, groups, tiles_y, row_items, row_pairs);
+                       hist, base, g);
+    hipLaunchKernelGGL(k_bin_rows_scan, dim3(256), dim3(256), 0, s, hist, groups, tiles_y, row_items, row_pairs,
+                       gate, gate_mode);
     auto pick = [&](auto ra) {
         constexpr bool RA = decltype(ra)::value;
         return tiles_y <= 128 ? (items == 4 ? k_bin_rows_scatter<4, 7, RA> : items == 8 ? k_bin_rows_scatter<8, 7, RA>
@@ -2844,21 +2907,22 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
     };
     auto scatter = rank_atomic ? pick(std::true_type{}) : pick(std::false_type{});
     hipLaunchKernelGGL(scatter, dim3(groups), dim3(256), 0, s, items0, items1, dstats, pay0, pay1, n, groups, hist,
-                       row_items, row_pairs, pair_capacity, tiles_y, rows_buf, spans);
+                       row_items, row_pairs, pair_capacity, tiles_y, rows_buf, spans, base, g);
     return hipGetLastError();
 }
 
 hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, const unsigned long long* row_pairs,
                            uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
                            uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,
-                           hipStream_t s, const uint32_t* dstats, int passes_launched, bool rank_atomic) {
+                           hipStream_t s, const uint32_t* dstats, int passes_launched, bool rank_atomic,
+                           const uint32_t* gate) {
     if (tiles_x < 1 || tiles_x > 256 || tiles_y < 1 || tiles_y > 256 || col_groups < 1 ||
         (items != 4 && items != 8 && items != 16))
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_bin_cols_count, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs,
-                       pair_capacity, tiles_x, cbins);
+                       pair_capacity, tiles_x, cbins, gate);
     hipLaunchKernelGGL(k_bin_cols_scan, dim3(tiles_y), dim3(256), 0, s, row_items, row_pairs, pair_capacity, tiles_x,
-                       cbins, ranges, stats, host_mapped_stats, dstats, passes_launched);
+                       cbins, ranges, stats, host_mapped_stats, dstats, passes_launched, gate);
     auto pick = [&](auto ra) {
         constexpr bool RA = decltype(ra)::value;
         return tiles_x <= 128 ? (items == 4 ? k_bin_cols_scatter<4, 7, RA> : items == 8 ? k_bin_cols_scatter<8, 7, RA>
@@ -2868,7 +2932,7 @@ hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, 
     };
     auto scatter = rank_atomic ? pick(std::true_type{}) : pick(std::false_type{});
     hipLaunchKernelGGL(scatter, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs, pair_capacity,
-                       tiles_x, cbins, ranges, vals);
+                       tiles_x, cbins, ranges, vals, gate);
     return hipGetLastError();
 }
 
@@ -2910,7 +2974,7 @@ hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* ke
 
 hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,
                         float* out, unsigned long long* consumed, bool stamps, int band_tiles, int blend_exp,
-                        hipStream_t s) {
+                        hipStream_t s, const BlendSplit* split) {
     // blend_exp 2 (test hook): the fast blend with a band of 100 %, so every block in
     // which a pixel saturates (or ends below 2e-3) is blended again exactly
     const bool fast_exp = blend_exp != 0;
@@ -2925,10 +2989,23 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
         bands = (nt + 8 * band_tiles - 1) / (8 * band_tiles);          // bands per XCD
         ng = 8 * bands * ((4 * nt + 8 * bands - 1) / (8 * bands));
     }
-#define GSR_BLEND(D, ST, FX)                                                                                \
-    hipLaunchKernelGGL((k_blend_w<D, ST, FX>), dim3(ng), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x, fr.tiles_y, \
-                       fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, bands, band0)
-    if (stamps && consumed) {
+    const int phase = split ? split->phase : 0;
+    if (phase < 0 || phase > 2 || (phase && (fast_exp || stamps || !split->tbuf || !split->bflag || !split->gate)))
+        return hipErrorInvalidValue;
+    const BlendSplit sp = split ? *split : BlendSplit{0, nullptr, nullptr, nullptr, nullptr};
+#define GSR_BLEND_S(D, ST, FX, SP)                                                                          \
+    hipLaunchKernelGGL((k_blend_w<D, ST, FX, SP>), dim3(ng), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,  \
+                       fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, bands, band0, sp)
+#define GSR_BLEND(D, ST, FX) GSR_BLEND_S(D, ST, FX, 0)
+    if (phase) {
+        if (consumed) {
+            if (phase == 1) GSR_BLEND_S(true, false, false, 1);
+            else GSR_BLEND_S(true, false, false, 2);
+        } else {
+            if (phase == 1) GSR_BLEND_S(false, false, false, 1);
+            else GSR_BLEND_S(false, false, false, 2);
+        }
+    } else if (stamps && consumed) {
         if (fast_exp) GSR_BLEND(false, true, true);
         else GSR_BLEND(false, true, false);
     } else if (consumed) {
@@ -2939,6 +3016,7 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
         else GSR_BLEND(false, false, false);
     }
 #undef GSR_BLEND
+#undef GSR_BLEND_S
     return hipGetLastError();
 }
 

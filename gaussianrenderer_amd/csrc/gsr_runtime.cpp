@@ -381,6 +381,18 @@ struct gsr_context {
     bool last_binned = false;        // the last sorted frame took the binning path
     int blend_exp = 0;               // blend: 0 = gsr_expf (bit-exact); 1 = fast exp with exact alpha
                                      // tests and guarded T tests (re-blends what it cannot vouch for)
+    int depth_split = 2;             // GSR_TUNE_DEPTH_SPLIT: 0 off, 1 on, 2 on above kLargeScene Gaussians
+    int split_pm = 250;              // split point: phase A bins the nearest split_pm / 1000 of the depth order
+    int split_floor = 0;             // 5/4 of the last split point that left blocks unsaturated
+    int split_clean = 0;             // checked split frames in a row that left none
+    bool split_frame = false;        // the sorted frame is split (phase A lists binned by sort_locked)
+    bool split_rebin = false;        // phase B's lists replaced phase A's: a repeated blend bins phase A again
+    bool split_seen = false;         // a split frame was blended since the last controller update
+    uint32_t split_na = 0;           // phase A's depth-order prefix
+    float* tbuf = nullptr;           // depth split: saved transmittance, 64 floats per 8x8 block
+    uint8_t* bflag = nullptr;        // depth split: per block, left unsaturated by phase A
+    uint32_t* gate = nullptr;        // depth split: count of such blocks (device word)
+    int64_t split_cap = 0;           // blocks tbuf / bflag hold
     int blend_band_tiles = 4;        // blend: tiles per spatial band, bands dealt round-robin to the
                                      // XCDs (0: one contiguous band per XCD)
     int completion_events = 1;       // 0: no completion event / overflow query (stream capture)
@@ -421,6 +433,11 @@ struct gsr_context {
 };
 
 namespace {
+
+// Scenes above this many Gaussians: tile row spans off (their by-index code gather
+// leaves the L2), the depth split on (GSR_TUNE_TILE_SPANS / GSR_TUNE_DEPTH_SPLIT = 2).
+constexpr int64_t kLargeScene = 3 << 19;
+constexpr int kSplitMinPm = 20;       // smallest split point (per mille)
 
 int groups_for(int64_t n, int64_t per) {
     int64_t g = (n + per - 1) / per;
@@ -485,6 +502,7 @@ int ensure_static(gsr_context* c) {
     if (int rc = realloc_dev(&c->dstats, 4 + 4 * (size_t)gsr::kMaxSortGroups)) return rc;
     if (int rc = realloc_dev(&c->nlive, 1)) return rc;
     if (int rc = realloc_dev(&c->binmeta, 256 + 128)) return rc;
+    if (int rc = realloc_dev(&c->gate, 1)) return rc;
     HIP_TRY(hipMemset(c->stats, 0, 2 * sizeof(Stats)));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->hstats), sizeof(Stats), hipHostMallocMapped));
     std::memset(c->hstats, 0, sizeof(Stats));
@@ -531,6 +549,17 @@ int ensure_tiles(gsr_context* c, int64_t t) {
     return GSR_OK;
 }
 
+// Depth split buffers for the current tile grid (4 blocks per tile).
+int ensure_split(gsr_context* c) {
+    const int64_t blocks = 4 * (int64_t)c->ntiles;
+    if (blocks <= c->split_cap) return GSR_OK;
+    HIP_TRY(hipDeviceSynchronize());
+    if (int rc = realloc_dev(&c->tbuf, 64 * (size_t)blocks)) return rc;
+    if (int rc = realloc_dev(&c->bflag, (size_t)blocks)) return rc;
+    c->split_cap = blocks;
+    return GSR_OK;
+}
+
 int ensure_soa(gsr_context* c, int64_t n) {
     const int64_t need = (int64_t)GSR_SCENE_NARRAYS * scene_stride(n);
     if (need <= c->soa_cap) return GSR_OK;
@@ -554,7 +583,8 @@ hipEvent_t get_event(gsr_context* c) {
 // Record the boundary event that opens stage `stage` (stage == GSR_NUM_STAGES closes the frame).
 void mark(gsr_context* c, int stage) {
     if (!c->timing || !c->timing_now) return;
-    const bool want = (c->timing == 2) || stage == GSR_STAGE_BLEND || stage == GSR_NUM_STAGES;
+    const bool want = (c->timing == 2) || stage == GSR_STAGE_BLEND || stage == GSR_STAGE_RESUME ||
+                      stage == GSR_NUM_STAGES;
     if (!want) return;
     hipEvent_t e = get_event(c);
     if (!e) return;
@@ -580,6 +610,20 @@ int check_overflow(gsr_context* c, bool blocking) {
     s.pairs_eff = hv->pairs_eff;
     s.overflow = hv->overflow;
     s.depth_passes = hv->depth_passes;
+    if (!s.overflow && c->split_seen) {
+        // depth split point: up by half when phase A left blocks unsaturated (phase B
+        // ran), down by an eighth after 8 checked frames in a row that needed no phase B,
+        // never below 5/4 of the last point that needed it
+        c->split_seen = false;
+        if (hv->split_unsat > 0) {
+            c->split_floor = std::min(1000, c->split_pm * 5 / 4 + 1);
+            c->split_pm = std::min(1000, c->split_pm * 3 / 2 + 1);
+            c->split_clean = 0;
+        } else if (++c->split_clean >= 8) {
+            c->split_clean = 0;
+            c->split_pm = std::max(std::max(kSplitMinPm, c->split_floor), c->split_pm * 7 / 8);
+        }
+    }
     if (!s.overflow) {
         // lower the pass budget once 4 checked frames in a row needed fewer passes
         if (s.depth_passes >= 1 && (int)s.depth_passes < c->depth_budget) {
@@ -670,7 +714,8 @@ extern "C" void gsr_destroy(gsr_context* c) {
     for (auto* p : {(void*)c->rec, (void*)c->items[0], (void*)c->items[1], (void*)c->rect, (void*)c->pairs[0],
                     (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->dstats,
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
-                    (void*)c->cbins, (void*)c->srect, (void*)c->spans, (void*)c->nlive})
+                    (void*)c->cbins, (void*)c->srect, (void*)c->spans, (void*)c->nlive, (void*)c->tbuf,
+                    (void*)c->bflag, (void*)c->gate})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -731,8 +776,7 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     // Gaussians the codes (<= 3 MB) stay in an XCD's 4-MB L2 and the gather is cheap:
     // config 2 (1M) +0.8 % one frame at a time, +1.2 % in flight; config 5 (2M) -1 % in
     // flight, config 3 (5M) -3 / -6 % (profiles/r02_ab_tile_spans.txt)
-    constexpr int64_t kSpansAutoMax = 3 << 19;
-    c->spans_frame = c->rect_packed && (c->tile_spans == 1 || (c->tile_spans == 2 && n <= kSpansAutoMax));
+    c->spans_frame = c->rect_packed && (c->tile_spans == 1 || (c->tile_spans == 2 && n <= kLargeScene));
     HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[c->compact_frame ? 1 : 0], c->rect,
                                    c->rect_packed, layout == GSR_LAYOUT_SCENE_BLOCK_4D,
                                    layout == GSR_LAYOUT_SCENE_BLOCK_SH3, c->time, c->stream,
@@ -805,7 +849,38 @@ static int depth_sort_locked(gsr_context* c, bool with_rects) {
     return GSR_OK;
 }
 
-static int sort_locked(gsr_context* c) {
+// Row pass, then column pass (gsr_kernels.hip "tile binning") over the depth-order
+// positions [base, base + count): tile lists in pair_vals(c, 1), ranges.  gate_mode:
+// 0 plain; 1 = depth split phase A (clears the gate); 2 = phase B (every kernel returns
+// at once when the gate is 0).
+static int bin_locked(gsr_context* c, uint32_t base, uint32_t count, int gate_mode, bool marks) {
+    const uint32_t cap = (uint32_t)c->p_cap;
+    if (int rc = ensure_cbins(c)) return rc;
+    auto* row_pairs = reinterpret_cast<unsigned long long*>(c->binmeta);
+    auto* row_items = reinterpret_cast<uint32_t*>(c->binmeta + 256);
+    const int gb = std::min(groups_for(count, 1024), gsr::kMaxSortGroups / 2);
+    HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, count, pay_buf(c, 0),
+                                 pay_buf(c, 1), gb,
+                                 c->hist, row_items, row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items,
+                                 c->stream, c->spans_frame ? c->spans : nullptr, rank_atomic_on(c), base,
+                                 gate_mode ? c->gate : nullptr, gate_mode));
+    if (marks) mark(c, GSR_STAGE_TILE_SORT);
+    // column-pass workgroups: ~one 2048-item chunk each (config 3: 2048-4096 groups 12 us
+    // faster than 1024; config 2: 1024 best, profiles/r02_ab_col_groups.txt)
+    const int gcol = c->bin_col_groups ? c->bin_col_groups
+                                       : (int)std::min<int64_t>(4096, std::max<int64_t>(1024, c->n / 1024));
+    HIP_TRY(gsr::launch_bin_cols(c->pairs[0], row_items, row_pairs, c->cbins, gcol, cap,
+                                 c->fr.tiles_x, c->fr.tiles_y, pair_vals(c, 1), c->ranges, c->stats,
+                                 c->hstats_dev, c->bin_col_items, c->stream,
+                                 c->depth_skip ? c->dstats : nullptr, c->passes_launched, rank_atomic_on(c),
+                                 gate_mode == 2 ? c->gate : nullptr));
+    c->pair_buf = 1;
+    return GSR_OK;
+}
+
+// allow_split: the caller blends right after (gsr_render, gsr_render_path), so the
+// depth split may apply (the stage API gsr_sort / gsr_blend keeps one phase).
+static int sort_locked(gsr_context* c, bool allow_split) {
     if (!c->have_pre) return set_err(GSR_E_ARG, "gsr_sort before gsr_preprocess");
     const uint32_t n = (uint32_t)c->n;
     const bool bin = c->rect_packed;   // the path gsr_preprocess chose (its rect format)
@@ -820,27 +895,23 @@ static int sort_locked(gsr_context* c) {
     if (int rc = depth_sort_locked(c, bin)) return rc;
     // result in items[passes run & 1] (device-side plan; emission picks it)
     if (bin) {
-        // ---- row pass, then column pass (gsr_kernels.hip "tile binning") ----
-        const uint32_t cap = (uint32_t)c->p_cap;
-        if (int rc = ensure_cbins(c)) return rc;
-        auto* row_pairs = reinterpret_cast<unsigned long long*>(c->binmeta);
-        auto* row_items = reinterpret_cast<uint32_t*>(c->binmeta + 256);
-        const int gb = std::min(groups_for(c->n, 1024), gsr::kMaxSortGroups / 2);
+        // depth split: phase A bins the nearest split_pm / 1000 of the depth order
+        // (blend_locked blends it, then bins and blends the rest where needed)
+        c->split_frame = false;
+        c->split_rebin = false;
+        uint32_t count = n;
+        if (allow_split && n > 0 && c->blend_exp == 0 && c->blend_variant != 3 && c->split_pm < 1000 &&
+            (c->depth_split == 1 || (c->depth_split == 2 && c->n > kLargeScene))) {
+            const uint32_t na = (uint32_t)std::max<int64_t>(1, ((int64_t)n * c->split_pm + 999) / 1000);
+            if (na < n) {
+                if (int rc = ensure_split(c)) return rc;
+                c->split_frame = true;
+                c->split_na = na;
+                count = na;
+            }
+        }
         mark(c, GSR_STAGE_EMIT);
-        HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n, pay_buf(c, 0),
-                                     pay_buf(c, 1), gb,
-                                     c->hist, row_items, row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items,
-                                     c->stream, c->spans_frame ? c->spans : nullptr, rank_atomic_on(c)));
-        mark(c, GSR_STAGE_TILE_SORT);
-        // column-pass workgroups: ~one 2048-item chunk each (config 3: 2048-4096 groups 12 us
-        // faster than 1024; config 2: 1024 best, profiles/r02_ab_col_groups.txt)
-        const int gcol = c->bin_col_groups ? c->bin_col_groups
-                                           : (int)std::min<int64_t>(4096, std::max<int64_t>(1024, c->n / 1024));
-        HIP_TRY(gsr::launch_bin_cols(c->pairs[0], row_items, row_pairs, c->cbins, gcol, cap,
-                                     c->fr.tiles_x, c->fr.tiles_y, pair_vals(c, 1), c->ranges, c->stats,
-                                     c->hstats_dev, c->bin_col_items, c->stream,
-                                     c->depth_skip ? c->dstats : nullptr, c->passes_launched, rank_atomic_on(c)));
-        c->pair_buf = 1;
+        if (int rc = bin_locked(c, 0, count, c->split_frame ? 1 : 0, true)) return rc;
         mark(c, GSR_STAGE_RANGES);
         c->have_sort = true;
         return GSR_OK;
@@ -891,9 +962,40 @@ static int blend_locked(gsr_context* c, float* d_out) {
         }
         HIP_TRY(hipMemsetAsync(c->consumed, 0, (size_t)need * sizeof(unsigned long long), c->stream));
     }
-    HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
-                              c->diagnostics ? c->consumed : nullptr, c->blend_variant == 3,
-                              c->blend_band_tiles, c->blend_exp, c->stream));
+    if (c->split_frame) {
+        // depth split: blend phase A (saving the blocks it leaves unsaturated), bin the
+        // rest of the depth order, resume those blocks; phase B's kernels return at once
+        // on the device when phase A saturated every block
+        if (c->split_rebin && c->blend_exp == 0 && c->blend_variant != 3) {
+            if (int rc = bin_locked(c, 0, c->split_na, 1, false)) return rc;
+        }
+        if (c->blend_exp == 0 && c->blend_variant != 3) {
+            const uint32_t n = (uint32_t)c->n;
+            gsr::BlendSplit a{1, c->tbuf, c->bflag, c->gate, nullptr};
+            HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
+                                      c->diagnostics ? c->consumed : nullptr, false, c->blend_band_tiles, 0,
+                                      c->stream, &a));
+            mark(c, GSR_STAGE_RESUME);
+            if (int rc = bin_locked(c, c->split_na, n - c->split_na, 2, false)) return rc;
+            gsr::BlendSplit b{2, c->tbuf, c->bflag, c->gate, c->hstats_dev};
+            HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
+                                      c->diagnostics ? c->consumed : nullptr, false, c->blend_band_tiles, 0,
+                                      c->stream, &b));
+            c->split_rebin = true;
+            c->split_seen = true;
+        } else {
+            // knobs changed since the sort: bin the whole depth order again, one phase
+            if (int rc = bin_locked(c, 0, (uint32_t)c->n, 0, false)) return rc;
+            c->split_frame = false;
+            HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
+                                      c->diagnostics ? c->consumed : nullptr, c->blend_variant == 3,
+                                      c->blend_band_tiles, c->blend_exp, c->stream));
+        }
+    } else {
+        HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
+                                  c->diagnostics ? c->consumed : nullptr, c->blend_variant == 3,
+                                  c->blend_band_tiles, c->blend_exp, c->stream));
+    }
     mark(c, GSR_NUM_STAGES);
     if (c->timing && c->timing_now) c->ev_frames.push_back(c->cur);
     c->cur = FrameEvents{};
@@ -919,7 +1021,7 @@ extern "C" int gsr_sort(gsr_context* c, void* stream) {
     if (!c) return set_err(GSR_E_ARG, "null context");
     std::lock_guard<std::mutex> lk(c->mu);
     c->stream = static_cast<hipStream_t>(stream);
-    return sort_locked(c);
+    return sort_locked(c, false);
 }
 
 extern "C" int gsr_blend(gsr_context* c, float* d_out, void* stream) {
@@ -935,7 +1037,7 @@ extern "C" int gsr_render(gsr_context* c, const void* scene, int layout, int64_t
     std::lock_guard<std::mutex> lk(c->mu);
     int rc = preprocess_locked(c, scene, layout, n, cam, W, H, nx, ny, ws, hs, k, stream);
     if (rc != GSR_OK && rc != GSR_E_OVERFLOW) return rc;
-    if (int r2 = sort_locked(c)) return r2;
+    if (int r2 = sort_locked(c, true)) return r2;
     if (int r3 = blend_locked(c, d_out)) return r3;
     return rc;
 }
@@ -960,6 +1062,10 @@ void copy_settings(gsr_context* d, const gsr_context* s) {
     d->bin_col_groups = s->bin_col_groups;
     d->blend_band_tiles = s->blend_band_tiles;
     d->blend_exp = s->blend_exp;
+    d->depth_split = s->depth_split;
+    // the split point adapts per lane; each call starts the lanes from lane 0's
+    d->split_pm = s->split_pm;
+    d->split_floor = s->split_floor;
     d->completion_events = s->completion_events;
     d->depth_compact = s->depth_compact;
     d->rank_atomic = s->rank_atomic;
@@ -996,7 +1102,7 @@ int render_one_locked(gsr_context* c, const void* scene, int layout, int64_t n, 
                       int H, int nx, int ny, int ws, int hs, float k, float* d_out, hipStream_t s) {
     int rc = preprocess_locked(c, scene, layout, n, cam, W, H, nx, ny, ws, hs, k, s);
     if (rc != GSR_OK && rc != GSR_E_OVERFLOW) return rc;
-    if (int r2 = sort_locked(c)) return r2;
+    if (int r2 = sort_locked(c, true)) return r2;
     if (int r3 = blend_locked(c, d_out)) return r3;
     return rc;
 }
@@ -1374,6 +1480,9 @@ extern "C" int gsr_get_tuning(gsr_context* c, int knob, int* value) {
     case GSR_TUNE_DEPTH_COMPACT: *value = c->depth_compact; break;
     case GSR_TUNE_TILE_SPANS: *value = c->tile_spans; break;
     case GSR_TUNE_BLEND_EXP: *value = c->blend_exp; break;
+    case GSR_TUNE_DEPTH_SPLIT: *value = c->depth_split; break;
+    case GSR_TUNE_DEPTH_SPLIT_PERMILLE: *value = c->split_pm; break;
+    case GSR_TUNE_DEPTH_SPLIT_UNSAT: *value = c->hstats ? (int)((const volatile Stats*)c->hstats)->split_unsat : 0; break;
     case GSR_TUNE_RANK_ATOMIC: *value = c->rank_atomic < 0 ? default_rank_atomic() : c->rank_atomic; break;
     case GSR_TUNE_RANK_ATOMIC_ACTIVE: {
         RankCheck rk;
@@ -1443,12 +1552,23 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         if (value < 0 || value > 2) return set_err(GSR_E_ARG, "gsr_set_tuning: blend exp must be 0, 1 or 2");
         c->blend_exp = value;
         return GSR_OK;
+    case GSR_TUNE_DEPTH_SPLIT:
+        if (value < 0 || value > 2) return set_err(GSR_E_ARG, "gsr_set_tuning: depth split must be 0, 1 or 2");
+        c->depth_split = value;
+        return GSR_OK;
+    case GSR_TUNE_DEPTH_SPLIT_PERMILLE:
+        if (value < 1 || value > 999) return set_err(GSR_E_ARG, "gsr_set_tuning: split point must be 1..999");
+        c->split_pm = value;
+        c->split_floor = 0;
+        c->split_clean = 0;
+        return GSR_OK;
     case GSR_TUNE_RANK_ATOMIC:
         if (value != 0 && value != 1) return set_err(GSR_E_ARG, "gsr_set_tuning: rank path must be 0 or 1");
         c->rank_atomic = value;
         return GSR_OK;
     case GSR_TUNE_RANK_ATOMIC_ACTIVE:
-        return set_err(GSR_E_ARG, "gsr_set_tuning: GSR_TUNE_RANK_ATOMIC_ACTIVE is read-only");
+    case GSR_TUNE_DEPTH_SPLIT_UNSAT:
+        return set_err(GSR_E_ARG, "gsr_set_tuning: knob %d is read-only", knob);
     case GSR_TUNE_TILE_SORT_GROUPS:
     case GSR_TUNE_DEPTH_SORT_GROUPS:
         if (value < 0 || value > gsr::kMaxSortGroups) return set_err(GSR_E_ARG, "gsr_set_tuning: bad group cap");

@@ -76,8 +76,10 @@ enum {
     GSR_STAGE_EMIT = 2,           /* pair emission, or the binning row pass */
     GSR_STAGE_TILE_SORT = 3,      /* stable radix sort of pairs by tile, or the binning column pass */
     GSR_STAGE_RANGES = 4,         /* per-tile [start, end) from sorted pairs */
-    GSR_STAGE_BLEND = 5,          /* front-to-back alpha compositing */
-    GSR_NUM_STAGES = 6
+    GSR_STAGE_BLEND = 5,          /* front-to-back alpha compositing (with the depth split: phase A's) */
+    GSR_STAGE_RESUME = 6,         /* depth split phase B: binning the rest of the depth order and
+                                     resuming the blocks phase A left unsaturated (0 on other frames) */
+    GSR_NUM_STAGES = 7
 };
 
 #define GSR_TILE_PX 16            /* internal tile edge (pixels); output is tile-invariant */
@@ -307,7 +309,7 @@ enum {
                                         the default.  Same order, same image */
     GSR_TUNE_RANK_ATOMIC_ACTIVE = 21, /* read-only: 1 if the atomic ranks are in use (knob 20 at 1 and the
                                         self-check passed), 0 if the kernels rank with ballots */
-    GSR_TUNE_BLEND_EXP = 22          /* blend exp: 0 (default) = gsr_expf throughout (bit-exact with the
+    GSR_TUNE_BLEND_EXP = 22,         /* blend exp: 0 (default) = gsr_expf throughout (bit-exact with the
                                         oracle).  1 (environment GSR_BLEND_EXP=1 selects it) = hardware
                                         exp for alpha, with the alpha test exact on the exp argument and
                                         the transmittance test guarded by a proven band; suspect pixels
@@ -315,6 +317,19 @@ enum {
                                         blend, identical take map; measured slower on config 2.
                                         2 = test hook: 1 with a 100 % guard band, so every block
                                         in which a pixel saturates is blended again exactly. */
+    GSR_TUNE_DEPTH_SPLIT = 23,       /* binning path, exact blend, gsr_render / gsr_render_path: 1 = bin
+                                        the nearest part of the depth order first and blend it (phase
+                                        A), then bin the rest and resume only the 8x8 blocks phase A
+                                        left unsaturated (phase B, skipped on the device when there are
+                                        none); the split point adapts to the frames seen.  0 = one phase;
+                                        2 (default) = 1 above 1.5M Gaussians.  Same image.  After a split
+                                        frame gsr_read_pairs / gsr_read_tile_ranges hold the lists of its
+                                        last phase */
+    GSR_TUNE_DEPTH_SPLIT_PERMILLE = 24, /* the current split point: phase A bins the nearest
+                                        ceil(n * value / 1000) of the depth order (adapted per frame; a
+                                        set value is a new starting point, 1..999) */
+    GSR_TUNE_DEPTH_SPLIT_UNSAT = 25  /* read-only: 8x8 blocks the last completed split frame's phase A
+                                        left unsaturated (0: its phase B did nothing); read after gsr_sync */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Current value of a knob (what gsr_set_tuning last set, else the default). */

@@ -1,0 +1,220 @@
+"""Depth split (GSR_TUNE_DEPTH_SPLIT) against the oracle.
+
+Phase A bins only the nearest part of the depth order and blends it; a block whose
+pixels are not all saturated at the end of its phase-A list saves its transmittance.
+Phase B bins the rest of the depth order and resumes those blocks from the saved
+transmittance and the colours phase A wrote.  The reference blend walks each tile's
+depth-ordered list front to back and stops a pixel at T < 1e-3 (render.cu:323-341), so
+a pixel composites the same splats in the same order with the same operations either
+way: images are bit-exact against the oracle and the per-pixel take maps (which splats
+each pixel composited) equal the oracle's.  The split points below cover phase B doing
+nothing (config 3: every block saturates within the nearest ~10 % of the visible
+splats, tools/sim/depth_split.py), part of the work, and nearly all of it."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import assert_frames, exact_blend, scene_soa
+from test_gpu_parity import CAMS, cam_for, render_gpu
+
+pytestmark = pytest.mark.gpu
+
+KNOB_SPLIT, KNOB_PM, KNOB_UNSAT = 23, 24, 25
+ORC_THREADS = min(16, len(os.sched_getaffinity(0)))
+
+
+@pytest.fixture(scope="module")
+def torch(gpu):
+    import torch as t
+    assert t.cuda.is_available()
+    return t
+
+
+@pytest.fixture(scope="module")
+def c3(gpu, orc, tmp_path_factory):
+    path, soa = scene_soa(gpu, tmp_path_factory, 5_000_000, 3)
+    W, H = 1600, 1063
+    cam = cam_for(gpu, W, H)
+    want, takes = orc.render_takes(soa, cam, W, H, 3.0, threads=ORC_THREADS)
+    return gpu.Scene.from_ply(path), soa, cam, W, H, want, takes
+
+
+def split_renderer(gpu, split, pm=None):
+    r = exact_blend(gpu.Renderer())
+    r.set_tuning(KNOB_SPLIT, split)
+    if pm is not None:
+        r.set_tuning(KNOB_PM, pm)
+    return r
+
+
+def check_takes(gpu, torch, r, scene, cam, W, H, want, takes_want, **kw):
+    """Diagnostics render (the same kernels with counters and the take map): same image
+    as the plain render, take map equal to the oracle's.  Returns the counters."""
+    r.set_diagnostics(True)
+    img, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r, **kw)
+    takes = r.take_map(W, H)
+    counters = r.blend_counters_ex()
+    r.set_diagnostics(False)
+    assert_frames(img, want, exact=True)
+    bad = takes != takes_want
+    assert not bad.any(), (f"{int(bad.sum())} pixels composited other splats, e.g. "
+                           f"{np.argwhere(bad)[:3].tolist()}")
+    return counters
+
+
+def test_depth_split_knobs(gpu):
+    r = gpu.Renderer()
+    assert r.get_tuning(KNOB_SPLIT) == 2 and r.get_tuning(KNOB_PM) == 250
+    r.set_tuning(KNOB_PM, 40)
+    assert r.get_tuning(KNOB_PM) == 40
+    for bad in ((KNOB_SPLIT, 3), (KNOB_PM, 0), (KNOB_PM, 1000), (KNOB_UNSAT, 1)):
+        with pytest.raises(gpu.GsrError):
+            r.set_tuning(*bad)
+
+
+@pytest.mark.parametrize("pm", [20, 60, 250])
+def test_config3_split_points(gpu, orc, torch, c3, pm):
+    """Config 3 stand-in (5M Gaussians, 1600x1063).  At 2 % of the depth order phase A
+    leaves most blocks unsaturated and phase B does most of the work; at 6 % part of it;
+    at 25 % (the starting point) phase B does nothing.  Bit-exact with the oracle and the
+    same take maps in every case."""
+    scene, soa, cam, W, H, want, takes = c3
+    r = split_renderer(gpu, 1, pm)
+    img, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
+    unsat = r.get_tuning(KNOB_UNSAT)
+    nblocks = 4 * ((W + 15) // 16) * ((H + 15) // 16)
+    if pm == 20:
+        assert unsat > nblocks // 2
+    elif pm == 60:
+        assert 0 < unsat < nblocks
+    else:
+        assert unsat == 0
+    assert_frames(img, want, exact=True)
+    r.set_tuning(KNOB_PM, pm)
+    check_takes(gpu, torch, r, scene, cam, W, H, want, takes)
+    r.close()
+
+
+def test_config3_split_off_same_lists(gpu, orc, torch, c3):
+    """With the split off the tile lists are the whole depth order's; the default (on
+    for this size) renders the same image, and so does the stage API, which never
+    splits (gsr_sort lists every pair)."""
+    scene, soa, cam, W, H, want, _ = c3
+    r0 = split_renderer(gpu, 0)
+    img0, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r0)
+    assert_frames(img0, want, exact=True)
+    full = r0.read_pairs()
+    r1 = exact_blend(gpu.Renderer())
+    assert r1.get_tuning(KNOB_SPLIT) == 2
+    img1, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r1)
+    assert np.array_equal(img1.view(np.uint32), img0.view(np.uint32))
+    assert r1.get_tuning(KNOB_UNSAT) == 0
+    assert r1.read_pairs().size < full.size // 2           # phase A listed a prefix only
+    out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    for _ in range(3):     # the whole lists overflow the pair buffer sized by phase A's: grown, again
+        r1.preprocess(scene, cam, W, H)
+        r1.sort()
+        r1.blend(out.data_ptr())
+        if r1.sync() == 0:
+            break
+    assert np.array_equal(r1.read_pairs(), full)
+    assert np.array_equal(out.view(3, H, W).cpu().numpy().view(np.uint32), img0.view(np.uint32))
+    for r in (r0, r1):
+        r.close()
+
+
+def test_reblend_after_split_frame(gpu, orc, torch, c3):
+    """gsr_blend again after a split gsr_render (phase B's lists replaced phase A's):
+    the library bins phase A again, same image."""
+    scene, soa, cam, W, H, want, _ = c3
+    r = split_renderer(gpu, 1, 40)
+    img, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
+    assert r.get_tuning(KNOB_UNSAT) > 0
+    out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    r.blend(out.data_ptr())
+    assert r.sync() == 0
+    assert np.array_equal(out.view(3, H, W).cpu().numpy().view(np.uint32), img.view(np.uint32))
+    assert_frames(img, want, exact=True)
+    r.close()
+
+
+def test_split_point_adapts(gpu, orc, torch, c3):
+    """The split point grows by half after a frame whose phase B had work and shrinks by
+    an eighth after 8 checked frames in a row that had none (never below 5/4 of the last
+    point that needed phase B); every frame stays bit-exact."""
+    scene, soa, cam, W, H, want, _ = c3
+    r = split_renderer(gpu, 2, 20)
+    out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    r.render(scene, cam, W, H, out.data_ptr())
+    if r.sync() != 0:      # first frame: the pair buffer grew for phase B's lists
+        r.set_tuning(KNOB_PM, 20)
+        r.render(scene, cam, W, H, out.data_ptr())
+        assert r.sync() == 0
+    assert r.get_tuning(KNOB_UNSAT) > 0                     # gsr_sync checked the frame: 20 -> 31
+    assert r.get_tuning(KNOB_PM) == 31
+    r.set_tuning(KNOB_PM, 400)
+    for _ in range(20):
+        r.render(scene, cam, W, H, out.data_ptr())
+        assert r.sync() == 0
+    assert r.get_tuning(KNOB_PM) < 400
+    assert r.get_tuning(KNOB_UNSAT) == 0
+    assert_frames(out.view(3, H, W).cpu().numpy(), want, exact=True)
+    r.close()
+
+
+def test_config3_render_path_split(gpu, orc, torch, c3):
+    """Frames in flight (gsr_render_path, 4 lanes) with the split: each lane splits on
+    its own workspace; every frame bit-exact."""
+    scene, soa, cam, W, H, want, _ = c3
+    cam2 = cam_for(gpu, W, H, **CAMS[1])
+    want2 = orc.render(soa, cam2, W, H, 3.0, threads=ORC_THREADS)
+    r = split_renderer(gpu, 1, 60)
+    r.set_frames_in_flight(4)
+    cams = [cam, cam2] * 4
+    outs = [torch.empty(3 * W * H, dtype=torch.float32, device="cuda") for _ in cams]
+    for _ in range(3):
+        r.render_path(scene, cams, W, H, [o.data_ptr() for o in outs])
+        if r.sync() == 0:
+            break
+    for i, o in enumerate(outs):
+        assert_frames(o.view(3, H, W).cpu().numpy(), want if i % 2 == 0 else want2, exact=True)
+    r.close()
+
+
+def test_config2_split_with_unsaturated_background(gpu, orc, torch, tmp_path_factory):
+    """Config 2 (1M, 1080p): 13 % of its tiles never saturate, so phase B always has
+    blocks to resume whatever the split point.  Forced split at 30 %, bit-exact, same
+    take maps as the oracle."""
+    path, soa = scene_soa(gpu, tmp_path_factory, 1_000_000, 2)
+    W, H = 1920, 1080
+    cam = cam_for(gpu, W, H)
+    want, takes = orc.render_takes(soa, cam, W, H, 3.0, threads=ORC_THREADS)
+    scene = gpu.Scene.from_ply(path)
+    r = split_renderer(gpu, 1, 300)
+    img, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
+    assert r.get_tuning(KNOB_UNSAT) > 0
+    assert_frames(img, want, exact=True)
+    r.set_tuning(KNOB_PM, 300)
+    check_takes(gpu, torch, r, scene, cam, W, H, want, takes)
+    r.close()
+
+
+@pytest.mark.parametrize("ci", range(len(CAMS)))
+def test_split_odd_sizes_partial_tiling(gpu, orc, torch, tmp_path_factory, ci):
+    """Odd image size, a tiling that covers only part of it (pixels outside stay 0), four
+    cameras, split points 5 % and 50 %: bit-exact and the oracle's take maps."""
+    path, soa = scene_soa(gpu, tmp_path_factory, 200_000, 7)
+    W, H = 333, 197
+    t = gpu.TilingInformation(1, 1, H, W)
+    t.num_tile_x, t.num_tile_y, t.width_stride, t.height_stride = (4, 3, 70, 50)   # 280 x 150 of 333 x 197
+    cam = cam_for(gpu, W, H, **CAMS[ci])
+    scene = gpu.Scene.from_soa(soa)
+    want, takes = orc.render_takes(soa, cam, W, H, 3.0, tiling=(4, 3, 70, 50), threads=ORC_THREADS)
+    for pm in (50, 500):
+        r = split_renderer(gpu, 1, pm)
+        img, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r, tiling=t)
+        assert_frames(img, want, exact=True)
+        r.set_tuning(KNOB_PM, pm)
+        check_takes(gpu, torch, r, scene, cam, W, H, want, takes, tiling=t)
+        r.close()

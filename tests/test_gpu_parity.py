@@ -375,7 +375,8 @@ def test_tuning_defaults_read_back(gpu):
     """gsr_get_tuning returns the documented defaults (include/gsr.h) and what
     gsr_set_tuning set; unknown knobs are refused."""
     r = gpu.Renderer()
-    defaults = {1: 16, 2: 0, 3: 1024, 4: 0, 5: 1, 6: 1, 7: 1, 8: 4, 9: 8, 10: 0, 11: 1, 13: 4, 18: 2, 19: 2}
+    defaults = {1: 16, 2: 0, 3: 1024, 4: 0, 5: 1, 6: 1, 7: 1, 8: 4, 9: 8, 10: 0, 11: 1, 13: 4, 18: 2, 19: 2,
+                23: 2, 24: 250}
     for kn, v in defaults.items():
         assert r.get_tuning(kn) == v, kn
     r.set_tuning(9, 16)

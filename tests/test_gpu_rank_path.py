@@ -46,6 +46,7 @@ def render_both(gpu, torch, scene, n, cam, W, H):
     out = {}
     for ra in (0, 1):
         r = exact_blend(gpu.Renderer())      # images bit-exact against the oracle
+        r.set_tuning(gpu.TUNE_DEPTH_SPLIT, 0)  # whole-depth-order tile lists (config 3 splits by default)
         r.set_tuning(gpu.TUNE_RANK_ATOMIC, ra)
         assert r.get_tuning(gpu.TUNE_RANK_ATOMIC_ACTIVE) == ra
         img = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
