@@ -52,6 +52,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 BLEND_KERNELS = {1: "k_blend_w<false, false, true, 0>", 0: "k_blend_w<false, false, false, 0>",
                  "split": "k_blend_w<false, false, false, 1>"}
 BLEND_KERNEL = BLEND_KERNELS[0]
+SPLIT_STATES = {0: "one phase", 1: "whole order sorted", 2: "threshold partition, phase B queued",
+                3: "threshold partition, speculative (no phase B)"}
 
 
 def parse():
@@ -391,7 +393,8 @@ def main():
     consumed = counters["records_loaded"]
     global BLEND_KERNEL
     blend_exp = r.get_tuning(22)
-    split = stages.get("resume", 0.0) > 0.0          # the stage frames ran the depth split
+    split_state = r.get_tuning(26)                    # GSR_TUNE_DEPTH_SPLIT_STATE of the last frame
+    split = split_state != 0
     BLEND_KERNEL = BLEND_KERNELS["split" if split else min(blend_exp, 1)]
     r.set_diagnostics(False)
     tiles_x, tiles_y = r.tile_grid()
@@ -458,6 +461,7 @@ def main():
     else:
         elapsed, blend_times_pipe, timed_frames_pipe = seq_elapsed, blend_times, timed_frames
     overflow = r.sync() or seq_overflow
+    split_after = (r.get_tuning(26), r.get_tuning(24))   # depth split state and point after the timed frames
     telemetry_after = gpu_telemetry(pci) if rank == 0 else None
 
     max_elapsed = multi.max_over_ranks(dist, elapsed, "cpu" if gloo else "cuda")
@@ -518,8 +522,11 @@ def main():
                        "note": "same K frames one at a time on one stream (gsr_render; the viewer's use)"},
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
         "depth_split": ({"split_permille": r.get_tuning(24), "unsaturated_blocks_after_phase_a": r.get_tuning(25),
+                         "state": SPLIT_STATES[split_state],
+                         "after_timed": {"state": SPLIT_STATES[split_after[0]], "split_permille": split_after[1]},
                          "note": "pairs / row_items / stages emit+tile_sort are phase A's (the nearest "
-                                 "split_permille/1000 of the depth order); stage resume = phase B"}
+                                 "split_permille/1000 of the depth order); stage depth_sort = threshold "
+                                 "partition + near sort; stage resume = phase B"}
                         if split else None),
         "pairs": pairs,
         "row_items": row_items,

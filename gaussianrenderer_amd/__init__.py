@@ -510,6 +510,7 @@ TUNE_BLEND_EXP = 22
 TUNE_DEPTH_SPLIT = 23
 TUNE_DEPTH_SPLIT_PERMILLE = 24
 TUNE_DEPTH_SPLIT_UNSAT = 25
+TUNE_DEPTH_SPLIT_STATE = 26
 
 
 def rank_order_check() -> tuple[int, int]:

@@ -44,18 +44,44 @@ struct Stats {
     uint32_t depth_passes;            // passes the depth sort's device plan needed (binning path; 0: n/a)
     uint32_t split_unsat;             // depth split: blocks the last phase-A blend left unsaturated
                                       // (written to the host-mapped copy by the phase-B blend)
+    uint32_t spec_miss;               // depth split without phase B (speculative): a phase-A blend
+                                      // left a block unsaturated, the frame is incomplete (host copy,
+                                      // sticky until the host reads it)
 };
 
 // Depth split (GSR_TUNE_DEPTH_SPLIT): the frame's tiles are binned over the nearest
 // part of the depth order first (phase A); its blend saves the transmittance of
 // every block it leaves unsaturated, and phase B bins the rest of the depth order
 // and resumes those blocks.  phase: 1 = A (save), 2 = B (resume).
+// Depth split with a threshold partition (the near part sorted, the far part sorted
+// inside phase B): cut_mode 1 = the row pass reads [0, *cut), 2 = [*cut, n); na = the
+// host's split point (positions), sizes phase A's grid.
+struct RowSplit {
+    int cut_mode;
+    uint32_t na;
+};
+
+// The next frame's depth threshold (its partition puts keys < *kcut in the near part),
+// computed by phase A's blend from this frame's near depth order (gsr_kernels.hip
+// split_cut_update).  kcut == nullptr: no update.
+struct SplitCut {
+    const uint64_t* items0;
+    const uint64_t* items1;
+    const uint32_t* dstats;           // the near sort's pass plan (which buffer holds the result)
+    const uint32_t* nnear;            // near count (nullptr: this frame sorted the whole order)
+    uint32_t n, na;                   // items, the split point (positions)
+    uint32_t* kcut;
+};
+
 struct BlendSplit {
     int phase;
     float* tbuf;                      // 64 floats per 8x8 block (4 blocks per tile)
     uint8_t* bflag;                   // per block: 1 = left unsaturated by phase A (tbuf valid)
     uint32_t* gate;                   // count of such blocks (cleared by phase A's row scan)
     Stats* host_st;                   // phase B publishes the count here (nullable)
+    Stats* spec_host;                 // phase A with no phase B queued: an unsaturated block sets
+                                      // spec_host->spec_miss (nullable)
+    SplitCut cut;                     // phase A: the next frame's threshold
 };
 
 // ---- launch wrappers (gsr_kernels.hip) ----
@@ -75,7 +101,8 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
                              int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
                              uint2* ranges, hipStream_t s, uint32_t* dstats = nullptr, int pass = 0,
                              const uint32_t* rect = nullptr, int rect_direct = 0, uint32_t* pay0 = nullptr,
-                             uint32_t* pay1 = nullptr, bool rank_atomic = false);
+                             uint32_t* pay1 = nullptr, bool rank_atomic = false,
+                             const uint32_t* base_dev = nullptr, const uint32_t* gate = nullptr);
 // Pair emission in depth order: tile counts (gathering each Gaussian's rect
 // once into srect, and zeroing the tile ranges), scan, then keys (uint16_t if
 // key16 else uint32_t) + values.
@@ -102,7 +129,8 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
 // index order), visible count into *n_live; culled tail to out only, with dead
 // rects in srect (gsr_kernels.hip "live partition").  counts: groups words.
 hipError_t launch_partition(const uint64_t* in, uint32_t n, int groups, uint32_t* counts, uint32_t* n_live,
-                            uint64_t* out, const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, hipStream_t s);
+                            uint64_t* out, const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, hipStream_t s,
+                            const uint32_t* kcut = nullptr);
 // Tile binning (row pass + column pass, tile grids <= 256 x 256): replaces
 // launch_emit + the key-value tile sort.  hist: 512 x groups; row_items /
 // row_pairs: 256 each; cbins: 256 x bin_col_chunks_max(); rows_buf: pair
@@ -112,7 +140,8 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
                            uint32_t* row_items,
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
                            int items, hipStream_t s, const uint16_t* spans = nullptr, bool rank_atomic = false,
-                           uint32_t base = 0, uint32_t* gate = nullptr, int gate_mode = 0);
+                           uint32_t base = 0, uint32_t* gate = nullptr, int gate_mode = 0,
+                           const uint32_t* cut = nullptr, const RowSplit* rs = nullptr);
 hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, const unsigned long long* row_pairs,
                            uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
                            uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,

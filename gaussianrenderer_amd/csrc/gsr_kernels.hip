@@ -702,15 +702,25 @@ __device__ __forceinline__ int depth_passes_run(const uint32_t* __restrict__ dst
     return p;
 }
 
+// SortRange: the depth split's far part — positions [*base, n_host) sorted on their own
+// (base != nullptr; n_dev is then unused), and every kernel of the pass returns at once
+// when *gate is 0 (phase B not needed).
+struct SortRange {
+    const uint32_t* base;
+    const uint32_t* gate;
+};
+
 template <int ITEMS>
 __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* __restrict__ in,
                                                                 const uint32_t* __restrict__ n_dev,
                                                                 uint32_t n_host, int shift, uint32_t mask,
                                                                 int groups, uint32_t* __restrict__ hist,
-                                                                uint32_t* __restrict__ dstats, int pass) {
+                                                                uint32_t* __restrict__ dstats, int pass,
+                                                                SortRange sr) {
     GSR_GEOM_PRIO();
     __shared__ uint32_t h[4][256];
     __shared__ uint32_t s_st[4];
+    if (sr.gate && *sr.gate == 0u) return;
     if (depth_pass_skipped(dstats, pass)) return;
     const uint32_t t = threadIdx.x;
     const uint32_t w = t >> 6;
@@ -720,7 +730,9 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
 #pragma unroll
     for (int k = 0; k < 4; k++) h[k][t] = 0;
     __syncthreads();
-    const uint64_t n = n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
+    const uint32_t base = sr.base ? *sr.base : 0u;
+    in += base;
+    const uint64_t n = sr.base ? (uint64_t)(n_host - min(base, n_host)) : n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, kSortThreads * ITEMS, b, e);
     auto note = [&](uint64_t v) {
@@ -775,9 +787,11 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
 // One workgroup per digit: exclusive scan of hist[d][0..groups) in place.
 __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist, int groups,
                                                      uint32_t* __restrict__ totals,
-                                                     const uint32_t* __restrict__ dstats, int pass) {
+                                                     const uint32_t* __restrict__ dstats, int pass,
+                                                     const uint32_t* __restrict__ gate) {
     GSR_GEOM_PRIO();
     __shared__ uint32_t scratch[4];
+    if (gate && *gate == 0u) return;
     if (dstats && pass == 0 && blockIdx.x == 0) {
         // reduce the upsweep's per-workgroup plan words into dstats[0..3]
         __shared__ uint32_t r[4];
@@ -839,11 +853,19 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     uint32_t n_host, int shift, int bits, int groups, const uint32_t* __restrict__ hist,
     const uint32_t* __restrict__ totals, uint2* __restrict__ ranges, const uint32_t* __restrict__ dstats,
     int pass, const uint32_t* __restrict__ rect, int rect_direct, const uint32_t* __restrict__ pay_in,
-    uint32_t* __restrict__ pay_out) {
+    uint32_t* __restrict__ pay_out, SortRange sr) {
     GSR_GEOM_PRIO();
     constexpr int kTile = kSortThreads * ITEMS;
     __shared__ uint64_t s_items[kTile];
+    if (sr.gate && *sr.gate == 0u) return;
     if (depth_pass_skipped(dstats, pass)) return;
+    if (sr.base) {   // far part: every position-indexed array starts at *base (rect_direct is 0)
+        const uint32_t base = *sr.base;
+        in += base;
+        out += base;
+        if (pay_in) pay_in += base;
+        if (pay_out) pay_out += base;
+    }
     const bool carry = pay_out != nullptr;
     __shared__ uint32_t s_wc[4][256];           // per-wave digit counters, then wave bases
     __shared__ uint32_t s_gbase[256];           // running global offset per digit
@@ -858,7 +880,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const uint32_t lane = lane_id();
     const uint32_t w = t >> 6;
     const uint32_t mask = (1u << bits) - 1u;
-    const uint64_t n = n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
+    const uint64_t n = sr.base ? (uint64_t)(n_host - min(*sr.base, n_host)) : n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
     uint64_t b, e;
     const int chunk = GSR_XCD_DEPTH && ITEMS == 16 ? xcd_chunk((int)blockIdx.x, groups) : (int)blockIdx.x;
     chunk_range(n, groups, chunk, kTile, b, e);
@@ -1499,6 +1521,18 @@ __device__ __forceinline__ void publish_pair_stats(unsigned long long total, uin
     }
 }
 
+// Depth-order positions a row pass reads: [base, base + n) as the host passed them, or
+// with the depth split's device-side cut (the near part's size after the threshold
+// partition): mode 1 = [0, min(cut, n)) (phase A), mode 2 = [cut, n) (phase B).
+__device__ __forceinline__ void row_range(uint32_t& base, uint32_t& n, const uint32_t* cut, int mode) {
+    if (mode == 1) {
+        n = min(*cut, n);
+    } else if (mode == 2) {
+        base = min(*cut, n);
+        n -= base;
+    }
+}
+
 // Row pass, count: per workgroup (1024-Gaussian sub-chunks in depth order) the
 // number of row items and of pairs per tile row; hist[row][g] and
 // hist[256 + row][g].  Reads the rects in depth order (the payloads the depth
@@ -1507,9 +1541,11 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint32
                                                          const uint32_t* __restrict__ pay1,
                                                          const uint32_t* __restrict__ dstats, int groups,
                                                          int tiles_y, uint32_t* __restrict__ hist, uint32_t base,
-                                                         const uint32_t* __restrict__ gate) {
+                                                         const uint32_t* __restrict__ gate,
+                                                         const uint32_t* __restrict__ cut, int cut_mode) {
     GSR_GEOM_PRIO();
     if (gate && *gate == 0u) return;   // depth split, phase B: every block saturated in phase A
+    row_range(base, n, cut, cut_mode);
     __shared__ uint32_t h_items[4][256], h_pairs[4][256];
     const uint32_t t = threadIdx.x, w = t >> 6;
 #pragma unroll
@@ -1555,6 +1591,30 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint32
         hist[t * (uint32_t)groups + blockIdx.x] = ci;
         hist[(256 + t) * (uint32_t)groups + blockIdx.x] = cp;
     }
+}
+
+
+
+// Depth split: the next frame's threshold from this frame's near depth order: the key
+// at position na (the host's split point) when the near part holds more than na items,
+// else the threshold widened in proportion from the smallest key.  Any threshold gives
+// the same image.
+__device__ __forceinline__ void split_cut_update(const SplitCut& sc) {
+    const uint64_t* sorted = depth_sorted(sc.items0, sc.items1, sc.dstats);
+    const uint32_t m = sc.nnear ? min(*sc.nnear, sc.n) : sc.n;
+    uint32_t K;
+    if (sc.na < m) {
+        K = (uint32_t)(sorted[sc.na] >> 32);
+    } else {
+        const uint32_t k0 = *sc.kcut, kmin = m ? (uint32_t)(sorted[0] >> 32) : 0u;
+        if (m == 0 || k0 == 0xffffffffu || k0 <= kmin) {
+            K = 0xffffffffu;
+        } else {
+            const uint64_t span = (uint64_t)(k0 - kmin) * sc.na / m + 1u;
+            K = (uint32_t)min((uint64_t)kmin + span, (uint64_t)0xffffffffu);
+        }
+    }
+    *sc.kcut = K;
 }
 
 // Row pass, scan: one workgroup per row.  Exclusive scan of the row's item
@@ -1621,9 +1681,11 @@ __global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(co
                                                            const unsigned long long* __restrict__ row_pairs,
                                                            uint32_t cap, int tiles_y, uint64_t* __restrict__ rows_out,
                                                            const uint16_t* __restrict__ spans, uint32_t base,
-                                                           const uint32_t* __restrict__ gate) {
+                                                           const uint32_t* __restrict__ gate,
+                                                           const uint32_t* __restrict__ cut, int cut_mode) {
     GSR_GEOM_PRIO();
     if (gate && *gate == 0u) return;
+    row_range(base, n, cut, cut_mode);
     constexpr uint32_t kTile = 256u * ITEMS;
     __shared__ uint32_t s_pref[kRowSources], s_idx[kRowSources];
     // per source: packed rect (pack_rect) | tile row spans << 32 (no LDS beyond the
@@ -1959,14 +2021,18 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
 // ends depth-ordered is decided on the device); the binning never reads items whose
 // rect is dead, and gsr_read_depth_order takes the tail from `out`.  Three launches: per-chunk
 // visible counts, their exclusive scan (+ total), the scatter.
+// kcut (nullable): the depth split's threshold — items with key < *kcut come first
+// (the near part), the rest after with their real rects in pay0 (phase B sorts them);
+// without it the threshold is 0xFFFFFFFF (the live partition).
 __global__ __launch_bounds__(256) void k_part_count(const uint64_t* __restrict__ in, uint32_t n, int groups,
-                                                     uint32_t* __restrict__ counts) {
+                                                     uint32_t* __restrict__ counts, const uint32_t* __restrict__ kcut) {
     GSR_GEOM_PRIO();
     __shared__ uint32_t s_scr[4];
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, 256, b, e);
+    const uint32_t K = kcut ? *kcut : 0xffffffffu;
     uint32_t c = 0;
-    for (uint64_t i = b + threadIdx.x; i < e; i += 256) c += (uint32_t)(in[i] >> 32) != 0xffffffffu ? 1u : 0u;
+    for (uint64_t i = b + threadIdx.x; i < e; i += 256) c += (uint32_t)(in[i] >> 32) < K ? 1u : 0u;
     uint32_t tot;
     (void)block_exclusive_scan<uint32_t>(c, s_scr, tot);
     if (threadIdx.x == 0) counts[blockIdx.x] = tot;
@@ -1997,9 +2063,11 @@ __global__ __launch_bounds__(256) void k_part_scatter(const uint64_t* __restrict
                                                        const uint32_t* __restrict__ n_live,
                                                        uint64_t* __restrict__ out,
                                                        const uint32_t* __restrict__ rect,
-                                                       uint32_t* __restrict__ pay0, uint32_t* __restrict__ pay1) {
+                                                       uint32_t* __restrict__ pay0, uint32_t* __restrict__ pay1,
+                                                       const uint32_t* __restrict__ kcut) {
     GSR_GEOM_PRIO();
     __shared__ uint32_t s_w[4];
+    const uint32_t K = kcut ? *kcut : 0xffffffffu;
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, 256, b, e);
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
@@ -2011,7 +2079,7 @@ __global__ __launch_bounds__(256) void k_part_scatter(const uint64_t* __restrict
         const uint64_t i = c0 + t;
         const bool valid = i < e;
         const uint64_t v = valid ? in[i] : 0ull;
-        const bool live = valid && (uint32_t)(v >> 32) != 0xffffffffu;
+        const bool live = valid && (uint32_t)(v >> 32) < K;
         const bool dead = valid && !live;
         const uint64_t bl = __ballot(live), bd = __ballot(dead);
         if (lane == 0) s_w[w] = (uint32_t)__popcll(bl) | ((uint32_t)__popcll(bd) << 16);
@@ -2035,8 +2103,12 @@ __global__ __launch_bounds__(256) void k_part_scatter(const uint64_t* __restrict
         if (dead) {
             const uint32_t q = dead_base + db + (uint32_t)__popcll(bd & lt);
             out[q] = v;
-            pay0[q] = pack_rect(kDeadRect);   // the sort's result parity is decided on the device
-            pay1[q] = pack_rect(kDeadRect);
+            if (kcut) {
+                pay0[q] = rect[(uint32_t)v];      // the far part: phase B's sort pass 0 reads pay0
+            } else {
+                pay0[q] = pack_rect(kDeadRect);   // the sort's result parity is decided on the device
+                pay1[q] = pack_rect(kDeadRect);
+            }
         }
         live_base += ltot;
         dead_base += dtot;
@@ -2524,6 +2596,7 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
             *flag = unsat ? 1u : 0u;
             if (unsat) atomicAdd(gate, 1u);
         }
+        suspect = unsat ? 1ull : 0ull;   // returned: the caller flags a speculative frame
     }
     // FX: every pixel but the suspect ones; exact: the pixels of `only`
     const bool write = FX ? ((suspect >> lane) & 1ull) == 0ull : mine;
@@ -2566,6 +2639,7 @@ __global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx
     __shared__ float4 sP[32 * (FX ? 24 : 20) / 4];
     const int ntiles = tiles_x * tiles_y;
     const int vb = (int)blockIdx.x;
+    if (SPLIT == 1 && vb == 0 && threadIdx.x == 0 && sp.cut.kcut) split_cut_update(sp.cut);
     if (SPLIT == 2) {
         const uint32_t g = *sp.gate;   // uniform
         if (vb == 0 && threadIdx.x == 0 && sp.host_st) {
@@ -2607,6 +2681,10 @@ __global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx
                                                        out, reinterpret_cast<float*>(sP), dg, tmap, band0, ~0ull,
                                                        SPLIT ? sp.tbuf + 64 * (size_t)L : nullptr,
                                                        SPLIT ? sp.bflag + L : nullptr, sp.gate);
+    if (SPLIT == 1 && redo && sp.spec_host && lane == 0) {
+        sp.spec_host->spec_miss = 1u;   // no phase B queued for this frame: it is incomplete
+        __threadfence_system();
+    }
     if (FX && redo) {
         if (DIAG && lane == 0) {
             atomicAdd(counters + 8, 1ull);
@@ -2817,43 +2895,46 @@ template <int ITEMS, bool RA>
 static void radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host, int shift,
                        int bits, int groups, uint32_t* hist, uint32_t* totals, uint2* ranges, uint32_t* dstats,
                        int pass, const uint32_t* rect, int rect_direct, uint32_t* pay0, uint32_t* pay1,
-                       hipStream_t s) {
+                       hipStream_t s, SortRange sr) {
     const uint32_t mask = (1u << bits) - 1u;
     hipLaunchKernelGGL(k_radix_upsweep<ITEMS>, dim3(groups), dim3(kSortThreads), 0, s, in, n_dev, n_host, shift,
-                       mask, groups, hist, dstats, pass);
+                       mask, groups, hist, dstats, pass, sr);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, hist, groups, totals,
-                       static_cast<const uint32_t*>(dstats), pass);
+                       static_cast<const uint32_t*>(dstats), pass, sr.gate);
     // rect payloads (binning): pass p reads pay[p & 1] (pass 0: rect, or pay[0] when
     // rect_direct < 0 — the live partition wrote it) and writes pay[(p + 1) & 1]
     const uint32_t* pay_in = pay0 && (pass > 0 || rect_direct < 0) ? ((pass & 1) ? pay1 : pay0) : nullptr;
     uint32_t* pay_out = pay0 ? ((pass & 1) ? pay0 : pay1) : nullptr;
     hipLaunchKernelGGL((k_radix_downsweep<ITEMS, RA>), dim3(groups), dim3(kSortThreads), 0, s, in, out, n_dev, n_host,
                        shift, bits, groups, hist, totals, ranges, static_cast<const uint32_t*>(dstats), pass, rect,
-                       rect_direct > 0 ? 1 : 0, pay_in, pay_out);
+                       rect_direct > 0 ? 1 : 0, pay_in, pay_out, sr);
 }
 
 hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
                              int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
                              uint2* ranges, hipStream_t s, uint32_t* dstats, int pass, const uint32_t* rect,
-                             int rect_direct, uint32_t* pay0, uint32_t* pay1, bool rank_atomic) {
+                             int rect_direct, uint32_t* pay0, uint32_t* pay1, bool rank_atomic,
+                             const uint32_t* base_dev, const uint32_t* gate) {
     if ((rect == nullptr) != (pay0 == nullptr) || (pay0 == nullptr) != (pay1 == nullptr))
         return hipErrorInvalidValue;
+    if (base_dev && (n_dev || rect_direct > 0)) return hipErrorInvalidValue;
+    const SortRange sr{base_dev, gate};
     // 16 items per thread always rank with ballots (k_radix_downsweep)
     if (items == 4 && rank_atomic)
         radix_pass<4, true>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
-                            rect_direct, pay0, pay1, s);
+                            rect_direct, pay0, pay1, s, sr);
     else if (items == 4)
         radix_pass<4, false>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
-                             rect_direct, pay0, pay1, s);
+                             rect_direct, pay0, pay1, s, sr);
     else if (items == 8 && rank_atomic)
         radix_pass<8, true>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
-                            rect_direct, pay0, pay1, s);
+                            rect_direct, pay0, pay1, s, sr);
     else if (items == 8)
         radix_pass<8, false>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
-                             rect_direct, pay0, pay1, s);
+                             rect_direct, pay0, pay1, s, sr);
     else
         radix_pass<16, false>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
-                              rect_direct, pay0, pay1, s);
+                              rect_direct, pay0, pay1, s, sr);
     return hipGetLastError();
 }
 
@@ -2875,12 +2956,13 @@ hipError_t launch_emit(const uint64_t* items0, const uint64_t* items1, const uin
 }
 
 hipError_t launch_partition(const uint64_t* in, uint32_t n, int groups, uint32_t* counts, uint32_t* n_live,
-                            uint64_t* out, const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, hipStream_t s) {
+                            uint64_t* out, const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, hipStream_t s,
+                            const uint32_t* kcut) {
     if (groups < 1 || groups > kMaxSortGroups) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_part_count, dim3(groups), dim3(256), 0, s, in, n, groups, counts);
+    hipLaunchKernelGGL(k_part_count, dim3(groups), dim3(256), 0, s, in, n, groups, counts, kcut);
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(256), 0, s, counts, groups, n_live);
     hipLaunchKernelGGL(k_part_scatter, dim3(groups), dim3(256), 0, s, in, n, groups, counts, n_live, out, rect,
-                       pay0, pay1);
+                       pay0, pay1, kcut);
     return hipGetLastError();
 }
 
@@ -2889,13 +2971,15 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
                            uint32_t* row_items,
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
                            int items, hipStream_t s, const uint16_t* spans, bool rank_atomic, uint32_t base,
-                           uint32_t* gate, int gate_mode) {
+                           uint32_t* gate, int gate_mode, const uint32_t* cut, const RowSplit* rs) {
+    const int cut_mode = rs ? rs->cut_mode : 0;
     if (tiles_y < 1 || tiles_y > 256 || groups < 1 || groups > kMaxSortGroups / 2 ||
-        (items != 4 && items != 8 && items != 16) || (gate_mode != 0 && !gate) || gate_mode < 0 || gate_mode > 2)
+        (items != 4 && items != 8 && items != 16) || (gate_mode != 0 && !gate) || gate_mode < 0 || gate_mode > 2 ||
+        (cut_mode != 0 && !cut) || cut_mode < 0 || cut_mode > 2)
         return hipErrorInvalidValue;
     const uint32_t* g = gate_mode == 2 ? gate : nullptr;
     hipLaunchKernelGGL(k_bin_rows_count, dim3(groups), dim3(256), 0, s, n, pay0, pay1, dstats, groups, tiles_y,
-                       hist, base, g);
+                       hist, base, g, cut, cut_mode);
     hipLaunchKernelGGL(k_bin_rows_scan, dim3(256), dim3(256), 0, s, hist, groups, tiles_y, row_items, row_pairs,
                        gate, gate_mode);
     auto pick = [&](auto ra) {
@@ -2907,7 +2991,7 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
     };
     auto scatter = rank_atomic ? pick(std::true_type{}) : pick(std::false_type{});
     hipLaunchKernelGGL(scatter, dim3(groups), dim3(256), 0, s, items0, items1, dstats, pay0, pay1, n, groups, hist,
-                       row_items, row_pairs, pair_capacity, tiles_y, rows_buf, spans, base, g);
+                       row_items, row_pairs, pair_capacity, tiles_y, rows_buf, spans, base, g, cut, cut_mode);
     return hipGetLastError();
 }
 
@@ -2947,7 +3031,7 @@ static void kv_pass(const K* kin, const uint32_t* vin, K* kout, uint32_t* vout, 
     hipLaunchKernelGGL((k_kv_upsweep<K, ITEMS>), dim3(groups), dim3(kSortThreads), 0, s, kin, n_dev, shift, mask,
                        groups, hist);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, hist, groups, totals,
-                       static_cast<const uint32_t*>(nullptr), 0);
+                       static_cast<const uint32_t*>(nullptr), 0, static_cast<const uint32_t*>(nullptr));
     hipLaunchKernelGGL((k_kv_downsweep<K, ITEMS>), dim3(groups), dim3(kSortThreads), 0, s, kin, vin, kout, vout,
                        n_dev, shift, bits, groups, hist, totals, ranges);
 }
@@ -2992,7 +3076,7 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
     const int phase = split ? split->phase : 0;
     if (phase < 0 || phase > 2 || (phase && (fast_exp || stamps || !split->tbuf || !split->bflag || !split->gate)))
         return hipErrorInvalidValue;
-    const BlendSplit sp = split ? *split : BlendSplit{0, nullptr, nullptr, nullptr, nullptr};
+    const BlendSplit sp = split ? *split : BlendSplit{0, nullptr, nullptr, nullptr, nullptr, nullptr, {}};
 #define GSR_BLEND_S(D, ST, FX, SP)                                                                          \
     hipLaunchKernelGGL((k_blend_w<D, ST, FX, SP>), dim3(ng), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,  \
                        fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, bands, band0, sp)

@@ -388,7 +388,19 @@ struct gsr_context {
     bool split_frame = false;        // the sorted frame is split (phase A lists binned by sort_locked)
     bool split_rebin = false;        // phase B's lists replaced phase A's: a repeated blend bins phase A again
     bool split_seen = false;         // a split frame was blended since the last controller update
-    uint32_t split_na = 0;           // phase A's depth-order prefix
+    bool split_spec = false;         // speculate: queue no phase B (the split point cannot shrink further
+                                     // and 8 checked frames in a row needed none); a frame that then
+                                     // leaves a block unsaturated is reported as GSR_E_OVERFLOW
+    bool frame_spec = false;         // the sorted frame is blended without phase B
+    uint32_t split_na = 0;           // phase A's depth-order prefix (count mode) / the split point
+    bool split_key = false;          // the preprocess left its items in items[1] for a threshold partition
+    bool frame_key = false;          // the sorted frame is split in key mode (near part sorted, far part
+                                     // sorted by phase B)
+    bool split_key_ready = false;    // *kcut holds a threshold from an earlier split frame of this context
+    bool last_split_key = false;     // the last sorted frame left its far part unsorted (phase B may not run)
+    uint32_t* kcut = nullptr;        // depth split: the next frame's depth threshold (device word)
+    uint32_t* dstats_far = nullptr;  // depth split: the far sort's pass plan
+    int far_launched = 4;            // passes the far sort launched
     float* tbuf = nullptr;           // depth split: saved transmittance, 64 floats per 8x8 block
     uint8_t* bflag = nullptr;        // depth split: per block, left unsaturated by phase A
     uint32_t* gate = nullptr;        // depth split: count of such blocks (device word)
@@ -438,6 +450,13 @@ namespace {
 // leaves the L2), the depth split on (GSR_TUNE_TILE_SPANS / GSR_TUNE_DEPTH_SPLIT = 2).
 constexpr int64_t kLargeScene = 3 << 19;
 constexpr int kSplitMinPm = 20;       // smallest split point (per mille)
+
+// The depth split applies to this context's frames of n Gaussians (binning path and the
+// exact blend; gsr_render / gsr_render_path decide it per frame, the stage API never).
+bool split_enabled(const gsr_context* c, int64_t n) {
+    return n > 0 && c->blend_exp == 0 && c->blend_variant != 3 && c->split_pm < 1000 &&
+           (c->depth_split == 1 || (c->depth_split == 2 && n > kLargeScene));
+}
 
 int groups_for(int64_t n, int64_t per) {
     int64_t g = (n + per - 1) / per;
@@ -503,6 +522,9 @@ int ensure_static(gsr_context* c) {
     if (int rc = realloc_dev(&c->nlive, 1)) return rc;
     if (int rc = realloc_dev(&c->binmeta, 256 + 128)) return rc;
     if (int rc = realloc_dev(&c->gate, 1)) return rc;
+    if (int rc = realloc_dev(&c->kcut, 1)) return rc;
+    if (int rc = realloc_dev(&c->dstats_far, 4 + 4 * (size_t)gsr::kMaxSortGroups)) return rc;
+    HIP_TRY(hipMemset(c->kcut, 0xff, sizeof(uint32_t)));
     HIP_TRY(hipMemset(c->stats, 0, 2 * sizeof(Stats)));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->hstats), sizeof(Stats), hipHostMallocMapped));
     std::memset(c->hstats, 0, sizeof(Stats));
@@ -596,6 +618,19 @@ void mark(gsr_context* c, int stage) {
 // An overflow (pairs over capacity, or a depth sort short of passes) is reported
 // once here and remembered in overflow_seen until gsr_sync, so a blocking sync also
 // reports what a non-blocking check inside a render call already consumed.
+// Depth split point after a frame that needed phase B: up by half, floor at 5/4 of the
+// old point, no speculation.
+void split_grow(gsr_context* c) {
+    c->split_floor = std::min(1000, c->split_pm * 5 / 4 + 1);
+    c->split_pm = std::min(1000, c->split_pm * 3 / 2 + 1);
+    c->split_clean = 0;
+    c->split_spec = false;
+}
+
+void hv_clear_spec(gsr_context* c) {
+    reinterpret_cast<volatile Stats*>(c->hstats)->spec_miss = 0;
+}
+
 int check_overflow(gsr_context* c, bool blocking) {
     if (!c->pending) return GSR_OK;
     if (blocking) {
@@ -610,18 +645,29 @@ int check_overflow(gsr_context* c, bool blocking) {
     s.pairs_eff = hv->pairs_eff;
     s.overflow = hv->overflow;
     s.depth_passes = hv->depth_passes;
+    if (!s.overflow && hv->spec_miss) {
+        // a speculative frame (no phase B queued) left a block unsaturated: drain, then
+        // report it like an overflow (the caller re-renders) and stop speculating
+        HIP_TRY(hipDeviceSynchronize());
+        hv_clear_spec(c);
+        split_grow(c);
+        c->overflow_seen = true;
+        return set_err(GSR_E_OVERFLOW, "depth split: a frame rendered without phase B left blocks unsaturated; "
+                                       "re-render");
+    }
     if (!s.overflow && c->split_seen) {
         // depth split point: up by half when phase A left blocks unsaturated (phase B
         // ran), down by an eighth after 8 checked frames in a row that needed no phase B,
-        // never below 5/4 of the last point that needed it
+        // never below 5/4 of the last point that needed it; when it cannot shrink any
+        // further, the next frames speculate (no phase B queued)
         c->split_seen = false;
         if (hv->split_unsat > 0) {
-            c->split_floor = std::min(1000, c->split_pm * 5 / 4 + 1);
-            c->split_pm = std::min(1000, c->split_pm * 3 / 2 + 1);
-            c->split_clean = 0;
+            split_grow(c);
         } else if (++c->split_clean >= 8) {
             c->split_clean = 0;
-            c->split_pm = std::max(std::max(kSplitMinPm, c->split_floor), c->split_pm * 7 / 8);
+            const int next = std::max(std::max(kSplitMinPm, c->split_floor), c->split_pm * 7 / 8);
+            if (next >= c->split_pm) c->split_spec = true;
+            c->split_pm = next;
         }
     }
     if (!s.overflow) {
@@ -715,7 +761,7 @@ extern "C" void gsr_destroy(gsr_context* c) {
                     (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->dstats,
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
                     (void*)c->cbins, (void*)c->srect, (void*)c->spans, (void*)c->nlive, (void*)c->tbuf,
-                    (void*)c->bflag, (void*)c->gate})
+                    (void*)c->bflag, (void*)c->gate, (void*)c->kcut, (void*)c->dstats_far})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -765,9 +811,14 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     } else {
         arrays = reinterpret_cast<const float*>(static_cast<const char*>(scene) + GSR_SCENE_HEADER_BYTES);
     }
+    // depth split with a threshold partition (a threshold exists from an earlier split
+    // frame): the items go to items[1], the partition writes near-first into items[0]
+    c->split_key = split_enabled(c, n) && c->split_key_ready && c->tile_binning && c->fr.tiles_x <= 256 &&
+                   c->fr.tiles_y <= 256;
     // live partition (global depth sort on the binning path): the items go to
     // items[1] and the partition writes the visible-first order into items[0]
-    c->compact_frame = n > 0 && (c->depth_compact == 1 || (c->depth_compact == 2 && layout == GSR_LAYOUT_SCENE_BLOCK_4D)) &&
+    c->compact_frame = n > 0 && !c->split_key &&
+                       (c->depth_compact == 1 || (c->depth_compact == 2 && layout == GSR_LAYOUT_SCENE_BLOCK_4D)) &&
                        c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
     // the binning path takes the tile rects packed to 4 B (pack_rect), the pair path 8 B;
     // the sort follows the path chosen here (rect_packed)
@@ -777,7 +828,8 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     // config 2 (1M) +0.8 % one frame at a time, +1.2 % in flight; config 5 (2M) -1 % in
     // flight, config 3 (5M) -3 / -6 % (profiles/r02_ab_tile_spans.txt)
     c->spans_frame = c->rect_packed && (c->tile_spans == 1 || (c->tile_spans == 2 && n <= kLargeScene));
-    HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[c->compact_frame ? 1 : 0], c->rect,
+    HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[c->compact_frame || c->split_key ? 1 : 0],
+                                   c->rect,
                                    c->rect_packed, layout == GSR_LAYOUT_SCENE_BLOCK_4D,
                                    layout == GSR_LAYOUT_SCENE_BLOCK_SH3, c->time, c->stream,
                                    c->spans_frame ? c->spans : nullptr));
@@ -818,15 +870,26 @@ static int depth_sort_locked(gsr_context* c, bool with_rects) {
     // smaller tiles for the 1M-item depth sort: ~500 workgroups instead of ~250 (-2.6 %
     // frame time one at a time; in flight 8 and 16 measure within 1.5 % of each other,
     // either way round: profiles/r02_ab_depth_items.txt)
-    const int di = c->depth_items ? c->depth_items : (c->n < (int64_t(4) << 20) ? 8 : 16);
-    int gd = groups_for(c->n, 256 * di);
+    // depth split, threshold partition: the passes sort only the near part (about
+    // 2 x the split point's items; the far part is sorted inside phase B)
+    const bool key = with_rects && c->split_key;
+    const int64_t n_sorted =
+        key ? std::min<int64_t>(c->n, std::max<int64_t>(2 * ((int64_t)c->n * c->split_pm / 1000), 65536)) : c->n;
+    const int di = c->depth_items ? c->depth_items : (n_sorted < (int64_t(4) << 20) ? 8 : 16);
+    int gd = groups_for(n_sorted, 256 * di);
     if (c->depth_groups) gd = std::min(gd, c->depth_groups);
-    const bool part = with_rects && c->compact_frame;
-    if (part)   // visible items first (index order) into items[0]; the passes sort only those
+    const bool part = with_rects && (c->compact_frame || key);
+    // visible items (key mode: keys below the threshold) first, in index order, into
+    // items[0]; the passes sort only those
+    if (part)
         HIP_TRY(gsr::launch_partition(c->items[1], n, std::min(groups_for(c->n, 4096), gsr::kMaxSortGroups), c->hist,
                                       c->nlive, c->items[0], reinterpret_cast<const uint32_t*>(c->rect),
-                                      pay_buf(c, 0), pay_buf(c, 1), c->stream));
-    c->last_compact = part;
+                                      pay_buf(c, 0), pay_buf(c, 1), c->stream, key ? c->kcut : nullptr));
+    c->last_compact = part && !key;
+    c->last_split_key = key;
+    // a repeated sort of a key-mode frame sorts the whole partitioned items[0] (near and
+    // far keys never tie, so the order is the same)
+    if (key) c->split_key = false;
     // pass 0's rect payloads: from the partition (-1), read at the item's position when
     // items[0] is still the preprocess order (1: item j has index j), else gathered (0)
     const int rect_mode = part ? -1 : (c->have_sort ? 0 : 1);
@@ -849,21 +912,46 @@ static int depth_sort_locked(gsr_context* c, bool with_rects) {
     return GSR_OK;
 }
 
+// Depth split, key mode, phase B: the far part [nlive, n) sorted on its own (its own
+// pass plan), every kernel returning at once when phase A saturated every block.
+static int far_sort_locked(gsr_context* c) {
+    const uint32_t n = (uint32_t)c->n;
+    const int di = c->depth_items ? c->depth_items : (c->n < (int64_t(4) << 20) ? 8 : 16);
+    int gd = groups_for(c->n, 256 * di);
+    if (c->depth_groups) gd = std::min(gd, c->depth_groups);
+    const int launch = c->depth_skip ? std::max(1, std::min(4, c->depth_budget)) : 4;
+    c->far_launched = launch;
+    for (int p = 0; p < launch; p++)
+        HIP_TRY(gsr::launch_radix_pass(c->items[p & 1], c->items[(p + 1) & 1], nullptr, n, 32 + 8 * p, 8, gd, di,
+                                       c->hist, c->totals, nullptr, c->stream, c->depth_skip ? c->dstats_far : nullptr,
+                                       p, reinterpret_cast<const uint32_t*>(c->rect), -1, pay_buf(c, 0), pay_buf(c, 1),
+                                       rank_atomic_on(c), c->nlive, c->gate));
+    return GSR_OK;
+}
+
 // Row pass, then column pass (gsr_kernels.hip "tile binning") over the depth-order
 // positions [base, base + count): tile lists in pair_vals(c, 1), ranges.  gate_mode:
 // 0 plain; 1 = depth split phase A (clears the gate); 2 = phase B (every kernel returns
 // at once when the gate is 0).
-static int bin_locked(gsr_context* c, uint32_t base, uint32_t count, int gate_mode, bool marks) {
+// rs (nullable): the depth split's device-side ranges and threshold update; far: the
+// positions were sorted by far_sort_locked (its pass plan and pass count apply).
+static int bin_locked(gsr_context* c, uint32_t base, uint32_t count, int gate_mode, bool marks,
+                      const gsr::RowSplit* rs = nullptr, bool far = false) {
     const uint32_t cap = (uint32_t)c->p_cap;
     if (int rc = ensure_cbins(c)) return rc;
     auto* row_pairs = reinterpret_cast<unsigned long long*>(c->binmeta);
     auto* row_items = reinterpret_cast<uint32_t*>(c->binmeta + 256);
-    const int gb = std::min(groups_for(count, 1024), gsr::kMaxSortGroups / 2);
-    HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, count, pay_buf(c, 0),
+    // key mode, phase A: about 2 x the split point's items (the count is on the device)
+    const int64_t est = rs && rs->cut_mode == 1 ? std::min<int64_t>(count, std::max<int64_t>(2 * (int64_t)rs->na, 65536))
+                                                : (int64_t)count;
+    const int gb = std::min(groups_for(est, 1024), gsr::kMaxSortGroups / 2);
+    uint32_t* dst = c->depth_skip ? (far ? c->dstats_far : c->dstats) : nullptr;
+    HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], dst, count, pay_buf(c, 0),
                                  pay_buf(c, 1), gb,
                                  c->hist, row_items, row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items,
                                  c->stream, c->spans_frame ? c->spans : nullptr, rank_atomic_on(c), base,
-                                 gate_mode ? c->gate : nullptr, gate_mode));
+                                 gate_mode ? c->gate : nullptr, gate_mode, rs && rs->cut_mode ? c->nlive : nullptr,
+                                 rs));
     if (marks) mark(c, GSR_STAGE_TILE_SORT);
     // column-pass workgroups: ~one 2048-item chunk each (config 3: 2048-4096 groups 12 us
     // faster than 1024; config 2: 1024 best, profiles/r02_ab_col_groups.txt)
@@ -872,7 +960,7 @@ static int bin_locked(gsr_context* c, uint32_t base, uint32_t count, int gate_mo
     HIP_TRY(gsr::launch_bin_cols(c->pairs[0], row_items, row_pairs, c->cbins, gcol, cap,
                                  c->fr.tiles_x, c->fr.tiles_y, pair_vals(c, 1), c->ranges, c->stats,
                                  c->hstats_dev, c->bin_col_items, c->stream,
-                                 c->depth_skip ? c->dstats : nullptr, c->passes_launched, rank_atomic_on(c),
+                                 dst, far ? c->far_launched : c->passes_launched, rank_atomic_on(c),
                                  gate_mode == 2 ? c->gate : nullptr));
     c->pair_buf = 1;
     return GSR_OK;
@@ -885,33 +973,42 @@ static int sort_locked(gsr_context* c, bool allow_split) {
     const uint32_t n = (uint32_t)c->n;
     const bool bin = c->rect_packed;   // the path gsr_preprocess chose (its rect format)
     c->last_binned = bin;
+    // depth split for this frame (gsr_render / gsr_render_path on the binning path):
+    // count mode sorts the whole order and phase A bins its nearest na positions; key
+    // mode (a threshold from an earlier split frame exists) partitions by the threshold
+    // and sorts only the near part, which phase A bins
+    const uint32_t na = (uint32_t)std::max<int64_t>(1, ((int64_t)n * c->split_pm + 999) / 1000);
+    const bool split = bin && allow_split && split_enabled(c, c->n) && na < n;
+    if (c->split_key && !split) {   // preprocessed for key mode: sort every visible item instead
+        c->split_key = false;
+        c->compact_frame = true;
+    }
     if (c->compact_frame && !bin) {   // knobs changed since gsr_preprocess
         HIP_TRY(hipMemcpyAsync(c->items[0], c->items[1], (size_t)n * 8, hipMemcpyDeviceToDevice, c->stream));
         c->compact_frame = false;
     }
+    const bool key = split && c->split_key;
     // ---- stable depth sort of (key << 32 | index), 4 x 8 bits; for the binning
     // path the passes carry the rects, depth-ordered at the end (pay_buf) ----
     mark(c, GSR_STAGE_DEPTH_SORT);
     if (int rc = depth_sort_locked(c, bin)) return rc;
     // result in items[passes run & 1] (device-side plan; emission picks it)
     if (bin) {
-        // depth split: phase A bins the nearest split_pm / 1000 of the depth order
-        // (blend_locked blends it, then bins and blends the rest where needed)
-        c->split_frame = false;
+        // depth split: phase A bins the near part (blend_locked blends it, then sorts
+        // and bins the rest where needed)
+        c->split_frame = split;
         c->split_rebin = false;
-        uint32_t count = n;
-        if (allow_split && n > 0 && c->blend_exp == 0 && c->blend_variant != 3 && c->split_pm < 1000 &&
-            (c->depth_split == 1 || (c->depth_split == 2 && c->n > kLargeScene))) {
-            const uint32_t na = (uint32_t)std::max<int64_t>(1, ((int64_t)n * c->split_pm + 999) / 1000);
-            if (na < n) {
-                if (int rc = ensure_split(c)) return rc;
-                c->split_frame = true;
-                c->split_na = na;
-                count = na;
-            }
-        }
+        c->frame_key = key;
+        c->frame_spec = split && key && c->split_spec;
         mark(c, GSR_STAGE_EMIT);
-        if (int rc = bin_locked(c, 0, count, c->split_frame ? 1 : 0, true)) return rc;
+        if (split) {
+            if (int rc = ensure_split(c)) return rc;
+            c->split_na = na;
+            const gsr::RowSplit rs{key ? 1 : 0, na};
+            if (int rc = bin_locked(c, 0, key ? n : na, 1, true, &rs)) return rc;
+        } else {
+            if (int rc = bin_locked(c, 0, n, 0, true)) return rc;
+        }
         mark(c, GSR_STAGE_RANGES);
         c->have_sort = true;
         return GSR_OK;
@@ -966,23 +1063,41 @@ static int blend_locked(gsr_context* c, float* d_out) {
         // depth split: blend phase A (saving the blocks it leaves unsaturated), bin the
         // rest of the depth order, resume those blocks; phase B's kernels return at once
         // on the device when phase A saturated every block
+        const uint32_t n = (uint32_t)c->n;
+        const bool key = c->frame_key;
+        if (key && (c->blend_exp != 0 || c->blend_variant == 3))
+            return set_err(GSR_E_ARG, "gsr_blend: blend knobs changed after a depth-split frame; render it again");
+        const gsr::RowSplit ra{key ? 1 : 0, c->split_na};
         if (c->split_rebin && c->blend_exp == 0 && c->blend_variant != 3) {
-            if (int rc = bin_locked(c, 0, c->split_na, 1, false)) return rc;
+            if (int rc = bin_locked(c, 0, key ? n : c->split_na, 1, false, &ra)) return rc;
         }
         if (c->blend_exp == 0 && c->blend_variant != 3) {
-            const uint32_t n = (uint32_t)c->n;
-            gsr::BlendSplit a{1, c->tbuf, c->bflag, c->gate, nullptr};
+            // phase A; its workgroup 0 also sets the next frame's threshold from the near
+            // depth order (key mode: the near part; count mode: the whole order)
+            const bool spec = c->frame_spec;
+            const gsr::SplitCut cut{c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr,
+                                    key ? c->nlive : nullptr, n, c->split_na, c->split_rebin ? nullptr : c->kcut};
+            gsr::BlendSplit a{1, c->tbuf, c->bflag, c->gate, nullptr, spec ? c->hstats_dev : nullptr, cut};
             HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
                                       c->diagnostics ? c->consumed : nullptr, false, c->blend_band_tiles, 0,
                                       c->stream, &a));
+            c->split_key_ready = true;
             mark(c, GSR_STAGE_RESUME);
-            if (int rc = bin_locked(c, c->split_na, n - c->split_na, 2, false)) return rc;
-            gsr::BlendSplit b{2, c->tbuf, c->bflag, c->gate, c->hstats_dev};
-            HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
-                                      c->diagnostics ? c->consumed : nullptr, false, c->blend_band_tiles, 0,
-                                      c->stream, &b));
+            if (!spec) {
+                // phase B: (key mode) sort the far part, then bin the rest of the order
+                const gsr::RowSplit rb{key ? 2 : 0, c->split_na};
+                if (key && !c->split_rebin) {
+                    if (int rc = far_sort_locked(c)) return rc;
+                }
+                if (int rc = bin_locked(c, key ? 0 : c->split_na, key ? n : n - c->split_na, 2, false, &rb, key))
+                    return rc;
+                gsr::BlendSplit b{2, c->tbuf, c->bflag, c->gate, c->hstats_dev, nullptr, {}};
+                HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
+                                          c->diagnostics ? c->consumed : nullptr, false, c->blend_band_tiles, 0,
+                                          c->stream, &b));
+                c->split_seen = true;
+            }
             c->split_rebin = true;
-            c->split_seen = true;
         } else {
             // knobs changed since the sort: bin the whole depth order again, one phase
             if (int rc = bin_locked(c, 0, (uint32_t)c->n, 0, false)) return rc;
@@ -1062,10 +1177,7 @@ void copy_settings(gsr_context* d, const gsr_context* s) {
     d->bin_col_groups = s->bin_col_groups;
     d->blend_band_tiles = s->blend_band_tiles;
     d->blend_exp = s->blend_exp;
-    d->depth_split = s->depth_split;
-    // the split point adapts per lane; each call starts the lanes from lane 0's
-    d->split_pm = s->split_pm;
-    d->split_floor = s->split_floor;
+    d->depth_split = s->depth_split;   // the split point adapts per lane (set at creation and by the knob)
     d->completion_events = s->completion_events;
     d->depth_compact = s->depth_compact;
     d->rank_atomic = s->rank_atomic;
@@ -1077,6 +1189,8 @@ int ensure_lanes(gsr_context* c, int F) {
     while ((int)c->lanes.size() < F - 1) {
         gsr_context* l = new gsr_context();
         l->inflight = 1;
+        l->split_pm = c->split_pm;
+        l->split_floor = c->split_floor;
         hipStream_t s = nullptr;
         hipEvent_t e = nullptr;
         if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
@@ -1276,7 +1390,11 @@ extern "C" int gsr_read_splats(gsr_context* c, void* host, int64_t n) {
     } else {
         HIP_TRY(hipMemcpy(rect.data(), c->rect, (size_t)n * 8, hipMemcpyDeviceToHost));
     }
-    if (c->have_sort) {
+    if (c->have_sort && c->last_split_key) {
+        // a key-mode split frame: items[0] holds every item (each region a permutation of
+        // its items), which is all the key lookup below needs
+        HIP_TRY(hipMemcpy(items.data(), c->items[0], (size_t)c->n * 8, hipMemcpyDeviceToHost));
+    } else if (c->have_sort) {
         if (int rc = sorted_items_locked(c, items.data(), c->n)) return rc;
     } else {   // preprocess order (items[1] when the frame is set up for the live partition)
         HIP_TRY(hipMemcpy(items.data(), c->items[c->compact_frame && !c->have_sort ? 1 : 0], (size_t)c->n * 8,
@@ -1323,6 +1441,9 @@ static int depth_passes_locked(gsr_context* c, int* passes) {
 
 // First n items of the last globally sorted frame's depth order (stream drained).
 static int sorted_items_locked(gsr_context* c, uint64_t* host, int64_t n) {
+    if (c->last_split_key)
+        return set_err(GSR_E_ARG, "depth order unavailable: the last frame was depth-split by a threshold (its far "
+                                  "part is sorted only when phase B runs); set GSR_TUNE_DEPTH_SPLIT to 0");
     int p = 4;
     if (int rc = depth_passes_locked(c, &p)) return rc;
     int64_t head = n;
@@ -1483,6 +1604,7 @@ extern "C" int gsr_get_tuning(gsr_context* c, int knob, int* value) {
     case GSR_TUNE_DEPTH_SPLIT: *value = c->depth_split; break;
     case GSR_TUNE_DEPTH_SPLIT_PERMILLE: *value = c->split_pm; break;
     case GSR_TUNE_DEPTH_SPLIT_UNSAT: *value = c->hstats ? (int)((const volatile Stats*)c->hstats)->split_unsat : 0; break;
+    case GSR_TUNE_DEPTH_SPLIT_STATE: *value = !c->split_frame ? 0 : !c->frame_key ? 1 : c->frame_spec ? 3 : 2; break;
     case GSR_TUNE_RANK_ATOMIC: *value = c->rank_atomic < 0 ? default_rank_atomic() : c->rank_atomic; break;
     case GSR_TUNE_RANK_ATOMIC_ACTIVE: {
         RankCheck rk;
@@ -1555,19 +1677,31 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     case GSR_TUNE_DEPTH_SPLIT:
         if (value < 0 || value > 2) return set_err(GSR_E_ARG, "gsr_set_tuning: depth split must be 0, 1 or 2");
         c->depth_split = value;
+        // the next split frame sorts the whole order (count mode), queues phase B
+        c->split_key_ready = c->split_spec = false;
+        for (auto* l : c->lanes) l->split_key_ready = l->split_spec = false;
         return GSR_OK;
     case GSR_TUNE_DEPTH_SPLIT_PERMILLE:
         if (value < 1 || value > 999) return set_err(GSR_E_ARG, "gsr_set_tuning: split point must be 1..999");
-        c->split_pm = value;
-        c->split_floor = 0;
-        c->split_clean = 0;
+    {
+        auto restart = [value](gsr_context* x) {   // a new starting point for every lane
+            x->split_pm = value;
+            x->split_floor = 0;
+            x->split_clean = 0;
+            x->split_spec = false;
+            x->split_key_ready = false;
+        };
+        restart(c);
+        for (auto* l : c->lanes) restart(l);
         return GSR_OK;
+    }
     case GSR_TUNE_RANK_ATOMIC:
         if (value != 0 && value != 1) return set_err(GSR_E_ARG, "gsr_set_tuning: rank path must be 0 or 1");
         c->rank_atomic = value;
         return GSR_OK;
     case GSR_TUNE_RANK_ATOMIC_ACTIVE:
     case GSR_TUNE_DEPTH_SPLIT_UNSAT:
+    case GSR_TUNE_DEPTH_SPLIT_STATE:
         return set_err(GSR_E_ARG, "gsr_set_tuning: knob %d is read-only", knob);
     case GSR_TUNE_TILE_SORT_GROUPS:
     case GSR_TUNE_DEPTH_SORT_GROUPS:

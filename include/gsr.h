@@ -321,15 +321,26 @@ enum {
                                         the nearest part of the depth order first and blend it (phase
                                         A), then bin the rest and resume only the 8x8 blocks phase A
                                         left unsaturated (phase B, skipped on the device when there are
-                                        none); the split point adapts to the frames seen.  0 = one phase;
-                                        2 (default) = 1 above 1.5M Gaussians.  Same image.  After a split
-                                        frame gsr_read_pairs / gsr_read_tile_ranges hold the lists of its
-                                        last phase */
+                                        none).  After the first split frame the items are partitioned
+                                        by a depth threshold and only the near part is sorted (phase B
+                                        sorts the far part when it runs); the split point adapts to the
+                                        frames seen, and once it cannot shrink further frames are
+                                        rendered without phase B until one needs it (that frame returns
+                                        GSR_E_OVERFLOW: render it again).  0 = one phase; 2 (default) =
+                                        1 above 1.5M Gaussians.  Same image.  After a split frame
+                                        gsr_read_pairs / gsr_read_tile_ranges hold the lists of its last
+                                        phase, and after a threshold split gsr_read_depth_order is refused */
     GSR_TUNE_DEPTH_SPLIT_PERMILLE = 24, /* the current split point: phase A bins the nearest
                                         ceil(n * value / 1000) of the depth order (adapted per frame; a
                                         set value is a new starting point, 1..999) */
-    GSR_TUNE_DEPTH_SPLIT_UNSAT = 25  /* read-only: 8x8 blocks the last completed split frame's phase A
+    GSR_TUNE_DEPTH_SPLIT_UNSAT = 25, /* read-only: 8x8 blocks the last completed split frame's phase A
                                         left unsaturated (0: its phase B did nothing); read after gsr_sync */
+    GSR_TUNE_DEPTH_SPLIT_STATE = 26  /* read-only: how the last sorted frame ran: 0 one phase; 1 split,
+                                        whole depth order sorted (count mode: the first split frame);
+                                        2 split by a depth threshold (near part sorted, far part sorted
+                                        in phase B); 3 as 2 with no phase B queued (speculative: a frame
+                                        that then leaves a block unsaturated is reported as
+                                        GSR_E_OVERFLOW and rendered again by the caller) */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Current value of a knob (what gsr_set_tuning last set, else the default). */

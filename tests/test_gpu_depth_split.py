@@ -20,7 +20,7 @@ from test_gpu_parity import CAMS, cam_for, render_gpu
 
 pytestmark = pytest.mark.gpu
 
-KNOB_SPLIT, KNOB_PM, KNOB_UNSAT = 23, 24, 25
+KNOB_SPLIT, KNOB_PM, KNOB_UNSAT, KNOB_STATE = 23, 24, 25, 26
 ORC_THREADS = min(16, len(os.sched_getaffinity(0)))
 
 
@@ -68,7 +68,8 @@ def test_depth_split_knobs(gpu):
     assert r.get_tuning(KNOB_SPLIT) == 2 and r.get_tuning(KNOB_PM) == 250
     r.set_tuning(KNOB_PM, 40)
     assert r.get_tuning(KNOB_PM) == 40
-    for bad in ((KNOB_SPLIT, 3), (KNOB_PM, 0), (KNOB_PM, 1000), (KNOB_UNSAT, 1)):
+    assert r.get_tuning(KNOB_STATE) == 0
+    for bad in ((KNOB_SPLIT, 3), (KNOB_PM, 0), (KNOB_PM, 1000), (KNOB_UNSAT, 1), (KNOB_STATE, 1)):
         with pytest.raises(gpu.GsrError):
             r.set_tuning(*bad)
 
@@ -93,6 +94,71 @@ def test_config3_split_points(gpu, orc, torch, c3, pm):
     assert_frames(img, want, exact=True)
     r.set_tuning(KNOB_PM, pm)
     check_takes(gpu, torch, r, scene, cam, W, H, want, takes)
+    r.close()
+
+
+@pytest.mark.parametrize("pm", [20, 60, 250])
+def test_config3_key_mode(gpu, orc, torch, c3, pm):
+    """Key mode: after the first split frame (which sorts the whole order and sets the
+    threshold), each frame partitions its items by a depth threshold and sorts only the
+    near part; phase B sorts the far part on its own, only when blocks are left
+    unsaturated.  Frames 2 and 3 at each split point: bit-exact, the oracle's take maps;
+    the whole depth order is then not readable."""
+    scene, soa, cam, W, H, want, takes = c3
+    r = split_renderer(gpu, 1, pm)
+    for _ in range(2):
+        img, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
+        assert_frames(img, want, exact=True)
+    unsat = r.get_tuning(KNOB_UNSAT)
+    assert (unsat > 0) if pm < 100 else (unsat == 0)
+    check_takes(gpu, torch, r, scene, cam, W, H, want, takes)
+    with pytest.raises(gpu.GsrError):
+        r.read_depth_order(soa.shape[1])
+    r.close()
+
+
+def test_config3_key_mode_camera_change(gpu, orc, torch, c3):
+    """The threshold comes from the previous frame; with another camera it is only a
+    worse guess (any threshold gives the same image): alternate two cameras."""
+    scene, soa, cam, W, H, want, _ = c3
+    cam2 = cam_for(gpu, W, H, **CAMS[2])
+    want2 = orc.render(soa, cam2, W, H, 3.0, threads=ORC_THREADS)
+    r = split_renderer(gpu, 1, 100)
+    for i in range(4):
+        img, _ = render_gpu(gpu, torch, scene, cam if i % 2 == 0 else cam2, W, H, renderer=r)
+        assert_frames(img, want if i % 2 == 0 else want2, exact=True)
+    r.close()
+
+
+def test_config3_speculation_and_miss(gpu, orc, torch, c3):
+    """From a split point too small for the scene the controller grows it (phase B runs),
+    then shrinks it to 5/4 of the last point that needed phase B and, when it cannot
+    shrink further, renders without phase B (state 3).  A frame that then leaves a
+    block unsaturated — here the camera moves back, so the previous frame's threshold
+    covers too little — is reported by gsr_sync as GSR_E_OVERFLOW; rendered again it is
+    bit-exact, and the controller has left speculation."""
+    scene, soa, cam, W, H, want, _ = c3
+    r = split_renderer(gpu, 2, 30)
+    out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    states, misses = [], 0
+    for i in range(120):
+        r.render(scene, cam, W, H, out.data_ptr())
+        while r.sync() != 0:                        # the re-render contract (pair buffer, misses)
+            misses += 1
+            assert misses < 10
+            r.render(scene, cam, W, H, out.data_ptr())
+        states.append(r.get_tuning(KNOB_STATE))
+        if states[-1] == 3 and states.count(3) >= 4:
+            break
+    assert 2 in states and states[-1] == 3, str(states)
+    assert_frames(out.view(3, H, W).cpu().numpy(), want, exact=True)
+    far = cam_for(gpu, W, H, pos=(0, 0, 7))
+    want_far = orc.render(soa, far, W, H, 3.0, threads=ORC_THREADS)
+    r.render(scene, far, W, H, out.data_ptr())
+    assert r.sync() != 0, "a speculative frame that needed phase B was not reported"
+    r.render(scene, far, W, H, out.data_ptr())
+    assert r.sync() == 0 and r.get_tuning(KNOB_STATE) == 2
+    assert_frames(out.view(3, H, W).cpu().numpy(), want_far, exact=True)
     r.close()
 
 
