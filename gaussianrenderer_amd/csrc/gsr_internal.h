@@ -53,6 +53,17 @@ struct Stats {
 // part of the depth order first (phase A); its blend saves the transmittance of
 // every block it leaves unsaturated, and phase B bins the rest of the depth order
 // and resumes those blocks.  phase: 1 = A (save), 2 = B (resume).
+// Depth split, key mode: the preprocess writes splat records only for Gaussians nearer
+// than the frame's threshold (mode 1; it copies *kcut to *kcut_frame for mode 2); mode
+// 2 (phase B, or a frame that ends up not split) writes only the far ones' records and
+// nothing else, and returns at once when *gate is 0 (gate nullptr: always runs).
+struct RecSplit {
+    int mode;
+    const uint32_t* kcut;
+    uint32_t* kcut_frame;
+    const uint32_t* gate;
+};
+
 // Depth split with a threshold partition (the near part sorted, the far part sorted
 // inside phase B): cut_mode 1 = the row pass reads [0, *cut), 2 = [*cut, n); na = the
 // host's split point (positions), sizes phase A's grid.
@@ -89,7 +100,8 @@ hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, 
                              hipStream_t s);
 hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
                              uint4* rec, uint64_t* items, uint64_t* rect, bool packed, bool four_d, bool sh3,
-                             float t, hipStream_t s, uint16_t* spans = nullptr);
+                             float t, hipStream_t s, uint16_t* spans = nullptr,
+                             const RecSplit* rs = nullptr);
 // One stable LSD pass over u64 items on bits [shift, shift + bits) (bits <= 8).
 // n = n_dev ? *n_dev : n_host.  hist: 256 * groups u32, totals: 256 u32.
 // ranges (nullable, final tile-sort pass): per-tile {~start, end} of key (item >> 32),

@@ -407,10 +407,16 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
                                                     int64_t n, Frame fr, uint4* __restrict__ rec,
                                                     uint64_t* __restrict__ items, uint64_t* __restrict__ rect,
                                                     int packed, uint16_t* __restrict__ spans,
-                                                    float tnow) {
+                                                    float tnow, RecSplit rs) {
     GSR_GEOM_PRIO();
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
+    // depth split, key mode (RecSplit): 1 = records of the near Gaussians only, 2 = the
+    // far ones' records only (no item, rect or span writes: those are sorted already)
+    const bool far_pass = rs.mode == 2;
+    if (far_pass && rs.gate && *rs.gate == 0u) return;
+    const uint32_t kcut = rs.mode == 1 ? *rs.kcut : far_pass ? *rs.kcut_frame : 0xffffffffu;
+    if (rs.mode == 1 && i == 0) *rs.kcut_frame = kcut;
     float gx = arr[GSR_A_X * stride + i];
     float gy = arr[GSR_A_Y * stride + i];
     float gz = arr[GSR_A_Z * stride + i];
@@ -442,14 +448,14 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
         for (int k = 0; k < 27; k++) sh_in[k] = arr[(GSR_A_SH0 + k) * stride + i];
     }
     uint4* R = rec + 4 * i;
-    items[i] = ((uint64_t)0xffffffffu << 32) | (uint64_t)(uint32_t)i;
+    if (!far_pass) items[i] = ((uint64_t)0xffffffffu << 32) | (uint64_t)(uint32_t)i;
 
     // ---- view + clip transform and cull (render.cu:535-556) ----
     const float old_xyz[4] = {gx, gy, gz, 1.0f};
     float tmp_xyz[4], new_xyz[4];
     mv4(fr.V, old_xyz, tmp_xyz);
     if (!isfinite(tmp_xyz[0]) || !isfinite(tmp_xyz[1]) || !isfinite(tmp_xyz[2])) {
-        put_rect(rect, i, kDeadRect, packed);
+        if (!far_pass) put_rect(rect, i, kDeadRect, packed);
         return;
     }
     mv4(fr.P, tmp_xyz, new_xyz);
@@ -458,7 +464,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     new_xyz[2] = new_xyz[2] / new_xyz[3];
     if (!isfinite(new_xyz[0]) || !isfinite(new_xyz[1]) || !isfinite(new_xyz[2]) ||
         tmp_xyz[2] >= -fr.znear || new_xyz[2] < -1.0f || new_xyz[2] > 1.0f) {
-        put_rect(rect, i, kDeadRect, packed);
+        if (!far_pass) put_rect(rect, i, kDeadRect, packed);
         return;
     }
 
@@ -505,7 +511,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     S2[3] = (H * 0.5f) * (H * 0.5f) * S2[3];
     const float det = S2[0] * S2[3] - S2[1] * S2[2];
     if (!isfinite(det) || det < 1e-8f) {                        // render.cu:690
-        put_rect(rect, i, kDeadRect, packed);
+        if (!far_pass) put_rect(rect, i, kDeadRect, packed);
         return;
     }
     const float invDet = 1.0f / det;
@@ -518,7 +524,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
         const float opt = op_in * tfac;
         const float hh = 0.5f * (ic1 + ic2);
         if (opt < 0.9e-3f && ic0 > 0.0f && ic3 > 0.0f && (ic0 * ic3 - hh * hh) > 1e-4f * (ic0 * ic3)) {
-            put_rect(rect, i, kDeadRect, packed);
+            if (!far_pass) put_rect(rect, i, kDeadRect, packed);
             return;
         }
     }
@@ -544,7 +550,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     float xmin = new_xyz[0] - ex, xmax = new_xyz[0] + ex;
     float ymin = new_xyz[1] - ey, ymax = new_xyz[1] + ey;
     if (xmax < -0.99f || xmin > 0.99f || ymax < -0.99f || ymin > 0.99f) {   // render.cu:737
-        put_rect(rect, i, kDeadRect, packed);
+        if (!far_pass) put_rect(rect, i, kDeadRect, packed);
         return;
     }
     xmin = fmaxf(xmin, -1.0f);
@@ -564,6 +570,15 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     const int tx1 = min(fr.tiles_x - 1, xmax_px / GSR_TILE_PX);
     const int ty0 = ymin_px / GSR_TILE_PX;
     const int ty1 = min(fr.tiles_y - 1, ymax_px / GSR_TILE_PX);
+    const uint64_t trect =
+        (uint64_t)((uint32_t)tx0 | ((uint32_t)tx1 << 16)) | ((uint64_t)((uint32_t)ty0 | ((uint32_t)ty1 << 16)) << 32);
+    if (rs.mode == 1 && key >= kcut && !spans) {
+        // far (key mode): no record unless phase B needs it (mode 2 writes it then)
+        put_rect(rect, i, trect, packed);
+        items[i] = ((uint64_t)key << 32) | (uint64_t)(uint32_t)i;
+        return;
+    }
+    if (far_pass && key < kcut) return;
 
     // ---- SH colour, bands 0..2 (render.cu:500-534), only for survivors ----
     float dir[3] = {gx - fr.campos[0], gy - fr.campos[1], gz - fr.campos[2]};
@@ -630,14 +645,13 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
                       (uint32_t)ymin_px | ((uint32_t)ymax_px << 16));
     const uint4 cw = cull_word(ic0, ic1, ic2, ic3, opacity, col[0], col[1], col[2]);
     R[3] = cw;
+    if (far_pass) return;
     if (spans)
         spans[i] = tile_row_spans((float)px_x, (float)px_y, ic0, ic1, ic2, ic3,
                                   cw.x == __float_as_uint(-__builtin_huge_valf()) ? __builtin_huge_valf()
                                                                                  : md2_cutoff(opacity),
                                   cw, xmin_px, xmax_px, ymin_px, ymax_px, tx0, tx1, ty0, ty1);
-    put_rect(rect, i,
-             (uint64_t)((uint32_t)tx0 | ((uint32_t)tx1 << 16)) | ((uint64_t)((uint32_t)ty0 | ((uint32_t)ty1 << 16)) << 32),
-             packed);
+    put_rect(rect, i, trect, packed);
     items[i] = ((uint64_t)key << 32) | (uint64_t)(uint32_t)i;
 }
 
@@ -2875,19 +2889,23 @@ hipError_t launch_aos_to_soa(const gsr_gaussian* aos, int64_t n, float* arrays, 
 
 hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, const Frame& fr,
                              uint4* rec, uint64_t* items, uint64_t* rect, bool packed, bool four_d, bool sh3,
-                             float t, hipStream_t s, uint16_t* spans) {
+                             float t, hipStream_t s, uint16_t* spans, const RecSplit* rsp) {
     if (n <= 0) return hipSuccess;
+    const RecSplit rs = rsp ? *rsp : RecSplit{0, nullptr, nullptr, nullptr};
+    if ((rs.mode == 1 && (!rs.kcut || !rs.kcut_frame || spans)) || (rs.mode == 2 && !rs.kcut_frame) || rs.mode < 0 ||
+        rs.mode > 2)
+        return hipErrorInvalidValue;
     const dim3 g(grid_for(n, 256));
     const int pk = packed ? 1 : 0;
     if (four_d)
         hipLaunchKernelGGL((k_preprocess<true, false>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect,
-                           pk, packed ? spans : nullptr, t);
+                           pk, packed ? spans : nullptr, t, rs);
     else if (sh3)
         hipLaunchKernelGGL((k_preprocess<false, true>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect,
-                           pk, packed ? spans : nullptr, t);
+                           pk, packed ? spans : nullptr, t, rs);
     else
         hipLaunchKernelGGL((k_preprocess<false, false>), g, dim3(256), 0, s, arrays, stride, n, fr, rec, items, rect,
-                           pk, packed ? spans : nullptr, t);
+                           pk, packed ? spans : nullptr, t, rs);
     return hipGetLastError();
 }
 

@@ -399,6 +399,11 @@ struct gsr_context {
     bool split_key_ready = false;    // *kcut holds a threshold from an earlier split frame of this context
     bool last_split_key = false;     // the last sorted frame left its far part unsorted (phase B may not run)
     uint32_t* kcut = nullptr;        // depth split: the next frame's depth threshold (device word)
+    uint32_t* kcut_frame = nullptr;  // depth split: this frame's threshold (the preprocess copies it)
+    bool records_partial = false;    // the preprocess wrote only the near Gaussians' records
+    const float* pre_arrays = nullptr;   // the preprocessed scene arrays (the far record pass re-reads them)
+    int64_t pre_stride = 0;
+    int pre_layout = 0;
     uint32_t* dstats_far = nullptr;  // depth split: the far sort's pass plan
     int far_launched = 4;            // passes the far sort launched
     float* tbuf = nullptr;           // depth split: saved transmittance, 64 floats per 8x8 block
@@ -523,6 +528,7 @@ int ensure_static(gsr_context* c) {
     if (int rc = realloc_dev(&c->binmeta, 256 + 128)) return rc;
     if (int rc = realloc_dev(&c->gate, 1)) return rc;
     if (int rc = realloc_dev(&c->kcut, 1)) return rc;
+    if (int rc = realloc_dev(&c->kcut_frame, 1)) return rc;
     if (int rc = realloc_dev(&c->dstats_far, 4 + 4 * (size_t)gsr::kMaxSortGroups)) return rc;
     HIP_TRY(hipMemset(c->kcut, 0xff, sizeof(uint32_t)));
     HIP_TRY(hipMemset(c->stats, 0, 2 * sizeof(Stats)));
@@ -761,7 +767,7 @@ extern "C" void gsr_destroy(gsr_context* c) {
                     (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->dstats,
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
                     (void*)c->cbins, (void*)c->srect, (void*)c->spans, (void*)c->nlive, (void*)c->tbuf,
-                    (void*)c->bflag, (void*)c->gate, (void*)c->kcut, (void*)c->dstats_far})
+                    (void*)c->bflag, (void*)c->gate, (void*)c->kcut, (void*)c->dstats_far, (void*)c->kcut_frame})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -828,11 +834,18 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     // config 2 (1M) +0.8 % one frame at a time, +1.2 % in flight; config 5 (2M) -1 % in
     // flight, config 3 (5M) -3 / -6 % (profiles/r02_ab_tile_spans.txt)
     c->spans_frame = c->rect_packed && (c->tile_spans == 1 || (c->tile_spans == 2 && n <= kLargeScene));
+    // key mode: records only for the Gaussians nearer than the threshold (the far ones
+    // are written by a second pass if phase B or a one-phase sort needs them)
+    c->records_partial = c->split_key && !c->spans_frame;
+    c->pre_arrays = arrays;
+    c->pre_stride = stride;
+    c->pre_layout = layout;
+    const gsr::RecSplit rsp{c->records_partial ? 1 : 0, c->kcut, c->kcut_frame, nullptr};
     HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[c->compact_frame || c->split_key ? 1 : 0],
                                    c->rect,
                                    c->rect_packed, layout == GSR_LAYOUT_SCENE_BLOCK_4D,
                                    layout == GSR_LAYOUT_SCENE_BLOCK_SH3, c->time, c->stream,
-                                   c->spans_frame ? c->spans : nullptr));
+                                   c->spans_frame ? c->spans : nullptr, &rsp));
     c->have_pre = true;
     c->have_sort = false;
     return rc_over;
@@ -929,6 +942,18 @@ static int far_sort_locked(gsr_context* c) {
     return GSR_OK;
 }
 
+// The far Gaussians' records, when the preprocess wrote only the near ones (key mode):
+// gated = phase B (returns at once when phase A saturated every block), else always.
+static int far_records_locked(gsr_context* c, bool gated) {
+    if (!c->records_partial) return GSR_OK;
+    const gsr::RecSplit rsp{2, nullptr, c->kcut_frame, gated ? c->gate : nullptr};
+    HIP_TRY(gsr::launch_preprocess(c->pre_arrays, c->pre_stride, c->n, c->fr, c->rec, c->items[0], c->rect,
+                                   c->rect_packed, c->pre_layout == GSR_LAYOUT_SCENE_BLOCK_4D,
+                                   c->pre_layout == GSR_LAYOUT_SCENE_BLOCK_SH3, c->time, c->stream, nullptr, &rsp));
+    if (!gated) c->records_partial = false;
+    return GSR_OK;
+}
+
 // Row pass, then column pass (gsr_kernels.hip "tile binning") over the depth-order
 // positions [base, base + count): tile lists in pair_vals(c, 1), ranges.  gate_mode:
 // 0 plain; 1 = depth split phase A (clears the gate); 2 = phase B (every kernel returns
@@ -988,6 +1013,9 @@ static int sort_locked(gsr_context* c, bool allow_split) {
         c->compact_frame = false;
     }
     const bool key = split && c->split_key;
+    if (!key) {   // a frame preprocessed for key mode that is not split that way: all records
+        if (int rc = far_records_locked(c, false)) return rc;
+    }
     // ---- stable depth sort of (key << 32 | index), 4 x 8 bits; for the binning
     // path the passes carry the rects, depth-ordered at the end (pay_buf) ----
     mark(c, GSR_STAGE_DEPTH_SORT);
@@ -1088,6 +1116,7 @@ static int blend_locked(gsr_context* c, float* d_out) {
                 const gsr::RowSplit rb{key ? 2 : 0, c->split_na};
                 if (key && !c->split_rebin) {
                     if (int rc = far_sort_locked(c)) return rc;
+                    if (int rc = far_records_locked(c, true)) return rc;
                 }
                 if (int rc = bin_locked(c, key ? 0 : c->split_na, key ? n : n - c->split_na, 2, false, &rb, key))
                     return rc;
@@ -1379,6 +1408,10 @@ extern "C" int gsr_read_splats(gsr_context* c, void* host, int64_t n) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (!n) return GSR_OK;
     if (!c->have_pre) return set_err(GSR_E_ARG, "gsr_read_splats: no preprocessed frame");
+    if (c->records_partial) {   // key-mode split frame: the far Gaussians' records first
+        if (int rc = far_records_locked(c, false)) return rc;
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
     HIP_TRY(hipMemcpy(host, c->rec, (size_t)n * GSR_SPLAT_RECORD_BYTES, hipMemcpyDeviceToHost));
     std::vector<uint64_t> rect((size_t)n), items((size_t)c->n);
     if (c->rect_packed) {   // 4-B rects (gsr_kernels.hip pack_rect): tx0 | tx1 << 8 | ty0 << 16 | ty1 << 24

@@ -117,6 +117,27 @@ def test_config3_key_mode(gpu, orc, torch, c3, pm):
     r.close()
 
 
+def test_key_mode_records(gpu, orc, torch, c3):
+    """In key mode the preprocess writes records only for the Gaussians nearer than the
+    threshold; phase B (or gsr_read_splats) writes the far ones.  The records read back
+    after a key-mode frame equal those of a frame without the split."""
+    scene, soa, cam, W, H, want, _ = c3
+    n = soa.shape[1]
+    r0 = split_renderer(gpu, 0)
+    render_gpu(gpu, torch, scene, cam, W, H, renderer=r0)
+    ref = r0.read_splats(n)
+    r = split_renderer(gpu, 1, 250)
+    for _ in range(3):
+        img, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
+    assert r.get_tuning(KNOB_STATE) in (2, 3)
+    assert_frames(img, want, exact=True)
+    got = r.read_splats(n)
+    vis = ref["depth_key"] != 0xFFFFFFFF
+    assert vis.sum() > 4_000_000 and got[vis].tobytes() == ref[vis].tobytes()
+    for x in (r0, r):
+        x.close()
+
+
 def test_config3_key_mode_camera_change(gpu, orc, torch, c3):
     """The threshold comes from the previous frame; with another camera it is only a
     worse guess (any threshold gives the same image): alternate two cameras."""
