@@ -3,7 +3,8 @@ two-phase binning would list if phase A bins only the nearest fraction f of the
 depth-ordered visible splats and phase B bins the rest for the tiles that phase A
 did not saturate (every pixel's transmittance below 1e-3).  Oracle records, AABB
 tile rects (no tile row spans).  N, W, H, SEED from the environment (config 3 by
-default)."""
+default); FOURD=1 with T: config 5's 4D scene at time T (no temporal cull: 8 % of
+its pixels saturate, no tile does, so the split turns itself off there)."""
 import ctypes, os, subprocess, sys, time
 import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -19,10 +20,13 @@ if not os.path.exists(so):
     subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-fopenmp", "-shared", "-fPIC",
                            "-I" + os.path.join(ROOT, "include"), os.path.join(HERE, "depth_split.c"),
                            "-o", so, "-lm"])
-ply = f"/tmp/sim_{n}_s{seed}.ply"
+four_d = os.environ.get("FOURD", "0") == "1"     # config 5: a 4D scene at time T (default 0.5)
+ply = f"/tmp/sim_{n}_s{seed}{'_4d' if four_d else ''}.ply"
 if not os.path.exists(ply):
-    gsr.write_synthetic_ply(ply, n, seed)
-soa = gsr.read_ply(ply)
+    (gsr.write_synthetic_ply4d if four_d else gsr.write_synthetic_ply)(ply, n, seed)
+soa = gsr.read_ply(ply, four_d=four_d)
+if four_d:
+    soa = orc.temporal(soa, float(os.environ.get("T", 0.5)))
 cam = gsr.make_camera(position=(0, 0, 4), fov_y=50, aspect=W / H)
 t0 = time.time()
 sp = orc.preprocess(soa, cam, W, H, 3.0)
