@@ -53,6 +53,17 @@ struct Stats {
 // part of the depth order first (phase A); its blend saves the transmittance of
 // every block it leaves unsaturated, and phase B bins the rest of the depth order
 // and resumes those blocks.  phase: 1 = A (save), 2 = B (resume).
+// Depth split, key mode: pass 0 of a depth sort reads the whole preprocess order and
+// keeps key < *kcut (mode 1, the near part: the kept count goes to *count_out and the
+// threshold is copied to *kcut_copy) or key >= *kcut (mode 2, the far part, written from
+// the pass's base).
+struct SortFilter {
+    int mode;
+    const uint32_t* kcut;
+    uint32_t* count_out;
+    uint32_t* kcut_copy;
+};
+
 // Depth split, key mode: the preprocess writes splat records only for Gaussians nearer
 // than the frame's threshold (mode 1; it copies *kcut to *kcut_frame for mode 2); mode
 // 2 (phase B, or a frame that ends up not split) writes only the far ones' records and
@@ -114,7 +125,8 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
                              uint2* ranges, hipStream_t s, uint32_t* dstats = nullptr, int pass = 0,
                              const uint32_t* rect = nullptr, int rect_direct = 0, uint32_t* pay0 = nullptr,
                              uint32_t* pay1 = nullptr, bool rank_atomic = false,
-                             const uint32_t* base_dev = nullptr, const uint32_t* gate = nullptr);
+                             const uint32_t* base_dev = nullptr, const uint32_t* gate = nullptr,
+                             const SortFilter* filter = nullptr);
 // Pair emission in depth order: tile counts (gathering each Gaussian's rect
 // once into srect, and zeroing the tile ranges), scan, then keys (uint16_t if
 // key16 else uint32_t) + values.
@@ -141,8 +153,7 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
 // index order), visible count into *n_live; culled tail to out only, with dead
 // rects in srect (gsr_kernels.hip "live partition").  counts: groups words.
 hipError_t launch_partition(const uint64_t* in, uint32_t n, int groups, uint32_t* counts, uint32_t* n_live,
-                            uint64_t* out, const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, hipStream_t s,
-                            const uint32_t* kcut = nullptr);
+                            uint64_t* out, const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, hipStream_t s);
 // Tile binning (row pass + column pass, tile grids <= 256 x 256): replaces
 // launch_emit + the key-value tile sort.  hist: 512 x groups; row_items /
 // row_pairs: 256 each; cbins: 256 x bin_col_chunks_max(); rows_buf: pair

@@ -416,6 +416,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     const bool far_pass = rs.mode == 2;
     if (far_pass && rs.gate && *rs.gate == 0u) return;
     const uint32_t kcut = rs.mode == 1 ? *rs.kcut : far_pass ? *rs.kcut_frame : 0xffffffffu;
+    // the frame's threshold, for the far record pass (the near sort copies it too)
     if (rs.mode == 1 && i == 0) *rs.kcut_frame = kcut;
     float gx = arr[GSR_A_X * stride + i];
     float gy = arr[GSR_A_Y * stride + i];
@@ -716,13 +717,27 @@ __device__ __forceinline__ int depth_passes_run(const uint32_t* __restrict__ dst
     return p;
 }
 
-// SortRange: the depth split's far part — positions [*base, n_host) sorted on their own
-// (base != nullptr; n_dev is then unused), and every kernel of the pass returns at once
-// when *gate is 0 (phase B not needed).
+// SortRange (depth split, key mode; all fields null / 0 otherwise):
+//   base   the far part's positions [*base, n_host) are sorted on their own (n_dev unused)
+//   gate   every kernel of the pass returns at once when *gate is 0 (phase B not needed)
+//   filter pass 0 reads all n_host items of the preprocess order and keeps only those with
+//          key < *kcut (1, the near part) or key >= *kcut (2, the far part), written from
+//          position 0 (near) or *base (far); the near pass's downsweep stores the kept
+//          count in *count_out, and its upsweep copies *kcut to *kcut_copy (the frame's
+//          threshold, for phase B)
 struct SortRange {
     const uint32_t* base;
     const uint32_t* gate;
+    const uint32_t* kcut;
+    int filter;
+    uint32_t* count_out;
+    uint32_t* kcut_copy;
 };
+
+__device__ __forceinline__ bool sort_keep(const SortRange& sr, uint32_t K, uint64_t v) {
+    const uint32_t k = (uint32_t)(v >> 32);
+    return sr.filter == 0 || (sr.filter == 1 ? k < K : k >= K);
+}
 
 template <int ITEMS>
 __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* __restrict__ in,
@@ -732,7 +747,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
                                                                 uint32_t* __restrict__ dstats, int pass,
                                                                 SortRange sr) {
     GSR_GEOM_PRIO();
-    __shared__ uint32_t h[4][256];
+    __shared__ uint32_t h[4][257];   // [256]: items a filtered pass 0 drops
     __shared__ uint32_t s_st[4];
     if (sr.gate && *sr.gate == 0u) return;
     if (depth_pass_skipped(dstats, pass)) return;
@@ -744,14 +759,19 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
 #pragma unroll
     for (int k = 0; k < 4; k++) h[k][t] = 0;
     __syncthreads();
+    const uint32_t K = sr.filter ? *sr.kcut : 0u;
+    if (sr.filter == 1 && sr.kcut_copy && blockIdx.x == 0 && t == 0) *sr.kcut_copy = K;
     const uint32_t base = sr.base ? *sr.base : 0u;
-    in += base;
-    const uint64_t n = sr.base ? (uint64_t)(n_host - min(base, n_host)) : n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
+    if (!sr.filter) in += base;
+    const uint64_t n = sr.filter ? (uint64_t)n_host
+                                 : sr.base ? (uint64_t)(n_host - min(base, n_host)) : n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, kSortThreads * ITEMS, b, e);
+    // the digit's counter, or the drop counter for an item a filtered pass 0 does not keep
+    auto dig = [&](uint64_t v) { return sort_keep(sr, K, v) ? ((uint32_t)(v >> shift) & mask) : 256u; };
     auto note = [&](uint64_t v) {
         const uint32_t k = (uint32_t)(v >> 32);
-        if (k != 0xffffffffu) {
+        if (k != 0xffffffffu && sort_keep(sr, K, v)) {
             inv_min = max(inv_min, ~k);
             kmax = max(kmax, k);
             any = 1u;
@@ -763,10 +783,10 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
     for (; i + 3 * kSortThreads < e; i += 4 * kSortThreads) {
         const uint64_t v0 = in[i], v1 = in[i + kSortThreads], v2 = in[i + 2 * kSortThreads],
                        v3 = in[i + 3 * kSortThreads];
-        atomicAdd(&h[w][(uint32_t)(v0 >> shift) & mask], 1u);
-        atomicAdd(&h[w][(uint32_t)(v1 >> shift) & mask], 1u);
-        atomicAdd(&h[w][(uint32_t)(v2 >> shift) & mask], 1u);
-        atomicAdd(&h[w][(uint32_t)(v3 >> shift) & mask], 1u);
+        atomicAdd(&h[w][dig(v0)], 1u);
+        atomicAdd(&h[w][dig(v1)], 1u);
+        atomicAdd(&h[w][dig(v2)], 1u);
+        atomicAdd(&h[w][dig(v3)], 1u);
         if (plan) {
             note(v0);
             note(v1);
@@ -776,7 +796,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
     }
     for (; i < e; i += kSortThreads) {
         const uint64_t v = in[i];
-        atomicAdd(&h[w][(uint32_t)(v >> shift) & mask], 1u);
+        atomicAdd(&h[w][dig(v)], 1u);
         if (plan) note(v);
     }
     if (plan) {   // wave reductions first: one LDS atomic per wave and word
@@ -873,13 +893,16 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     __shared__ uint64_t s_items[kTile];
     if (sr.gate && *sr.gate == 0u) return;
     if (depth_pass_skipped(dstats, pass)) return;
-    if (sr.base) {   // far part: every position-indexed array starts at *base (rect_direct is 0)
+    if (sr.base) {   // far part: the outputs start at *base, and so do the inputs unless filtered
         const uint32_t base = *sr.base;
-        in += base;
         out += base;
-        if (pay_in) pay_in += base;
         if (pay_out) pay_out += base;
+        if (!sr.filter) {
+            in += base;
+            if (pay_in) pay_in += base;
+        }
     }
+    const uint32_t K = sr.filter ? *sr.kcut : 0u;
     const bool carry = pay_out != nullptr;
     __shared__ uint32_t s_wc[4][256];           // per-wave digit counters, then wave bases
     __shared__ uint32_t s_gbase[256];           // running global offset per digit
@@ -894,18 +917,21 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const uint32_t lane = lane_id();
     const uint32_t w = t >> 6;
     const uint32_t mask = (1u << bits) - 1u;
-    const uint64_t n = sr.base ? (uint64_t)(n_host - min(*sr.base, n_host)) : n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
+    const uint64_t n = sr.filter ? (uint64_t)n_host
+                                 : sr.base ? (uint64_t)(n_host - min(*sr.base, n_host)) : n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
     uint64_t b, e;
     const int chunk = GSR_XCD_DEPTH && ITEMS == 16 ? xcd_chunk((int)blockIdx.x, groups) : (int)blockIdx.x;
     chunk_range(n, groups, chunk, kTile, b, e);
-    if (b >= e) return;                          // uniform per workgroup
 
-    // global base of each digit for this workgroup
+    // global base of each digit for this workgroup (a filtered pass 0: the kept count is
+    // the sum of the digit totals)
     {
         uint32_t tot;
         const uint32_t dig_excl = block_exclusive_scan<uint32_t>(totals[t], s_scr, tot);
         s_gbase[t] = dig_excl + hist[t * (uint32_t)groups + chunk];
+        if (sr.count_out && blockIdx.x == 0 && t == 0) *sr.count_out = tot;
     }
+    if (b >= e) return;                          // uniform per workgroup
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
     for (uint64_t tb = b; tb < e; tb += kTile) {
@@ -916,6 +942,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
 
         uint64_t it[ITEMS];
         uint32_t rk[ITEMS], pv[ITEMS];
+        bool kp[ITEMS];   // in the tile and kept (a filtered pass 0 drops the other part)
         const uint32_t wbase = w * 64 * ITEMS;
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
@@ -942,7 +969,8 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
             const uint32_t el = wbase + k * 64 + lane;
-            const bool valid = el < tn;
+            const bool valid = el < tn && sort_keep(sr, K, it[k]);
+            kp[k] = valid;
             const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
             uint32_t r = 0;
             // returning atomics at 4-8 items per thread; at 16 (4M+ items) ballot matching
@@ -962,7 +990,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
         }
         __syncthreads();
         // per digit t: exclusive prefix over the four waves, tile count, tile-local base
-        uint32_t tcount;
+        uint32_t tcount, tv;   // tv: the tile's kept items (tn unless filtered)
         {
             const uint32_t c0 = s_wc[0][t], c1 = s_wc[1][t], c2 = s_wc[2][t], c3 = s_wc[3][t];
             s_wc[0][t] = 0;
@@ -970,14 +998,12 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
             s_wc[2][t] = c0 + c1;
             s_wc[3][t] = c0 + c1 + c2;
             tcount = c0 + c1 + c2 + c3;
-            uint32_t tot;
-            s_lbase[t] = block_exclusive_scan<uint32_t>(tcount, s_scr, tot);
+            s_lbase[t] = block_exclusive_scan<uint32_t>(tcount, s_scr, tv);
         }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
-            const uint32_t el = wbase + k * 64 + lane;
-            if (el < tn) {
+            if (kp[k]) {
                 const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
                 const uint32_t slot = s_lbase[d] + s_wc[w][d] + rk[k];
                 s_items[slot] = it[k];
@@ -989,7 +1015,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
             const uint32_t q = t + k * kSortThreads;
-            if (q < tn) {
+            if (q < tv) {
                 const uint64_t v = s_items[q];
                 const uint32_t d = (uint32_t)(v >> shift) & mask;
                 const uint32_t dst = s_gbase[d] + (q - s_lbase[d]);
@@ -1003,7 +1029,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
                     // (replaces a separate boundary-detection kernel).
                     const uint32_t key = (uint32_t)(v >> 32);
                     if (q == 0 || (uint32_t)(s_items[q - 1] >> 32) != key) atomicMax(&ranges[key].x, ~dst);
-                    if (q == tn - 1 || (uint32_t)(s_items[q + 1] >> 32) != key) atomicMax(&ranges[key].y, dst + 1);
+                    if (q == tv - 1 || (uint32_t)(s_items[q + 1] >> 32) != key) atomicMax(&ranges[key].y, dst + 1);
                 }
             }
         }
@@ -1014,8 +1040,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < ITEMS; k++) {
-                const uint32_t el = wbase + k * 64 + lane;
-                if (el < tn) {
+                if (kp[k]) {
                     const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
                     s_pay[s_lbase[d] + s_wc[w][d] + rk[k]] = pv[k];
                 }
@@ -1024,7 +1049,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
 #pragma unroll
             for (int k = 0; k < ITEMS; k++) {
                 const uint32_t q = t + k * kSortThreads;
-                if (q < tn) pay_out[dq[k]] = s_pay[q];
+                if (q < tv) pay_out[dq[k]] = s_pay[q];
             }
         }
         __syncthreads();
@@ -2035,18 +2060,14 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
 // ends depth-ordered is decided on the device); the binning never reads items whose
 // rect is dead, and gsr_read_depth_order takes the tail from `out`.  Three launches: per-chunk
 // visible counts, their exclusive scan (+ total), the scatter.
-// kcut (nullable): the depth split's threshold — items with key < *kcut come first
-// (the near part), the rest after with their real rects in pay0 (phase B sorts them);
-// without it the threshold is 0xFFFFFFFF (the live partition).
 __global__ __launch_bounds__(256) void k_part_count(const uint64_t* __restrict__ in, uint32_t n, int groups,
-                                                     uint32_t* __restrict__ counts, const uint32_t* __restrict__ kcut) {
+                                                     uint32_t* __restrict__ counts) {
     GSR_GEOM_PRIO();
     __shared__ uint32_t s_scr[4];
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, 256, b, e);
-    const uint32_t K = kcut ? *kcut : 0xffffffffu;
     uint32_t c = 0;
-    for (uint64_t i = b + threadIdx.x; i < e; i += 256) c += (uint32_t)(in[i] >> 32) < K ? 1u : 0u;
+    for (uint64_t i = b + threadIdx.x; i < e; i += 256) c += (uint32_t)(in[i] >> 32) != 0xffffffffu ? 1u : 0u;
     uint32_t tot;
     (void)block_exclusive_scan<uint32_t>(c, s_scr, tot);
     if (threadIdx.x == 0) counts[blockIdx.x] = tot;
@@ -2077,11 +2098,9 @@ __global__ __launch_bounds__(256) void k_part_scatter(const uint64_t* __restrict
                                                        const uint32_t* __restrict__ n_live,
                                                        uint64_t* __restrict__ out,
                                                        const uint32_t* __restrict__ rect,
-                                                       uint32_t* __restrict__ pay0, uint32_t* __restrict__ pay1,
-                                                       const uint32_t* __restrict__ kcut) {
+                                                       uint32_t* __restrict__ pay0, uint32_t* __restrict__ pay1) {
     GSR_GEOM_PRIO();
     __shared__ uint32_t s_w[4];
-    const uint32_t K = kcut ? *kcut : 0xffffffffu;
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, 256, b, e);
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
@@ -2093,7 +2112,7 @@ __global__ __launch_bounds__(256) void k_part_scatter(const uint64_t* __restrict
         const uint64_t i = c0 + t;
         const bool valid = i < e;
         const uint64_t v = valid ? in[i] : 0ull;
-        const bool live = valid && (uint32_t)(v >> 32) < K;
+        const bool live = valid && (uint32_t)(v >> 32) != 0xffffffffu;
         const bool dead = valid && !live;
         const uint64_t bl = __ballot(live), bd = __ballot(dead);
         if (lane == 0) s_w[w] = (uint32_t)__popcll(bl) | ((uint32_t)__popcll(bd) << 16);
@@ -2117,12 +2136,8 @@ __global__ __launch_bounds__(256) void k_part_scatter(const uint64_t* __restrict
         if (dead) {
             const uint32_t q = dead_base + db + (uint32_t)__popcll(bd & lt);
             out[q] = v;
-            if (kcut) {
-                pay0[q] = rect[(uint32_t)v];      // the far part: phase B's sort pass 0 reads pay0
-            } else {
-                pay0[q] = pack_rect(kDeadRect);   // the sort's result parity is decided on the device
-                pay1[q] = pack_rect(kDeadRect);
-            }
+            pay0[q] = pack_rect(kDeadRect);   // the sort's result parity is decided on the device
+            pay1[q] = pack_rect(kDeadRect);
         }
         live_base += ltot;
         dead_base += dtot;
@@ -2932,11 +2947,15 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
                              int shift, int bits, int groups, int items, uint32_t* hist, uint32_t* totals,
                              uint2* ranges, hipStream_t s, uint32_t* dstats, int pass, const uint32_t* rect,
                              int rect_direct, uint32_t* pay0, uint32_t* pay1, bool rank_atomic,
-                             const uint32_t* base_dev, const uint32_t* gate) {
+                             const uint32_t* base_dev, const uint32_t* gate, const SortFilter* f) {
     if ((rect == nullptr) != (pay0 == nullptr) || (pay0 == nullptr) != (pay1 == nullptr))
         return hipErrorInvalidValue;
-    if (base_dev && (n_dev || rect_direct > 0)) return hipErrorInvalidValue;
-    const SortRange sr{base_dev, gate};
+    const int filter = f ? f->mode : 0;
+    if (filter < 0 || filter > 2 || (filter && (pass != 0 || !f->kcut || n_dev || (filter == 2) != (base_dev != nullptr))))
+        return hipErrorInvalidValue;
+    if (base_dev && !filter && (n_dev || rect_direct > 0)) return hipErrorInvalidValue;
+    const SortRange sr{base_dev, gate, filter ? f->kcut : nullptr, filter, filter == 1 ? f->count_out : nullptr,
+                       filter == 1 ? f->kcut_copy : nullptr};
     // 16 items per thread always rank with ballots (k_radix_downsweep)
     if (items == 4 && rank_atomic)
         radix_pass<4, true>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
@@ -2974,13 +2993,12 @@ hipError_t launch_emit(const uint64_t* items0, const uint64_t* items1, const uin
 }
 
 hipError_t launch_partition(const uint64_t* in, uint32_t n, int groups, uint32_t* counts, uint32_t* n_live,
-                            uint64_t* out, const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, hipStream_t s,
-                            const uint32_t* kcut) {
+                            uint64_t* out, const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, hipStream_t s) {
     if (groups < 1 || groups > kMaxSortGroups) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_part_count, dim3(groups), dim3(256), 0, s, in, n, groups, counts, kcut);
+    hipLaunchKernelGGL(k_part_count, dim3(groups), dim3(256), 0, s, in, n, groups, counts);
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(256), 0, s, counts, groups, n_live);
     hipLaunchKernelGGL(k_part_scatter, dim3(groups), dim3(256), 0, s, in, n, groups, counts, n_live, out, rect,
-                       pay0, pay1, kcut);
+                       pay0, pay1);
     return hipGetLastError();
 }
 

@@ -399,7 +399,10 @@ struct gsr_context {
     bool split_key_ready = false;    // *kcut holds a threshold from an earlier split frame of this context
     bool last_split_key = false;     // the last sorted frame left its far part unsorted (phase B may not run)
     uint32_t* kcut = nullptr;        // depth split: the next frame's depth threshold (device word)
-    uint32_t* kcut_frame = nullptr;  // depth split: this frame's threshold (the preprocess copies it)
+    uint32_t* kcut_frame = nullptr;  // depth split: this frame's threshold (the near sort copies it)
+    uint64_t* src_items = nullptr;   // depth split, key mode: the preprocess order (both sorts' pass 0 read it)
+    int64_t src_cap = 0;
+    uint64_t* pre_out = nullptr;     // where the preprocess wrote its items
     bool records_partial = false;    // the preprocess wrote only the near Gaussians' records
     const float* pre_arrays = nullptr;   // the preprocessed scene arrays (the far record pass re-reads them)
     int64_t pre_stride = 0;
@@ -574,6 +577,15 @@ int ensure_tiles(gsr_context* c, int64_t t) {
     HIP_TRY(hipDeviceSynchronize());
     if (int rc = realloc_dev(&c->ranges, (size_t)t)) return rc;
     c->t_cap = t;
+    return GSR_OK;
+}
+
+// Depth split, key mode: the preprocess order of n items.
+int ensure_src(gsr_context* c, int64_t n) {
+    if (n <= c->src_cap) return GSR_OK;
+    HIP_TRY(hipDeviceSynchronize());
+    if (int rc = realloc_dev(&c->src_items, (size_t)std::max<int64_t>(n, 1024))) return rc;
+    c->src_cap = std::max<int64_t>(n, 1024);
     return GSR_OK;
 }
 
@@ -767,7 +779,8 @@ extern "C" void gsr_destroy(gsr_context* c) {
                     (void*)c->pairs[1], (void*)c->hist, (void*)c->totals, (void*)c->wg, (void*)c->stats, (void*)c->dstats,
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
                     (void*)c->cbins, (void*)c->srect, (void*)c->spans, (void*)c->nlive, (void*)c->tbuf,
-                    (void*)c->bflag, (void*)c->gate, (void*)c->kcut, (void*)c->dstats_far, (void*)c->kcut_frame})
+                    (void*)c->bflag, (void*)c->gate, (void*)c->kcut, (void*)c->dstats_far, (void*)c->kcut_frame,
+                    (void*)c->src_items})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -841,7 +854,11 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     c->pre_stride = stride;
     c->pre_layout = layout;
     const gsr::RecSplit rsp{c->records_partial ? 1 : 0, c->kcut, c->kcut_frame, nullptr};
-    HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->items[c->compact_frame || c->split_key ? 1 : 0],
+    if (c->split_key) {
+        if (int rc = ensure_src(c, n)) return rc;
+    }
+    c->pre_out = c->split_key ? c->src_items : c->items[c->compact_frame ? 1 : 0];
+    HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->pre_out,
                                    c->rect,
                                    c->rect_packed, layout == GSR_LAYOUT_SCENE_BLOCK_4D,
                                    layout == GSR_LAYOUT_SCENE_BLOCK_SH3, c->time, c->stream,
@@ -883,29 +900,35 @@ static int depth_sort_locked(gsr_context* c, bool with_rects) {
     // smaller tiles for the 1M-item depth sort: ~500 workgroups instead of ~250 (-2.6 %
     // frame time one at a time; in flight 8 and 16 measure within 1.5 % of each other,
     // either way round: profiles/r02_ab_depth_items.txt)
-    // depth split, threshold partition: the passes sort only the near part (about
-    // 2 x the split point's items; the far part is sorted inside phase B)
+    // depth split, key mode: pass 0 reads the whole preprocess order (src_items) and keeps
+    // the keys below the threshold; the passes sort only that near part (its count goes to
+    // nlive; about 2 x the split point's items), the far part is sorted inside phase B
     const bool key = with_rects && c->split_key;
     const int64_t n_sorted =
         key ? std::min<int64_t>(c->n, std::max<int64_t>(2 * ((int64_t)c->n * c->split_pm / 1000), 65536)) : c->n;
     const int di = c->depth_items ? c->depth_items : (n_sorted < (int64_t(4) << 20) ? 8 : 16);
-    int gd = groups_for(n_sorted, 256 * di);
-    if (c->depth_groups) gd = std::min(gd, c->depth_groups);
-    const bool part = with_rects && (c->compact_frame || key);
-    // visible items (key mode: keys below the threshold) first, in index order, into
-    // items[0]; the passes sort only those
+    int gd = groups_for(key ? c->n : n_sorted, 256 * di);   // pass 0 reads all n
+    int gd_near = groups_for(n_sorted, 256 * di);
+    if (c->depth_groups) {
+        gd = std::min(gd, c->depth_groups);
+        gd_near = std::min(gd_near, c->depth_groups);
+    }
+    const bool part = with_rects && c->compact_frame;
+    // visible items first (index order) into items[0]; the passes sort only those
     if (part)
-        HIP_TRY(gsr::launch_partition(c->items[1], n, std::min(groups_for(c->n, 4096), gsr::kMaxSortGroups), c->hist,
+        HIP_TRY(gsr::launch_partition(c->pre_out, n, std::min(groups_for(c->n, 4096), gsr::kMaxSortGroups), c->hist,
                                       c->nlive, c->items[0], reinterpret_cast<const uint32_t*>(c->rect),
-                                      pay_buf(c, 0), pay_buf(c, 1), c->stream, key ? c->kcut : nullptr));
-    c->last_compact = part && !key;
+                                      pay_buf(c, 0), pay_buf(c, 1), c->stream));
+    // a repeated sort of a key-mode frame starts again from the preprocess order
+    const bool resort_src = !key && !part && c->have_sort && c->last_split_key;
+    if (resort_src)
+        HIP_TRY(hipMemcpyAsync(c->items[0], c->src_items, (size_t)n * 8, hipMemcpyDeviceToDevice, c->stream));
+    c->last_compact = part;
     c->last_split_key = key;
-    // a repeated sort of a key-mode frame sorts the whole partitioned items[0] (near and
-    // far keys never tie, so the order is the same)
     if (key) c->split_key = false;
     // pass 0's rect payloads: from the partition (-1), read at the item's position when
-    // items[0] is still the preprocess order (1: item j has index j), else gathered (0)
-    const int rect_mode = part ? -1 : (c->have_sort ? 0 : 1);
+    // the input is the preprocess order (1: item j has index j), else gathered (0)
+    const int rect_mode = part ? -1 : (key || resort_src || !c->have_sort ? 1 : 0);
     // items[1] is the sort's scratch from here on; a repeated sort of this frame sorts
     // the whole partitioned items[0] (same order: visible and culled keys never tie)
     if (part) c->compact_frame = false;
@@ -916,12 +939,18 @@ static int depth_sort_locked(gsr_context* c, bool with_rects) {
     // column scan and re-rendered with all four, like a pair-buffer overflow.
     const int launch = with_rects && c->depth_skip ? std::max(1, std::min(4, c->depth_budget)) : 4;
     c->passes_launched = launch;
-    for (int p = 0; p < launch; p++)
-        HIP_TRY(gsr::launch_radix_pass(c->items[p & 1], c->items[(p + 1) & 1], part ? c->nlive : nullptr, n, 32 + 8 * p, 8, gd, di,
+    const gsr::SortFilter near{1, c->kcut, c->nlive, c->kcut_frame};
+    for (int p = 0; p < launch; p++) {
+        const bool f0 = key && p == 0;
+        HIP_TRY(gsr::launch_radix_pass(f0 ? c->src_items : c->items[p & 1], c->items[(p + 1) & 1],
+                                       (part || (key && p > 0)) ? c->nlive : nullptr, n, 32 + 8 * p, 8,
+                                       key && p > 0 ? gd_near : gd, di,
                                        c->hist, c->totals, nullptr, c->stream, c->depth_skip ? c->dstats : nullptr,
                                        p, with_rects ? reinterpret_cast<const uint32_t*>(c->rect) : nullptr, rect_mode,
                                        with_rects ? pay_buf(c, 0) : nullptr,
-                                       with_rects ? pay_buf(c, 1) : nullptr, rank_atomic_on(c)));
+                                       with_rects ? pay_buf(c, 1) : nullptr, rank_atomic_on(c), nullptr, nullptr,
+                                       f0 ? &near : nullptr));
+    }
     return GSR_OK;
 }
 
@@ -934,11 +963,15 @@ static int far_sort_locked(gsr_context* c) {
     if (c->depth_groups) gd = std::min(gd, c->depth_groups);
     const int launch = c->depth_skip ? std::max(1, std::min(4, c->depth_budget)) : 4;
     c->far_launched = launch;
+    // pass 0 reads the whole preprocess order and keeps the keys at or above the frame's
+    // threshold, writing from position nlive; the later passes sort [nlive, n)
+    const gsr::SortFilter far{2, c->kcut_frame, nullptr, nullptr};
     for (int p = 0; p < launch; p++)
-        HIP_TRY(gsr::launch_radix_pass(c->items[p & 1], c->items[(p + 1) & 1], nullptr, n, 32 + 8 * p, 8, gd, di,
-                                       c->hist, c->totals, nullptr, c->stream, c->depth_skip ? c->dstats_far : nullptr,
-                                       p, reinterpret_cast<const uint32_t*>(c->rect), -1, pay_buf(c, 0), pay_buf(c, 1),
-                                       rank_atomic_on(c), c->nlive, c->gate));
+        HIP_TRY(gsr::launch_radix_pass(p == 0 ? c->src_items : c->items[p & 1], c->items[(p + 1) & 1], nullptr, n,
+                                       32 + 8 * p, 8, gd, di, c->hist, c->totals, nullptr, c->stream,
+                                       c->depth_skip ? c->dstats_far : nullptr, p,
+                                       reinterpret_cast<const uint32_t*>(c->rect), p == 0 ? 1 : 0, pay_buf(c, 0),
+                                       pay_buf(c, 1), rank_atomic_on(c), c->nlive, c->gate, p == 0 ? &far : nullptr));
     return GSR_OK;
 }
 
@@ -1009,7 +1042,7 @@ static int sort_locked(gsr_context* c, bool allow_split) {
         c->compact_frame = true;
     }
     if (c->compact_frame && !bin) {   // knobs changed since gsr_preprocess
-        HIP_TRY(hipMemcpyAsync(c->items[0], c->items[1], (size_t)n * 8, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->items[0], c->pre_out, (size_t)n * 8, hipMemcpyDeviceToDevice, c->stream));
         c->compact_frame = false;
     }
     const bool key = split && c->split_key;
@@ -1424,13 +1457,12 @@ extern "C" int gsr_read_splats(gsr_context* c, void* host, int64_t n) {
         HIP_TRY(hipMemcpy(rect.data(), c->rect, (size_t)n * 8, hipMemcpyDeviceToHost));
     }
     if (c->have_sort && c->last_split_key) {
-        // a key-mode split frame: items[0] holds every item (each region a permutation of
-        // its items), which is all the key lookup below needs
-        HIP_TRY(hipMemcpy(items.data(), c->items[0], (size_t)c->n * 8, hipMemcpyDeviceToHost));
+        // a key-mode split frame: its preprocess order holds every item's key
+        HIP_TRY(hipMemcpy(items.data(), c->src_items, (size_t)c->n * 8, hipMemcpyDeviceToHost));
     } else if (c->have_sort) {
         if (int rc = sorted_items_locked(c, items.data(), c->n)) return rc;
-    } else {   // preprocess order (items[1] when the frame is set up for the live partition)
-        HIP_TRY(hipMemcpy(items.data(), c->items[c->compact_frame && !c->have_sort ? 1 : 0], (size_t)c->n * 8,
+    } else {   // preprocess order (items[1] for the live partition, src_items for a key-mode split)
+        HIP_TRY(hipMemcpy(items.data(), c->pre_out ? c->pre_out : c->items[0], (size_t)c->n * 8,
                           hipMemcpyDeviceToHost));
     }
     auto* w = static_cast<uint32_t*>(host);
