@@ -739,7 +739,7 @@ __device__ __forceinline__ bool sort_keep(const SortRange& sr, uint32_t K, uint6
     return sr.filter == 0 || (sr.filter == 1 ? k < K : k >= K);
 }
 
-template <int ITEMS>
+template <int ITEMS, bool FILT>   // FILT: a filtered pass 0 (SortRange::filter != 0)
 __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* __restrict__ in,
                                                                 const uint32_t* __restrict__ n_dev,
                                                                 uint32_t n_host, int shift, uint32_t mask,
@@ -747,7 +747,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
                                                                 uint32_t* __restrict__ dstats, int pass,
                                                                 SortRange sr) {
     GSR_GEOM_PRIO();
-    __shared__ uint32_t h[4][257];   // [256]: items a filtered pass 0 drops
+    __shared__ uint32_t h[4][FILT ? 257 : 256];   // [256]: items a filtered pass 0 drops
     __shared__ uint32_t s_st[4];
     if (sr.gate && *sr.gate == 0u) return;
     if (depth_pass_skipped(dstats, pass)) return;
@@ -759,19 +759,21 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
 #pragma unroll
     for (int k = 0; k < 4; k++) h[k][t] = 0;
     __syncthreads();
-    const uint32_t K = sr.filter ? *sr.kcut : 0u;
-    if (sr.filter == 1 && sr.kcut_copy && blockIdx.x == 0 && t == 0) *sr.kcut_copy = K;
+    const uint32_t K = FILT ? *sr.kcut : 0u;
+    if (FILT && sr.filter == 1 && sr.kcut_copy && blockIdx.x == 0 && t == 0) *sr.kcut_copy = K;
     const uint32_t base = sr.base ? *sr.base : 0u;
-    if (!sr.filter) in += base;
-    const uint64_t n = sr.filter ? (uint64_t)n_host
-                                 : sr.base ? (uint64_t)(n_host - min(base, n_host)) : n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
+    if (!FILT) in += base;
+    const uint64_t n = FILT ? (uint64_t)n_host
+                            : sr.base ? (uint64_t)(n_host - min(base, n_host)) : n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, kSortThreads * ITEMS, b, e);
     // the digit's counter, or the drop counter for an item a filtered pass 0 does not keep
-    auto dig = [&](uint64_t v) { return sort_keep(sr, K, v) ? ((uint32_t)(v >> shift) & mask) : 256u; };
+    auto dig = [&](uint64_t v) {
+        return !FILT || sort_keep(sr, K, v) ? ((uint32_t)(v >> shift) & mask) : 256u;
+    };
     auto note = [&](uint64_t v) {
         const uint32_t k = (uint32_t)(v >> 32);
-        if (k != 0xffffffffu && sort_keep(sr, K, v)) {
+        if (k != 0xffffffffu && (!FILT || sort_keep(sr, K, v))) {
             inv_min = max(inv_min, ~k);
             kmax = max(kmax, k);
             any = 1u;
@@ -881,7 +883,7 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
 // Payloads leave through the items' LDS slots, in the same digit runs.
 // (The rects used to be gathered in the last pass only: a random 8-B read per item
 // that cost the 5M-Gaussian frame 76 us of its 110-us pass, profiles/r02_geom_pmc.txt.)
-template <int ITEMS, bool RA>
+template <int ITEMS, bool RA, bool FILT>   // FILT: a filtered pass 0 (SortRange::filter != 0)
 __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const uint64_t* __restrict__ in, uint64_t* __restrict__ out, const uint32_t* __restrict__ n_dev,
     uint32_t n_host, int shift, int bits, int groups, const uint32_t* __restrict__ hist,
@@ -897,12 +899,12 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
         const uint32_t base = *sr.base;
         out += base;
         if (pay_out) pay_out += base;
-        if (!sr.filter) {
+        if (!FILT) {
             in += base;
             if (pay_in) pay_in += base;
         }
     }
-    const uint32_t K = sr.filter ? *sr.kcut : 0u;
+    const uint32_t K = FILT ? *sr.kcut : 0u;
     const bool carry = pay_out != nullptr;
     __shared__ uint32_t s_wc[4][256];           // per-wave digit counters, then wave bases
     __shared__ uint32_t s_gbase[256];           // running global offset per digit
@@ -917,8 +919,8 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const uint32_t lane = lane_id();
     const uint32_t w = t >> 6;
     const uint32_t mask = (1u << bits) - 1u;
-    const uint64_t n = sr.filter ? (uint64_t)n_host
-                                 : sr.base ? (uint64_t)(n_host - min(*sr.base, n_host)) : n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
+    const uint64_t n = FILT ? (uint64_t)n_host
+                            : sr.base ? (uint64_t)(n_host - min(*sr.base, n_host)) : n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
     uint64_t b, e;
     const int chunk = GSR_XCD_DEPTH && ITEMS == 16 ? xcd_chunk((int)blockIdx.x, groups) : (int)blockIdx.x;
     chunk_range(n, groups, chunk, kTile, b, e);
@@ -929,7 +931,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
         uint32_t tot;
         const uint32_t dig_excl = block_exclusive_scan<uint32_t>(totals[t], s_scr, tot);
         s_gbase[t] = dig_excl + hist[t * (uint32_t)groups + chunk];
-        if (sr.count_out && blockIdx.x == 0 && t == 0) *sr.count_out = tot;
+        if (FILT && sr.count_out && blockIdx.x == 0 && t == 0) *sr.count_out = tot;
     }
     if (b >= e) return;                          // uniform per workgroup
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -969,7 +971,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
             const uint32_t el = wbase + k * 64 + lane;
-            const bool valid = el < tn && sort_keep(sr, K, it[k]);
+            const bool valid = el < tn && (!FILT || sort_keep(sr, K, it[k]));
             kp[k] = valid;
             const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
             uint32_t r = 0;
@@ -2930,17 +2932,26 @@ static void radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev,
                        int pass, const uint32_t* rect, int rect_direct, uint32_t* pay0, uint32_t* pay1,
                        hipStream_t s, SortRange sr) {
     const uint32_t mask = (1u << bits) - 1u;
-    hipLaunchKernelGGL(k_radix_upsweep<ITEMS>, dim3(groups), dim3(kSortThreads), 0, s, in, n_dev, n_host, shift,
-                       mask, groups, hist, dstats, pass, sr);
+    if (sr.filter)
+        hipLaunchKernelGGL((k_radix_upsweep<ITEMS, true>), dim3(groups), dim3(kSortThreads), 0, s, in, n_dev, n_host,
+                           shift, mask, groups, hist, dstats, pass, sr);
+    else
+        hipLaunchKernelGGL((k_radix_upsweep<ITEMS, false>), dim3(groups), dim3(kSortThreads), 0, s, in, n_dev, n_host,
+                           shift, mask, groups, hist, dstats, pass, sr);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, hist, groups, totals,
                        static_cast<const uint32_t*>(dstats), pass, sr.gate);
     // rect payloads (binning): pass p reads pay[p & 1] (pass 0: rect, or pay[0] when
     // rect_direct < 0 — the live partition wrote it) and writes pay[(p + 1) & 1]
     const uint32_t* pay_in = pay0 && (pass > 0 || rect_direct < 0) ? ((pass & 1) ? pay1 : pay0) : nullptr;
     uint32_t* pay_out = pay0 ? ((pass & 1) ? pay0 : pay1) : nullptr;
-    hipLaunchKernelGGL((k_radix_downsweep<ITEMS, RA>), dim3(groups), dim3(kSortThreads), 0, s, in, out, n_dev, n_host,
-                       shift, bits, groups, hist, totals, ranges, static_cast<const uint32_t*>(dstats), pass, rect,
-                       rect_direct > 0 ? 1 : 0, pay_in, pay_out, sr);
+    if (sr.filter)
+        hipLaunchKernelGGL((k_radix_downsweep<ITEMS, RA, true>), dim3(groups), dim3(kSortThreads), 0, s, in, out, n_dev,
+                           n_host, shift, bits, groups, hist, totals, ranges, static_cast<const uint32_t*>(dstats), pass,
+                           rect, rect_direct > 0 ? 1 : 0, pay_in, pay_out, sr);
+    else
+        hipLaunchKernelGGL((k_radix_downsweep<ITEMS, RA, false>), dim3(groups), dim3(kSortThreads), 0, s, in, out, n_dev,
+                           n_host, shift, bits, groups, hist, totals, ranges, static_cast<const uint32_t*>(dstats), pass,
+                           rect, rect_direct > 0 ? 1 : 0, pay_in, pay_out, sr);
 }
 
 hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host,
