@@ -183,6 +183,22 @@ def test_config3_speculation_and_miss(gpu, orc, torch, c3):
     r.close()
 
 
+def test_dropin_config3_split(gpu, orc, torch, c3):
+    """The drop-in preprocessCUDAGaussians (synchronous, host image, one process-wide
+    context) at config-3 size: its frames go through the split too (count mode, then
+    the depth threshold, later speculation; it re-renders what it must), every call
+    bit-exact.  The reference viewer's tiling (50 x 50 tiles)."""
+    scene, soa, cam, W, H, want, _ = c3
+    t = gpu.TilingInformation(50, 50, H, W)
+    want_t = orc.render(soa, cam, W, H, 3.0, tiling=(t.num_tile_x, t.num_tile_y, t.width_stride, t.height_stride),
+                        threads=ORC_THREADS)
+    out = None
+    for _ in range(12):
+        out = gpu.preprocessCUDAGaussians(scene.ptr, scene.n, cam, t.num_tile_y, t.num_tile_x, t.width_stride,
+                                          t.height_stride, W, H, 3.0, out=out)
+        assert_frames(out, want_t, exact=True)
+
+
 def test_config3_split_off_same_lists(gpu, orc, torch, c3):
     """With the split off the tile lists are the whole depth order's; the default (on
     for this size) renders the same image, and so does the stage API, which never
