@@ -44,6 +44,7 @@ struct Stats {
     uint32_t depth_passes;            // passes the depth sort's device plan needed (binning path; 0: n/a)
     uint32_t split_unsat;             // depth split: blocks the last phase-A blend left unsaturated
                                       // (written to the host-mapped copy by the phase-B blend)
+    uint32_t split_pm;                // the split point of the frame whose split_unsat that is
     uint32_t spec_miss;               // depth split without phase B (speculative): a phase-A blend
                                       // left a block unsaturated, the frame is incomplete (host copy,
                                       // sticky until the host reads it)
@@ -56,12 +57,17 @@ struct Stats {
 // Depth split, key mode: pass 0 of a depth sort reads the whole preprocess order and
 // keeps key < *kcut (mode 1, the near part: the kept count goes to *count_out and the
 // threshold is copied to *kcut_copy) or key >= *kcut (mode 2, the far part, written from
-// the pass's base).
+// the pass's base; with sat, only items whose tile rect holds a tile phase A left
+// unsaturated — the summed-area table of k_split_sat, sat_w = tiles_x + 1 — and the kept
+// count goes to *count_out).  mode 0 with count: a later far pass, length *count.
 struct SortFilter {
     int mode;
     const uint32_t* kcut;
     uint32_t* count_out;
     uint32_t* kcut_copy;
+    const uint32_t* sat;
+    int sat_w;
+    const uint32_t* count;
 };
 
 // Depth split, key mode: the preprocess writes splat records only for Gaussians nearer
@@ -81,6 +87,7 @@ struct RecSplit {
 struct RowSplit {
     int cut_mode;
     uint32_t na;
+    const uint32_t* cut_n;            // mode 2: the far part's kept length (a masked far sort)
 };
 
 // The next frame's depth threshold (its partition puts keys < *kcut in the near part),
@@ -104,6 +111,7 @@ struct BlendSplit {
     Stats* spec_host;                 // phase A with no phase B queued: an unsaturated block sets
                                       // spec_host->spec_miss (nullable)
     SplitCut cut;                     // phase A: the next frame's threshold
+    uint32_t pm;                      // phase B publishes it with the count (Stats::split_pm)
 };
 
 // ---- launch wrappers (gsr_kernels.hip) ----
@@ -152,6 +160,10 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
 // Stable partition of the preprocess items: visible first, culled last (both in
 // index order), visible count into *n_live; culled tail to out only, with dead
 // rects in srect (gsr_kernels.hip "live partition").  counts: groups words.
+// Depth split, phase B: summed-area table of the tiles phase A left unsaturated
+// ((tiles_y + 1) x (tiles_x + 1) words), gated.
+hipError_t launch_split_sat(const uint8_t* bflag, int tiles_x, int tiles_y, uint32_t* sat, const uint32_t* gate,
+                            hipStream_t s);
 hipError_t launch_partition(const uint64_t* in, uint32_t n, int groups, uint32_t* counts, uint32_t* n_live,
                             uint64_t* out, const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, hipStream_t s);
 // Tile binning (row pass + column pass, tile grids <= 256 x 256): replaces

@@ -725,6 +725,10 @@ __device__ __forceinline__ int depth_passes_run(const uint32_t* __restrict__ dst
 //          position 0 (near) or *base (far); the near pass's downsweep stores the kept
 //          count in *count_out, and its upsweep copies *kcut to *kcut_copy (the frame's
 //          threshold, for phase B)
+//   sat    (far pass 0) also drop an item whose tile rect (rect[position], packed) holds
+//          no tile phase A left unsaturated: sat is the summed-area table of those tiles,
+//          (tiles_y + 1) x sat_w words, sat_w = tiles_x + 1 (k_split_sat)
+//   count  with base: the far part's length (the far pass 0's kept count), else n_host - base
 struct SortRange {
     const uint32_t* base;
     const uint32_t* gate;
@@ -732,11 +736,34 @@ struct SortRange {
     int filter;
     uint32_t* count_out;
     uint32_t* kcut_copy;
+    const uint32_t* sat;
+    int sat_w;
+    const uint32_t* rect;
+    const uint32_t* count;
 };
 
-__device__ __forceinline__ bool sort_keep(const SortRange& sr, uint32_t K, uint64_t v) {
+// Some tile of the packed rect pr (tx0 | tx1 << 8 | ty0 << 16 | ty1 << 24) is counted
+// in the summed-area table (dead rects hold none).
+__device__ __forceinline__ bool rect_hits(const uint32_t* __restrict__ sat, int w, uint32_t pr) {
+    const uint32_t x0 = pr & 0xffu, x1 = (pr >> 8) & 0xffu, y0 = (pr >> 16) & 0xffu, y1 = pr >> 24;
+    if (x0 > x1 || y0 > y1) return false;
+    const uint32_t* r0 = sat + (size_t)y0 * (uint32_t)w;
+    const uint32_t* r1 = sat + (size_t)(y1 + 1u) * (uint32_t)w;
+    return r1[x1 + 1u] - r0[x1 + 1u] - r1[x0] + r0[x0] != 0u;
+}
+
+__device__ __forceinline__ bool sort_keep(const SortRange& sr, uint32_t K, uint64_t v, uint32_t pr) {
     const uint32_t k = (uint32_t)(v >> 32);
-    return sr.filter == 0 || (sr.filter == 1 ? k < K : k >= K);
+    if (sr.filter == 1) return k < K;
+    return sr.filter == 0 || (k >= K && (!sr.sat || rect_hits(sr.sat, sr.sat_w, pr)));
+}
+
+__device__ __forceinline__ uint64_t sort_len(const SortRange& sr, const uint32_t* n_dev, uint32_t n_host) {
+    if (sr.base) {
+        const uint32_t base = min(*sr.base, n_host);
+        return sr.count ? (uint64_t)min(*sr.count, n_host - base) : (uint64_t)(n_host - base);
+    }
+    return n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
 }
 
 template <int ITEMS, bool FILT>   // FILT: a filtered pass 0 (SortRange::filter != 0)
@@ -763,17 +790,17 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
     if (FILT && sr.filter == 1 && sr.kcut_copy && blockIdx.x == 0 && t == 0) *sr.kcut_copy = K;
     const uint32_t base = sr.base ? *sr.base : 0u;
     if (!FILT) in += base;
-    const uint64_t n = FILT ? (uint64_t)n_host
-                            : sr.base ? (uint64_t)(n_host - min(base, n_host)) : n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
+    const uint64_t n = FILT ? (uint64_t)n_host : sort_len(sr, n_dev, n_host);
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, kSortThreads * ITEMS, b, e);
+    const bool masked = FILT && sr.sat;   // the far pass 0's rect test reads rect[position]
     // the digit's counter, or the drop counter for an item a filtered pass 0 does not keep
-    auto dig = [&](uint64_t v) {
-        return !FILT || sort_keep(sr, K, v) ? ((uint32_t)(v >> shift) & mask) : 256u;
+    auto dig = [&](uint64_t v, uint64_t i) {
+        return !FILT || sort_keep(sr, K, v, masked ? sr.rect[i] : 0u) ? ((uint32_t)(v >> shift) & mask) : 256u;
     };
-    auto note = [&](uint64_t v) {
+    auto note = [&](uint64_t v, uint64_t i) {
         const uint32_t k = (uint32_t)(v >> 32);
-        if (k != 0xffffffffu && (!FILT || sort_keep(sr, K, v))) {
+        if (k != 0xffffffffu && (!FILT || sort_keep(sr, K, v, masked ? sr.rect[i] : 0u))) {
             inv_min = max(inv_min, ~k);
             kmax = max(kmax, k);
             any = 1u;
@@ -785,21 +812,21 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
     for (; i + 3 * kSortThreads < e; i += 4 * kSortThreads) {
         const uint64_t v0 = in[i], v1 = in[i + kSortThreads], v2 = in[i + 2 * kSortThreads],
                        v3 = in[i + 3 * kSortThreads];
-        atomicAdd(&h[w][dig(v0)], 1u);
-        atomicAdd(&h[w][dig(v1)], 1u);
-        atomicAdd(&h[w][dig(v2)], 1u);
-        atomicAdd(&h[w][dig(v3)], 1u);
+        atomicAdd(&h[w][dig(v0, i)], 1u);
+        atomicAdd(&h[w][dig(v1, i + kSortThreads)], 1u);
+        atomicAdd(&h[w][dig(v2, i + 2 * kSortThreads)], 1u);
+        atomicAdd(&h[w][dig(v3, i + 3 * kSortThreads)], 1u);
         if (plan) {
-            note(v0);
-            note(v1);
-            note(v2);
-            note(v3);
+            note(v0, i);
+            note(v1, i + kSortThreads);
+            note(v2, i + 2 * kSortThreads);
+            note(v3, i + 3 * kSortThreads);
         }
     }
     for (; i < e; i += kSortThreads) {
         const uint64_t v = in[i];
-        atomicAdd(&h[w][dig(v)], 1u);
-        if (plan) note(v);
+        atomicAdd(&h[w][dig(v, i)], 1u);
+        if (plan) note(v, i);
     }
     if (plan) {   // wave reductions first: one LDS atomic per wave and word
         inv_min = wave_max_u32(inv_min);
@@ -919,8 +946,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const uint32_t lane = lane_id();
     const uint32_t w = t >> 6;
     const uint32_t mask = (1u << bits) - 1u;
-    const uint64_t n = FILT ? (uint64_t)n_host
-                            : sr.base ? (uint64_t)(n_host - min(*sr.base, n_host)) : n_dev ? (uint64_t)*n_dev : (uint64_t)n_host;
+    const uint64_t n = FILT ? (uint64_t)n_host : sort_len(sr, n_dev, n_host);
     uint64_t b, e;
     const int chunk = GSR_XCD_DEPTH && ITEMS == 16 ? xcd_chunk((int)blockIdx.x, groups) : (int)blockIdx.x;
     chunk_range(n, groups, chunk, kTile, b, e);
@@ -971,7 +997,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
             const uint32_t el = wbase + k * 64 + lane;
-            const bool valid = el < tn && (!FILT || sort_keep(sr, K, it[k]));
+            const bool valid = el < tn && (!FILT || sort_keep(sr, K, it[k], pv[k]));
             kp[k] = valid;
             const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
             uint32_t r = 0;
@@ -1565,12 +1591,44 @@ __device__ __forceinline__ void publish_pair_stats(unsigned long long total, uin
 // Depth-order positions a row pass reads: [base, base + n) as the host passed them, or
 // with the depth split's device-side cut (the near part's size after the threshold
 // partition): mode 1 = [0, min(cut, n)) (phase A), mode 2 = [cut, n) (phase B).
-__device__ __forceinline__ void row_range(uint32_t& base, uint32_t& n, const uint32_t* cut, int mode) {
+// (mode 2 with cut_n: the far part's kept length *cut_n, a masked far sort's count.)
+__device__ __forceinline__ void row_range(uint32_t& base, uint32_t& n, const uint32_t* cut, int mode,
+                                          const uint32_t* cut_n) {
     if (mode == 1) {
         n = min(*cut, n);
     } else if (mode == 2) {
         base = min(*cut, n);
         n -= base;
+        if (cut_n) n = min(*cut_n, n);
+    }
+}
+
+// Depth split, phase B: the summed-area table of the tiles phase A left unsaturated
+// (a tile counts when any of its four blocks' flags is set; the flags of a tile are
+// consecutive bytes), (tiles_y + 1) x (tiles_x + 1) words with a zero first row and
+// column.  One workgroup: row prefix sums, then column prefix sums.
+__global__ __launch_bounds__(256) void k_split_sat(const uint8_t* __restrict__ bflag, int tiles_x, int tiles_y,
+                                                    uint32_t* __restrict__ sat, const uint32_t* __restrict__ gate) {
+    GSR_GEOM_PRIO();
+    if (*gate == 0u) return;
+    const int w = tiles_x + 1;
+    const uint32_t* tf = reinterpret_cast<const uint32_t*>(bflag);
+    for (int y = (int)threadIdx.x; y <= tiles_y; y += 256) {
+        uint32_t* row = sat + (size_t)y * (uint32_t)w;
+        uint32_t run = 0;
+        row[0] = 0;
+        for (int x = 0; x < tiles_x; x++) {
+            if (y > 0) run += tf[(size_t)(y - 1) * (uint32_t)tiles_x + (uint32_t)x] != 0u ? 1u : 0u;
+            row[x + 1] = run;
+        }
+    }
+    __syncthreads();
+    for (int x = (int)threadIdx.x + 1; x <= tiles_x; x += 256) {
+        uint32_t run = 0;
+        for (int y = 1; y <= tiles_y; y++) {
+            run += sat[(size_t)y * (uint32_t)w + (uint32_t)x];
+            sat[(size_t)y * (uint32_t)w + (uint32_t)x] = run;
+        }
     }
 }
 
@@ -1583,10 +1641,11 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint32
                                                          const uint32_t* __restrict__ dstats, int groups,
                                                          int tiles_y, uint32_t* __restrict__ hist, uint32_t base,
                                                          const uint32_t* __restrict__ gate,
-                                                         const uint32_t* __restrict__ cut, int cut_mode) {
+                                                         const uint32_t* __restrict__ cut, int cut_mode,
+                                                         const uint32_t* __restrict__ cut_n) {
     GSR_GEOM_PRIO();
     if (gate && *gate == 0u) return;   // depth split, phase B: every block saturated in phase A
-    row_range(base, n, cut, cut_mode);
+    row_range(base, n, cut, cut_mode, cut_n);
     __shared__ uint32_t h_items[4][256], h_pairs[4][256];
     const uint32_t t = threadIdx.x, w = t >> 6;
 #pragma unroll
@@ -1723,10 +1782,11 @@ __global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(co
                                                            uint32_t cap, int tiles_y, uint64_t* __restrict__ rows_out,
                                                            const uint16_t* __restrict__ spans, uint32_t base,
                                                            const uint32_t* __restrict__ gate,
-                                                           const uint32_t* __restrict__ cut, int cut_mode) {
+                                                           const uint32_t* __restrict__ cut, int cut_mode,
+                                                           const uint32_t* __restrict__ cut_n) {
     GSR_GEOM_PRIO();
     if (gate && *gate == 0u) return;
-    row_range(base, n, cut, cut_mode);
+    row_range(base, n, cut, cut_mode, cut_n);
     constexpr uint32_t kTile = 256u * ITEMS;
     __shared__ uint32_t s_pref[kRowSources], s_idx[kRowSources];
     // per source: packed rect (pack_rect) | tile row spans << 32 (no LDS beyond the
@@ -2675,6 +2735,7 @@ __global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx
         const uint32_t g = *sp.gate;   // uniform
         if (vb == 0 && threadIdx.x == 0 && sp.host_st) {
             sp.host_st->split_unsat = g;
+            sp.host_st->split_pm = sp.pm;
             __threadfence_system();
         }
         if (g == 0u) return;
@@ -2926,6 +2987,9 @@ hipError_t launch_preprocess(const float* arrays, int64_t stride, int64_t n, con
     return hipGetLastError();
 }
 
+// A filtered pass 0 ranks by the rect payloads it reads at each position (rect_direct).
+static bool carry_ok(const uint32_t* pay0, int rect_direct) { return pay0 != nullptr && rect_direct > 0; }
+
 template <int ITEMS, bool RA>
 static void radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* n_dev, uint32_t n_host, int shift,
                        int bits, int groups, uint32_t* hist, uint32_t* totals, uint2* ranges, uint32_t* dstats,
@@ -2965,8 +3029,10 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
     if (filter < 0 || filter > 2 || (filter && (pass != 0 || !f->kcut || n_dev || (filter == 2) != (base_dev != nullptr))))
         return hipErrorInvalidValue;
     if (base_dev && !filter && (n_dev || rect_direct > 0)) return hipErrorInvalidValue;
-    const SortRange sr{base_dev, gate, filter ? f->kcut : nullptr, filter, filter == 1 ? f->count_out : nullptr,
-                       filter == 1 ? f->kcut_copy : nullptr};
+    if (filter && !carry_ok(pay0, rect_direct)) return hipErrorInvalidValue;
+    const SortRange sr{base_dev, gate, filter ? f->kcut : nullptr, filter, filter ? f->count_out : nullptr,
+                       filter == 1 ? f->kcut_copy : nullptr, filter == 2 ? f->sat : nullptr, f ? f->sat_w : 0,
+                       filter == 2 && f->sat ? rect : nullptr, f && !filter ? f->count : nullptr};
     // 16 items per thread always rank with ballots (k_radix_downsweep)
     if (items == 4 && rank_atomic)
         radix_pass<4, true>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
@@ -3025,8 +3091,9 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
         (cut_mode != 0 && !cut) || cut_mode < 0 || cut_mode > 2)
         return hipErrorInvalidValue;
     const uint32_t* g = gate_mode == 2 ? gate : nullptr;
+    const uint32_t* cut_n = rs ? rs->cut_n : nullptr;
     hipLaunchKernelGGL(k_bin_rows_count, dim3(groups), dim3(256), 0, s, n, pay0, pay1, dstats, groups, tiles_y,
-                       hist, base, g, cut, cut_mode);
+                       hist, base, g, cut, cut_mode, cut_n);
     hipLaunchKernelGGL(k_bin_rows_scan, dim3(256), dim3(256), 0, s, hist, groups, tiles_y, row_items, row_pairs,
                        gate, gate_mode);
     auto pick = [&](auto ra) {
@@ -3038,7 +3105,7 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
     };
     auto scatter = rank_atomic ? pick(std::true_type{}) : pick(std::false_type{});
     hipLaunchKernelGGL(scatter, dim3(groups), dim3(256), 0, s, items0, items1, dstats, pay0, pay1, n, groups, hist,
-                       row_items, row_pairs, pair_capacity, tiles_y, rows_buf, spans, base, g, cut, cut_mode);
+                       row_items, row_pairs, pair_capacity, tiles_y, rows_buf, spans, base, g, cut, cut_mode, cut_n);
     return hipGetLastError();
 }
 
@@ -3123,7 +3190,7 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
     const int phase = split ? split->phase : 0;
     if (phase < 0 || phase > 2 || (phase && (fast_exp || stamps || !split->tbuf || !split->bflag || !split->gate)))
         return hipErrorInvalidValue;
-    const BlendSplit sp = split ? *split : BlendSplit{0, nullptr, nullptr, nullptr, nullptr, nullptr, {}};
+    const BlendSplit sp = split ? *split : BlendSplit{0, nullptr, nullptr, nullptr, nullptr, nullptr, {}, 0u};
 #define GSR_BLEND_S(D, ST, FX, SP)                                                                          \
     hipLaunchKernelGGL((k_blend_w<D, ST, FX, SP>), dim3(ng), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,  \
                        fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, bands, band0, sp)
@@ -3148,6 +3215,13 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
     }
 #undef GSR_BLEND
 #undef GSR_BLEND_S
+    return hipGetLastError();
+}
+
+hipError_t launch_split_sat(const uint8_t* bflag, int tiles_x, int tiles_y, uint32_t* sat, const uint32_t* gate,
+                            hipStream_t s) {
+    if (tiles_x < 1 || tiles_x > 256 || tiles_y < 1 || tiles_y > 256 || !gate) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_split_sat, dim3(1), dim3(256), 0, s, bflag, tiles_x, tiles_y, sat, gate);
     return hipGetLastError();
 }
 

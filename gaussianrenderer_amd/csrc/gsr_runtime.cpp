@@ -401,6 +401,8 @@ struct gsr_context {
     uint32_t* kcut = nullptr;        // depth split: the next frame's depth threshold (device word)
     uint32_t* kcut_frame = nullptr;  // depth split: this frame's threshold (the near sort copies it)
     uint64_t* src_items = nullptr;   // depth split, key mode: the preprocess order (both sorts' pass 0 read it)
+    uint32_t* sat = nullptr;         // depth split, phase B: summed-area table of the unsaturated tiles
+    uint32_t* nfar = nullptr;        // depth split, phase B: far items whose rect touches one (device word)
     int64_t src_cap = 0;
     uint64_t* pre_out = nullptr;     // where the preprocess wrote its items
     bool records_partial = false;    // the preprocess wrote only the near Gaussians' records
@@ -532,6 +534,8 @@ int ensure_static(gsr_context* c) {
     if (int rc = realloc_dev(&c->gate, 1)) return rc;
     if (int rc = realloc_dev(&c->kcut, 1)) return rc;
     if (int rc = realloc_dev(&c->kcut_frame, 1)) return rc;
+    if (int rc = realloc_dev(&c->nfar, 1)) return rc;
+    if (int rc = realloc_dev(&c->sat, 257 * 257)) return rc;   // grids <= 256 x 256 tiles
     if (int rc = realloc_dev(&c->dstats_far, 4 + 4 * (size_t)gsr::kMaxSortGroups)) return rc;
     HIP_TRY(hipMemset(c->kcut, 0xff, sizeof(uint32_t)));
     HIP_TRY(hipMemset(c->stats, 0, 2 * sizeof(Stats)));
@@ -679,13 +683,19 @@ int check_overflow(gsr_context* c, bool blocking) {
         // never below 5/4 of the last point that needed it; when it cannot shrink any
         // further, the next frames speculate (no phase B queued)
         c->split_seen = false;
-        if (hv->split_unsat > 0) {
-            split_grow(c);
-        } else if (++c->split_clean >= 8) {
-            c->split_clean = 0;
-            const int next = std::max(std::max(kSplitMinPm, c->split_floor), c->split_pm * 7 / 8);
-            if (next >= c->split_pm) c->split_spec = true;
-            c->split_pm = next;
+        const int64_t u = hv->split_unsat;
+        if ((int)hv->split_pm != c->split_pm) {
+            // the newest phase B ran at an earlier split point (frames in flight): no
+            // evidence about the current one yet
+        } else if (u == 0) {
+            if (++c->split_clean >= 8) {
+                c->split_clean = 0;
+                const int next = std::max(std::max(kSplitMinPm, c->split_floor), c->split_pm * 7 / 8);
+                if (next >= c->split_pm) c->split_spec = true;
+                c->split_pm = next;
+            }
+        } else {
+            split_grow(c);   // phase A left blocks unsaturated
         }
     }
     if (!s.overflow) {
@@ -780,7 +790,7 @@ extern "C" void gsr_destroy(gsr_context* c) {
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
                     (void*)c->cbins, (void*)c->srect, (void*)c->spans, (void*)c->nlive, (void*)c->tbuf,
                     (void*)c->bflag, (void*)c->gate, (void*)c->kcut, (void*)c->dstats_far, (void*)c->kcut_frame,
-                    (void*)c->src_items})
+                    (void*)c->src_items, (void*)c->sat, (void*)c->nfar})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -849,7 +859,8 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     c->spans_frame = c->rect_packed && (c->tile_spans == 1 || (c->tile_spans == 2 && n <= kLargeScene));
     // key mode: records only for the Gaussians nearer than the threshold (the far ones
     // are written by a second pass if phase B or a one-phase sort needs them)
-    c->records_partial = c->split_key && !c->spans_frame;
+    // (speculative frames only: a frame that queues phase B needs every record there)
+    c->records_partial = c->split_key && c->split_spec && !c->spans_frame;
     c->pre_arrays = arrays;
     c->pre_stride = stride;
     c->pre_layout = layout;
@@ -963,15 +974,19 @@ static int far_sort_locked(gsr_context* c) {
     if (c->depth_groups) gd = std::min(gd, c->depth_groups);
     const int launch = c->depth_skip ? std::max(1, std::min(4, c->depth_budget)) : 4;
     c->far_launched = launch;
-    // pass 0 reads the whole preprocess order and keeps the keys at or above the frame's
-    // threshold, writing from position nlive; the later passes sort [nlive, n)
-    const gsr::SortFilter far{2, c->kcut_frame, nullptr, nullptr};
+    // the summed-area table of the tiles phase A left unsaturated; pass 0 reads the whole
+    // preprocess order and keeps the items with keys at or above the frame's threshold
+    // whose rect touches such a tile, writing them from position nlive (count in nfar);
+    // the later passes sort [nlive, nlive + nfar)
+    HIP_TRY(gsr::launch_split_sat(c->bflag, c->fr.tiles_x, c->fr.tiles_y, c->sat, c->gate, c->stream));
+    const gsr::SortFilter far{2, c->kcut_frame, c->nfar, nullptr, c->sat, c->fr.tiles_x + 1, nullptr};
+    const gsr::SortFilter rest{0, nullptr, nullptr, nullptr, nullptr, 0, c->nfar};
     for (int p = 0; p < launch; p++)
         HIP_TRY(gsr::launch_radix_pass(p == 0 ? c->src_items : c->items[p & 1], c->items[(p + 1) & 1], nullptr, n,
                                        32 + 8 * p, 8, gd, di, c->hist, c->totals, nullptr, c->stream,
                                        c->depth_skip ? c->dstats_far : nullptr, p,
                                        reinterpret_cast<const uint32_t*>(c->rect), p == 0 ? 1 : 0, pay_buf(c, 0),
-                                       pay_buf(c, 1), rank_atomic_on(c), c->nlive, c->gate, p == 0 ? &far : nullptr));
+                                       pay_buf(c, 1), rank_atomic_on(c), c->nlive, c->gate, p == 0 ? &far : &rest));
     return GSR_OK;
 }
 
@@ -1065,7 +1080,7 @@ static int sort_locked(gsr_context* c, bool allow_split) {
         if (split) {
             if (int rc = ensure_split(c)) return rc;
             c->split_na = na;
-            const gsr::RowSplit rs{key ? 1 : 0, na};
+            const gsr::RowSplit rs{key ? 1 : 0, na, nullptr};
             if (int rc = bin_locked(c, 0, key ? n : na, 1, true, &rs)) return rc;
         } else {
             if (int rc = bin_locked(c, 0, n, 0, true)) return rc;
@@ -1128,7 +1143,7 @@ static int blend_locked(gsr_context* c, float* d_out) {
         const bool key = c->frame_key;
         if (key && (c->blend_exp != 0 || c->blend_variant == 3))
             return set_err(GSR_E_ARG, "gsr_blend: blend knobs changed after a depth-split frame; render it again");
-        const gsr::RowSplit ra{key ? 1 : 0, c->split_na};
+        const gsr::RowSplit ra{key ? 1 : 0, c->split_na, nullptr};
         if (c->split_rebin && c->blend_exp == 0 && c->blend_variant != 3) {
             if (int rc = bin_locked(c, 0, key ? n : c->split_na, 1, false, &ra)) return rc;
         }
@@ -1138,7 +1153,7 @@ static int blend_locked(gsr_context* c, float* d_out) {
             const bool spec = c->frame_spec;
             const gsr::SplitCut cut{c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr,
                                     key ? c->nlive : nullptr, n, c->split_na, c->split_rebin ? nullptr : c->kcut};
-            gsr::BlendSplit a{1, c->tbuf, c->bflag, c->gate, nullptr, spec ? c->hstats_dev : nullptr, cut};
+            gsr::BlendSplit a{1, c->tbuf, c->bflag, c->gate, nullptr, spec ? c->hstats_dev : nullptr, cut, 0u};
             HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
                                       c->diagnostics ? c->consumed : nullptr, false, c->blend_band_tiles, 0,
                                       c->stream, &a));
@@ -1146,14 +1161,14 @@ static int blend_locked(gsr_context* c, float* d_out) {
             mark(c, GSR_STAGE_RESUME);
             if (!spec) {
                 // phase B: (key mode) sort the far part, then bin the rest of the order
-                const gsr::RowSplit rb{key ? 2 : 0, c->split_na};
+                const gsr::RowSplit rb{key ? 2 : 0, c->split_na, key ? c->nfar : nullptr};
                 if (key && !c->split_rebin) {
                     if (int rc = far_sort_locked(c)) return rc;
                     if (int rc = far_records_locked(c, true)) return rc;
                 }
                 if (int rc = bin_locked(c, key ? 0 : c->split_na, key ? n : n - c->split_na, 2, false, &rb, key))
                     return rc;
-                gsr::BlendSplit b{2, c->tbuf, c->bflag, c->gate, c->hstats_dev, nullptr, {}};
+                gsr::BlendSplit b{2, c->tbuf, c->bflag, c->gate, c->hstats_dev, nullptr, {}, (uint32_t)c->split_pm};
                 HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
                                           c->diagnostics ? c->consumed : nullptr, false, c->blend_band_tiles, 0,
                                           c->stream, &b));

@@ -199,6 +199,34 @@ def test_dropin_config3_split(gpu, orc, torch, c3):
         assert_frames(out, want_t, exact=True)
 
 
+def test_config3_background_masked_phase_b(gpu, orc, torch, c3):
+    """The camera turned off the scene's centre: 15 % of the tiles see past it and never
+    saturate, so phase B has blocks to resume on every frame.  In key mode its far sort
+    keeps only the far splats whose rect touches an unsaturated tile (summed-area table
+    of phase A's block flags).  Frames at a forced split are bit-exact with the oracle's
+    take maps; by default the controller grows the split point to 1000, which turns the
+    split off (no gain to be had), and the frames stay bit-exact."""
+    scene, soa, _, W, H, _, _ = c3
+    cam = cam_for(gpu, W, H, look=(1.2, 0, 0))
+    want, takes = orc.render_takes(soa, cam, W, H, 3.0, threads=ORC_THREADS)
+    r = split_renderer(gpu, 1, 250)
+    for _ in range(3):
+        img, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
+        assert_frames(img, want, exact=True)
+    assert r.get_tuning(KNOB_STATE) == 2 and r.get_tuning(KNOB_UNSAT) > 0
+    check_takes(gpu, torch, r, scene, cam, W, H, want, takes)
+    r.close()
+    r = split_renderer(gpu, 2)
+    out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    for i in range(16):
+        r.render(scene, cam, W, H, out.data_ptr())
+        while r.sync() != 0:
+            r.render(scene, cam, W, H, out.data_ptr())
+    assert r.get_tuning(KNOB_PM) == 1000 and r.get_tuning(KNOB_STATE) == 0
+    assert_frames(out.view(3, H, W).cpu().numpy(), want, exact=True)
+    r.close()
+
+
 def test_config3_split_off_same_lists(gpu, orc, torch, c3):
     """With the split off the tile lists are the whole depth order's; the default (on
     for this size) renders the same image, and so does the stage API, which never
