@@ -636,10 +636,6 @@ void mark(gsr_context* c, int stage) {
     (void)hipEventRecord(e, c->stream);
 }
 
-// Read the sticky stats of finished work; grow the pair buffer after an overflow.
-// An overflow (pairs over capacity, or a depth sort short of passes) is reported
-// once here and remembered in overflow_seen until gsr_sync, so a blocking sync also
-// reports what a non-blocking check inside a render call already consumed.
 // Depth split point after a frame that needed phase B: up by half, floor at 5/4 of the
 // old point, no speculation.
 void split_grow(gsr_context* c) {
@@ -653,6 +649,12 @@ void hv_clear_spec(gsr_context* c) {
     reinterpret_cast<volatile Stats*>(c->hstats)->spec_miss = 0;
 }
 
+// Read the sticky stats of finished work; grow the pair buffer after an overflow.
+// An overflow (pairs over capacity, a depth sort short of passes, or a speculative
+// depth-split frame that needed phase B) is reported once here and remembered in
+// overflow_seen until gsr_sync, so a blocking sync also reports what a non-blocking
+// check inside a render call already consumed.  The depth split's controller runs here
+// too (the counts phase B published for the finished frames).
 int check_overflow(gsr_context* c, bool blocking) {
     if (!c->pending) return GSR_OK;
     if (blocking) {
