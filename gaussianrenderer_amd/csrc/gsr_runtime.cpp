@@ -974,7 +974,10 @@ static int far_sort_locked(gsr_context* c) {
     const int di = c->depth_items ? c->depth_items : (c->n < (int64_t(4) << 20) ? 8 : 16);
     int gd = groups_for(c->n, 256 * di);
     if (c->depth_groups) gd = std::min(gd, c->depth_groups);
-    const int launch = c->depth_skip ? std::max(1, std::min(4, c->depth_budget)) : 4;
+    // the pass budget follows the near sorts (phase A's column scan reports them, and
+    // their key range can be far narrower); the far keys get at least three passes
+    // (keys below 2^24, depths under 16.7), so a phase B is rarely short of passes
+    const int launch = c->depth_skip ? std::max(3, std::min(4, c->depth_budget)) : 4;
     c->far_launched = launch;
     // the summed-area table of the tiles phase A left unsaturated; pass 0 reads the whole
     // preprocess order and keeps the items with keys at or above the frame's threshold

@@ -49,9 +49,13 @@ def main():
         cam = gsr.make_camera(position=(0, 0, 4), look_at=(x, 0, 0), fov_y=50, aspect=W / H)
         res = {}
         for rnd in range(2):
-            for split in (2, 0):
+            for split in [int(v) for v in os.environ.get("PMS", "2 0").split()]:
                 r = gsr.Renderer()
-                r.set_tuning(gsr.TUNE_DEPTH_SPLIT, split)
+                # PMS entries: 2 = the default controller, 0 = split off, > 2 = forced split
+                # starting at that split point (the controller still moves it)
+                r.set_tuning(gsr.TUNE_DEPTH_SPLIT, split if split <= 2 else 1)
+                if split > 2:
+                    r.set_tuning(gsr.TUNE_DEPTH_SPLIT_PERMILLE, split)
                 r.set_frames_in_flight(4)
                 for i in range(WARM):   # the controller settles; every lane's buffers grow
                     r.render_path(scene, [cam] * 8, W, H, [o.data_ptr() for o in outs]) if i % 2 else \
