@@ -385,6 +385,8 @@ struct gsr_context {
     int split_pm = 250;              // split point: phase A bins the nearest split_pm / 1000 of the depth order
     int split_floor = 0;             // 5/4 of the last split point that left blocks unsaturated
     int split_clean = 0;             // checked split frames in a row that left none
+    int split_off_frames = 0;        // frames since the split point reached 1000 (split off); at
+                                     // kSplitRetry the split is tried again from 250
     bool split_frame = false;        // the sorted frame is split (phase A lists binned by sort_locked)
     bool split_rebin = false;        // phase B's lists replaced phase A's: a repeated blend bins phase A again
     bool split_seen = false;         // a split frame was blended since the last controller update
@@ -392,6 +394,8 @@ struct gsr_context {
                                      // and 8 checked frames in a row needed none); a frame that then
                                      // leaves a block unsaturated is reported as GSR_E_OVERFLOW
     bool frame_spec = false;         // the sorted frame is blended without phase B
+    float split_view[32] = {};       // V and P of this context's last split frame: a frame speculates
+                                     // only with the same camera (its threshold then fits it)
     uint32_t split_na = 0;           // phase A's depth-order prefix (count mode) / the split point
     bool split_key = false;          // the preprocess left its items in items[1] for a threshold partition
     bool frame_key = false;          // the sorted frame is split in key mode (near part sorted, far part
@@ -460,6 +464,7 @@ namespace {
 // leaves the L2), the depth split on (GSR_TUNE_TILE_SPANS / GSR_TUNE_DEPTH_SPLIT = 2).
 constexpr int64_t kLargeScene = 3 << 19;
 constexpr int kSplitMinPm = 20;       // smallest split point (per mille)
+constexpr int kSplitRetry = 256;      // frames with the split turned off before it is tried again
 
 // The depth split applies to this context's frames of n Gaussians (binning path and the
 // exact blend; gsr_render / gsr_render_path decide it per frame, the stage API never).
@@ -842,8 +847,22 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     } else {
         arrays = reinterpret_cast<const float*>(static_cast<const char*>(scene) + GSR_SCENE_HEADER_BYTES);
     }
-    // depth split with a threshold partition (a threshold exists from an earlier split
-    // frame): the items go to items[1], the partition writes near-first into items[0]
+    // depth split: the controller turned it off (split point 1000) because phase A kept
+    // leaving blocks unsaturated; a moving camera can bring back views whose tiles all
+    // saturate, so it is tried again from the starting point every kSplitRetry frames
+    if (c->split_pm >= 1000 && (c->depth_split == 1 || (c->depth_split == 2 && n > kLargeScene))) {
+        if (++c->split_off_frames >= kSplitRetry) {
+            c->split_off_frames = 0;
+            c->split_pm = 250;
+            c->split_floor = 0;
+            c->split_clean = 0;
+            c->split_key_ready = false;
+        }
+    } else {
+        c->split_off_frames = 0;
+    }
+    // depth split with a depth threshold (a threshold exists from an earlier split
+    // frame): the items go to src_items, which both sorts' pass 0 read
     c->split_key = split_enabled(c, n) && c->split_key_ready && c->tile_binning && c->fr.tiles_x <= 256 &&
                    c->fr.tiles_y <= 256;
     // live partition (global depth sort on the binning path): the items go to
@@ -1080,7 +1099,15 @@ static int sort_locked(gsr_context* c, bool allow_split) {
         c->split_frame = split;
         c->split_rebin = false;
         c->frame_key = key;
-        c->frame_spec = split && key && c->split_spec;
+        // speculate only when the camera is the one the threshold came from (a moving camera
+        // would leave blocks unsaturated and cost a re-render)
+        const bool same_view = std::memcmp(c->split_view, c->fr.V, sizeof c->fr.V) == 0 &&
+                               std::memcmp(c->split_view + 16, c->fr.P, sizeof c->fr.P) == 0;
+        c->frame_spec = split && key && c->split_spec && same_view;
+        if (split) {
+            std::memcpy(c->split_view, c->fr.V, sizeof c->fr.V);
+            std::memcpy(c->split_view + 16, c->fr.P, sizeof c->fr.P);
+        }
         mark(c, GSR_STAGE_EMIT);
         if (split) {
             if (int rc = ensure_split(c)) return rc;

@@ -154,10 +154,11 @@ def test_config3_key_mode_camera_change(gpu, orc, torch, c3):
 def test_config3_speculation_and_miss(gpu, orc, torch, c3):
     """From a split point too small for the scene the controller grows it (phase B runs),
     then shrinks it to 5/4 of the last point that needed phase B and, when it cannot
-    shrink further, renders without phase B (state 3).  A frame that then leaves a
-    block unsaturated — here the camera moves back, so the previous frame's threshold
-    covers too little — is reported by gsr_sync as GSR_E_OVERFLOW; rendered again it is
-    bit-exact, and the controller has left speculation."""
+    shrink further, renders without phase B (state 3) — only while the camera stays the
+    one its threshold came from.  A moved camera queues phase B again (state 2, no miss).
+    A speculative frame that leaves a block unsaturated — here the same camera on a
+    scene with 30 % of the opacity, which the previous frame's threshold does not cover —
+    is reported by gsr_sync as GSR_E_OVERFLOW; rendered again it is bit-exact."""
     scene, soa, cam, W, H, want, _ = c3
     r = split_renderer(gpu, 2, 30)
     out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
@@ -176,10 +177,24 @@ def test_config3_speculation_and_miss(gpu, orc, torch, c3):
     far = cam_for(gpu, W, H, pos=(0, 0, 7))
     want_far = orc.render(soa, far, W, H, 3.0, threads=ORC_THREADS)
     r.render(scene, far, W, H, out.data_ptr())
-    assert r.sync() != 0, "a speculative frame that needed phase B was not reported"
-    r.render(scene, far, W, H, out.data_ptr())
-    assert r.sync() == 0 and r.get_tuning(KNOB_STATE) == 2
+    assert r.sync() == 0 and r.get_tuning(KNOB_STATE) == 2     # a moved camera: phase B queued
     assert_frames(out.view(3, H, W).cpu().numpy(), want_far, exact=True)
+    for _ in range(60):                                         # back to speculation on `cam`
+        r.render(scene, cam, W, H, out.data_ptr())
+        while r.sync() != 0:
+            r.render(scene, cam, W, H, out.data_ptr())
+        if r.get_tuning(KNOB_STATE) == 3:
+            break
+    assert r.get_tuning(KNOB_STATE) == 3
+    thin = soa.copy()
+    thin[3] *= 0.3                                              # opacity (sigmoid applied)
+    thin_scene = gpu.Scene.from_soa(thin)
+    want_thin = orc.render(thin, cam, W, H, 3.0, threads=ORC_THREADS)
+    r.render(thin_scene, cam, W, H, out.data_ptr())
+    assert r.sync() != 0, "a speculative frame that needed phase B was not reported"
+    r.render(thin_scene, cam, W, H, out.data_ptr())
+    assert r.sync() == 0 and r.get_tuning(KNOB_STATE) == 2
+    assert_frames(out.view(3, H, W).cpu().numpy(), want_thin, exact=True)
     r.close()
 
 
@@ -224,6 +239,18 @@ def test_config3_background_masked_phase_b(gpu, orc, torch, c3):
             r.render(scene, cam, W, H, out.data_ptr())
     assert r.get_tuning(KNOB_PM) == 1000 and r.get_tuning(KNOB_STATE) == 0
     assert_frames(out.view(3, H, W).cpu().numpy(), want, exact=True)
+    # the camera turns back to a view whose tiles all saturate: after 256 frames with the
+    # split off it is tried again, and it stays on
+    centred, want_c = c3[2], c3[5]
+    for i in range(300):
+        r.render(scene, centred, W, H, out.data_ptr())
+        if i % 16 == 15:
+            while r.sync() != 0:
+                r.render(scene, centred, W, H, out.data_ptr())
+    while r.sync() != 0:
+        r.render(scene, centred, W, H, out.data_ptr())
+    assert r.get_tuning(KNOB_STATE) in (1, 2, 3) and r.get_tuning(KNOB_PM) < 1000
+    assert_frames(out.view(3, H, W).cpu().numpy(), want_c, exact=True)
     r.close()
 
 
