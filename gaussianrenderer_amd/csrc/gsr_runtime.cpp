@@ -385,8 +385,11 @@ struct gsr_context {
     int split_pm = 250;              // split point: phase A bins the nearest split_pm / 1000 of the depth order
     int split_floor = 0;             // 5/4 of the last split point that left blocks unsaturated
     int split_clean = 0;             // checked split frames in a row that left none
-    int split_off_frames = 0;        // frames since the split point reached 1000 (split off); at
-                                     // kSplitRetry the split is tried again from 250
+    int split_off_frames = 0;        // frames since the split point reached 1000 (split off); after
+                                     // split_retry of them, on a new camera, the split is tried again
+    int split_retry = 0;             // frames before the next retry (kSplitRetry, doubling after each
+                                     // retry that found no saturating view, back after a clean one)
+    float split_off_view[32] = {};   // V and P of the frame the split was turned off on
     bool split_frame = false;        // the sorted frame is split (phase A lists binned by sort_locked)
     bool split_rebin = false;        // phase B's lists replaced phase A's: a repeated blend bins phase A again
     bool split_seen = false;         // a split frame was blended since the last controller update
@@ -465,6 +468,7 @@ namespace {
 constexpr int64_t kLargeScene = 3 << 19;
 constexpr int kSplitMinPm = 20;       // smallest split point (per mille)
 constexpr int kSplitRetry = 256;      // frames with the split turned off before it is tried again
+constexpr int kSplitRetryMax = 1 << 14;
 
 // The depth split applies to this context's frames of n Gaussians (binning path and the
 // exact blend; gsr_render / gsr_render_path decide it per frame, the stage API never).
@@ -695,6 +699,7 @@ int check_overflow(gsr_context* c, bool blocking) {
             // the newest phase B ran at an earlier split point (frames in flight): no
             // evidence about the current one yet
         } else if (u == 0) {
+            c->split_retry = kSplitRetry;   // a saturating view: the next turn-off retries soon
             if (++c->split_clean >= 8) {
                 c->split_clean = 0;
                 const int next = std::max(std::max(kSplitMinPm, c->split_floor), c->split_pm * 7 / 8);
@@ -849,9 +854,21 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     }
     // depth split: the controller turned it off (split point 1000) because phase A kept
     // leaving blocks unsaturated; a moving camera can bring back views whose tiles all
-    // saturate, so it is tried again from the starting point every kSplitRetry frames
+    // saturate, so after split_retry frames on another camera than the one it was turned
+    // off on (a fixed camera, or a 4D scene's fixed camera over time, never retries) it is
+    // tried again from the starting point; each retry doubles the next wait, up to
+    // kSplitRetryMax, until a retry finds a view whose tiles all saturate
     if (c->split_pm >= 1000 && (c->depth_split == 1 || (c->depth_split == 2 && n > kLargeScene))) {
-        if (++c->split_off_frames >= kSplitRetry) {
+        if (c->split_off_frames == 0) {
+            std::memcpy(c->split_off_view, c->fr.V, sizeof c->fr.V);
+            std::memcpy(c->split_off_view + 16, c->fr.P, sizeof c->fr.P);
+        }
+        if (c->split_retry == 0) c->split_retry = kSplitRetry;
+        c->split_off_frames = std::min(c->split_off_frames + 1, 1 << 30);
+        const bool moved = std::memcmp(c->split_off_view, c->fr.V, sizeof c->fr.V) != 0 ||
+                           std::memcmp(c->split_off_view + 16, c->fr.P, sizeof c->fr.P) != 0;
+        if (c->split_off_frames >= c->split_retry && moved) {
+            c->split_retry = std::min(2 * c->split_retry, kSplitRetryMax);
             c->split_off_frames = 0;
             c->split_pm = 250;
             c->split_floor = 0;

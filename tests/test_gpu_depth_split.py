@@ -239,8 +239,15 @@ def test_config3_background_masked_phase_b(gpu, orc, torch, c3):
             r.render(scene, cam, W, H, out.data_ptr())
     assert r.get_tuning(KNOB_PM) == 1000 and r.get_tuning(KNOB_STATE) == 0
     assert_frames(out.view(3, H, W).cpu().numpy(), want, exact=True)
-    # the camera turns back to a view whose tiles all saturate: after 256 frames with the
-    # split off it is tried again, and it stays on
+    # the same camera never retries the split (nothing in its view can change)
+    for i in range(300):
+        r.render(scene, cam, W, H, out.data_ptr())
+        if i % 16 == 15:
+            assert r.sync() == 0
+            assert r.get_tuning(KNOB_PM) == 1000 and r.get_tuning(KNOB_STATE) == 0
+    assert r.sync() == 0
+    # the camera turns back to a view whose tiles all saturate: 256 frames after the split
+    # was turned off, on another camera, it is tried again, and it stays on
     centred, want_c = c3[2], c3[5]
     for i in range(300):
         r.render(scene, centred, W, H, out.data_ptr())
