@@ -326,7 +326,9 @@ enum {
                                         sorts the far part when it runs); the split point adapts to the
                                         frames seen, and once it cannot shrink further frames are
                                         rendered without phase B until one needs it (that frame returns
-                                        GSR_E_OVERFLOW: render it again).  0 = one phase; 2 (default) =
+                                        GSR_E_OVERFLOW: render it again).  A split point grown to 1000
+                                        turns it off; it is tried again 256+ frames later, only on
+                                        another camera.  0 = one phase; 2 (default) =
                                         1 above 1.5M Gaussians.  Same image.  After a split frame
                                         gsr_read_pairs / gsr_read_tile_ranges hold the lists of its last
                                         phase, and after a threshold split gsr_read_depth_order is refused */
