@@ -707,7 +707,15 @@ int check_overflow(gsr_context* c, bool blocking) {
                 c->split_pm = next;
             }
         } else {
+            const int pm_old = c->split_pm;
             split_grow(c);   // phase A left blocks unsaturated
+            if (c->split_pm >= 1000) {
+                // the split turned itself off: the next frames list the whole order's pairs.
+                // Size the pair buffer for them now (the split frames' pairs scaled to the
+                // whole order) rather than overflow and re-render a chunk
+                const int64_t want = (int64_t)(s.pairs_total * 1000 / (unsigned)pm_old) * 5 / 4 + 4096;
+                if (int rc = ensure_pairs(c, want)) return rc;
+            }
         }
     }
     if (!s.overflow) {
