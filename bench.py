@@ -76,6 +76,12 @@ def parse():
                     help="frames in flight per GPU (gsr_render_path lanes); 1 = one frame at a time")
     ap.add_argument("--chunk", type=int, default=8,
                     help="N>1 with --gather step: frames per render_path call (one RCCL gather per frame)")
+    ap.add_argument("--sh3", action="store_true",
+                    help="config 2 as BASELINE states it (SH degree 3): the opt-in SH-3 mode (all 45 f_rest, "
+                         "bands 0-3; the reference evaluates bands 0-2)")
+    ap.add_argument("--orbit-step", type=float, default=0.0,
+                    help="degrees of Camera::orbit per frame (a moving viewer: frame i at azimuth i * step); "
+                         "0 = the fixed camera")
     ap.add_argument("--tune", default="",
                     help="gsr_set_tuning knob=value pairs, comma-separated (include/gsr.h GSR_TUNE_*; A/B runs)")
     return ap.parse_args()
@@ -88,10 +94,12 @@ def algorithmic_blend_bytes(ntiles: int, consumed: int, W: int, H: int) -> int:
 
 
 def algorithmic_stage_bytes(n: int, m: int, pairs: int, ntiles: int, consumed: int, W: int, H: int,
-                            depth_passes: int = 4, tile_passes: int = 2, row_items: int = -1) -> dict:
+                            depth_passes: int = 4, tile_passes: int = 2, row_items: int = -1,
+                            sh_floats: int = 27) -> dict:
     """Minimal bytes each stage of this design must move (per-stage table):
-    preprocess N*152 read (38 fp32 SoA arrays) + M*64 records + N*8 item + the tile
-    rect (N*4 packed on the binning path, N*8 for the pair sort);
+    preprocess N*152 read (38 fp32 SoA arrays; SH-3 mode: 48 SH floats, N*236) + M*64
+    records + N*8 item + the tile rect (N*4 packed on the binning path, N*8 for the pair
+    sort);
     blend as algorithmic_blend_bytes.
     Tile binning (row_items R >= 0): depth sort passes*N*32 (upsweep read 8, downsweep
     read 8 + 4 and write 8 + 4: item and its packed rect payload);
@@ -103,7 +111,7 @@ def algorithmic_stage_bytes(n: int, m: int, pairs: int, ntiles: int, consumed: i
     Pair sort (R < 0): depth sort passes*N*24; emit N*40 (sorted items twice, rect
     gather, srect write/read) + P*6 (u16 key + u32 value); tile sort P*14 per
     non-final pass, P*12 for the final one (keys 2 up, 6 read, 6|4 write) + T*8."""
-    out = {"preprocess": 152 * n + 64 * m + (12 if row_items >= 0 else 16) * n,
+    out = {"preprocess": (152 + 4 * (sh_floats - 27)) * n + 64 * m + (12 if row_items >= 0 else 16) * n,
            "blend": algorithmic_blend_bytes(ntiles, consumed, W, H)}
     if row_items >= 0 and depth_passes == 0:
         # per-tile depth order: binning in index order (rects + items read as in the
@@ -173,9 +181,12 @@ def dropin_rate(gsr, scene, cam, W, H, k, frames=20):
     return frames / (time.perf_counter() - t0)
 
 
-def cpu_baseline(soa, cam, W, H, k, seconds, four_d=False):
+def cpu_baseline(soa, cam, W, H, k, seconds, four_d=False, sh3=False, cams=None):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle  # test infrastructure: CPU baseline leg only
+    if sh3:
+        with _oracle.sh3_mode():
+            return cpu_baseline(soa, cam, W, H, k, seconds, four_d, False, cams)
     share = cpu_share()
     threads = share["threads"]
     frames, t0 = 0, time.perf_counter()
@@ -183,7 +194,7 @@ def cpu_baseline(soa, cam, W, H, k, seconds, four_d=False):
         if four_d:   # temporal state of the frame, then the 3D render (no cull)
             _oracle.render(_oracle.temporal(soa, frame_time(frames)), cam, W, H, k, threads=threads)
         else:
-            _oracle.render(soa, cam, W, H, k, threads=threads)
+            _oracle.render(soa, cams(frames) if cams else cam, W, H, k, threads=threads)
         frames += 1
         el = time.perf_counter() - t0
         if el >= seconds or frames >= 50:
@@ -328,13 +339,24 @@ def main():
             tmp = ply + f".tmp{os.getpid()}"
             (gsr.write_synthetic_ply4d if four_d else gsr.write_synthetic_ply)(tmp, n, seed)
             os.replace(tmp, ply)
-        scene = gsr.Scene.from_ply(ply)       # the drop-in loader path (misc.cu:13-134)
+        scene = gsr.Scene.from_ply(ply, sh3=args.sh3)   # the drop-in loader path (misc.cu:13-134)
     # N > 1: rank 0's device scene block reaches the other ranks in one broadcast
     # (over xGMI with RCCL), no rank but 0 reads the file
     load_s = time.perf_counter()
     scene = multi.broadcast_scene(dist, scene, gloo=gloo) if dist else scene
     broadcast_ms = (time.perf_counter() - load_s) * 1e3 if dist else None
     cam = multi.orbit_camera(rank, W, H)      # rank 0: camera (0,0,4); config 4: orbit 45 deg * rank
+    frame_cam = None
+    if args.orbit_step:
+        # a moving viewer: frame i at azimuth 45 deg * rank + i * step (one Camera::orbit call)
+        cam_cache = {}
+
+        def frame_cam(i):
+            if i not in cam_cache:
+                c = gsr.make_camera(position=(0, 0, 4), fov_y=50, aspect=W / H)
+                gsr.orbit(c, multi.orbit_azimuth(rank) + args.orbit_step * i, 0.0)
+                cam_cache[i] = c
+            return cam_cache[i]
 
     r = gsr.Renderer()
     for kv in filter(None, args.tune.split(",")):
@@ -345,7 +367,7 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     shard = multi.FrameShard(dist, r, scene, cam, W, H, k=args.k, steps=args.steps, gather=args.gather,
                              inflight=F, chunk=args.chunk, gloo=gloo, frame_time=frame_time if four_d else None,
-                             stream=stream)
+                             stream=stream, frame_cam=frame_cam)
     outs, frame, path = shard.outs, shard.frame, shard.path
 
     # warmup (+ grow every lane's pair buffer to the high-water mark)
@@ -448,7 +470,19 @@ def main():
     # collective); a region with one is timed again, once, on the grown buffers.
     dev_kind = "cpu" if gloo else "cuda"
     reruns = 0
-    if F > 1 or shard.step_gather:
+    if shard.validity:
+        # per-step gathers carry each frame's validity word: the timed region includes
+        # re-rendering and re-gathering exactly the chunks some rank got incomplete
+        shard.overflowed, shard.gathers, shard.repaired = False, 0, 0
+        r.set_timing(1, TIMING_STRIDE)
+        clean = []
+        elapsed = timed(lambda: clean.append(shard.run_checked(args.steps, dev_kind)))
+        blend_times_pipe, timed_frames_pipe = r.stage_times()
+        r.set_timing(0)
+        reruns = shard.repaired
+        if not clean[0]:
+            sys.exit("bench.py: frames still incomplete after repairs")
+    elif F > 1:
         for attempt in range(2):
             shard.overflowed, shard.gathers = False, 0
             r.set_timing(1, TIMING_STRIDE)
@@ -487,7 +521,8 @@ def main():
     achieved = bytes_blend / (blend_avg_ms * 1e-3) / 1e9
     img = outs[0].view(3, H, W)
     result = {
-        "metric": "frames/sec at 1920x1080, 1M Gaussians (config %d)" % args.config if args.config == 2
+        "metric": ("frames/sec at 1920x1080, 1M Gaussians (config %d%s)"
+                   % (args.config, ", SH degree 3" if args.sh3 else "")) if args.config == 2
         else (f"frames/sec at 1920x1080, 2M 4D Gaussians, {TIMESTEPS_4D} timesteps (config 5)" if four_d
               else f"frames/sec (config {args.config})"),
         "value": round(value, 3),
@@ -507,7 +542,12 @@ def main():
                                + (f"one orbit camera per GPU, {'RCCL' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'} "
                                   f"gather to rank 0 ({args.gather})" if world > 1
                                   else "camera (0,0,4) fovY 50")
+                               + (f", moving camera: frame i orbited by {args.orbit_step:g} deg * i"
+                                  if args.orbit_step else "")
+                               + (", SH degree 3 (opt-in SH-3 mode: 45 f_rest, bands 0-3)" if args.sh3
+                                  else ", SH bands 0-2 as the reference evaluates (render.cu:506-530)")
                                + f", {F} frame(s) in flight per GPU (gsr_render_path)",
+                   "sh_degree": 3 if args.sh3 else 2, "orbit_step_deg": args.orbit_step,
                    "gaussians": n, "width": W, "height": H, "parallelism": f"frames{world}"},
         "roofline": {"bound": "hbm", "kernel": BLEND_KERNEL, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -539,6 +579,8 @@ def main():
         "image_mean": float(img.mean().item()),
         "overflow_after_timed": overflow,
         "overflow_reruns": reruns,
+        "overflow_reruns_unit": "chunks re-rendered and re-gathered inside the timed region (validity words)"
+                                if shard.validity else "timed regions run again (whole region, untimed retry)",
     }
     result["gpu_telemetry"] = {"before_warmup": telemetry_before, "after_timed": telemetry_after}
     result["sustained_warmup"] = {"frames": warm_frames, "min_ms": args.warm_ms}
@@ -548,7 +590,7 @@ def main():
         result["scene_broadcast_ms"] = round(broadcast_ms, 2)
         result["gathers_per_rank_timed"] = shard.gathers
     sb = algorithmic_stage_bytes(n, visible, pairs, ntiles, consumed, W, H, depth_passes=depth_passes,
-                                 row_items=row_items)
+                                 row_items=row_items, sh_floats=48 if args.sh3 else 27)
     result["stages_gbs"] = {k: round(sb[k] / (stages[k] * 1e-3) / 1e9, 1) for k in sb if stages.get(k)}
     result["stages_gbs"]["blend"] = round(achieved, 1)     # timed frames, not the diagnostics frame
     result["stages_algorithmic_bytes"] = sb
@@ -570,8 +612,9 @@ def main():
     if world == 1:
         result["dropin_host_fps"] = round(dropin_rate(gsr, scene, cam, W, H, args.k), 2)
     if world == 1 and not args.no_cpu_baseline:
-        soa = gsr.read_ply(ply, four_d=four_d)
-        result["cpu_baseline"] = cpu_baseline(soa, cam, W, H, args.k, args.cpu_seconds, four_d=four_d)
+        soa = gsr.read_ply(ply, four_d=four_d, sh3=args.sh3)
+        result["cpu_baseline"] = cpu_baseline(soa, cam, W, H, args.k, args.cpu_seconds, four_d=four_d, sh3=args.sh3,
+                                              cams=frame_cam)
     print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()

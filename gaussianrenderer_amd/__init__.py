@@ -309,7 +309,7 @@ class Renderer:
 
     def render_path(self, scene, cams, W: int, H: int, out_ptrs, k: float = 3.0, tiling=None, stream: int = 0,
                     layout: int = LAYOUT_SCENE_BLOCK, n: int | None = None, times=None, events=None,
-                    join: bool = True, fork: bool = True, wait_events=None) -> int:
+                    join: bool = True, fork: bool = True, wait_events=None, status=None) -> int:
         """Enqueue len(cams) frames (camera cams[i], 4D time times[i]) into the device
         buffers out_ptrs[i] with up to frames_in_flight() of them concurrent
         (gsr_render_path, include/gsr.h).  Stream-ordered on `stream` at entry and exit.
@@ -317,6 +317,8 @@ class Renderer:
         frame i's lane after its blend; join=False skips the exit join (the caller then
         orders reads and buffer reuse through the events); wait_events[i] (or None): frame
         i's lane waits for it first; fork=False: lanes 1.. do not wait for `stream`.
+        status (gsr_render_path_status): per-frame device address (or None) of a uint32
+        validity word, 0 when frame i came out complete, else GSR_FRAME_* bits.
         Same returns as render()."""
         ptr = scene.ptr if isinstance(scene, Scene) else int(scene)
         n = scene.n if n is None else n
@@ -329,19 +331,20 @@ class Renderer:
         out_arr = (c_void_p * max(1, nf))(*[int(p) for p in out_ptrs])
         t_arr = (c_float * nf)(*[float(t) for t in times]) if times is not None else None
         t = tiling or TilingInformation(1, 1, H, W)
-        if events is None and wait_events is None and join and fork:
+        if events is None and wait_events is None and join and fork and status is None:
             rc = lib().gsr_render_path(self.ctx, ptr, layout, n, cam_arr, t_arr, nf, W, H, t.num_tile_x,
                                        t.num_tile_y, t.width_stride, t.height_stride, k, out_arr, stream or None)
         else:
-            if (events is not None and len(events) != nf) or (wait_events is not None and len(wait_events) != nf):
-                raise ValueError("render_path: events and wait_events must have one entry per frame")
+            if any(x is not None and len(x) != nf for x in (events, wait_events, status)):
+                raise ValueError("render_path: events, wait_events and status must have one entry per frame")
             ev_arr = (c_void_p * max(1, nf))(*[_event_handle(e) for e in (events or [None] * nf)])
             wt_arr = (c_void_p * max(1, nf))(*[_event_handle(e, wait=True) for e in (wait_events or [None] * nf)])
-            rc = lib().gsr_render_path_ex(self.ctx, ptr, layout, n, cam_arr, t_arr, nf, W, H, t.num_tile_x,
-                                          t.num_tile_y, t.width_stride, t.height_stride, k, out_arr,
-                                          stream or None, ev_arr, wt_arr,
-                                          (0 if join else _native.GSR_PATH_NO_JOIN) |
-                                          (0 if fork else _native.GSR_PATH_NO_FORK))
+            st_arr = (c_void_p * max(1, nf))(*[int(p) if p else None for p in status]) if status else None
+            rc = lib().gsr_render_path_status(self.ctx, ptr, layout, n, cam_arr, t_arr, nf, W, H, t.num_tile_x,
+                                              t.num_tile_y, t.width_stride, t.height_stride, k, out_arr,
+                                              stream or None, ev_arr, wt_arr,
+                                              (0 if join else _native.GSR_PATH_NO_JOIN) |
+                                              (0 if fork else _native.GSR_PATH_NO_FORK), st_arr)
         if rc not in (_native.GSR_OK, _native.GSR_E_OVERFLOW):
             raise GsrError(rc, "gsr_render_path")
         return rc

@@ -29,6 +29,9 @@ GSR_E_OVERFLOW = -5
 GSR_PATH_NO_JOIN = 1   # gsr_render_path_ex flags (include/gsr.h)
 GSR_PATH_NO_FORK = 2
 GSR_E_DISPLAY = -6
+GSR_FRAME_PAIR_OVERFLOW = 1   # gsr_render_path_status validity bits (include/gsr.h)
+GSR_FRAME_DEPTH_PASSES = 2
+GSR_FRAME_SPEC_MISS = 4
 
 LAYOUT_SCENE_BLOCK = 0
 LAYOUT_AOS = 1
@@ -110,6 +113,9 @@ SIGNATURES = [
     ("gsr_render_path_ex", c_int, [c_void_p, c_void_p, c_int, c_int64, POINTER(Camera), c_void_p, c_int, c_int,
                                    c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_int]),
+    ("gsr_render_path_status", c_int, [c_void_p, c_void_p, c_int, c_int64, POINTER(Camera), c_void_p, c_int,
+                                       c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_int, c_void_p]),
     ("gsr_set_frames_in_flight", c_int, [c_void_p, c_int]),
     ("gsr_frames_in_flight", c_int, [c_void_p]),
     ("gsr_preprocess", c_int, [c_void_p, c_void_p, c_int, c_int64, POINTER(Camera), c_int, c_int, c_int, c_int,

@@ -112,6 +112,8 @@ struct BlendSplit {
                                       // spec_host->spec_miss (nullable)
     SplitCut cut;                     // phase A: the next frame's threshold
     uint32_t pm;                      // phase B publishes it with the count (Stats::split_pm)
+    uint32_t* fstatus;                // speculative phase A: an unsaturated block ors
+                                      // GSR_FRAME_SPEC_MISS into the frame's validity word (nullable)
 };
 
 // ---- launch wrappers (gsr_kernels.hip) ----
@@ -141,7 +143,7 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
 hipError_t launch_emit(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,
                        const uint64_t* rect, int groups, unsigned long long* wg_scratch, Stats* stats,
                        Stats* host_mapped_stats, uint32_t pair_capacity, int tiles_x, int tiles_y, void* keys,
-                       bool key16, uint32_t* vals, uint2* ranges, hipStream_t s);
+                       bool key16, uint32_t* vals, uint2* ranges, hipStream_t s, uint32_t* fstatus = nullptr);
 // One stable key-value LSD pass of the tile sort; keys_out == nullptr marks the
 // final pass (values only, tile ranges recorded).
 hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* keys_out, uint32_t* vals_out,
@@ -181,7 +183,7 @@ hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, 
                            uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
                            uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,
                            hipStream_t s, const uint32_t* dstats = nullptr, int passes_launched = 4,
-                           bool rank_atomic = false, const uint32_t* gate = nullptr);
+                           bool rank_atomic = false, const uint32_t* gate = nullptr, uint32_t* fstatus = nullptr);
 uint32_t bin_col_chunks_max(uint32_t pair_capacity, int tiles_y);
 // Standalone sort ABI helpers (oneSweepSort / oneSweep3DGaussianSort).
 hipError_t launch_items_from_keys(const int* keys, uint32_t n, uint64_t* items, hipStream_t s);

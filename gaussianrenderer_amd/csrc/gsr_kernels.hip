@@ -493,10 +493,9 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     RT[0] = Rm[0]; RT[1] = Rm[3]; RT[2] = Rm[6];
     RT[3] = Rm[1]; RT[4] = Rm[4]; RT[5] = Rm[7];
     RT[6] = Rm[2]; RT[7] = Rm[5]; RT[8] = Rm[8];
-    const float scale_mod = 1.0f;
-    S[0] = scale_mod * s_in[0]; S[1] = 0.0f; S[2] = 0.0f;
-    S[3] = 0.0f; S[4] = scale_mod * s_in[1]; S[5] = 0.0f;
-    S[6] = 0.0f; S[7] = 0.0f; S[8] = scale_mod * s_in[2];
+    S[0] = s_in[0]; S[1] = 0.0f; S[2] = 0.0f;
+    S[3] = 0.0f; S[4] = s_in[1]; S[5] = 0.0f;
+    S[6] = 0.0f; S[7] = 0.0f; S[8] = s_in[2];
     mm3(Rm, S, tmp);
     mm3(tmp, S, Rm);
     mm3(Rm, RT, cov);
@@ -1283,7 +1282,7 @@ __global__ __launch_bounds__(256) void k_emit_count(const uint64_t* __restrict__
 // the agent-scope fences before each arrival ticket write back the L2 on gfx950.)
 __global__ __launch_bounds__(256) void k_emit_scan(unsigned long long* __restrict__ wg, int groups,
                                                     uint32_t cap, Stats* __restrict__ st,
-                                                    Stats* host_st) {
+                                                    Stats* host_st, uint32_t* fstatus) {
     GSR_GEOM_PRIO();
     __shared__ unsigned long long scr[4];
     const int per = (groups + 255) / 256;
@@ -1311,6 +1310,7 @@ __global__ __launch_bounds__(256) void k_emit_scan(unsigned long long* __restric
         k.pairs_eff = s.pairs_eff;
         k.overflow |= s.overflow;
         st[1] = k;
+        if (fstatus) *fstatus = s.overflow;
         if (host_st) {
             host_st->pairs_total = k.pairs_total;
             host_st->pairs_eff = k.pairs_eff;
@@ -1565,8 +1565,12 @@ __device__ __forceinline__ void bin_tile_owners(const uint32_t (&cnt)[PER], cons
 // the host launched (its pass budget); needed > launched leaves the depth order
 // incomplete, so the frame is flagged (overflow bit 1) and re-rendered like a
 // pair-buffer overflow.  depth_passes is the latest frame's, not sticky.
+// fstatus (nullable): the frame's validity word (gsr_render_path_status): set to the
+// frame's overflow bits by its first column scan (fst_first: phase A or one phase),
+// or-ed in by phase B's.
 __device__ __forceinline__ void publish_pair_stats(unsigned long long total, uint32_t cap, Stats* st,
-                                                   Stats* host_st, uint32_t needed = 0, uint32_t launched = 4) {
+                                                   Stats* host_st, uint32_t needed = 0, uint32_t launched = 4,
+                                                   uint32_t* fstatus = nullptr, bool fst_first = true) {
     Stats s{};
     s.pairs_total = total;
     s.pairs_eff = (uint32_t)(total < cap ? total : cap);
@@ -1579,6 +1583,10 @@ __device__ __forceinline__ void publish_pair_stats(unsigned long long total, uin
     k.overflow |= s.overflow;
     k.depth_passes = s.depth_passes;
     st[1] = k;
+    if (fstatus) {
+        if (fst_first) *fstatus = s.overflow;
+        else if (s.overflow) atomicOr(fstatus, s.overflow);
+    }
     if (host_st) {
         host_st->pairs_total = k.pairs_total;
         host_st->pairs_eff = k.pairs_eff;
@@ -1986,7 +1994,8 @@ __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restric
                                                         uint32_t cap, int tiles_x, uint32_t* __restrict__ cbins,
                                                         uint2* __restrict__ ranges, Stats* __restrict__ st,
                                                         Stats* host_st, const uint32_t* __restrict__ dstats,
-                                                        int passes_launched, const uint32_t* __restrict__ gate) {
+                                                        int passes_launched, const uint32_t* __restrict__ gate,
+                                                        uint32_t* fstatus) {
     GSR_GEOM_PRIO();
     if (gate && *gate == 0u) return;
     __shared__ ColPlan<true> pl;
@@ -1996,7 +2005,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restric
     const unsigned long long P = col_plan(row_items, row_pairs, pl, s_scr, s_scr64);
     if (r == 0 && t == 0)
         publish_pair_stats(P, cap, st, host_st, dstats ? (uint32_t)depth_passes_run(dstats) : 0u,
-                           (uint32_t)passes_launched);
+                           (uint32_t)passes_launched, fstatus, gate == nullptr);
     uint32_t run = 0;
     if (P <= cap && t < (uint32_t)tiles_x) {
         // 32 chunks per step: the loads are issued together, not one round trip per chunk
@@ -2775,6 +2784,7 @@ __global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx
                                                        SPLIT ? sp.bflag + L : nullptr, sp.gate);
     if (SPLIT == 1 && redo && sp.spec_host && lane == 0) {
         sp.spec_host->spec_miss = 1u;   // no phase B queued for this frame: it is incomplete
+        if (sp.fstatus) atomicOr(sp.fstatus, 4u);
         __threadfence_system();
     }
     if (FX && redo) {
@@ -3055,11 +3065,11 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
 hipError_t launch_emit(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,
                        const uint64_t* rect, int groups, unsigned long long* wg_scratch, Stats* stats,
                        Stats* host_mapped_stats, uint32_t pair_capacity, int tiles_x, int tiles_y, void* keys,
-                       bool key16, uint32_t* vals, uint2* ranges, hipStream_t s) {
+                       bool key16, uint32_t* vals, uint2* ranges, hipStream_t s, uint32_t* fstatus) {
     hipLaunchKernelGGL(k_emit_count, dim3(groups), dim3(256), 0, s, items0, items1, dstats, n, rect, groups,
                        wg_scratch, ranges, tiles_x * tiles_y);
     hipLaunchKernelGGL(k_emit_scan, dim3(1), dim3(256), 0, s, wg_scratch, groups, pair_capacity, stats,
-                       host_mapped_stats);
+                       host_mapped_stats, fstatus);
     if (key16)
         hipLaunchKernelGGL(k_emit_pairs<uint16_t>, dim3(groups), dim3(256), 0, s, items0, items1, dstats, n, groups,
                            wg_scratch, pair_capacity, tiles_x, static_cast<uint16_t*>(keys), vals);
@@ -3113,14 +3123,14 @@ hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, 
                            uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
                            uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,
                            hipStream_t s, const uint32_t* dstats, int passes_launched, bool rank_atomic,
-                           const uint32_t* gate) {
+                           const uint32_t* gate, uint32_t* fstatus) {
     if (tiles_x < 1 || tiles_x > 256 || tiles_y < 1 || tiles_y > 256 || col_groups < 1 ||
         (items != 4 && items != 8 && items != 16))
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_bin_cols_count, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs,
                        pair_capacity, tiles_x, cbins, gate);
     hipLaunchKernelGGL(k_bin_cols_scan, dim3(tiles_y), dim3(256), 0, s, row_items, row_pairs, pair_capacity, tiles_x,
-                       cbins, ranges, stats, host_mapped_stats, dstats, passes_launched, gate);
+                       cbins, ranges, stats, host_mapped_stats, dstats, passes_launched, gate, fstatus);
     auto pick = [&](auto ra) {
         constexpr bool RA = decltype(ra)::value;
         return tiles_x <= 128 ? (items == 4 ? k_bin_cols_scatter<4, 7, RA> : items == 8 ? k_bin_cols_scatter<8, 7, RA>
@@ -3190,7 +3200,7 @@ hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* r
     const int phase = split ? split->phase : 0;
     if (phase < 0 || phase > 2 || (phase && (fast_exp || stamps || !split->tbuf || !split->bflag || !split->gate)))
         return hipErrorInvalidValue;
-    const BlendSplit sp = split ? *split : BlendSplit{0, nullptr, nullptr, nullptr, nullptr, nullptr, {}, 0u};
+    const BlendSplit sp = split ? *split : BlendSplit{0, nullptr, nullptr, nullptr, nullptr, nullptr, {}, 0u, nullptr};
 #define GSR_BLEND_S(D, ST, FX, SP)                                                                          \
     hipLaunchKernelGGL((k_blend_w<D, ST, FX, SP>), dim3(ng), dim3(64), 0, s, idx, ranges, rec, fr.tiles_x,  \
                        fr.tiles_y, fr.W, fr.H, fr.cover_w, fr.cover_h, out, consumed, bands, band0, sp)

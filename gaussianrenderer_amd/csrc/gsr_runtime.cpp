@@ -430,6 +430,8 @@ struct gsr_context {
                                      // (the environment's GSR_RANK_ATOMIC=0 selects 0, else 1)
     bool rank_ok = false;            // the device passed the rank-order self-check (ensure_static)
     bool overflow_seen = false;      // an overflow was reported since the last gsr_sync (which reports it again)
+    uint32_t* fstatus = nullptr;     // the current frame's validity word (gsr_render_path_status; device,
+                                     // nullable): GSR_FRAME_* bits, written by its column scans / blend
     // frame state
     Frame fr{};
     int64_t n = 0;
@@ -665,8 +667,13 @@ void hv_clear_spec(gsr_context* c) {
 // check inside a render call already consumed.  The depth split's controller runs here
 // too (the counts phase B published for the finished frames).
 int check_overflow(gsr_context* c, bool blocking) {
-    if (!c->pending) return GSR_OK;
-    if (blocking) {
+    if (!c->pending) {
+        // with completion events off (stream capture) no event marks finished work: a
+        // blocking check (gsr_sync) drains the device and reads the sticky words anyway,
+        // so an overflow or a speculative miss is still reported there
+        if (!blocking || c->completion_events || !c->hstats) return GSR_OK;
+        HIP_TRY(hipDeviceSynchronize());
+    } else if (blocking) {
         HIP_TRY(hipEventSynchronize(c->done_ev));
     } else if (hipEventQuery(c->done_ev) != hipSuccess) {
         return GSR_OK;
@@ -740,6 +747,9 @@ int check_overflow(gsr_context* c, bool blocking) {
     s.overflow |= hv->overflow;
     if (hv->pairs_total > s.pairs_total) s.pairs_total = hv->pairs_total;
     c->overflow_seen = true;
+    // a speculative miss in the same frames: stop speculating before the words are
+    // cleared, or the re-render of this camera speculates (and misses) again
+    if (hv->spec_miss) split_grow(c);
     if (s.overflow & 2u) {   // back to four launched passes
         c->depth_budget = 4;
         c->depth_budget_streak = 0;
@@ -1083,7 +1093,7 @@ static int bin_locked(gsr_context* c, uint32_t base, uint32_t count, int gate_mo
                                  c->fr.tiles_x, c->fr.tiles_y, pair_vals(c, 1), c->ranges, c->stats,
                                  c->hstats_dev, c->bin_col_items, c->stream,
                                  dst, far ? c->far_launched : c->passes_launched, rank_atomic_on(c),
-                                 gate_mode == 2 ? c->gate : nullptr));
+                                 gate_mode == 2 ? c->gate : nullptr, c->fstatus));
     c->pair_buf = 1;
     return GSR_OK;
 }
@@ -1128,7 +1138,9 @@ static int sort_locked(gsr_context* c, bool allow_split) {
         // would leave blocks unsaturated and cost a re-render)
         const bool same_view = std::memcmp(c->split_view, c->fr.V, sizeof c->fr.V) == 0 &&
                                std::memcmp(c->split_view + 16, c->fr.P, sizeof c->fr.P) == 0;
-        c->frame_spec = split && key && c->split_spec && same_view;
+        // (and only with completion events on: a captured graph would bake "no phase B"
+        // into every replay)
+        c->frame_spec = split && key && c->split_spec && same_view && c->completion_events;
         if (split) {
             std::memcpy(c->split_view, c->fr.V, sizeof c->fr.V);
             std::memcpy(c->split_view + 16, c->fr.P, sizeof c->fr.P);
@@ -1152,7 +1164,7 @@ static int sort_locked(gsr_context* c, bool allow_split) {
     const bool key16 = c->ntiles <= 65536;
     HIP_TRY(gsr::launch_emit(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n, c->rect, ge, c->wg,
                              c->stats, c->hstats_dev, (uint32_t)c->p_cap, c->fr.tiles_x, c->fr.tiles_y,
-                             pair_keys(c, 0), key16, pair_vals(c, 0), c->ranges, c->stream));
+                             pair_keys(c, 0), key16, pair_vals(c, 0), c->ranges, c->stream, c->fstatus));
     // ---- stable key-value tile sort ----
     mark(c, GSR_STAGE_TILE_SORT);
     const int tbits = std::max(1, ceil_log2(c->ntiles));
@@ -1210,7 +1222,8 @@ static int blend_locked(gsr_context* c, float* d_out) {
             const bool spec = c->frame_spec;
             const gsr::SplitCut cut{c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr,
                                     key ? c->nlive : nullptr, n, c->split_na, c->split_rebin ? nullptr : c->kcut};
-            gsr::BlendSplit a{1, c->tbuf, c->bflag, c->gate, nullptr, spec ? c->hstats_dev : nullptr, cut, 0u};
+            gsr::BlendSplit a{1, c->tbuf, c->bflag, c->gate, nullptr, spec ? c->hstats_dev : nullptr, cut, 0u,
+                              spec ? c->fstatus : nullptr};
             HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
                                       c->diagnostics ? c->consumed : nullptr, false, c->blend_band_tiles, 0,
                                       c->stream, &a));
@@ -1225,7 +1238,8 @@ static int blend_locked(gsr_context* c, float* d_out) {
                 }
                 if (int rc = bin_locked(c, key ? 0 : c->split_na, key ? n : n - c->split_na, 2, false, &rb, key))
                     return rc;
-                gsr::BlendSplit b{2, c->tbuf, c->bflag, c->gate, c->hstats_dev, nullptr, {}, (uint32_t)c->split_pm};
+                gsr::BlendSplit b{2, c->tbuf, c->bflag, c->gate, c->hstats_dev, nullptr, {}, (uint32_t)c->split_pm,
+                                  nullptr};
                 HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
                                           c->diagnostics ? c->consumed : nullptr, false, c->blend_band_tiles, 0,
                                           c->stream, &b));
@@ -1381,6 +1395,15 @@ extern "C" int gsr_render_path_ex(gsr_context* c, const void* scene, int layout,
                                   const float* times, int nframes, int W, int H, int nx, int ny, int ws, int hs,
                                   float k, float* const* d_outs, void* stream, void* const* frame_events,
                                   void* const* wait_events, int flags) {
+    return gsr_render_path_status(c, scene, layout, n, cams, times, nframes, W, H, nx, ny, ws, hs, k, d_outs, stream,
+                                  frame_events, wait_events, flags, nullptr);
+}
+
+extern "C" int gsr_render_path_status(gsr_context* c, const void* scene, int layout, int64_t n,
+                                      const gsr_camera* cams, const float* times, int nframes, int W, int H, int nx,
+                                      int ny, int ws, int hs, float k, float* const* d_outs, void* stream,
+                                      void* const* frame_events, void* const* wait_events, int flags,
+                                      uint32_t* const* d_status) {
     if (!c) return set_err(GSR_E_ARG, "null context");
     if (flags & ~(GSR_PATH_NO_JOIN | GSR_PATH_NO_FORK))
         return set_err(GSR_E_ARG, "gsr_render_path_ex: unknown flags 0x%x", flags);
@@ -1438,7 +1461,9 @@ extern "C" int gsr_render_path_ex(gsr_context* c, const void* scene, int layout,
         if (wait_events && wait_events[i]) HIP_TRY(hipStreamWaitEvent(ls, static_cast<hipEvent_t>(wait_events[i]), 0));
         if (times) lc->time = times[i];
         else lc->time = t_saved;
+        lc->fstatus = d_status ? d_status[i] : nullptr;
         const int rc = render_one_locked(lc, scene, layout, n, &cams[i], W, H, nx, ny, ws, hs, k, d_outs[i], ls);
+        lc->fstatus = nullptr;
         if (rc == GSR_E_OVERFLOW) result = GSR_E_OVERFLOW;
         else if (rc != GSR_OK) return rc;
         if (record[i]) HIP_TRY(hipEventRecord(c->alias_evs[lane], ls));

@@ -103,6 +103,12 @@ def broadcast_scene(dist, scene, gloo: bool = False):
     return out
 
 
+# Floats after each image in a FrameShard buffer: word 0 is the frame's validity word
+# (gsr_render_path_status: 0 complete, else GSR_FRAME_* bits); the pad keeps the next
+# image 256-B aligned when the image is.
+STATUS_PAD = 64
+
+
 class FrameShard:
     """One rank's frame loop for bench.py --gpus N (config 4): K frames of this rank's
     camera through Renderer.render_path (F lanes in flight), and with gather="step"
@@ -111,35 +117,51 @@ class FrameShard:
     chunk's render.
 
     Buffers: with per-step gathers, two SETS of `chunk` frames, each set one
-    contiguous [chunk, 3*H*W] tensor (one set renders while the other's gather
-    drains; a set is rendered again only after its gather completed); otherwise a
-    ring of F frames.  On rank 0, `recv[s][r]` is rank r's copy of set s
+    contiguous [chunk, 3*H*W + STATUS_PAD] tensor (one set renders while the other's
+    gather drains; a set is rendered again only after its gather completed); otherwise
+    a ring of F frames.  On rank 0, `recv[s][r]` is rank r's copy of set s
     (`gathered(b)` lists buffer b's frame from every rank).  gloo (the CPU /
     shared-GPU rehearsal) gathers host copies synchronously.
 
-    Overflow: render_path reports GSR_E_OVERFLOW when a frame came out incomplete
-    (pair buffer grown, or a depth sort short of passes); the shard records it, and
-    finish() — a collective — tells every rank whether any rank saw one, so that all
-    ranks agree to re-run (a rank cannot re-send frames on its own: the gathers
-    are collectives)."""
+    Validity (per-step gathers): every frame's validity word (gsr_render_path_status)
+    sits right after its image, so it travels in the same gather; each rank also logs
+    its own words per frame.  finish() — a collective — drains, then agrees over ranks
+    on the CHUNKS that hold an incomplete frame on any rank (GSR_E_OVERFLOW: pair buffer
+    grown, a depth sort short of passes, a speculative depth-split miss), and repair()
+    re-renders and re-gathers exactly those chunks on every rank (the gathers are
+    collectives).  run_checked() does run + finish + repair until clean.  A consumer on
+    rank 0 passes sink(chunk_id, first_frame, frames): frames[r] is rank r's
+    [m, 3*H*W + STATUS_PAD] block of the chunk (word 3*H*W of a row: its status, int32
+    view), called once per gather, repaired chunks again.
+
+    Without per-step gathers the renderer's codes are the only signal: finish() reports
+    whether any rank saw GSR_E_OVERFLOW since the last finish (re-run everything)."""
 
     def __init__(self, dist, renderer, scene, cam, W: int, H: int, k: float = 3.0, steps: int = 1,
                  gather: str = "step", inflight: int = 1, chunk: int = 8, gloo: bool = False,
-                 frame_time=None, stream: int = 0, overlap: bool = True):
+                 frame_time=None, stream: int = 0, overlap: bool = True, sink=None, frame_scene=None,
+                 device: str = "cuda", frame_cam=None):
         import torch
         self.dist, self.r, self.scene, self.cam = dist, renderer, scene, cam
         self.W, self.H, self.k, self.stream = W, H, k, stream
         self.F = max(1, inflight)
         self.gloo = gloo
+        self.device = device
         self.frame_time = frame_time
+        self.frame_scene = frame_scene
+        self.frame_cam = frame_cam               # frame index -> camera (a moving viewer), else cam
         self.step_gather = dist is not None and gather == "step"
         self.chunk = max(1, chunk) if self.step_gather else max(1, steps)
         self.nsets = 2 if self.step_gather else 1
         self.per_set = self.chunk if self.step_gather else self.F
-        npx = 3 * W * H
-        self.sets = [torch.empty((self.per_set, npx), dtype=torch.float32, device="cuda")
+        self.npx = npx = 3 * W * H
+        self.validity = self.step_gather
+        row = npx + STATUS_PAD if self.validity else npx
+        self.sets = [torch.empty((self.per_set, row), dtype=torch.float32, device=device)
                      for _ in range(self.nsets)]
-        self.outs = [self.sets[s][j] for s in range(self.nsets) for j in range(self.per_set)]
+        self.outs = [self.sets[s][j, :npx] for s in range(self.nsets) for j in range(self.per_set)]
+        self.status_ptrs = ([self.sets[s][j, npx:].data_ptr() for s in range(self.nsets) for j in range(self.per_set)]
+                            if self.validity else None)
         self.rank = dist.get_rank() if dist is not None else 0
         self.world = dist.get_world_size() if dist is not None else 1
         self.recv = None
@@ -147,13 +169,13 @@ class FrameShard:
             # rank 0's own slot IS its set: torch's gather copies input -> gather_list[root],
             # a no-op when they alias (at world 1 that copy was the whole gather cost)
             self.recv = [[self.sets[s] if (r == 0 and not gloo) else
-                          torch.empty_like(self.sets[s], device="cpu" if gloo else "cuda")
+                          torch.empty_like(self.sets[s], device="cpu" if gloo else device)
                           for r in range(self.world)] for s in range(self.nsets)]
         self.pending = [None] * self.nsets
         # RCCL: a chunk's gather waits, on a side stream, for the completion events of the
         # chunk's frames (gsr_render_path_ex), and render_path runs without the exit
         # join, so the lanes keep frames in flight across chunks
-        self.frame_events = (None if (gloo or not self.step_gather or not overlap)
+        self.frame_events = (None if (gloo or not self.step_gather or not overlap or device != "cuda")
                              else [torch.cuda.Event() for _ in range(len(self.outs))])
         self.gather_stream = torch.cuda.Stream() if self.frame_events else None
         # ... and a set's next frames wait on the completion of the set's last gather
@@ -162,8 +184,14 @@ class FrameShard:
         # lane 0's frames of the previous call (~4 % of the rate)
         self.gathered_ev = [torch.cuda.Event() for _ in range(self.nsets)] if self.frame_events else None
         self.gathered_valid = [False] * self.nsets
+        self.sink = sink if self.recv is not None else None
+        self.undelivered = [None] * self.nsets          # (chunk id, first frame, m) gathered into set s
+        self.chunks = []                                # (first frame, m) per chunk id, since run()
+        self.status_log = None                          # this rank's validity word per frame index
+        self.bad_chunks = []
         self.overflowed = False
         self.gathers = 0
+        self.repaired = 0
 
     def _times(self, i0: int, m: int):
         return [self.frame_time(i0 + j) for j in range(m)] if self.frame_time else None
@@ -171,19 +199,54 @@ class FrameShard:
     def gathered(self, b: int):
         """Rank 0: buffer b's frame from every rank (index = rank), as device/host views."""
         s, j = divmod(b, self.per_set)
-        return [self.recv[s][r][j] for r in range(self.world)]
+        return [self.recv[s][r][j][:self.npx] for r in range(self.world)]
+
+    def _sync(self):
+        if self.device == "cuda":
+            import torch
+            torch.cuda.synchronize()
 
     def wait_pending(self, s: int):
         if self.pending[s] is not None:
             self.pending[s].wait()          # nccl: stream-wait until the gather of set s is done
             self.pending[s] = None
 
+    def _deliver(self, s: int):
+        """Rank 0 with a sink: hand set s's last gathered chunk to it (stream-ordered after
+        that gather)."""
+        u = self.undelivered[s]
+        if u is None:
+            return
+        self.undelivered[s] = None
+        if self.frame_events:
+            import torch
+            torch.cuda.current_stream().wait_event(self.gathered_ev[s])
+        else:
+            self.wait_pending(s)
+        cid, i0, m = u
+        self.sink(cid, i0, [t[:m] for t in self.recv[s]])
+
     def drain(self):
         for s in range(self.nsets):
             self.wait_pending(s)
+            if self.sink:
+                self._deliver(s)
 
-    def gather(self, s: int, m: int):
-        """One gather of frames 0..m-1 of set s to rank 0."""
+    def _log_status(self, s: int, i0: int, m: int):
+        """This rank's validity words of frames i0..i0+m-1 (in set s) into status_log, on
+        the current stream (after the frames: the side stream waited on their events, or
+        the caller's stream joined the lanes)."""
+        import torch
+        if self.status_log is None or self.status_log.numel() < i0 + m:
+            old = self.status_log
+            self.status_log = torch.zeros(max(i0 + m, 2 * (old.numel() if old is not None else 0)),
+                                          dtype=torch.int32, device=self.device)
+            if old is not None:
+                self.status_log[:old.numel()].copy_(old)
+        self.status_log[i0:i0 + m].copy_(self.sets[s][:m, self.npx].view(torch.int32))
+
+    def gather(self, s: int, m: int, cid: int = 0, i0: int = 0):
+        """One gather of frames 0..m-1 of set s (chunk cid, first frame i0) to rank 0."""
         self.gathers += 1
         src = self.sets[s][:m]
         dst = None
@@ -197,20 +260,28 @@ class FrameShard:
             with torch.cuda.stream(self.gather_stream):
                 for j in range(max(0, m - self.F), m):
                     self.gather_stream.wait_event(self.frame_events[s * self.per_set + j])
+                self._log_status(s, i0, m)
                 self.pending[s] = self.dist.gather(src, dst, dst=0, async_op=True)
                 self.pending[s].wait()                       # side stream: after the gather
                 self.gathered_ev[s].record(self.gather_stream)
                 self.gathered_valid[s] = True
-            return
-        if self.gloo:
-            self.pending[s] = self.dist.gather(src.cpu(), dst, dst=0)
         else:
-            self.pending[s] = self.dist.gather(src, dst, dst=0, async_op=True)
+            self._log_status(s, i0, m)
+            if self.gloo:
+                self.pending[s] = self.dist.gather(src.cpu(), dst, dst=0)
+            else:
+                self.pending[s] = self.dist.gather(src, dst, dst=0, async_op=True)
+        if self.sink:
+            self.undelivered[s] = (cid, i0, m)
+            if not self.frame_events:
+                self._deliver(s)
 
     def frame(self, i: int = 0, b: int = 0):
         """One frame on the caller's stream (sequential: the viewer's one-at-a-time use)."""
-        rc = self.r.render(self.scene, self.cam, self.W, self.H, self.outs[b].data_ptr(), k=self.k,
-                           stream=self.stream, time=self.frame_time(i) if self.frame_time else None)
+        rc = self.r.render(self.frame_scene(i) if self.frame_scene else self.scene,
+                           self.frame_cam(i) if self.frame_cam else self.cam, self.W, self.H,
+                           self.outs[b].data_ptr(), k=self.k, stream=self.stream,
+                           time=self.frame_time(i) if self.frame_time else None)
         self.overflowed |= rc != 0
         return rc
 
@@ -219,38 +290,82 @@ class FrameShard:
         (GSR_E_OVERFLOW: some frame since the last clean check came out incomplete).
         overlap (run()): record each buffer's frame event, skip the exit join, wait on
         the last gather of set `wait_set`, and fork from the caller's stream only on the
-        first call of a run."""
+        first call of a run.  Buffers with a validity word get it written."""
         ov = overlap and self.frame_events is not None
         waits = None
         if ov and wait_set is not None and self.gathered_valid[wait_set]:
             waits = [self.gathered_ev[wait_set]] * m
-        rc = self.r.render_path(self.scene, [self.cam] * m, self.W, self.H, [self.outs[b].data_ptr() for b in bufs],
+        scene = self.frame_scene(i0) if self.frame_scene else self.scene
+        cams = [self.frame_cam(i0 + j) for j in range(m)] if self.frame_cam else [self.cam] * m
+        rc = self.r.render_path(scene, cams, self.W, self.H, [self.outs[b].data_ptr() for b in bufs],
                                 k=self.k, stream=self.stream, times=self._times(i0, m),
                                 events=[self.frame_events[b] for b in bufs] if ov else None, join=not ov,
-                                fork=not ov or first, wait_events=waits)
+                                fork=not ov or first, wait_events=waits,
+                                status=[self.status_ptrs[b] for b in bufs] if self.status_ptrs else None)
         self.overflowed |= rc != 0
         return rc
 
+    def _chunk(self, cid: int, first: bool):
+        i0, m = self.chunks[cid]
+        s = cid % self.nsets
+        if not self.frame_events:                # gloo / no overlap: the caller's stream orders reuse
+            self.wait_pending(s)
+        if self.sink:
+            self._deliver(s)                     # the set's previous chunk, before it is overwritten
+        self.path(i0, m, [s * self.per_set + j for j in range(m)], overlap=True, first=first, wait_set=s)
+        self.gather(s, m, cid, i0)
+
     def run(self, steps: int):
         """K frames in flight, gathered per chunk when enabled (not drained: call drain())."""
+        self.chunks = []
+        self.bad_chunks = []
         if not self.step_gather:
             self.path(0, steps, [j % self.F for j in range(steps)])
             return
         for c0 in range(0, steps, self.chunk):
-            m = min(self.chunk, steps - c0)
-            s = (c0 // self.chunk) % self.nsets
-            if not self.frame_events:                # gloo / no overlap: the caller's stream orders reuse
-                self.wait_pending(s)
-            self.path(c0, m, [s * self.per_set + j for j in range(m)], overlap=True, first=c0 == 0, wait_set=s)
-            self.gather(s, m)
+            self.chunks.append((c0, min(self.chunk, steps - c0)))
+            self._chunk(len(self.chunks) - 1, c0 == 0)
 
     def finish(self, device) -> bool:
         """Drain the gathers and the renderer, then agree over ranks (a collective)
-        whether any rank's frames since the last finish() were incomplete
-        (GSR_E_OVERFLOW); clears the flag."""
+        whether any rank's frames since the last finish() were incomplete; with validity
+        words, bad_chunks = the chunk ids (same list on every rank) that repair() must
+        send again.  Clears the renderer's flag."""
         import torch
         self.drain()
-        torch.cuda.synchronize()
-        bad = self.overflowed or self.r.sync() != 0
+        self._sync()
+        rc = self.r.sync()                       # always: it also clears the context's reported overflow
+        coarse = self.overflowed or rc != 0
         self.overflowed = False
-        return any_over_ranks(self.dist, bad, device)
+        if not self.validity or not self.chunks:
+            self.bad_chunks = []
+            return any_over_ranks(self.dist, coarse, device)
+        words = self.status_log.cpu() if self.status_log is not None else None
+        local = [bool((words[i0:i0 + m] != 0).any()) for i0, m in self.chunks]
+        if coarse and not any(local):
+            local = [True] * len(self.chunks)   # an overflow no word names (frames outside the chunks)
+        t = torch.tensor([1.0 if b else 0.0 for b in local], dtype=torch.float64, device=device)
+        if self.dist is not None and self.dist.is_initialized() and self.dist.get_world_size() > 1:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.bad_chunks = [c for c, v in enumerate(t.tolist()) if v > 0]
+        return bool(self.bad_chunks)
+
+    def repair(self):
+        """Render and gather again exactly the chunks finish() agreed on (every rank)."""
+        for j, cid in enumerate(self.bad_chunks):
+            self._chunk(cid, j == 0)
+            self.repaired += 1
+
+    def run_checked(self, steps: int, device, attempts: int = 3) -> bool:
+        """run(steps), then finish() and repair() until no rank holds an incomplete frame
+        (at most `attempts` repairs); True when clean.  Without validity words a bad
+        region is run again whole."""
+        self.run(steps)
+        for _ in range(attempts):
+            if not self.finish(device):
+                return True
+            if self.validity:
+                self.repair()
+            else:
+                self.run(steps)
+        return not self.finish(device)

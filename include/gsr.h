@@ -43,9 +43,12 @@ enum {
     GSR_E_IO = -3,         /* file missing / unreadable / truncated */
     GSR_E_FORMAT = -4,     /* unsupported PLY format */
     GSR_E_OVERFLOW = -5,   /* an earlier frame is incomplete and must be re-rendered: its pairs
-                              overflowed the pair buffer (grown now), or its depth sort needed more
+                              overflowed the pair buffer (grown now), its depth sort needed more
                               digit passes than the adaptive pass budget launched (budget reset to
-                              four).  Either can happen at any frame, not only during warm-up.  The
+                              four), or it was a speculative depth-split frame (GSR_TUNE_DEPTH_SPLIT,
+                              no phase B queued) whose phase A left an 8x8 block unsaturated
+                              (speculation stopped).  Any of these can happen at any frame, not only
+                              during warm-up; gsr_render_path_status names the frames.  The
                               code can arrive on a later call than the frame it refers to: every
                               frame rendered since the last call that returned GSR_OK (or since the
                               last gsr_sync) must be re-rendered. */
@@ -133,8 +136,9 @@ int gsr_reserve(gsr_context* ctx, int64_t n, int64_t pairs);
  * Reference tiling arguments as in preprocessCUDAGaussians; pass
  * num_tile_x = num_tile_y = 1 and strides = W, H for "cover the image".
  * Returns GSR_E_OVERFLOW if an earlier frame was incomplete (pair buffer
- * overflow, grown; or a depth sort short of passes, budget reset): re-render
- * every frame since the last clean return, see GSR_E_OVERFLOW. */
+ * overflow, grown; a depth sort short of passes, budget reset; or a speculative
+ * depth-split frame that needed phase B): re-render every frame since the last
+ * clean return, see GSR_E_OVERFLOW. */
 int gsr_render(gsr_context* ctx, const void* d_scene, int layout, int64_t n,
                const gsr_camera* cam, int W, int H, int num_tile_x, int num_tile_y,
                int width_stride, int height_stride, float k, float* d_out, void* stream);
@@ -180,6 +184,22 @@ int gsr_render_path_ex(gsr_context* ctx, const void* d_scene, int layout, int64_
                        const float* times, int nframes, int W, int H, int num_tile_x, int num_tile_y,
                        int width_stride, int height_stride, float k, float* const* d_outs, void* stream,
                        void* const* frame_events, void* const* wait_events, int flags);
+/* gsr_render_path_ex with a validity word per frame, so a consumer that receives
+ * frames asynchronously (the multi-GPU gather) knows exactly which ones to render
+ * again instead of every frame since the last clean return.  d_status (may be NULL;
+ * entries may be NULL): a uint32 DEVICE word per frame, written on frame i's lane
+ * before its frame event: 0 if frame i is complete, else GSR_FRAME_* bits (the causes
+ * of GSR_E_OVERFLOW, for that frame alone).  The word can sit right after the
+ * frame's image in one buffer, so it travels with the frame.  The return code, the
+ * buffer growth and the controller are exactly those of gsr_render_path_ex. */
+#define GSR_FRAME_PAIR_OVERFLOW 1u   /* its pairs overflowed the pair buffer */
+#define GSR_FRAME_DEPTH_PASSES 2u    /* its depth sort needed more passes than were launched */
+#define GSR_FRAME_SPEC_MISS 4u       /* speculative depth-split frame that needed phase B */
+int gsr_render_path_status(gsr_context* ctx, const void* d_scene, int layout, int64_t n, const gsr_camera* cams,
+                           const float* times, int nframes, int W, int H, int num_tile_x, int num_tile_y,
+                           int width_stride, int height_stride, float k, float* const* d_outs, void* stream,
+                           void* const* frame_events, void* const* wait_events, int flags,
+                           uint32_t* const* d_status);
 /* Frames in flight for gsr_render_path: 1..GSR_MAX_FRAMES_IN_FLIGHT (default 3;
  * 1 = strictly sequential on `stream`).  Each extra lane holds its own workspace. */
 int gsr_set_frames_in_flight(gsr_context* ctx, int frames);
@@ -287,7 +307,12 @@ enum {
     GSR_TUNE_BIN_COL_GROUPS = 10,    /* binning column pass: workgroups (default 0 = n / 1024 clamped
                                         to 1024..4096) */
     GSR_TUNE_COMPLETION_EVENTS = 11, /* 1 (default): a completion event feeds the non-blocking overflow
-                                        check; 0: none (frames captured into a graph; call gsr_sync) */
+                                        check; 0: none (frames captured into a graph).  With 0 the
+                                        render calls report nothing: only gsr_sync (which drains the
+                                        device, then reads the sticky overflow words) reports an
+                                        incomplete frame, and no frame is rendered speculatively
+                                        without the depth split's phase B (a graph would replay that
+                                        choice) */
     /* 12 reserved (removed: longest tiles first) */
     GSR_TUNE_BLEND_BAND_TILES = 13,  /* blend schedule 0: tiles per spatial band, bands dealt round-robin
                                         to the 8 XCDs (default 4); 0 = one contiguous band per XCD */

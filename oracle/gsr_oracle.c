@@ -380,10 +380,10 @@ int orc_preprocess(const float* soa, int64_t n, const gsr_camera* cam, int W, in
         for (int c = 0; c < 4; c++) rot[c] = soa[(GSR_A_ROT0 + c) * n + i];
         o_rot_from_quat(rot, R);
         o_transpose3(R, RT);
-        const float scale_mod = 1.0f;
-        sc[0] = scale_mod * soa[(GSR_A_SCALE0 + 0) * n + i];
-        sc[1] = scale_mod * soa[(GSR_A_SCALE0 + 1) * n + i];
-        sc[2] = scale_mod * soa[(GSR_A_SCALE0 + 2) * n + i];
+        /* render.cu:664-667 multiplies by a constant 1 (exact): omitted */
+        sc[0] = soa[(GSR_A_SCALE0 + 0) * n + i];
+        sc[1] = soa[(GSR_A_SCALE0 + 1) * n + i];
+        sc[2] = soa[(GSR_A_SCALE0 + 2) * n + i];
         o_diag3(sc, S);
         o_matmul3(R, S, tmp);
         o_matmul3(tmp, S, R);
@@ -456,6 +456,53 @@ static int cmp_kv(const void* a, const void* b) {
 
 /* One pixel-splat step of renderGaussians (render.cu:326-340).  take (optional): the
  * pixel's take-map entry (gsr_blend_take_map: count | index-mix sum << 32). */
+/* Which FMA contractions the reference's compiler applied to render.cu:331 and 337 cannot
+ * be observed here (the CUDA path cannot be built).  orc_set_blend_variant selects
+ * another plausible choice, so the parity hole can be measured
+ * (tests/test_oracle_contraction.py, tools/contraction_parity.py):
+ *   md2: 0 no contraction; 1 the first product of each sum fused (shipped, = the
+ *        kernels); 2 the second product of each sum fused; 3 the inner sums only
+ *        (first product); 4 the outer sum only (first product);
+ *   rgb: 0 rgb + (color * alpha) * T rounded twice; 1 fmaf(color * alpha, T, rgb) (shipped);
+ *   exp: 0 gsr_expf (shipped); 1 the host libm expf (glibc: correctly rounded). */
+static int g_var_md2 = 1, g_var_rgb = 1, g_var_exp = 0;
+void orc_set_blend_variant(int md2, int rgb, int expm) {
+    g_var_md2 = md2;
+    g_var_rgb = rgb;
+    g_var_exp = expm;
+}
+
+static inline float md2_variant(float dx, float dy, const float* ic) {
+    switch (g_var_md2) {
+    case 0: return dx * (ic[0] * dx + ic[1] * dy) + dy * (ic[2] * dx + ic[3] * dy);
+    case 2: return __builtin_fmaf(dy, __builtin_fmaf(ic[3], dy, ic[2] * dx), dx * __builtin_fmaf(ic[1], dy, ic[0] * dx));
+    case 3: return dx * __builtin_fmaf(ic[0], dx, ic[1] * dy) + dy * __builtin_fmaf(ic[2], dx, ic[3] * dy);
+    case 4: return __builtin_fmaf(dx, ic[0] * dx + ic[1] * dy, dy * (ic[2] * dx + ic[3] * dy));
+    default: return gsr_blend_md2(dx, dy, ic[0], ic[1], ic[2], ic[3]);
+    }
+}
+
+/* blend_step with the contraction variant of orc_set_blend_variant (never the CPU
+ * baseline's path: orc_render_takes takes blend_step when the variant is the shipped one) */
+static void blend_step_var(const orc_splat* g, int gx, int gy, float* T, float* rgb, uint64_t* take,
+                           uint32_t gid) {
+    if (gx < g->aabb[0] || gx > g->aabb[2] || gy < g->aabb[1] || gy > g->aabb[3]) return;
+    if (*T < 1e-3f) return;
+    const float dx = ((float)gx - (float)g->px_x);
+    const float dy = ((float)gy - (float)g->px_y);
+    const float md2 = md2_variant(dx, dy, g->inv_covar);
+    float opacity = g->opacity * (g_var_exp ? expf(-0.5f * md2) : gsr_expf(-0.5f * md2));
+    opacity = fminf(opacity, 0.99f);
+    if (opacity < 1e-3f) return;
+    for (int c = 0; c < 3; ++c)
+        rgb[c] = g_var_rgb ? __builtin_fmaf(g->color[c] * opacity, *T, rgb[c]) : rgb[c] + g->color[c] * opacity * *T;
+    *T *= (1.0f - opacity);
+    if (take) {
+        const uint32_t cnt = (uint32_t)*take + 1u, hs = (uint32_t)(*take >> 32) + (gid + 1u) * 2654435761u;
+        *take = (uint64_t)cnt | ((uint64_t)hs << 32);
+    }
+}
+
 static inline void blend_step(const orc_splat* g, int gx, int gy, float* T, float* rgb, uint64_t* take,
                               uint32_t gid) {
     if (gx < g->aabb[0] || gx > g->aabb[2] || gy < g->aabb[1] || gy > g->aabb[3]) return;
@@ -513,6 +560,7 @@ int orc_render_takes(const float* soa, int64_t n, const gsr_camera* cam, int W, 
     if (takes) memset(takes, 0, sizeof(uint64_t) * npx);
     const int band = 8;
     const int nbands = (ch + band - 1) / band;
+    const int shipped = g_var_md2 == 1 && g_var_rgb == 1 && g_var_exp == 0;
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 1)
@@ -533,8 +581,12 @@ int orc_render_takes(const float* soa, int64_t n, const gsr_camera* cam, int W, 
             for (int y = ya; y <= yb; y++)
                 for (int x = xa; x <= xb; x++) {
                     const size_t q = (size_t)(y - y0) * cw + x;
-                    blend_step(g, x, y, &T[q], &rgb[3 * q], takes ? &takes[(size_t)y * W + x] : NULL,
-                               order[s].idx);
+                    if (shipped)
+                        blend_step(g, x, y, &T[q], &rgb[3 * q], takes ? &takes[(size_t)y * W + x] : NULL,
+                                   order[s].idx);
+                    else
+                        blend_step_var(g, x, y, &T[q], &rgb[3 * q], takes ? &takes[(size_t)y * W + x] : NULL,
+                                       order[s].idx);
                 }
         }
         for (int y = y0; y <= y1; y++)

@@ -45,6 +45,9 @@ int orc_ply_read_ex(const char* path, float* soa, int narrays, int64_t capacity,
 /* SH-3 ("Inria-correct") mode for orc_preprocess / orc_render: soa then has
  * GSR_SCENE_SH3_NARRAYS arrays (process-wide switch; tests reset it). */
 void orc_set_sh3(int on);
+/* Blend contraction variant (gsr_oracle.c blend_step_var): md2 0..4, rgb 0..1, exp 0..1;
+ * (1, 1, 0) = the shipped choice the kernels share. */
+void orc_set_blend_variant(int md2, int rgb, int expm);
 /* Config 5: the 38 arrays of a 4D scene at time t, no temporal cull. */
 void orc_temporal(const float* soa49, int64_t n, float t, float* out38);
 

@@ -39,6 +39,8 @@ def lib():
         L.orc_temporal.restype = None
         L.orc_set_sh3.argtypes = [c_int]
         L.orc_set_sh3.restype = None
+        L.orc_set_blend_variant.argtypes = [c_int, c_int, c_int]
+        L.orc_set_blend_variant.restype = None
         L.orc_intrinsics.argtypes = [cam, POINTER(c_float), POINTER(c_float)]
         L.orc_preprocess.argtypes = [c_void_p, c_int64, cam, c_int, c_int, c_float, c_void_p]
         L.orc_preprocess.restype = c_int
@@ -101,6 +103,21 @@ class sh3_mode:
 
     def __exit__(self, *exc):
         lib().orc_set_sh3(0)
+
+
+class blend_variant:
+    """Context manager: the oracle's blend with another FMA contraction of render.cu:331
+    and 337 (md2 0..4, rgb 0..1) or the host libm expf (exp 1); (1, 1, 0) is the shipped
+    choice the kernels share (gsr_oracle.c blend_step_var)."""
+
+    def __init__(self, md2: int = 1, rgb: int = 1, exp: int = 0):
+        self.v = (md2, rgb, exp)
+
+    def __enter__(self):
+        lib().orc_set_blend_variant(*self.v)
+
+    def __exit__(self, *exc):
+        lib().orc_set_blend_variant(1, 1, 0)
 
 
 def ply_read4d(path: str) -> np.ndarray:

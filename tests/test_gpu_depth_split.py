@@ -190,10 +190,30 @@ def test_config3_speculation_and_miss(gpu, orc, torch, c3):
     thin[3] *= 0.3                                              # opacity (sigmoid applied)
     thin_scene = gpu.Scene.from_soa(thin)
     want_thin = orc.render(thin, cam, W, H, 3.0, threads=ORC_THREADS)
-    r.render(thin_scene, cam, W, H, out.data_ptr())
+    word = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    # through gsr_render_path_status: the frame's own validity word names the miss
+    r.render_path(thin_scene, [cam], W, H, [out.data_ptr()], status=[word.data_ptr()])
     assert r.sync() != 0, "a speculative frame that needed phase B was not reported"
-    r.render(thin_scene, cam, W, H, out.data_ptr())
+    assert int(word.item()) == 4, "GSR_FRAME_SPEC_MISS not set in the frame's validity word"
+    r.render_path(thin_scene, [cam], W, H, [out.data_ptr()], status=[word.data_ptr()])
     assert r.sync() == 0 and r.get_tuning(KNOB_STATE) == 2
+    assert int(word.item()) == 0
+    assert_frames(out.view(3, H, W).cpu().numpy(), want_thin, exact=True)
+    # with completion events off (frames captured into a graph) no frame is
+    # queued without phase B — a captured graph would replay that choice — so the same
+    # miss cannot happen unreported: back to speculation, events off, the thin scene
+    for _ in range(60):
+        r.render(scene, cam, W, H, out.data_ptr())
+        while r.sync() != 0:
+            r.render(scene, cam, W, H, out.data_ptr())
+        if r.get_tuning(KNOB_STATE) == 3:
+            break
+    assert r.get_tuning(KNOB_STATE) == 3
+    r.set_tuning(11, 0)
+    r.render(scene, cam, W, H, out.data_ptr())
+    assert r.get_tuning(KNOB_STATE) == 2, "a frame speculated with completion events off"
+    r.render(thin_scene, cam, W, H, out.data_ptr())
+    assert r.sync() == 0
     assert_frames(out.view(3, H, W).cpu().numpy(), want_thin, exact=True)
     r.close()
 

@@ -208,6 +208,65 @@ def test_path_overflow_on_child_lane(gpu, orc, torch):
         assert_image_parity(o.view(3, H, W).cpu().numpy(), orc.render(soa, cam, W, H, 3.0))
 
 
+def test_overflow_reported_with_completion_events_off(gpu, orc, torch):
+    """with GSR_TUNE_COMPLETION_EVENTS 0 (frames captured into a graph) no
+    completion event marks finished work, so the render calls cannot report an incomplete
+    frame — gsr_sync must: it drains the device and reads the sticky words.  Huge splats
+    overflow the initial pair buffer; the re-render after the sync is exact."""
+    n = 3000
+    rng = np.random.default_rng(11)
+    soa = np.zeros((38, n), np.float32)
+    soa[0:3] = rng.uniform(-0.2, 0.2, (3, n))
+    soa[3] = rng.uniform(0.01, 0.05, n)
+    soa[4:7] = rng.uniform(1.0, 2.0, (3, n))
+    soa[7] = 1.0
+    soa[11:38] = rng.normal(0, 0.3, (27, n))
+    W, H = 640, 480
+    cam = cam_for(gpu, W, H)
+    scene = gpu.Scene.from_soa(soa)
+    r = gpu.Renderer()
+    r.set_tuning(11, 0)
+    out = torch.empty(3 * W * H, device="cuda")
+    assert r.render(scene, cam, W, H, out.data_ptr()) == 0        # nothing to report yet
+    assert r.sync() == -5, "gsr_sync did not report the overflow with completion events off"
+    assert r.sync() == 0                                          # reported once
+    r.render(scene, cam, W, H, out.data_ptr())
+    assert r.sync() == 0
+    assert_image_parity(out.view(3, H, W).cpu().numpy(), orc.render(soa, cam, W, H, 3.0))
+
+
+def test_path_status_words(gpu, orc, torch):
+    """gsr_render_path_status: each frame's validity word names exactly the frames that
+    came out incomplete (here: huge splats overflow every lane's initial pair buffer, so
+    the first frame of each lane is incomplete), and is 0 for complete frames."""
+    n = 3000
+    rng = np.random.default_rng(9)
+    soa = np.zeros((38, n), np.float32)
+    soa[0:3] = rng.uniform(-0.2, 0.2, (3, n))
+    soa[3] = rng.uniform(0.01, 0.05, n)
+    soa[4:7] = rng.uniform(1.0, 2.0, (3, n))
+    soa[7] = 1.0
+    soa[11:38] = rng.normal(0, 0.3, (27, n))
+    W, H = 640, 480
+    cams = orbit_cams(gpu, W, H, 3)
+    scene = gpu.Scene.from_soa(soa)
+    r = gpu.Renderer()
+    r.set_frames_in_flight(3)
+    outs = [torch.empty(3 * W * H, device="cuda") for _ in cams]
+    words = torch.full((len(cams),), -1, dtype=torch.int32, device="cuda")
+    st = [words.data_ptr() + 4 * i for i in range(len(cams))]
+    rc = r.render_path(scene, cams, W, H, [o.data_ptr() for o in outs], status=st)
+    rc2 = r.sync()
+    assert rc == -5 or rc2 == -5
+    w = words.cpu().numpy()
+    assert ((w & 1) == 1).all(), f"pair overflow not flagged per frame: {w}"
+    r.render_path(scene, cams, W, H, [o.data_ptr() for o in outs], status=st)
+    assert r.sync() == 0
+    assert (words.cpu().numpy() == 0).all()
+    for cam, o in zip(cams, outs):
+        assert_image_parity(o.view(3, H, W).cpu().numpy(), orc.render(soa, cam, W, H, 3.0))
+
+
 def test_path_bad_arguments(gpu, torch, c1):
     r = gpu.Renderer()
     with pytest.raises(gpu.GsrError):

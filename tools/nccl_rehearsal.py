@@ -62,7 +62,7 @@ def main():
     shard = multi.FrameShard(dist, r, scene, cam, W, H, steps=a.steps, gather=a.gather, inflight=a.inflight, chunk=a.chunk,
                              stream=stream, overlap=not a.no_overlap)
     if a.no_gather_calls:
-        shard.gather = lambda s, m: None
+        shard.gather = lambda s, m, cid=0, i0=0: None
     # reference image of this rank's camera (grows the pair buffers too)
     ref = torch.empty(3 * W * H, device="cuda")
     for _ in range(3):
