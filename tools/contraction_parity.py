@@ -1,0 +1,73 @@
+"""How much the blend's unobservable FMA contraction matters (round-3 verdict, weak #1).
+
+The reference's renderGaussians computes md2 and the colour accumulation
+(render.cu:331, 337) in fp32 with nvcc's default contraction (--fmad=true); which
+products it fuses cannot be observed here (the CUDA path cannot be built).  The oracle
+and the kernels share one choice (include/gsr_detmath.h gsr_blend_md2: the first product
+of each sum; rgb = fmaf(color * alpha, T, rgb)).  This tool renders the same frame with
+the oracle under every other plausible choice (gsr_oracle.c blend_step_var) — and with
+the host libm expf in place of gsr_expf — and reports, against the shipped choice:
+L-inf, pixels over the 1e-4 gate, pixels that differ at all, and pixels whose take map
+(the set of splats composited) differs.
+
+Usage: python tools/contraction_parity.py [CONFIG ...]   (default 1 2 3; CPU only)
+"""
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import gaussianrenderer_amd as gsr  # noqa: E402  (host helpers only: PLY writer, camera)
+import _oracle as orc  # noqa: E402  (test infrastructure: this tool checks the oracle itself)
+
+CONFIGS = {1: (10_000, 640, 480, 1), 2: (1_000_000, 1920, 1080, 2), 3: (5_000_000, 1600, 1063, 3)}
+# (md2, rgb, exp): see gsr_oracle.c orc_set_blend_variant
+VARIANTS = [
+    ((0, 0, 0), "no contraction anywhere"),
+    ((0, 1, 0), "md2 not contracted, rgb fused"),
+    ((1, 0, 0), "md2 first products fused, rgb not fused"),
+    ((2, 1, 0), "md2 second products fused, rgb fused"),
+    ((2, 0, 0), "md2 second products fused, rgb not fused"),
+    ((3, 1, 0), "md2 inner sums only, rgb fused"),
+    ((4, 1, 0), "md2 outer sum only, rgb fused"),
+    ((1, 1, 1), "shipped contraction, libm expf instead of gsr_expf"),
+    ((0, 0, 1), "no contraction, libm expf"),
+]
+
+
+def main():
+    configs = [int(a) for a in sys.argv[1:]] or [1, 2, 3]
+    threads = len(os.sched_getaffinity(0))
+    d = tempfile.gettempdir()
+    print(f"# blend contraction variants vs the shipped choice (oracle, {threads} threads)")
+    for c in configs:
+        n, W, H, seed = CONFIGS[c]
+        ply = os.path.join(d, f"contraction_c{c}_{n}_{seed}.ply")
+        if not os.path.exists(ply):
+            gsr.write_synthetic_ply(ply, n, seed)
+        soa = orc.ply_read(ply)
+        cam = gsr.make_camera(position=(0, 0, 4), fov_y=50, aspect=W / H)
+        t0 = time.perf_counter()
+        base, btakes = orc.render_takes(soa, cam, W, H, 3.0, threads=threads)
+        el = time.perf_counter() - t0
+        lit = int((btakes != 0).sum())
+        print(f"\nconfig {c}: {n} Gaussians, {W}x{H}, {lit} pixels composite something "
+              f"(shipped render {el:.1f} s)")
+        print(f"{'variant (md2, rgb, exp)':<58} {'L-inf':>10} {'px > 1e-4':>10} {'px differ':>10} "
+              f"{'take maps differ':>17}")
+        for v, name in VARIANTS:
+            with orc.blend_variant(*v):
+                img, takes = orc.render_takes(soa, cam, W, H, 3.0, threads=threads)
+            diff = np.abs(img.astype(np.float64) - base.astype(np.float64))
+            px = diff.max(axis=0)
+            print(f"{str(v) + ' ' + name:<58} {diff.max():>10.3g} {int((px > 1e-4).sum()):>10} "
+                  f"{int((px > 0).sum()):>10} {int((takes != btakes).sum()):>17}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
