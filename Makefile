@@ -46,3 +46,9 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean
+
+# host-code ASan + UBSan build of libgsr.so and the oracle (tools/asan.mk; CPU tests only)
+asan: $(OBJDIR)/gsr_kernels.o
+	$(MAKE) -f tools/asan.mk -j $(JOBS)
+
+.PHONY: asan

@@ -18,6 +18,7 @@
 // motion_0..8) into arrays 38..48 when the caller asks for 49 arrays, and
 // (GSR_PLY_SH3, 59 arrays) all 45 f_rest mapped channel-major -> sh[3k + c].
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -180,8 +181,9 @@ int parse_header_typed(std::ifstream& file, PlyHeader& h, bool sh3) {
                 p.is_list = true;
                 p.count_type = parse_type(ct);
                 p.type = parse_type(it);
-                if (p.count_type == T_BAD || p.type == T_BAD)
-                    return set_error(GSR_E_FORMAT, "PLY: bad list property '%s'", line.c_str());
+                if (p.count_type == T_BAD || p.type == T_BAD || p.count_type == T_F32 || p.count_type == T_F64)
+                    return set_error(GSR_E_FORMAT, "PLY: bad list property '%s' (integer count type required)",
+                                     line.c_str());
             } else {
                 iss >> name;
                 p.type = parse_type(t1);
@@ -234,6 +236,37 @@ inline void store(const Prop& p, float* soa, int narrays, int64_t n, int64_t i, 
     case S_MOTION: if (narrays == GSR_SCENE4D_NARRAYS) soa[(GSR_A_MOTION0 + p.index) * n + i] = v; break;
     default: break;   // normals and skipped properties are not used by the render path
     }
+}
+
+// A decoded value as the float the SoA arrays hold: out-of-range magnitudes become
+// +-inf and NaN stays NaN (IEEE conversion, without the undefined behaviour of a
+// double -> float cast out of range).
+float to_float(double d) {
+    if (d > (double)FLT_MAX) return INFINITY;
+    if (d < -(double)FLT_MAX) return -INFINITY;
+    return (float)d;
+}
+
+// List lengths beyond this are malformed (a PLY face has a handful of indices).
+constexpr int64_t kMaxListLen = int64_t(1) << 24;
+
+// Bytes the rows of the vertex element need, when they can be known from the header
+// (binary formats, every element before and including it fixed-size); -1 otherwise.
+int64_t vertex_data_bytes(const PlyHeader& h, bool typed) {
+    if (!typed) return (int64_t)h.props.size() * 4 * h.n;
+    if (h.format == "ascii") return -1;
+    int64_t total = 0;
+    for (int ei = 0; ei <= h.vertex_element; ei++) {
+        int64_t row = 0;
+        for (const Prop& p : h.elements[ei].props) {
+            if (p.is_list) return -1;
+            row += type_size(p.type);
+        }
+        const int64_t cnt = h.elements[ei].count;
+        if (row && cnt > (INT64_MAX - total) / row) return INT64_MAX;
+        total += row * cnt;
+    }
+    return total;
 }
 
 template <typename T>
@@ -295,17 +328,19 @@ int read_typed(std::ifstream& file, const PlyHeader& h, float* soa, int narrays,
                 std::istringstream iss(line);
                 for (const Prop& p : e.props) {
                     if (p.is_list) {
-                        double cnt = 0;
-                        iss >> cnt;
+                        double cnt = -1;
+                        if (!(iss >> cnt) || !(cnt >= 0 && cnt <= (double)kMaxListLen))   // NaN included
+                            return set_error(GSR_E_FORMAT, "PLY: bad ascii list length in row %lld", (long long)r);
                         for (int64_t k = 0; k < (int64_t)cnt; k++) {
                             double d;
-                            iss >> d;
+                            if (!(iss >> d))
+                                return set_error(GSR_E_FORMAT, "PLY: short ascii list in row %lld", (long long)r);
                         }
                         continue;
                     }
                     double d = 0;
                     if (!(iss >> d)) return set_error(GSR_E_FORMAT, "PLY: bad ascii row %lld", (long long)r);
-                    if (vert) store(p, soa, narrays, n, r, (float)d);
+                    if (vert) store(p, soa, narrays, n, r, to_float(d));
                 }
             }
             if (vert) return GSR_OK;   // rows after the vertex element are not needed
@@ -322,6 +357,10 @@ int read_typed(std::ifstream& file, const PlyHeader& h, float* soa, int narrays,
             if (p.is_list) fixed = false;
             row += (size_t)type_size(p.type);
         }
+        if (fixed && row == 0) {   // an element without properties has no data
+            if (vert) return GSR_OK;
+            continue;
+        }
         if (fixed) {
             const int64_t chunk = std::max<int64_t>(1, (int64_t)((8u << 20) / std::max<size_t>(row, 1)));
             std::vector<unsigned char> buf;
@@ -334,7 +373,7 @@ int read_typed(std::ifstream& file, const PlyHeader& h, float* soa, int narrays,
                 for (int64_t r = 0; r < m; r++) {
                     const unsigned char* b = buf.data() + (size_t)r * row;
                     for (const Prop& p : e.props) {
-                        if (p.slot != S_SKIP) store(p, soa, narrays, n, i0 + r, (float)decode(p.type, b, swap));
+                        if (p.slot != S_SKIP) store(p, soa, narrays, n, i0 + r, to_float(decode(p.type, b, swap)));
                         b += type_size(p.type);
                     }
                 }
@@ -346,14 +385,16 @@ int read_typed(std::ifstream& file, const PlyHeader& h, float* soa, int narrays,
                     if (p.is_list) {
                         if (!file.read(reinterpret_cast<char*>(b), type_size(p.count_type)))
                             return set_error(GSR_E_IO, "PLY: truncated data in %s", path);
-                        const int64_t cnt = (int64_t)decode(p.count_type, b, swap);
-                        if (cnt < 0) return set_error(GSR_E_FORMAT, "PLY: negative list length");
+                        const double dc = decode(p.count_type, b, swap);   // an integer type (header check)
+                        if (dc < 0 || dc > (double)kMaxListLen)
+                            return set_error(GSR_E_FORMAT, "PLY: bad list length %.0f", dc);
+                        const int64_t cnt = (int64_t)dc;
                         file.seekg((std::streamoff)(cnt * type_size(p.type)), std::ios::cur);
                         continue;
                     }
                     if (!file.read(reinterpret_cast<char*>(b), type_size(p.type)))
                         return set_error(GSR_E_IO, "PLY: truncated data in %s", path);
-                    if (vert && p.slot != S_SKIP) store(p, soa, narrays, n, r, (float)decode(p.type, b, swap));
+                    if (vert && p.slot != S_SKIP) store(p, soa, narrays, n, r, to_float(decode(p.type, b, swap)));
                 }
         }
         if (vert) return GSR_OK;
@@ -378,6 +419,18 @@ extern "C" int gsr_ply_read_host_ex(const char* path, float* soa, int narrays, i
     if (h.n >= 0) *n_out = h.n;
     if (rc) return rc;
     if (is_4d) *is_4d = has_4d(typed ? h.elements[h.vertex_element].props : h.props) ? 1 : 0;
+    // a header whose vertex count the data cannot hold is refused before the caller
+    // sizes buffers from it (counts come from the file: hostile or truncated headers)
+    const int64_t need = vertex_data_bytes(h, typed);
+    if (need >= 0) {
+        const std::streampos here = file.tellg();
+        file.seekg(0, std::ios::end);
+        const std::streamoff avail = file.tellg() - here;
+        file.seekg(here);
+        if (!file || need > (int64_t)avail)
+            return set_error(GSR_E_IO, "PLY: %s holds %lld data bytes, its header needs %lld", path,
+                             (long long)avail, (long long)need);
+    }
     if (!soa || capacity < h.n) return GSR_OK;
     std::fill(soa, soa + (size_t)narrays * (size_t)h.n, 0.0f);   // Gaussian g{} (misc.cu:97)
     if (narrays == GSR_SCENE4D_NARRAYS)   // 4D defaults: static Gaussian (centre 0, scale 1, no motion)

@@ -91,7 +91,7 @@ int orc_ply_read_ex(const char* path, float* soa, int narrays, int64_t capacity,
         else if (!strcmp(name, "f_dc_2")) { kind = S_DC; idx = 2; }
         else if (starts_with(name, "f_rest_")) {
             int r = atoi(name + 7);
-            if (r < (narrays == GSR_SCENE_SH3_NARRAYS ? 45 : 24)) { kind = S_REST; idx = r; }   /* misc.cu:76 */
+            if (r >= 0 && r < (narrays == GSR_SCENE_SH3_NARRAYS ? 45 : 24)) { kind = S_REST; idx = r; }   /* misc.cu:76 */
         } else if (!strcmp(name, "opacity")) kind = S_OPACITY;
         else if (starts_with(name, "scale_")) { idx = atoi(name + 6); kind = (idx >= 0 && idx < 3) ? S_SCALE : S_SKIP; }
         else if (starts_with(name, "rot_")) { idx = atoi(name + 4); kind = (idx >= 0 && idx < 4) ? S_ROT : S_SKIP; }
@@ -103,7 +103,16 @@ int orc_ply_read_ex(const char* path, float* soa, int narrays, int64_t capacity,
         nprops++;
     }
     free(line);
-    if (strcmp(format, "binary_little_endian 1.0") != 0 || nprops > 1024) { fclose(f); return -4; }
+    if (strcmp(format, "binary_little_endian 1.0") != 0 || nprops > 1024 || nv > 2147483647LL) {
+        fclose(f);
+        return -4;
+    }
+    /* the data must hold the header's rows (the reference trusts the count; a test
+     * oracle refuses what the product refuses, tests/test_ply_malformed.py) */
+    const long here = ftell(f);
+    if (here < 0 || fseek(f, 0, SEEK_END) != 0) { fclose(f); return -3; }
+    const long avail = ftell(f) - here;
+    if (fseek(f, here, SEEK_SET) != 0 || (long long)nprops * 4 * nv > (long long)avail) { fclose(f); return -3; }
     if (!soa || capacity < nv) { fclose(f); return 0; }
 
     const int64_t n = nv;

@@ -11,7 +11,9 @@ from ctypes import POINTER, c_float, c_int, c_int64, c_void_p
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+# GSR_ORACLE_LIBRARY: another build of the oracle (tests/test_sanitizers.py runs the loader
+# and golden tests against the ASan/UBSan build, build/asan/liboracle.so)
+ORACLE_SO = os.environ.get("GSR_ORACLE_LIBRARY") or os.path.join(ROOT, "oracle", "liboracle.so")
 REF_DRIVER = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
 
 SPLAT_DTYPE = np.dtype([
