@@ -381,12 +381,16 @@ def main():
             break
     torch.cuda.synchronize()
 
+    warm_pos = [0]
+
     def warm(ms):
-        """Untimed frames in flight for at least `ms` of wall time; returns the count."""
+        """Untimed frames in flight for at least `ms` of wall time; returns the count.  A
+        moving camera (--orbit-step) keeps moving through them (frame indices continue)."""
         frames, w0 = 0, time.perf_counter()
         while (time.perf_counter() - w0) * 1e3 < ms:
             m = 4 * F
-            path(0, m, [j % min(F, len(outs)) for j in range(m)])
+            path(warm_pos[0] if frame_cam else 0, m, [j % min(F, len(outs)) for j in range(m)])
+            warm_pos[0] += m
             frames += m
             torch.cuda.synchronize()
         r.sync()

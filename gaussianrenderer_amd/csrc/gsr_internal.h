@@ -44,7 +44,8 @@ struct Stats {
     uint32_t depth_passes;            // passes the depth sort's device plan needed (binning path; 0: n/a)
     uint32_t split_unsat;             // depth split: blocks the last phase-A blend left unsaturated
                                       // (written to the host-mapped copy by the phase-B blend)
-    uint32_t split_pm;                // the split point of the frame whose split_unsat that is
+    uint32_t split_pm;                // the split point of the frame whose split_unsat that is, | the
+                                      // controller's epoch << 16 (gsr_runtime.cpp split_tag)
     uint32_t spec_miss;               // depth split without phase B (speculative): a phase-A blend
                                       // left a block unsaturated, the frame is incomplete (host copy,
                                       // sticky until the host reads it)
@@ -111,7 +112,8 @@ struct BlendSplit {
     Stats* spec_host;                 // phase A with no phase B queued: an unsaturated block sets
                                       // spec_host->spec_miss (nullable)
     SplitCut cut;                     // phase A: the next frame's threshold
-    uint32_t pm;                      // phase B publishes it with the count (Stats::split_pm)
+    uint32_t pm;                      // phase B publishes it with the count (Stats::split_pm: the split
+                                      // point | the controller's epoch << 16)
     uint32_t* fstatus;                // speculative phase A: an unsaturated block ors
                                       // GSR_FRAME_SPEC_MISS into the frame's validity word (nullable)
 };

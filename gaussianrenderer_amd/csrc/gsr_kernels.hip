@@ -402,19 +402,17 @@ __device__ __forceinline__ uint16_t tile_row_spans(float cx, float cy, float a, 
 // this exact operation order (the oracle restates it, oracle/gsr_oracle.c):
 // dt = t - c; x_t = ((x + m0 dt) + m3 dt^2) + m6 dt^3 (dt^2 = dt dt, dt^3 =
 // dt^2 dt; y, z with m1/m4/m7, m2/m5/m8); temporal factor exp(-(dt/s)^2).
+// One Gaussian i < n; returns the depth key of its item (0xFFFFFFFF: culled or dead).
 template <bool T4D, bool SH3>
-__global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ arr, int64_t stride,
-                                                    int64_t n, Frame fr, uint4* __restrict__ rec,
-                                                    uint64_t* __restrict__ items, uint64_t* __restrict__ rect,
-                                                    int packed, uint16_t* __restrict__ spans,
-                                                    float tnow, RecSplit rs) {
-    GSR_GEOM_PRIO();
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
+__device__ __forceinline__ uint32_t preprocess_one(const float* __restrict__ arr, int64_t stride,
+                                                   const Frame& fr, uint4* __restrict__ rec,
+                                                   uint64_t* __restrict__ items, uint64_t* __restrict__ rect,
+                                                   int packed, uint16_t* __restrict__ spans, float tnow,
+                                                   const RecSplit& rs, int64_t i) {
     // depth split, key mode (RecSplit): 1 = records of the near Gaussians only, 2 = the
     // far ones' records only (no item, rect or span writes: those are sorted already)
     const bool far_pass = rs.mode == 2;
-    if (far_pass && rs.gate && *rs.gate == 0u) return;
+    if (far_pass && rs.gate && *rs.gate == 0u) return 0xffffffffu;
     const uint32_t kcut = rs.mode == 1 ? *rs.kcut : far_pass ? *rs.kcut_frame : 0xffffffffu;
     // the frame's threshold, for the far record pass (the near sort copies it too)
     if (rs.mode == 1 && i == 0) *rs.kcut_frame = kcut;
@@ -457,7 +455,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     mv4(fr.V, old_xyz, tmp_xyz);
     if (!isfinite(tmp_xyz[0]) || !isfinite(tmp_xyz[1]) || !isfinite(tmp_xyz[2])) {
         if (!far_pass) put_rect(rect, i, kDeadRect, packed);
-        return;
+        return 0xffffffffu;
     }
     mv4(fr.P, tmp_xyz, new_xyz);
     new_xyz[0] = new_xyz[0] / new_xyz[3];
@@ -466,7 +464,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     if (!isfinite(new_xyz[0]) || !isfinite(new_xyz[1]) || !isfinite(new_xyz[2]) ||
         tmp_xyz[2] >= -fr.znear || new_xyz[2] < -1.0f || new_xyz[2] > 1.0f) {
         if (!far_pass) put_rect(rect, i, kDeadRect, packed);
-        return;
+        return 0xffffffffu;
     }
 
     // ---- 2D covariance (render.cu:655-686) ----
@@ -512,7 +510,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     const float det = S2[0] * S2[3] - S2[1] * S2[2];
     if (!isfinite(det) || det < 1e-8f) {                        // render.cu:690
         if (!far_pass) put_rect(rect, i, kDeadRect, packed);
-        return;
+        return 0xffffffffu;
     }
     const float invDet = 1.0f / det;
     const float ic0 = S2[3] * invDet, ic1 = -S2[1] * invDet;
@@ -525,7 +523,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
         const float hh = 0.5f * (ic1 + ic2);
         if (opt < 0.9e-3f && ic0 > 0.0f && ic3 > 0.0f && (ic0 * ic3 - hh * hh) > 1e-4f * (ic0 * ic3)) {
             if (!far_pass) put_rect(rect, i, kDeadRect, packed);
-            return;
+            return 0xffffffffu;
         }
     }
 
@@ -551,7 +549,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
     float ymin = new_xyz[1] - ey, ymax = new_xyz[1] + ey;
     if (xmax < -0.99f || xmin > 0.99f || ymax < -0.99f || ymin > 0.99f) {   // render.cu:737
         if (!far_pass) put_rect(rect, i, kDeadRect, packed);
-        return;
+        return 0xffffffffu;
     }
     xmin = fmaxf(xmin, -1.0f);
     xmax = fminf(xmax, 1.0f);
@@ -576,9 +574,9 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
         // far (key mode): no record unless phase B needs it (mode 2 writes it then)
         put_rect(rect, i, trect, packed);
         items[i] = ((uint64_t)key << 32) | (uint64_t)(uint32_t)i;
-        return;
+        return key;
     }
-    if (far_pass && key < kcut) return;
+    if (far_pass && key < kcut) return key;
 
     // ---- SH colour, bands 0..2 (render.cu:500-534), only for survivors ----
     float dir[3] = {gx - fr.campos[0], gy - fr.campos[1], gz - fr.campos[2]};
@@ -645,7 +643,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
                       (uint32_t)ymin_px | ((uint32_t)ymax_px << 16));
     const uint4 cw = cull_word(ic0, ic1, ic2, ic3, opacity, col[0], col[1], col[2]);
     R[3] = cw;
-    if (far_pass) return;
+    if (far_pass) return key;
     if (spans)
         spans[i] = tile_row_spans((float)px_x, (float)px_y, ic0, ic1, ic2, ic3,
                                   cw.x == __float_as_uint(-__builtin_huge_valf()) ? __builtin_huge_valf()
@@ -653,6 +651,19 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
                                   cw, xmin_px, xmax_px, ymin_px, ymax_px, tx0, tx1, ty0, ty1);
     put_rect(rect, i, trect, packed);
     items[i] = ((uint64_t)key << 32) | (uint64_t)(uint32_t)i;
+    return key;
+}
+
+template <bool T4D, bool SH3>
+__global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ arr, int64_t stride,
+                                                    int64_t n, Frame fr, uint4* __restrict__ rec,
+                                                    uint64_t* __restrict__ items, uint64_t* __restrict__ rect,
+                                                    int packed, uint16_t* __restrict__ spans,
+                                                    float tnow, RecSplit rs) {
+    GSR_GEOM_PRIO();
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    (void)preprocess_one<T4D, SH3>(arr, stride, fr, rec, items, rect, packed, spans, tnow, rs, i);
 }
 
 // Lanes of the wave whose `bits`-bit digit equals this lane's, among the lanes in

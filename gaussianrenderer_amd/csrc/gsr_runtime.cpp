@@ -383,6 +383,9 @@ struct gsr_context {
                                      // tests and guarded T tests (re-blends what it cannot vouch for)
     int depth_split = 2;             // GSR_TUNE_DEPTH_SPLIT: 0 off, 1 on, 2 on above kLargeScene Gaussians
     int split_pm = 250;              // split point: phase A bins the nearest split_pm / 1000 of the depth order
+    uint32_t split_epoch = 0;        // bumped at every restart of the controller (retry, knob): phase B
+                                     // publishes it with the split point, so evidence from before the
+                                     // restart is never taken for the restarted split point's
     int split_floor = 0;             // 5/4 of the last split point that left blocks unsaturated
     int split_clean = 0;             // checked split frames in a row that left none
     int split_off_frames = 0;        // frames since the split point reached 1000 (split off); after
@@ -390,6 +393,7 @@ struct gsr_context {
     int split_retry = 0;             // frames before the next retry (kSplitRetry, doubling after each
                                      // retry that found no saturating view, back after a clean one)
     float split_off_view[32] = {};   // V and P of the frame the split was turned off on
+    float prev_view[32] = {};        // V and P of the previous frame (a still camera: the same twice)
     bool split_frame = false;        // the sorted frame is split (phase A lists binned by sort_locked)
     bool split_rebin = false;        // phase B's lists replaced phase A's: a repeated blend bins phase A again
     bool split_seen = false;         // a split frame was blended since the last controller update
@@ -647,6 +651,9 @@ void mark(gsr_context* c, int stage) {
     (void)hipEventRecord(e, c->stream);
 }
 
+// The split point and the controller's epoch as phase B publishes them (Stats::split_pm).
+uint32_t split_tag(const gsr_context* c) { return (uint32_t)c->split_pm | ((c->split_epoch & 0xffffu) << 16); }
+
 // Depth split point after a frame that needed phase B: up by half, floor at 5/4 of the
 // old point, no speculation.
 void split_grow(gsr_context* c) {
@@ -702,7 +709,7 @@ int check_overflow(gsr_context* c, bool blocking) {
         // further, the next frames speculate (no phase B queued)
         c->split_seen = false;
         const int64_t u = hv->split_unsat;
-        if ((int)hv->split_pm != c->split_pm) {
+        if (hv->split_pm != split_tag(c)) {
             // the newest phase B ran at an earlier split point (frames in flight): no
             // evidence about the current one yet
         } else if (u == 0) {
@@ -716,6 +723,11 @@ int check_overflow(gsr_context* c, bool blocking) {
         } else {
             const int pm_old = c->split_pm;
             split_grow(c);   // phase A left blocks unsaturated
+            // at or above the starting point, 2 % of the blocks or more left unsaturated
+            // means tiles that see past the scene, which no split point saturates (phase B
+            // would run on every frame, at a cost above the unsplit frame's): off at once
+            // rather than in four growth steps (automatic mode; a forced split keeps growing)
+            if (c->depth_split == 2 && pm_old >= 250 && u * 50 >= 4 * (int64_t)c->ntiles) c->split_pm = 1000;
             if (c->split_pm >= 1000) {
                 // the split turned itself off: the next frames list the whole order's pairs.
                 // Size the pair buffer for them now (the split frames' pairs scaled to the
@@ -871,11 +883,18 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
         arrays = reinterpret_cast<const float*>(static_cast<const char*>(scene) + GSR_SCENE_HEADER_BYTES);
     }
     // depth split: the controller turned it off (split point 1000) because phase A kept
-    // leaving blocks unsaturated; a moving camera can bring back views whose tiles all
-    // saturate, so after split_retry frames on another camera than the one it was turned
-    // off on (a fixed camera, or a 4D scene's fixed camera over time, never retries) it is
-    // tried again from the starting point; each retry doubles the next wait, up to
-    // kSplitRetryMax, until a retry finds a view whose tiles all saturate
+    // leaving blocks unsaturated; a camera that moved elsewhere can bring back views whose
+    // tiles all saturate, so after split_retry frames, once the camera differs from the
+    // one it was turned off on (a fixed camera, or a 4D scene's fixed camera over time,
+    // never retries) and has stopped there (the same camera two frames running: a camera
+    // that keeps moving, e.g. an orbit, never retries — its threshold would always come
+    // from another view, and the controller's evidence lags the frames queued ahead of
+    // it), it is tried again from the starting point; each retry doubles the next wait,
+    // up to kSplitRetryMax, until a retry finds a view whose tiles all saturate
+    const bool still = std::memcmp(c->prev_view, c->fr.V, sizeof c->fr.V) == 0 &&
+                       std::memcmp(c->prev_view + 16, c->fr.P, sizeof c->fr.P) == 0;
+    std::memcpy(c->prev_view, c->fr.V, sizeof c->fr.V);
+    std::memcpy(c->prev_view + 16, c->fr.P, sizeof c->fr.P);
     if (c->split_pm >= 1000 && (c->depth_split == 1 || (c->depth_split == 2 && n > kLargeScene))) {
         if (c->split_off_frames == 0) {
             std::memcpy(c->split_off_view, c->fr.V, sizeof c->fr.V);
@@ -885,10 +904,11 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
         c->split_off_frames = std::min(c->split_off_frames + 1, 1 << 30);
         const bool moved = std::memcmp(c->split_off_view, c->fr.V, sizeof c->fr.V) != 0 ||
                            std::memcmp(c->split_off_view + 16, c->fr.P, sizeof c->fr.P) != 0;
-        if (c->split_off_frames >= c->split_retry && moved) {
+        if (c->split_off_frames >= c->split_retry && moved && still) {
             c->split_retry = std::min(2 * c->split_retry, kSplitRetryMax);
             c->split_off_frames = 0;
             c->split_pm = 250;
+            c->split_epoch++;
             c->split_floor = 0;
             c->split_clean = 0;
             c->split_key_ready = false;
@@ -1238,7 +1258,7 @@ static int blend_locked(gsr_context* c, float* d_out) {
                 }
                 if (int rc = bin_locked(c, key ? 0 : c->split_na, key ? n : n - c->split_na, 2, false, &rb, key))
                     return rc;
-                gsr::BlendSplit b{2, c->tbuf, c->bflag, c->gate, c->hstats_dev, nullptr, {}, (uint32_t)c->split_pm,
+                gsr::BlendSplit b{2, c->tbuf, c->bflag, c->gate, c->hstats_dev, nullptr, {}, split_tag(c),
                                   nullptr};
                 HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
                                           c->diagnostics ? c->consumed : nullptr, false, c->blend_band_tiles, 0,
@@ -1848,6 +1868,7 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     {
         auto restart = [value](gsr_context* x) {   // a new starting point for every lane
             x->split_pm = value;
+            x->split_epoch++;
             x->split_floor = 0;
             x->split_clean = 0;
             x->split_spec = false;

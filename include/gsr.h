@@ -368,6 +368,10 @@ enum {
                                         in phase B); 3 as 2 with no phase B queued (speculative: a frame
                                         that then leaves a block unsaturated is reported as
                                         GSR_E_OVERFLOW and rendered again by the caller) */
+    /* 27 reserved (removed, measured slower: the preprocess building the depth sort's pass-0
+       histograms in 512-thread workgroups of 2048 Gaussians, pass 0 without its upsweep launch:
+       preprocess 49.4 -> 60.3 us against the 5.7-us upsweep, -1.1 % one frame at a time and
+       -1.2 % in flight, profiles/r04_ab_pre_hist.txt) */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Current value of a knob (what gsr_set_tuning last set, else the default). */

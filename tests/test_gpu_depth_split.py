@@ -201,8 +201,12 @@ def test_config3_speculation_and_miss(gpu, orc, torch, c3):
     assert_frames(out.view(3, H, W).cpu().numpy(), want_thin, exact=True)
     # with completion events off (frames captured into a graph) no frame is
     # queued without phase B — a captured graph would replay that choice — so the same
-    # miss cannot happen unreported: back to speculation, events off, the thin scene
-    for _ in range(60):
+    # miss cannot happen unreported: back to speculation (a fresh context: the thin
+    # scene's unsaturated blocks may have turned this one's split off for good, since the
+    # camera never moves), events off, the thin scene
+    r.close()
+    r = split_renderer(gpu, 2, 30)
+    for _ in range(120):
         r.render(scene, cam, W, H, out.data_ptr())
         while r.sync() != 0:
             r.render(scene, cam, W, H, out.data_ptr())
@@ -253,6 +257,15 @@ def test_config3_background_masked_phase_b(gpu, orc, torch, c3):
     r.close()
     r = split_renderer(gpu, 2)
     out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    checked = 0
+    while r.get_tuning(KNOB_PM) < 1000:
+        # at the starting point 15 % of the blocks stay unsaturated: the controller turns
+        # the split off after the first checked frame (no growth steps)
+        r.render(scene, cam, W, H, out.data_ptr())
+        while r.sync() != 0:
+            r.render(scene, cam, W, H, out.data_ptr())
+        checked += 1
+        assert checked <= 2, f"split point {r.get_tuning(KNOB_PM)} after {checked} checked frames"
     for i in range(16):
         r.render(scene, cam, W, H, out.data_ptr())
         while r.sync() != 0:
@@ -269,6 +282,45 @@ def test_config3_background_masked_phase_b(gpu, orc, torch, c3):
     # the camera turns back to a view whose tiles all saturate: 256 frames after the split
     # was turned off, on another camera, it is tried again, and it stays on
     centred, want_c = c3[2], c3[5]
+    for i in range(300):
+        r.render(scene, centred, W, H, out.data_ptr())
+        if i % 16 == 15:
+            while r.sync() != 0:
+                r.render(scene, centred, W, H, out.data_ptr())
+    while r.sync() != 0:
+        r.render(scene, centred, W, H, out.data_ptr())
+    assert r.get_tuning(KNOB_STATE) in (1, 2, 3) and r.get_tuning(KNOB_PM) < 1000
+    assert_frames(out.view(3, H, W).cpu().numpy(), want_c, exact=True)
+    r.close()
+
+
+def test_moving_camera_never_retries_the_split(gpu, orc, torch, c3):
+    """A camera that keeps moving (an orbit, 0.5 deg per frame) never retries the split
+    once background turned it off: its threshold would always come from another view.
+    Stopped on a view whose tiles all saturate, it retries (256 frames after the turn-off)
+    and stays on.  Frames stay bit-exact."""
+    scene, soa, centred, W, H, want_c, _ = c3
+    r = split_renderer(gpu, 2)
+    out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+
+    def orbit_cam(deg):
+        c = cam_for(gpu, W, H)
+        gpu.orbit(c, deg, 0.0)
+        return c
+    pms = []
+    for i in range(700):
+        c = orbit_cam(40.0 + 0.5 * i)
+        r.render(scene, c, W, H, out.data_ptr())
+        if i % 8 == 7:
+            while r.sync() != 0:
+                r.render(scene, c, W, H, out.data_ptr())
+            pms.append(r.get_tuning(KNOB_PM))
+    off = pms.index(1000)
+    assert off < 20, f"the split did not turn off on the orbit: {pms[:20]}"
+    assert all(p == 1000 for p in pms[off:]), "the split was retried while the camera kept moving"
+    assert r.sync() == 0
+    want = orc.render(soa, c, W, H, 3.0, threads=ORC_THREADS)
+    assert_frames(out.view(3, H, W).cpu().numpy(), want, exact=True)
     for i in range(300):
         r.render(scene, centred, W, H, out.data_ptr())
         if i % 16 == 15:

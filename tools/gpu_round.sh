@@ -17,6 +17,13 @@
 #   abtune     interleaved knob A/B in one process (tools/ab_path.py, AB_ARGS)
 #   ablibs     interleaved A/B of two library builds            (tools/ab_libs.sh)
 #
+#   sh3        config 2 as BASELINE states it (SH degree 3): bench.py --sh3, 200 steps, then the
+#              kernel trace and FETCH/WRITE PMC of its one-frame-at-a-time run -> prof_${TAG}_sh3
+#   orbit      config 3 on a moving camera (--orbit-step 0.25; depth split on and off) beside the
+#              fixed camera, twice interleaved -> bench_${TAG}_c3_{fixed,orbit,orbitoff}_{1,2}.log
+#   stretch    kernel trace of the frames-in-flight bench and tools/blend_stretch.py: which
+#              geometry kernels beside a blend lengthen it -> prof_${TAG}_stretch/stretch.txt
+#
 #   STEPS="suite smoke bench" TAG=r03 bash tools/gpu_round.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -97,6 +104,30 @@ for step in ${STEPS:-suite smoke bench}; do
     rc=$?; tail -20 gpurun_out/abtune_$TAG.log; fatal $rc abtune; [ $rc = 0 ] || exit $rc ;;
   ablibs)
     bash tools/ab_libs.sh; rc=$?; fatal $rc ablibs; [ $rc = 0 ] || exit $rc ;;
+  sh3)
+    timeout -k 10 300 python bench.py --config 2 --sh3 --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/bench_${TAG}_sh3.log 2>&1
+    rc=$?; fatal $rc sh3; [ $rc = 0 ] || { tail -5 gpurun_out/bench_${TAG}_sh3.log; exit $rc; }
+    line gpurun_out/bench_${TAG}_sh3.log sh3
+    OUT=gpurun_out/prof_${TAG}_sh3 BENCH_ARGS="--sh3 --inflight 1" PMC_GROUPS="FETCH_SIZE;WRITE_SIZE" bash tools/profile.sh
+    rc=$?; fatal $rc sh3prof; [ $rc = 0 ] || exit $rc
+    python3 tools/summarize_prof.py gpurun_out/prof_${TAG}_sh3 > gpurun_out/prof_${TAG}_sh3/summary.txt 2>&1
+    head -16 gpurun_out/prof_${TAG}_sh3/summary.txt; slim gpurun_out/prof_${TAG}_sh3 ;;
+  orbit)
+    for rep in 1 2; do
+      for cam in fixed orbit orbitoff; do
+        extra=""; [ $cam = orbit ] && extra="--orbit-step 0.25"; [ $cam = orbitoff ] && extra="--orbit-step 0.25 --tune 23=0"
+        timeout -k 10 300 python bench.py --config 3 --steps 200 --warmup 20 --no-cpu-baseline $extra > gpurun_out/bench_${TAG}_c3_${cam}_$rep.log 2>&1
+        rc=$?; fatal $rc orbit; [ $rc = 0 ] || { tail -5 gpurun_out/bench_${TAG}_c3_${cam}_$rep.log; exit $rc; }
+        line gpurun_out/bench_${TAG}_c3_${cam}_$rep.log "config3 $cam"
+      done
+    done ;;
+  stretch)
+    O=gpurun_out/prof_${TAG}_stretch; mkdir -p $O
+    timeout -k 10 300 rocprofv3 --kernel-trace -d $O/kt -o kt --output-format csv -- python3 bench.py --config ${CONFIGS:-2} --steps 200 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > $O/kt.log 2>&1
+    rc=$?; echo "stretch trace rc=$rc"; fatal $rc stretch; [ $rc = 0 ] || { tail -5 $O/kt.log; exit $rc; }
+    python3 tools/blend_stretch.py $O > $O/stretch.txt 2>&1; cat $O/stretch.txt
+    python3 tools/overlap.py $O > $O/overlap.txt 2>&1 || true
+    slim $O ;;
   *) echo "unknown step $step"; exit 2 ;;
   esac
 done
