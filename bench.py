@@ -577,7 +577,7 @@ def main():
         "depth_passes": depth_passes,
         "pairs_consumed": consumed,
         "blend_exp": {1: "fast (v_exp_f32 alpha, exact alpha tests, guarded T tests, exact re-blend of "
-                         "suspect pixels)", 0: "exact (gsr_expf)"}[min(blend_exp, 1)],
+                         "suspect pixels)", 0: "exact (gsr_blend_expf)"}[min(blend_exp, 1)],
         "blend_counters": counters,
         "blend_lane_efficiency": round(counters["active_lanes"] / max(1, counters["lane_slots"]), 4),
         "image_mean": float(img.mean().item()),

@@ -527,17 +527,18 @@ def rank_order_check() -> tuple[int, int]:
 def math_probe(xy: np.ndarray) -> np.ndarray:
     """Evaluate the gsr_detmath functions on the GPU (see include/gsr.h)."""
     xy = np.ascontiguousarray(xy, dtype=np.float32).reshape(-1, 2)
-    out = np.zeros((xy.shape[0], 8), dtype=np.float32)
+    out = np.zeros((xy.shape[0], 9), dtype=np.float32)
     check(lib().gsr_math_probe(xy.ctypes.data, xy.shape[0], out.ctypes.data), "gsr_math_probe")
     return out
 
 
-def exp_probe(x_lo: float, x_hi: float, x_big: float) -> tuple[int, float, float]:
-    """gsr_exp_probe: (monotonicity violations of gsr_expf, max relative fast-exp error,
-    the same over x >= x_big) over every float in [x_lo, x_hi), on the GPU."""
-    v, ea, eb = c_int64(0), ctypes.c_float(0), ctypes.c_float(0)
-    check(lib().gsr_exp_probe(x_lo, x_hi, x_big, byref(v), byref(ea), byref(eb)), "gsr_exp_probe")
-    return int(v.value), float(ea.value), float(eb.value)
+def exp_probe(x_lo: float, x_hi: float, x_big: float) -> tuple[int, int, float, float]:
+    """gsr_exp_probe: (monotonicity violations of gsr_blend_expf, packed-loop exp
+    mismatches, max relative fast-exp error, the same over x >= x_big) over every float
+    in [x_lo, x_hi), on the GPU."""
+    v, ea, eb = (c_int64 * 2)(0, 0), ctypes.c_float(0), ctypes.c_float(0)
+    check(lib().gsr_exp_probe(x_lo, x_hi, x_big, v, byref(ea), byref(eb)), "gsr_exp_probe")
+    return int(v[0]), int(v[1]), float(ea.value), float(eb.value)
 
 
 def alpha_cut_probe(op: np.ndarray) -> np.ndarray:

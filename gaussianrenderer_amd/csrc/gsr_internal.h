@@ -155,7 +155,7 @@ hipError_t launch_kv_pass(const void* keys_in, const uint32_t* vals_in, void* ke
 // (diagnostics: 16 counters, then a u64 take map entry per pixel), or with stamps the
 // per-wave timeline (tools/blend_timeline.py).  band_tiles > 0: bands of that many
 // tiles dealt round-robin to the XCDs; 0: one contiguous run of blocks per XCD.
-// blend_exp (GSR_TUNE_BLEND_EXP): 0 gsr_expf; 1 hardware exp with exact alpha tests
+// blend_exp (GSR_TUNE_BLEND_EXP): 0 gsr_blend_expf; 1 hardware exp with exact alpha tests
 // and guarded transmittance tests, blocks it cannot vouch for blended again exactly;
 // 2 the same with the guard band at 100 % (test hook for the exact re-blend).
 hipError_t launch_blend(const uint32_t* idx, const uint2* ranges, const uint4* rec, const Frame& fr,

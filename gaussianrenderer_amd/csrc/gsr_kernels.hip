@@ -236,7 +236,7 @@ __device__ __forceinline__ void put_rect(uint64_t* rect, int64_t i, uint64_t r, 
 // for every md2 > 2 ln(1000 op) (exp and the product are within a few ulp), so
 // lanes beyond the returned bound can never composite.  The bound is padded by
 // 1e-5 relative + 1e-3 absolute — orders of magnitude above the rounding of
-// gsr_expf, the product and the hardware log2 used here — and is NaN (never
+// gsr_blend_expf, the product and the hardware log2 used here — and is NaN (never
 // skip) for NaN opacity, +inf for infinite opacity, -inf for op <= 0.  It only
 // decides whether a wave may SKIP work; it never changes a composited value.
 __device__ __forceinline__ float md2_cutoff(float op) {
@@ -247,7 +247,7 @@ __device__ __forceinline__ float md2_cutoff(float op) {
 // Fast-path proof for one splat on one block (exactness, not a heuristic):
 // finite conic that is robustly positive definite with |a|+|b|+|c|+|e| times
 // the squared largest block offset <= 4e7 keeps every in-box md2 finite and
-// >= -10 (float error of the 9-op form < 10), so -md2/2 lies in gsr_expf_x2's
+// >= -10 (float error of the 9-op form < 10), so -md2/2 lies in gsr_blend_expf_x2's
 // proven range; finite colours make "alpha = 0 when not taken" leave the
 // accumulators bit-identical (c + (col*0)*T == c, T*(1-0) == T).
 // Every coefficient is also 0 or of magnitude >= 2^-60: the pixel offsets are
@@ -2261,29 +2261,27 @@ __device__ __forceinline__ f2 pk_fma_b_hi(f2 a, f2 b, f2 c) {
     return r;
 }
 
-// gsr_expf on two lanes at once (v_pk_* for every float op that has a packed
-// form), for inputs the caller has PROVEN finite and in [-2e7, 88.75]: there the
-// clamps and the NaN select of gsr_expf do not change the result, and every
-// remaining step is the same IEEE operation in the same order, so each half is
-// bit-identical to gsr_expf of that half.
-__device__ __forceinline__ f2 gsr_expf_x2(f2 xc) {
-    // No clamp: the fast-path proof bounds every in-box input to [-2e7, 5], where
-    // n = rint(x log2e) >= -2.9e7 keeps the Cody-Waite remainder accurate (one
-    // fma rounding on ~6e3) and ldexp(y, n) rounds to +0 for every x < -104 —
-    // gsr_expf's clamped result.  Out-of-box lanes are discarded by the caller.
-    const f2 t = xc * 1.44269504088896341f;
-    f2 n;
-    n.x = rintf(t.x);
-    n.y = rintf(t.y);
+// gsr_blend_expf on two lanes at once (v_pk_* for every float op that has a packed
+// form: 11 packed + 4 single VALU, against 11 + 6 for the Cephes gsr_expf), for
+// inputs the caller has PROVEN finite and in [-2e7, 5]: on [-104, 5] the clamp and
+// the NaN select do not change the result and every remaining step is the same IEEE
+// operation in the same order, so each half is bit-identical to gsr_blend_expf of
+// that half.  Below -104 (no clamp here) n <= -150 — for |x log2 e| >= 2^22 the
+// shifter no longer rounds to an integer and the remainder r drifts to |r| < 1.5,
+// still finite — so ldexp(y, n) rounds to +0, the clamped result
+// (gsr_exp_probe counts the halves that differ from the scalar function over every
+// float of [-2e7, 5]: none).  Out-of-box lanes are discarded by the caller.
+__device__ __forceinline__ f2 gsr_blend_expf_x2(f2 xc) {
+    const f2 t = __builtin_elementwise_fma(xc, (f2)1.44269504088896341f, (f2)12582912.0f);
+    const f2 n = t - 12582912.0f;
     f2 r = __builtin_elementwise_fma(-n, (f2)0.693359375f, xc);
     r = __builtin_elementwise_fma(-n, (f2)-2.12194440e-4f, r);
-    f2 p = __builtin_elementwise_fma((f2)1.9875691500e-4f, r, (f2)1.3981999507e-3f);
-    p = __builtin_elementwise_fma(p, r, (f2)8.3334519073e-3f);
-    p = __builtin_elementwise_fma(p, r, (f2)4.1665795894e-2f);
-    p = __builtin_elementwise_fma(p, r, (f2)1.6666665459e-1f);
-    p = __builtin_elementwise_fma(p, r, (f2)5.0000001201e-1f);
+    f2 q = __builtin_elementwise_fma((f2)0x1.6b42a4p-10f, r, (f2)0x1.125e6cp-7f);
+    q = __builtin_elementwise_fma(q, r, (f2)0x1.5557c2p-5f);
+    q = __builtin_elementwise_fma(q, r, (f2)0x1.555452p-3f);
+    q = __builtin_elementwise_fma(q, r, (f2)0x1.fffffcp-2f);
     const f2 r2 = r * r;
-    const f2 y = __builtin_elementwise_fma(p, r2, r) + 1.0f;
+    const f2 y = __builtin_elementwise_fma(q, r2, r) + 1.0f;
     f2 res;
     res.x = __builtin_amdgcn_ldexpf(y.x, (int)n.x);
     res.y = __builtin_amdgcn_ldexpf(y.y, (int)n.y);
@@ -2291,7 +2289,7 @@ __device__ __forceinline__ f2 gsr_expf_x2(f2 xc) {
 }
 
 // The blend's fast exp (GSR_TUNE_BLEND_EXP 1): e^x as the hardware 2^t (v_exp_f32) of
-// t = x log2(e), two lanes at once.  Its relative difference from gsr_expf, with the
+// t = x log2(e), two lanes at once.  Its relative difference from gsr_blend_expf, with the
 // alpha product, is bounded on the argument range a composited lane can have
 // (kFxEpsMax, kFxEpsBig below; measured exhaustively by gsr_exp_probe); the
 // alpha decisions never use it (xs), and the transmittance test is guarded.
@@ -2306,7 +2304,7 @@ __device__ __forceinline__ f2 fast_expf_x2(f2 x) {
 // Fast-exp blend: bounds on |alpha_fast / alpha_exact - 1| for a composited lane
 // (opacity in [0, 1] and alpha_exact >= 1e-3, so the exp argument x lies in
 // [ln(1e-3), 5]; alpha > 0.5 needs x > ln 0.5, alpha > 0.9 needs x > ln 0.9).  Each is
-// the exhaustive maximum of |fast_expf / gsr_expf - 1| over every float x of its
+// the exhaustive maximum of |fast_expf / gsr_blend_expf - 1| over every float x of its
 // range (gsr_exp_probe; tests/test_gpu_fastexp.py checks these constants stay above
 // it) plus 2^-23 for the two roundings of op * e:
 //   kFxEps3  all composited lanes (x >= -6.95)
@@ -2360,7 +2358,7 @@ __device__ __forceinline__ float fx_band(float band0, uint32_t n, float m) {
 // and feed v_pk_* instructions directly.  The compositing loop takes two
 // splats per iteration: md2, exp and alpha packed, then the two composites in
 // list order.  Batches holding a survivor without the fast-path proof run an
-// exact one-splat path instead (same values, full gsr_expf, plain selects).
+// exact one-splat path instead (same values, full gsr_blend_expf, plain selects).
 //
 // Pair slot dwords (h = 0 / 1 for the first / second splat of the pair):
 //   [0+h] cx  [2+h] cy  [4+h] a  [6+h] b  [8+h] c  [10+h] e  [12+h] opacity
@@ -2567,7 +2565,7 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                 const f2 u = __builtin_elementwise_fma((f2){q1.x, q1.y}, dx, (f2){q1.z, q1.w} * dy);
                 const f2 v = __builtin_elementwise_fma((f2){q2.x, q2.y}, dx, (f2){q2.z, q2.w} * dy);
                 const f2 mdh = __builtin_elementwise_fma(dx, u, dy * v);
-                const f2 ee = FX ? fast_expf_x2(mdh) : gsr_expf_x2(mdh);
+                const f2 ee = FX ? fast_expf_x2(mdh) : gsr_blend_expf_x2(mdh);
                 const f2 al = (f2){q3.x, q3.y} * ee;
                 const float al0 = fminf(al.x, 0.99f), al1 = fminf(al.y, 0.99f);
                 // alpha tests (render.cu:335): on alpha itself, or (FX) on the exp
@@ -2660,7 +2658,7 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
             }
             T = TT.x;
         } else {
-            // exact one-splat path (render.cu:329-340 with gsr_expf and selects)
+            // exact one-splat path (render.cu:329-340 with gsr_blend_expf and selects)
             for (uint32_t k = 0; mm && alive; ++k) {
                 const int s = __builtin_ctzll(mm);
                 mm &= mm - 1;
@@ -2670,7 +2668,7 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                 const int h = (int)(k & 1u);
                 const float dx = fpx - S[0 + h], dy = fpy - S[2 + h];
                 const float md = gsr_blend_md2(dx, dy, S[4 + h], S[6 + h], S[8 + h], S[10 + h]);
-                const float ee = gsr_expf(-0.5f * md);
+                const float ee = gsr_blend_expf(-0.5f * md);
                 float alpha = S[12 + h] * ee;
                 alpha = fminf(alpha, 0.99f);
                 const bool in = __builtin_amdgcn_inverse_ballot_w64(box);
@@ -2926,8 +2924,9 @@ __global__ void k_math_probe(const float* __restrict__ in, int n, float* __restr
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float x = in[2 * i], y = in[2 * i + 1];
-    float* o = out + 8 * i;
+    float* o = out + 9 * i;
     o[0] = gsr_expf(x);
+    o[8] = gsr_blend_expf(x);
     o[1] = gsr_sinf(x);
     o[2] = gsr_cosf(x);
     o[3] = gsr_atan2f(x, y);
@@ -2937,25 +2936,33 @@ __global__ void k_math_probe(const float* __restrict__ in, int n, float* __restr
     o[7] = __int_as_float(gsr_f2i_sat(x * 1000.0f));
 }
 
-// Exhaustive checks behind the fast-exp blend (gsr_exp_probe).  Over every float key k
-// in [key_lo, key_hi): viol[0] counts gsr_expf(x_k) > gsr_expf(x_k+1) (monotonicity of
-// the exact exp, which makes the alpha test a threshold on its argument), and
-// over the same keys the largest |fast_expf / gsr_expf - 1| is kept as float bits,
-// split at x >= x_big: errs[0] every key (x in the range), errs[1] x >= x_big.
+// Exhaustive checks behind the blend's exp (gsr_exp_probe).  Over every float key k
+// in [key_lo, key_hi): viol[0] counts gsr_blend_expf(x_k) > gsr_blend_expf(x_k+1)
+// (monotonicity of the exact exp, which makes the alpha test a threshold on its
+// argument); viol[1] counts the x in [-2e7, 5] where a half of gsr_blend_expf_x2 differs
+// from gsr_blend_expf (the packed path's unclamped domain); and over the same keys the
+// largest |fast_expf / gsr_blend_expf - 1| is kept as float bits, split at x >= x_big:
+// errs[0] every key (x in the range), errs[1] x >= x_big.
 __global__ __launch_bounds__(256) void k_exp_probe(uint32_t key_lo, uint32_t key_hi, float x_big,
                                                    unsigned long long* __restrict__ viol,
                                                    uint32_t* __restrict__ errs) {
     const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t bad = 0;
+    uint64_t bad = 0, pk_bad = 0;
     float emax = 0.0f, ebig = 0.0f;
     for (uint64_t k = (uint64_t)key_lo + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < key_hi; k += nthr) {
         const float x = gsr_key_float((uint32_t)k);
-        const float e = gsr_expf(x);
-        const float en = gsr_expf(gsr_key_float((uint32_t)k + 1u));
+        const float e = gsr_blend_expf(x);
+        const float en = gsr_blend_expf(gsr_key_float((uint32_t)k + 1u));
         bad += e > en ? 1u : 0u;
         f2 xx;
         xx.x = x;
-        xx.y = x;
+        xx.y = -x;
+        if (x >= -2e7f && x <= 5.0f) {
+            const f2 pk = gsr_blend_expf_x2(xx);
+            pk_bad += __float_as_uint(pk.x) != __float_as_uint(e) ? 1u : 0u;
+            if (-x >= -2e7f && -x <= 5.0f)
+                pk_bad += __float_as_uint(pk.y) != __float_as_uint(gsr_blend_expf(-x)) ? 1u : 0u;
+        }
         const float f = fast_expf_x2(xx).x;
         const float r = (float)fabs((double)f / (double)e - 1.0);   // rounded up below
         const float ru = __uint_as_float(__float_as_uint(r) + 1u);
@@ -2963,6 +2970,7 @@ __global__ __launch_bounds__(256) void k_exp_probe(uint32_t key_lo, uint32_t key
         if (x >= x_big) ebig = fmaxf(ebig, ru);
     }
     if (bad) atomicAdd(viol, (unsigned long long)bad);
+    if (pk_bad) atomicAdd(viol + 1, (unsigned long long)pk_bad);
     atomicMax(errs, __float_as_uint(emax));
     atomicMax(errs + 1, __float_as_uint(ebig));
 }

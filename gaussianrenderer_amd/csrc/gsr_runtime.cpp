@@ -379,7 +379,7 @@ struct gsr_context {
     uint32_t* cbins = nullptr;       // binning: column counts per chunk (256 x chunks)
     int64_t cbins_cap = 0;
     bool last_binned = false;        // the last sorted frame took the binning path
-    int blend_exp = 0;               // blend: 0 = gsr_expf (bit-exact); 1 = fast exp with exact alpha
+    int blend_exp = 0;               // blend: 0 = gsr_blend_expf (bit-exact); 1 = fast exp with exact alpha
                                      // tests and guarded T tests (re-blends what it cannot vouch for)
     int depth_split = 2;             // GSR_TUNE_DEPTH_SPLIT: 0 off, 1 on, 2 on above kLargeScene Gaussians
     int split_pm = 250;              // split point: phase A bins the nearest split_pm / 1000 of the depth order
@@ -1966,10 +1966,10 @@ extern "C" int gsr_math_probe(const float* host_in, int n, float* host_out) {
     if (!host_in || !host_out || n <= 0) return set_err(GSR_E_ARG, "gsr_math_probe: bad argument");
     float *din = nullptr, *dout = nullptr;
     HIP_TRY(hipMalloc(&din, sizeof(float) * 2 * (size_t)n));
-    HIP_TRY(hipMalloc(&dout, sizeof(float) * 8 * (size_t)n));
+    HIP_TRY(hipMalloc(&dout, sizeof(float) * 9 * (size_t)n));
     HIP_TRY(hipMemcpy(din, host_in, sizeof(float) * 2 * (size_t)n, hipMemcpyHostToDevice));
     HIP_TRY(gsr::launch_math_probe(din, n, dout, nullptr));
-    HIP_TRY(hipMemcpy(host_out, dout, sizeof(float) * 8 * (size_t)n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(host_out, dout, sizeof(float) * 9 * (size_t)n, hipMemcpyDeviceToHost));
     (void)hipFree(din);
     (void)hipFree(dout);
     return GSR_OK;
@@ -1981,18 +1981,19 @@ extern "C" int gsr_exp_probe(float x_lo, float x_hi, float x_big, int64_t* viola
         return set_err(GSR_E_ARG, "gsr_exp_probe: bad argument");
     unsigned long long* dv = nullptr;
     uint32_t* de = nullptr;
-    HIP_TRY(hipMalloc(&dv, sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&dv, 2 * sizeof(unsigned long long)));
     HIP_TRY(hipMalloc(&de, 2 * sizeof(uint32_t)));
-    HIP_TRY(hipMemset(dv, 0, sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(dv, 0, 2 * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(de, 0, 2 * sizeof(uint32_t)));
     HIP_TRY(gsr::launch_exp_probe(gsr_float_key(x_lo), gsr_float_key(x_hi), x_big, dv, de, nullptr));
-    unsigned long long v = 0;
+    unsigned long long v[2] = {0, 0};
     uint32_t e[2] = {0, 0};
-    HIP_TRY(hipMemcpy(&v, dv, sizeof v, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(v, dv, sizeof v, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(e, de, sizeof e, hipMemcpyDeviceToHost));
     (void)hipFree(dv);
     (void)hipFree(de);
-    *violations = (int64_t)v;
+    violations[0] = (int64_t)v[0];
+    violations[1] = (int64_t)v[1];
     *err_all = gsr_bits_to_float(e[0]);
     *err_big = gsr_bits_to_float(e[1]);
     return GSR_OK;

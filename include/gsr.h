@@ -334,7 +334,7 @@ enum {
                                         the default.  Same order, same image */
     GSR_TUNE_RANK_ATOMIC_ACTIVE = 21, /* read-only: 1 if the atomic ranks are in use (knob 20 at 1 and the
                                         self-check passed), 0 if the kernels rank with ballots */
-    GSR_TUNE_BLEND_EXP = 22,         /* blend exp: 0 (default) = gsr_expf throughout (bit-exact with the
+    GSR_TUNE_BLEND_EXP = 22,         /* blend exp: 0 (default) = gsr_blend_expf throughout (bit-exact with the
                                         oracle).  1 (environment GSR_BLEND_EXP=1 selects it) = hardware
                                         exp for alpha, with the alpha test exact on the exp argument and
                                         the transmittance test guarded by a proven band; suspect pixels
@@ -445,14 +445,17 @@ void gsr_camera_intrinsics(const gsr_camera* cam, float* fx, float* fy);
 
 /* Device self-test used by the parity tests: for each (x, y) pair of host_in
  * (2n floats) evaluates on the GPU {gsr_expf(x), gsr_sinf(x), gsr_cosf(x),
- * gsr_atan2f(x, y), sqrtf(x), x / y, roundf(x), bits(gsr_f2i_sat(1000x))}
- * into host_out (8n floats), so the CPU twins can be compared bit for bit. */
+ * gsr_atan2f(x, y), sqrtf(x), x / y, roundf(x), bits(gsr_f2i_sat(1000x)),
+ * gsr_blend_expf(x)} into host_out (9n floats), so the CPU twins can be compared
+ * bit for bit. */
 int gsr_math_probe(const float* host_in, int n, float* host_out);
-/* Exhaustive device checks behind GSR_TUNE_BLEND_EXP, over every float x in
- * [x_lo, x_hi): *violations = the number of x with gsr_expf(x) > gsr_expf(next x)
+/* Exhaustive device checks of the blend's exp, over every float x in [x_lo, x_hi):
+ * violations[0] = the number of x with gsr_blend_expf(x) > gsr_blend_expf(next x)
  * (0: the exact exp is monotone, so the alpha test is a threshold on -md2/2);
- * *err_all / *err_big = the largest |fast exp / gsr_expf - 1| over the range / over
- * x >= x_big (rounded up). */
+ * violations[1] = the number of x in [-2e7, 5] (and of -x there) where the packed
+ * compositing loop's exp differs from gsr_blend_expf; *err_all / *err_big = the
+ * largest |fast exp / gsr_blend_expf - 1| (GSR_TUNE_BLEND_EXP 1) over the range /
+ * over x >= x_big (rounded up).  violations points at two int64. */
 int gsr_exp_probe(float x_lo, float x_hi, float x_big, int64_t* violations, float* err_all, float* err_big);
 /* gsr_alpha_take_min_x (gsr_detmath.h) evaluated on the device for n opacities. */
 int gsr_alpha_cut_probe(const float* host_op, int n, float* host_out);

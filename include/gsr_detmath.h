@@ -115,6 +115,44 @@ GSR_HD float gsr_expf(float x) {
     return (x != x) ? x + x : res;                        /* NaN */
 }
 
+/*
+ * The blend's expf (render.cu:333, one per pixel-splat pair: the renderer's hottest
+ * function).  Same domain handling as gsr_expf (clamp to [-104, 88.75], NaN kept) and
+ * the same accuracy class (<= 1.006 ulp against exp over every float, 0.9991 ulp on
+ * [-7, 0], monotone non-decreasing on every float: tests/test_detmath.py sweeps it
+ * exhaustively), but two instructions cheaper per packed pair on gfx950:
+ *   - n = rint(x log2 e) by the 1.5 * 2^23 shifter inside one fma (the rounding of the
+ *     exact product, ties to even) instead of a product and two v_rndne_f32;
+ *   - a degree-6 minimax e^r = 1 + r + r^2 Q(r) on |r| <= ln2/2 (Q of degree 4, fitted
+ *     for relative error 5.5e-9 with float coefficients) instead of Cephes' degree 7.
+ * The reference's own expf is CUDA libdevice's, which cannot run here; gsr_expf was
+ * the previous stand-in.  Against it this one differs on 0.24 % of all floats, by
+ * one ulp; the rendered effect is measured in profiles/r04_blend_exp_parity.txt.
+ */
+GSR_HD float gsr_blend_expf(float x) {
+    const float xc = fminf(fmaxf(x, -104.0f), 88.75f);   /* NaN -> -104 (replaced below) */
+    const float t = __builtin_fmaf(xc, 1.44269504088896341f, 12582912.0f);
+    const float n = t - 12582912.0f;                      /* rint(xc log2 e), exact */
+    float r = __builtin_fmaf(-n, 0.693359375f, xc);
+    r = __builtin_fmaf(-n, -2.12194440e-4f, r);
+    float q = 0x1.6b42a4p-10f;                            /* 1.38572813e-3 */
+    q = __builtin_fmaf(q, r, 0x1.125e6cp-7f);              /* 8.37307237e-3 */
+    q = __builtin_fmaf(q, r, 0x1.5557c2p-5f);              /* 4.16678227e-2 */
+    q = __builtin_fmaf(q, r, 0x1.555452p-3f);              /* 1.66664734e-1 */
+    q = __builtin_fmaf(q, r, 0x1.fffffcp-2f);              /* 4.99999940e-1 */
+    const float r2 = r * r;
+    const float y = __builtin_fmaf(q, r2, r) + 1.0f;
+    const int ni = (int)n;                                /* n in [-150, 128] */
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float res = __builtin_amdgcn_ldexpf(y, ni);
+#else
+    const int e1 = ni / 2;
+    const int e2 = ni - e1;
+    const float res = (y * gsr_pow2i(e1)) * gsr_pow2i(e2);
+#endif
+    return (x != x) ? x + x : res;
+}
+
 /* md2 of renderGaussians (render.cu:331),
  *   dx * (ic0 * dx + ic1 * dy) + dy * (ic2 * dx + ic3 * dy),
  * with the fused multiply-adds the reference's compiler forms: nvcc contracts
@@ -142,18 +180,18 @@ GSR_HD float gsr_key_float(uint32_t k) {
 /* The blend's alpha test (render.cu:333-335) as a predicate of the exp argument
  * x = -md2 / 2: is fminf(op * expf(x), 0.99f) >= 1e-3f? */
 GSR_HD int gsr_alpha_taken(float op, float x) {
-    return !(fminf(op * gsr_expf(x), 0.99f) < 1e-3f);
+    return !(fminf(op * gsr_blend_expf(x), 0.99f) < 1e-3f);
 }
 
 /*
  * Smallest float x with gsr_alpha_taken(op, x): a splat is composited on a pixel
  * (alpha test passed) iff its exp argument -md2/2 >= this value, because
- * gsr_expf is monotone non-decreasing on every float (checked exhaustively on
+ * gsr_blend_expf is monotone non-decreasing on every float (checked exhaustively on
  * [-104, 88.75], tests/test_gpu_fastexp.py; constant outside) and so is the
  * rounded product op * y for op > 0.  NaN op: alpha = fminf(NaN, 0.99) passes for
  * every x (-inf); op <= 0 never passes (+inf); op = +inf always passes (-inf).
- * For finite op > 0 the answer lies in (-104, 88.75]: gsr_expf(-104) = +0 fails
- * and gsr_expf(88.75) = +inf passes.  A few steps from the log estimate find it
+ * For finite op > 0 the answer lies in (-104, 88.75]: gsr_blend_expf(-104) = +0
+ * fails and gsr_blend_expf(88.75) = +inf passes.  A few steps from the log estimate find it
  * (the estimate is within a few ulp), with bisection on the float order as the
  * bound.  Host and device give the same value: the estimate only picks where the
  * search starts.

@@ -25,6 +25,32 @@
 #endif
 
 float orc_expf(float x) { return gsr_expf(x); }
+float orc_blend_expf(float x) { return gsr_blend_expf(x); }
+
+/* Exhaustive sweep of gsr_blend_expf over every float in [x_lo, x_hi] (OpenMP):
+ * *viol = the number of x with f(x) > f(next float), *max_ulp = the largest error
+ * against the double-precision exp in units of the float spacing at the result, over
+ * the x of the sweep that lie in [-87, 88.7] (normal results, no overflow). */
+void orc_blend_exp_sweep(float x_lo, float x_hi, int64_t* viol, double* max_ulp) {
+    const uint32_t klo = gsr_float_key(x_lo), khi = gsr_float_key(x_hi);
+    int64_t v = 0;
+    double mu = 0.0;
+#pragma omp parallel for schedule(static) reduction(+ : v) reduction(max : mu)
+    for (int64_t k = (int64_t)klo; k < (int64_t)khi; ++k) {
+        const float x = gsr_key_float((uint32_t)k);
+        const float e = gsr_blend_expf(x);
+        if (e > gsr_blend_expf(gsr_key_float((uint32_t)k + 1u))) v++;
+        if (x >= -87.0f && x <= 88.7f) {
+            const double ref = exp((double)x);
+            int ex;
+            frexp(ref, &ex);
+            const double u = fabs((double)e - ref) / ldexp(1.0, ex - 24);
+            if (u > mu) mu = u;
+        }
+    }
+    *viol = v;
+    *max_ulp = mu;
+}
 float orc_sinf(float x) { return gsr_sinf(x); }
 float orc_cosf(float x) { return gsr_cosf(x); }
 float orc_atan2f(float y, float x) { return gsr_atan2f(y, x); }
@@ -473,7 +499,8 @@ static int cmp_kv(const void* a, const void* b) {
  *        kernels); 2 the second product of each sum fused; 3 the inner sums only
  *        (first product); 4 the outer sum only (first product);
  *   rgb: 0 rgb + (color * alpha) * T rounded twice; 1 fmaf(color * alpha, T, rgb) (shipped);
- *   exp: 0 gsr_expf (shipped); 1 the host libm expf (glibc: correctly rounded). */
+ *   exp: 0 gsr_blend_expf (shipped); 1 the host libm expf (glibc: correctly rounded);
+ *        2 gsr_expf (Cephes, the blend's exp up to round 3). */
 static int g_var_md2 = 1, g_var_rgb = 1, g_var_exp = 0;
 void orc_set_blend_variant(int md2, int rgb, int expm) {
     g_var_md2 = md2;
@@ -500,7 +527,8 @@ static void blend_step_var(const orc_splat* g, int gx, int gy, float* T, float* 
     const float dx = ((float)gx - (float)g->px_x);
     const float dy = ((float)gy - (float)g->px_y);
     const float md2 = md2_variant(dx, dy, g->inv_covar);
-    float opacity = g->opacity * (g_var_exp ? expf(-0.5f * md2) : gsr_expf(-0.5f * md2));
+    const float x = -0.5f * md2;
+    float opacity = g->opacity * (g_var_exp == 1 ? expf(x) : g_var_exp == 2 ? gsr_expf(x) : gsr_blend_expf(x));
     opacity = fminf(opacity, 0.99f);
     if (opacity < 1e-3f) return;
     for (int c = 0; c < 3; ++c)
@@ -521,7 +549,7 @@ static inline void blend_step(const orc_splat* g, int gx, int gy, float* T, floa
     const float* ic = g->inv_covar;
     /* render.cu:331 and 337 with nvcc's default FMA contraction (gsr_blend_md2) */
     const float md2 = gsr_blend_md2(dx, dy, ic[0], ic[1], ic[2], ic[3]);
-    float opacity = g->opacity * gsr_expf(-0.5f * md2);
+    float opacity = g->opacity * gsr_blend_expf(-0.5f * md2);
     opacity = fminf(opacity, 0.99f);
     if (opacity < 1e-3f) return;
     for (int c = 0; c < 3; ++c) rgb[c] = __builtin_fmaf(g->color[c] * opacity, *T, rgb[c]);

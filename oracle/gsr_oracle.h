@@ -45,7 +45,7 @@ int orc_ply_read_ex(const char* path, float* soa, int narrays, int64_t capacity,
 /* SH-3 ("Inria-correct") mode for orc_preprocess / orc_render: soa then has
  * GSR_SCENE_SH3_NARRAYS arrays (process-wide switch; tests reset it). */
 void orc_set_sh3(int on);
-/* Blend contraction variant (gsr_oracle.c blend_step_var): md2 0..4, rgb 0..1, exp 0..1;
+/* Blend contraction variant (gsr_oracle.c blend_step_var): md2 0..4, rgb 0..1, exp 0..2;
  * (1, 1, 0) = the shipped choice the kernels share. */
 void orc_set_blend_variant(int md2, int rgb, int expm);
 /* Config 5: the 38 arrays of a 4D scene at time t, no temporal cull. */
@@ -83,6 +83,8 @@ void orc_covariance_chain(const float quat[4], const float scale[3], const float
 
 /* Deterministic math exported for the detmath tests (gsr_detmath.h). */
 float orc_expf(float x);
+float orc_blend_expf(float x);
+void orc_blend_exp_sweep(float x_lo, float x_hi, int64_t* viol, double* max_ulp);
 float orc_sinf(float x);
 float orc_cosf(float x);
 float orc_atan2f(float y, float x);

@@ -62,9 +62,11 @@ def lib():
         L.orc_project.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
         L.orc_covariance_chain.argtypes = [c_void_p, c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p,
                                            c_void_p]
-        for f in ("orc_expf", "orc_sinf", "orc_cosf"):
+        for f in ("orc_expf", "orc_blend_expf", "orc_sinf", "orc_cosf"):
             getattr(L, f).argtypes = [c_float]
             getattr(L, f).restype = c_float
+        L.orc_blend_exp_sweep.argtypes = [c_float, c_float, c_void_p, c_void_p]
+        L.orc_blend_exp_sweep.restype = None
         L.orc_atan2f.argtypes = [c_float, c_float]
         L.orc_atan2f.restype = c_float
         assert SPLAT_DTYPE.itemsize == 88

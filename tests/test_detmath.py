@@ -37,6 +37,29 @@ def test_expf_blend_range_accuracy(L):
     assert ulp_err(got, np.exp(x.astype(np.float64))).max() <= 1.0
 
 
+def test_blend_expf_exhaustive(L):
+    """gsr_blend_expf, the blend's exp (render.cu:333), over EVERY float of [-104, 88.75]
+    (constant outside, by its clamp): monotone non-decreasing — the alpha test is then a
+    threshold on the exp argument (gsr_alpha_take_min_x, the blend's cull) — and within
+    1.006 ulp of exp, the accuracy of the Cephes gsr_expf it replaced (1.0103 ulp)."""
+    import ctypes
+    viol, mu = ctypes.c_int64(0), ctypes.c_double(0)
+    L.orc_blend_exp_sweep(-104.0, 88.75, ctypes.byref(viol), ctypes.byref(mu))
+    print(f"gsr_blend_expf: {viol.value} monotonicity violations, max {mu.value:.4f} ulp")
+    assert viol.value == 0
+    assert mu.value <= 1.006
+
+
+def test_blend_expf_special_cases(L):
+    f = L.orc_blend_expf
+    assert f(float("-inf")) == 0.0 and f(-104.0) == 0.0 and f(-200.0) == 0.0
+    assert f(float("inf")) == float("inf") and f(88.75) == float("inf")
+    assert math.isnan(f(float("nan")))
+    assert f(0.0) == 1.0 and f(-0.0) == 1.0
+    # denormal results keep IEEE rounding (ldexp on the device, two products here)
+    assert 0.0 < f(-100.0) < 1.2e-38
+
+
 def test_sincos_accuracy(L):
     x = np.linspace(-math.pi, math.pi, 200_001, dtype=np.float32)
     for f, r in ((L.orc_sinf, np.sin), (L.orc_cosf, np.cos)):

@@ -61,6 +61,7 @@ def test_math_probe_bitwise(gpu, orc):
     xs, ys = xy[:, 0], xy[:, 1]
     ref = np.zeros_like(got)
     ref[:, 0] = [L.orc_expf(v) for v in xs]
+    ref[:, 8] = [L.orc_blend_expf(v) for v in xs]
     ref[:, 1] = [L.orc_sinf(v) for v in xs]
     ref[:, 2] = [L.orc_cosf(v) for v in xs]
     ref[:, 3] = [L.orc_atan2f(a, b) for a, b in zip(xs, ys)]
@@ -70,7 +71,8 @@ def test_math_probe_bitwise(gpu, orc):
         tr = np.trunc(xs)
         ref[:, 6] = np.where(np.abs(xs - tr) >= np.float32(0.5), tr + np.sign(xs), tr).astype(np.float32)
     same = (got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref))
-    for col, name in enumerate(["exp", "sin", "cos", "atan2", "sqrt", "div", "round"]):
+    for col, name in [(0, "exp"), (1, "sin"), (2, "cos"), (3, "atan2"), (4, "sqrt"), (5, "div"), (6, "round"),
+                      (8, "blend exp")]:
         bad = np.where(~same[:, col])[0]
         assert bad.size == 0, f"{name}: {bad.size} mismatches, e.g. x={xs[bad[:3]]} y={ys[bad[:3]]} got={got[bad[:3], col]} ref={ref[bad[:3], col]}"
 

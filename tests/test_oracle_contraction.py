@@ -6,8 +6,8 @@ which products it fuses cannot be observed (the CUDA path cannot be built here).
 oracle and the kernels share one choice (gsr_detmath.h gsr_blend_md2), so the GPU tests,
 which demand bits equal to the oracle, cannot see whether the choice matters.  This test
 renders config 1 under every other plausible contraction — none, the second products,
-the inner or outer sums only, the accumulation unfused — and with the host libm expf in
-place of gsr_expf, and measures each against the shipped choice: the images must stay
+the inner or outer sums only, the accumulation unfused — and with the host libm expf or
+round 3's Cephes gsr_expf in place of gsr_blend_expf, and measures each against the shipped choice: the images must stay
 within the north-star gate (L-inf <= 1e-4) and every pixel must composite the same
 splats (take maps equal).  tools/contraction_parity.py runs the same table at configs 2
 and 3 (profiles/r04_contraction_parity.txt)."""
@@ -16,7 +16,8 @@ import pytest
 
 from conftest import LINF_TOL
 
-VARIANTS = [(0, 0, 0), (0, 1, 0), (1, 0, 0), (2, 1, 0), (2, 0, 0), (3, 1, 0), (4, 1, 0), (1, 1, 1), (0, 0, 1)]
+VARIANTS = [(0, 0, 0), (0, 1, 0), (1, 0, 0), (2, 1, 0), (2, 0, 0), (3, 1, 0), (4, 1, 0), (1, 1, 1), (0, 0, 1),
+            (1, 1, 2)]
 
 
 @pytest.fixture(scope="module")

@@ -6,7 +6,7 @@ products it fuses cannot be observed here (the CUDA path cannot be built).  The 
 and the kernels share one choice (include/gsr_detmath.h gsr_blend_md2: the first product
 of each sum; rgb = fmaf(color * alpha, T, rgb)).  This tool renders the same frame with
 the oracle under every other plausible choice (gsr_oracle.c blend_step_var) — and with
-the host libm expf in place of gsr_expf — and reports, against the shipped choice:
+the host libm expf or round 3's Cephes gsr_expf in place of gsr_blend_expf — and reports, against the shipped choice:
 L-inf, pixels over the 1e-4 gate, pixels that differ at all, and pixels whose take map
 (the set of splats composited) differs.
 
@@ -35,8 +35,9 @@ VARIANTS = [
     ((2, 0, 0), "md2 second products fused, rgb not fused"),
     ((3, 1, 0), "md2 inner sums only, rgb fused"),
     ((4, 1, 0), "md2 outer sum only, rgb fused"),
-    ((1, 1, 1), "shipped contraction, libm expf instead of gsr_expf"),
+    ((1, 1, 1), "shipped contraction, libm expf instead of gsr_blend_expf"),
     ((0, 0, 1), "no contraction, libm expf"),
+    ((1, 1, 2), "shipped contraction, Cephes gsr_expf (up to round 3)"),
 ]
 
 

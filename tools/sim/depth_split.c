@@ -28,7 +28,7 @@ void sat_pos(const float* rec, int64_t m, int W, int H, int32_t* out) {
                     float* t = &T[(y - y0) * W + x];
                     if (*t < 1e-3f) continue;
                     const float md2 = gsr_blend_md2((float)x - r[0], (float)y - r[1], r[2], r[3], r[4], r[5]);
-                    float a = r[6] * gsr_expf(-0.5f * md2);
+                    float a = r[6] * gsr_blend_expf(-0.5f * md2);
                     a = a < 0.99f ? a : 0.99f;
                     if (a < 1e-3f) continue;
                     *t *= (1.0f - a);
