@@ -2363,6 +2363,7 @@ __device__ __forceinline__ float fx_band(float band0, uint32_t n, float m) {
 // Pair slot dwords (h = 0 / 1 for the first / second splat of the pair):
 //   [0+h] cx  [2+h] cy  [4+h] a  [6+h] b  [8+h] c  [10+h] e  [12+h] opacity
 //   [14+2h] red  [15+2h] green  [18+h] blue  (fast exp only: [20+h] xs)
+//   [22+h] box descriptor | survivor lane << 24 (0: no splat)
 struct BlendDiag {
     uint64_t loaded = 0, iter = 0, active = 0, taken = 0, slow = 0, zero_taken = 0, no_cand_pairs = 0;
 };
@@ -2411,7 +2412,7 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                                                 uint8_t* __restrict__ flag = nullptr,
                                                 uint32_t* __restrict__ gate = nullptr) {
     static_assert(SPLIT == 0 || !FX, "the depth split runs the exact blend");
-    constexpr int kSlot = FX ? 24 : 20;                     // dwords per pair slot
+    constexpr int kSlot = 24;                               // dwords per pair slot
     const int px = bx + (lane & 7), py = by + (lane >> 3);
     const bool inside = px < cover_w && py < cover_h;
     const float fpx = (float)px, fpy = (float)py;
@@ -2513,13 +2514,17 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
             S[15 + 2 * h] = __uint_as_float(rb.z);
             S[18 + h] = __uint_as_float(rb.w);
             if (FX) S[20 + h] = __uint_as_float(rd.x);
+            // box descriptor (box_mask) | survivor lane << 24: the compositing loop reads
+            // both splats' from the slot instead of walking the survivor mask
+            S[22 + h] = __uint_as_float(dsc | ((uint32_t)lane << 24));
         }
         const uint32_t nsurv = (uint32_t)__popcll(m);
-        if ((nsurv & 1u) && lane < 10) {
-            // odd count: zero the unused second half of the last slot (mask 0 keeps it inert)
-            // second-half dwords of a slot: 1 3 5 7 9 11 13 | 16 17 | 19 (arithmetic, not a
-            // table: a table load would stall the wave on memory once per odd batch)
-            wP[(nsurv >> 1) * kSlot + (lane < 7 ? 2 * lane + 1 : lane + 9 + (lane == 9))] = 0.0f;
+        if ((nsurv & 1u) && lane < 11) {
+            // odd count: zero the unused second half of the last slot (descriptor 0 = empty
+            // box keeps it inert); second-half dwords of a slot: 1 3 5 7 9 11 13 | 16 17 |
+            // 19 | 23 (arithmetic, not a table: a table load would stall the wave on memory
+            // once per odd batch)
+            wP[(nsurv >> 1) * kSlot + (lane < 7 ? 2 * lane + 1 : lane < 10 ? lane + 9 + (lane == 9) : 23)] = 0.0f;
         }
         if (DIAG) dg.loaded += cnt;
         const float xs_l = DIAG ? __uint_as_float(rd.x) : 0.0f;   // diagnostics: xs of record `lane`
@@ -2543,20 +2548,33 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
             f2 TT;
             TT.x = T;
             TT.y = T;
-            for (uint32_t j = 0; mm && alive; ++j) {
-                const int s0 = __builtin_ctzll(mm);
-                mm &= mm - 1;
-                const bool has1 = mm != 0ull;
-                const int s1 = has1 ? __builtin_ctzll(mm) : s0;
-                if (has1) mm &= mm - 1;
-                // one v_readlane per splat; the 64-bit lane masks are rebuilt from the
-                // descriptors by scalar instructions (the VALU is the kernel's bound)
-                const uint64_t box0 = box_mask((uint32_t)__builtin_amdgcn_readlane((int)dsc, s0));
-                const uint64_t box1 = box_mask((uint32_t)__builtin_amdgcn_readlane((int)dsc, s1)) &
-                                      (has1 ? ~0ull : 0ull);
+            const uint32_t npairs = (nsurv + 1u) >> 1;
+            for (uint32_t j = 0; j < npairs && live; ++j) {   // live = 0: block saturated
                 const float4 q0 = wP4[j * (kSlot / 4) + 0], q1 = wP4[j * (kSlot / 4) + 1];
                 const float4 q2 = wP4[j * (kSlot / 4) + 2], q3 = wP4[j * (kSlot / 4) + 3];
                 const float4 q4 = wP4[j * (kSlot / 4) + 4];
+                // the pair's box descriptors from the slot (one v_readfirstlane each); the
+                // 64-bit lane masks are rebuilt from them by scalar instructions.  The
+                // unused half of an odd batch's last slot holds descriptor 0: an empty box.
+                // No survivor-mask walk, no "second splat?" selects: the loop's scalar
+                // work is a co-bound of the VALU work (round 4).
+                uint32_t dd0, dd1;
+                float2 xs;
+                if (FX) {
+                    const float4 q5 = wP4[j * (kSlot / 4) + 5];
+                    xs = make_float2(q5.x, q5.y);
+                    dd0 = __float_as_uint(q5.z);
+                    dd1 = __float_as_uint(q5.w);
+                } else {
+                    const float2 dd = *reinterpret_cast<const float2*>(wP + j * kSlot + 22);
+                    dd0 = __float_as_uint(dd.x);
+                    dd1 = __float_as_uint(dd.y);
+                }
+                const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)dd0);
+                const uint32_t d1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)dd1);
+                const uint64_t box0 = box_mask(d0), box1 = box_mask(d1);
+                const bool has1 = (d1 & 0xffu) != 0u;                        // diagnostics
+                const int s0 = (int)(d0 >> 24), s1 = has1 ? (int)(d1 >> 24) : s0;
                 // render.cu:329-332, same operation order and fused multiply-adds
                 // (gsr_blend_md2), both splats at once; the conic is stored pre-scaled
                 // by -0.5, so this is -0.5f * md2 exactly
@@ -2572,7 +2590,6 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                 // argument against xs — the same decisions
                 bool pass0, pass1;
                 if (FX) {
-                    const float2 xs = *reinterpret_cast<const float2*>(&wP4[j * (kSlot / 4) + 5]);
                     pass0 = !(mdh.x < xs.x);
                     pass1 = !(mdh.y < xs.y);
                 } else {
@@ -2654,8 +2671,8 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                     }
                 }
                 live = live_new;
-                alive = live != 0ull;   // whole block saturated -> stop
             }
+            alive = live != 0ull;
             T = TT.x;
         } else {
             // exact one-splat path (render.cu:329-340 with gsr_blend_expf and selects)
@@ -2745,7 +2762,7 @@ __global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx
                                                  float* __restrict__ out,
                                                  unsigned long long* __restrict__ counters, int bands,
                                                  float band0, BlendSplit sp) {
-    __shared__ float4 sP[32 * (FX ? 24 : 20) / 4];
+    __shared__ float4 sP[32 * 24 / 4];
     const int ntiles = tiles_x * tiles_y;
     const int vb = (int)blockIdx.x;
     if (SPLIT == 1 && vb == 0 && threadIdx.x == 0 && sp.cut.kcut) split_cut_update(sp.cut);
