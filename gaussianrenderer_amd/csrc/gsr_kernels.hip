@@ -403,8 +403,25 @@ __device__ __forceinline__ uint16_t tile_row_spans(float cx, float cy, float a, 
 // dt = t - c; x_t = ((x + m0 dt) + m3 dt^2) + m6 dt^3 (dt^2 = dt dt, dt^3 =
 // dt^2 dt; y, z with m1/m4/m7, m2/m5/m8); temporal factor exp(-(dt/s)^2).
 // One Gaussian i < n; returns the depth key of its item (0xFFFFFFFF: culled or dead).
+// Array k of the scene block for the workgroup's Gaussians: the base (arr + k stride + the
+// workgroup's first index) is uniform, so it is formed by scalar instructions and the load
+// takes it as an SGPR pair beside the lane's 32-bit byte offset (global_load ... saddr).
+// Indexing arr[k * stride + i] with a 64-bit i made every load's address a per-lane
+// 64-bit multiply-add (v_mad_u64_u32) — ~150 VALU per Gaussian for 38 arrays.
+struct SoaWg {
+    const float* base;   // arr + first index of the workgroup (uniform)
+    int64_t stride;
+    uint32_t off;        // lane byte offset: 4 * (i - first index)
+    __device__ __forceinline__ float operator()(int64_t k) const {
+        typedef const __attribute__((address_space(1))) char* gptr;
+        gptr b = (gptr)(base + k * stride);
+        asm("" : "+s"(b));   // keep the base whole (the compiler re-associates it into the lane part)
+        return *(const __attribute__((address_space(1))) float*)(b + off);
+    }
+};
+
 template <bool T4D, bool SH3>
-__device__ __forceinline__ uint32_t preprocess_one(const float* __restrict__ arr, int64_t stride,
+__device__ __forceinline__ uint32_t preprocess_one(const SoaWg& A,
                                                    const Frame& fr, uint4* __restrict__ rec,
                                                    uint64_t* __restrict__ items, uint64_t* __restrict__ rect,
                                                    int packed, uint16_t* __restrict__ spans, float tnow,
@@ -416,18 +433,18 @@ __device__ __forceinline__ uint32_t preprocess_one(const float* __restrict__ arr
     const uint32_t kcut = rs.mode == 1 ? *rs.kcut : far_pass ? *rs.kcut_frame : 0xffffffffu;
     // the frame's threshold, for the far record pass (the near sort copies it too)
     if (rs.mode == 1 && i == 0) *rs.kcut_frame = kcut;
-    float gx = arr[GSR_A_X * stride + i];
-    float gy = arr[GSR_A_Y * stride + i];
-    float gz = arr[GSR_A_Z * stride + i];
+    float gx = A(GSR_A_X);
+    float gy = A(GSR_A_Y);
+    float gz = A(GSR_A_Z);
     float tfac = 1.0f;
     if (T4D) {
-        const float dt = tnow - arr[GSR_A_TCENTER * stride + i];
+        const float dt = tnow - A(GSR_A_TCENTER);
         const float dt2 = dt * dt, dt3 = dt2 * dt;
-        const float* m = arr + GSR_A_MOTION0 * stride + i;
-        gx = ((gx + m[0] * dt) + m[3 * stride] * dt2) + m[6 * stride] * dt3;
-        gy = ((gy + m[1 * stride] * dt) + m[4 * stride] * dt2) + m[7 * stride] * dt3;
-        gz = ((gz + m[2 * stride] * dt) + m[5 * stride] * dt2) + m[8 * stride] * dt3;
-        const float u = dt / arr[GSR_A_TSCALE * stride + i];
+        auto m = [&](int j) { return A(GSR_A_MOTION0 + j); };
+        gx = ((gx + m(0) * dt) + m(3) * dt2) + m(6) * dt3;
+        gy = ((gy + m(1) * dt) + m(4) * dt2) + m(7) * dt3;
+        gz = ((gz + m(2) * dt) + m(5) * dt2) + m(8) * dt3;
+        const float u = dt / A(GSR_A_TSCALE);
         tfac = gsr_expf(-(u * u));
     }
     // Every other load of this Gaussian is issued here, before the cull decides
@@ -438,13 +455,13 @@ __device__ __forceinline__ uint32_t preprocess_one(const float* __restrict__ arr
     constexpr bool kEarlySH = !T4D && !SH3;
     float q_in[4], s_in[3], op_in, sh_in[kEarlySH ? 27 : 1];
 #pragma unroll
-    for (int k = 0; k < 4; k++) q_in[k] = arr[(GSR_A_ROT0 + k) * stride + i];
+    for (int k = 0; k < 4; k++) q_in[k] = A(GSR_A_ROT0 + k);
 #pragma unroll
-    for (int k = 0; k < 3; k++) s_in[k] = arr[(GSR_A_SCALE0 + k) * stride + i];
-    op_in = arr[GSR_A_OPACITY * stride + i];
+    for (int k = 0; k < 3; k++) s_in[k] = A(GSR_A_SCALE0 + k);
+    op_in = A(GSR_A_OPACITY);
     if (kEarlySH) {
 #pragma unroll
-        for (int k = 0; k < 27; k++) sh_in[k] = arr[(GSR_A_SH0 + k) * stride + i];
+        for (int k = 0; k < 27; k++) sh_in[k] = A(GSR_A_SH0 + k);
     }
     uint4* R = rec + 4 * i;
     if (!far_pass) items[i] = ((uint64_t)0xffffffffu << 32) | (uint64_t)(uint32_t)i;
@@ -597,8 +614,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const float* __restrict__ arr
     if (!SH3) {
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) {
-            const float* sh = arr + (GSR_A_SH0 + ch) * stride + i;   // sh[ch], sh[3+ch], ...
-            auto SH = [&](int k) { return kEarlySH ? sh_in[ch + k] : sh[k * stride]; };
+            auto SH = [&](int k) { return kEarlySH ? sh_in[ch + k] : A(GSR_A_SH0 + ch + k); };   // sh[ch], sh[3+ch], ...
             float cc = SH(0) * kShC0;
             cc += kShC1 * z * SH(6);
             cc -= kShC1 * y * SH(3);
@@ -619,8 +635,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const float* __restrict__ arr
                     C3_6 = -0.5900435899266435f;
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) {
-            const float* sh = arr + (GSR_A_SH0 + ch) * stride + i;   // coefficient k at sh[3k * stride]
-            auto S = [&](int k) { return sh[3 * k * stride]; };
+            auto S = [&](int k) { return A(GSR_A_SH0 + ch + 3 * k); };   // coefficient k of channel ch
             float r = kShC0 * S(0);
             r = r - kShC1 * y * S(1) + kShC1 * z * S(2) - kShC1 * x * S(3);
             r = r + C2_0 * xy * S(4) + C2_1 * yz * S(5) + C2_2 * (2.0f * zz - xx - yy) * S(6) +
@@ -661,9 +676,11 @@ __global__ __launch_bounds__(256) void k_preprocess(const float* __restrict__ ar
                                                     int packed, uint16_t* __restrict__ spans,
                                                     float tnow, RecSplit rs) {
     GSR_GEOM_PRIO();
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t i0 = (int64_t)blockIdx.x * 256;
+    const int64_t i = i0 + threadIdx.x;
     if (i >= n) return;
-    (void)preprocess_one<T4D, SH3>(arr, stride, fr, rec, items, rect, packed, spans, tnow, rs, i);
+    const SoaWg A{arr + i0, stride, 4u * threadIdx.x};
+    (void)preprocess_one<T4D, SH3>(A, fr, rec, items, rect, packed, spans, tnow, rs, i);
 }
 
 // Lanes of the wave whose `bits`-bit digit equals this lane's, among the lanes in
@@ -2548,8 +2565,13 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
             f2 TT;
             TT.x = T;
             TT.y = T;
-            const uint32_t npairs = (nsurv + 1u) >> 1;
-            for (uint32_t j = 0; j < npairs && live; ++j) {   // live = 0: block saturated
+            const uint32_t npairs = (uint32_t)__builtin_amdgcn_readfirstlane((int)((nsurv + 1u) >> 1));
+            // one exit test per pair: after the batch's last pair `live` is forced to 0
+            // (the next batch recomputes it from T), so the loop stops when the block
+            // saturates or the batch ends
+            if (npairs != 0u) {
+#pragma unroll
+            for (uint32_t j = 0; j < 32u;) {   // unrolled: the slot offsets are immediates
                 const float4 q0 = wP4[j * (kSlot / 4) + 0], q1 = wP4[j * (kSlot / 4) + 1];
                 const float4 q2 = wP4[j * (kSlot / 4) + 2], q3 = wP4[j * (kSlot / 4) + 3];
                 const float4 q4 = wP4[j * (kSlot / 4) + 4];
@@ -2670,9 +2692,12 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                         suspect |= __ballot(nr) & (live & ~live_new);
                     }
                 }
-                live = live_new;
+                ++j;
+                live = live_new & (j < npairs ? ~0ull : 0ull);
+                if (live == 0ull) break;
             }
-            alive = live != 0ull;
+            }
+            alive = __ballot(!(TT.x < 1e-3f)) != 0ull;   // block not yet saturated
             T = TT.x;
         } else {
             // exact one-splat path (render.cu:329-340 with gsr_blend_expf and selects)
