@@ -294,7 +294,9 @@ __device__ __forceinline__ float block_cut(float xs) { return __builtin_fmaf(-2.
 // S = +inf (infinite margin); NaN anywhere: never culled.
 __device__ __forceinline__ bool block_may_reach(float a, float b, float c, float e, float ih, float iv, float S,
                                                 float dx0, float dx1, float dy0, float dy1, float M, float cut) {
-    if (dx0 <= 0.0f && dx1 >= 0.0f && dy0 <= 0.0f && dy1 >= 0.0f) return true;
+    // centre inside the rectangle: reachable.  Evaluated branch-free with the rest (the
+    // blend's cull runs it on every lane; a branch only adds exec-mask work)
+    const bool inside = (dx0 <= 0.0f) & (dx1 >= 0.0f) & (dy0 <= 0.0f) & (dy1 >= 0.0f);
     const float h = 0.5f * (b + c);
     auto q = [&](float x, float y) { return a * x * x + 2.0f * h * x * y + e * y * y; };
     // The form is convex with its minimum at the splat centre (offset 0,0), which
@@ -311,7 +313,7 @@ __device__ __forceinline__ bool block_may_reach(float a, float b, float c, float
     const bool x_out = dx0 > 0.0f || dx1 < 0.0f, y_out = dy0 > 0.0f || dy1 < 0.0f;
     const float qm = fminf(x_out ? qx : 3.0e38f, y_out ? qy : 3.0e38f);
     const float err = 4e-6f * S * M * M + 1e-3f;
-    return !(qm - err > cut);
+    return inside | !(qm - err > cut);
 }
 
 // Tile row spans (binning path, GSR_TUNE_TILE_SPANS).  A splat's tile rect is the
@@ -2477,13 +2479,17 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
         // pixels not yet saturated at the batch start: T only decreases, so a record
         // whose in-box pixels are all saturated here can never be taken in this batch
         const uint64_t live_b = __ballot(!(T < 1e-3f));
-        bool hit = false, fast = true;
-        uint32_t mlo = 0, mhi = 0, dsc = 0;
-        if ((uint32_t)lane < cnt) {
+        // branch-free over the 64 lanes: nearly every batch has lanes on both sides of each
+        // test, so branches would only add exec-mask work (lanes >= cnt hold stale
+        // registers: their results are discarded through `valid`)
+        bool hit, fast;
+        uint32_t dsc;
+        {
+            const bool valid = (uint32_t)lane < cnt;
             const int xmin = (int)(rc.z & 0xffffu), xmax = (int)(rc.z >> 16);
             const int ymin = (int)(rc.w & 0xffffu), ymax = (int)(rc.w >> 16);
-            hit = !(xmax < bx || xmin > bx + 7 || ymax < by || ymin > by + 7);
-            if (hit) {
+            const bool box_hit = valid & !((xmax < bx) | (xmin > bx + 7) | (ymax < by) | (ymin > by + 7));
+            {
                 const float cx = __uint_as_float(rc.x), cy = __uint_as_float(rc.y);
                 const float a = __uint_as_float(ra.x), b = __uint_as_float(ra.y);
                 const float c = __uint_as_float(ra.z), e = __uint_as_float(ra.w);
@@ -2491,18 +2497,22 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                 const int y0 = max(ymin - by, 0), y1 = min(ymax - by, 7);
                 const float dx0 = (float)(bx + x0) - cx, dx1 = (float)(bx + x1) - cx;
                 const float dy0 = (float)(by + y0) - cy, dy1 = (float)(by + y1) - cy;
-                // bit (row * 8 + col) of the block: pixel inside the AABB
-                const uint32_t rep = ((0xffu >> (7 - (x1 - x0))) << x0) * 0x01010101u;
-                const uint64_t rows = (y1 == 7 ? ~0ull : ((1ull << (8 * (y1 + 1))) - 1ull)) & (~0ull << (8 * y0));
-                mlo = rep & (uint32_t)rows;
-                mhi = rep & (uint32_t)(rows >> 32);
-                // the same box as a descriptor the compositing loop expands on the
-                // scalar unit (box_mask): column byte | (56 - 8 (y1 - y0)) << 8 | 8 y0 << 16
-                dsc = (rep & 0xffu) | ((uint32_t)(56 - 8 * (y1 - y0)) << 8) | ((uint32_t)(8 * y0) << 16);
+                // the box as a descriptor (box_mask: bit row * 8 + col of the block = pixel
+                // inside the AABB), expanded on the scalar unit by the compositing loop:
+                // column byte | (56 - 8 (y1 - y0)) << 8 | 8 y0 << 16
+                // (shift counts masked to the hardware's: only lanes outside the box can
+                // have them out of range, and their results are discarded)
+                const uint32_t colb = (0xffu >> ((uint32_t)(7 - (x1 - x0)) & 31u)) << ((uint32_t)x0 & 31u);
+                const uint32_t rsh = (uint32_t)(56 - 8 * (y1 - y0)) & 63u, lsh = (uint32_t)(8 * y0) & 63u;
+                dsc = colb | (rsh << 8) | (lsh << 16);
+                // the same 64-bit mask here, only for the saturation filter below
+                const uint64_t rows = (~0ull >> rsh) << lsh;
+                const uint32_t rep = __builtin_amdgcn_perm(colb, colb, 0u);   // colb in every byte
+                const uint64_t lrows = rows & live_b;
                 // cull word (cull_word): per-record parts of the block test and the proof
                 const float S = __uint_as_float(rd.w);
                 const float M = fmaxf(fmaxf(fabsf(dx0), fabsf(dx1)), fmaxf(fabsf(dy0), fabsf(dy1)));
-                hit = ((mlo & (uint32_t)live_b) | (mhi & (uint32_t)(live_b >> 32))) != 0u &&
+                hit = box_hit & ((((uint32_t)lrows | (uint32_t)(lrows >> 32)) & rep) != 0u) &
                       block_may_reach(a, b, c, e, __uint_as_float(rd.y), __uint_as_float(rd.z), S, dx0, dx1, dy0,
                                       dy1, M, block_cut(__uint_as_float(rd.x)));
                 fast = S * M * M <= 4e7f;   // per-block part of the fast-path proof
@@ -2704,8 +2714,7 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
             for (uint32_t k = 0; mm && alive; ++k) {
                 const int s = __builtin_ctzll(mm);
                 mm &= mm - 1;
-                const uint64_t box = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mhi, s) << 32) |
-                                     (uint32_t)__builtin_amdgcn_readlane((int)mlo, s);
+                const uint64_t box = box_mask((uint32_t)__builtin_amdgcn_readlane((int)dsc, s));
                 const float* S = wP + (k >> 1) * kSlot;
                 const int h = (int)(k & 1u);
                 const float dx = fpx - S[0 + h], dy = fpy - S[2 + h];
