@@ -2445,7 +2445,8 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
     const float4* wP4 = reinterpret_cast<const float4*>(wP);
     uint64_t suspect = 0;      // FX: pixels whose T decisions the band cannot vouch for
     uint32_t ntk = 0;          // FX: splats this pixel composited so far
-    f2 amax = (f2)0.0f;        // FX: largest alpha it composited (two halves)
+    float amax = 0.0f;         // FX: largest alpha it composited
+    float tprev = 1.0f;        // FX: T before the pixel's latest composite
     uint32_t tcount = 0, thash = 0;   // DIAG take map
     if (SPLIT == 2 && inside) {
         // inside => px < W and py < H (cover_w <= W, cover_h <= H)
@@ -2641,6 +2642,7 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                 if (FX) {
                     t0m = box0 & live & __builtin_amdgcn_ballot_w64(pass0);
                     take0 = __builtin_amdgcn_inverse_ballot_w64(t0m);
+                    tprev = take0 ? TT.x : tprev;
                 } else {
                     take0 = in0 & pass0;
                 }
@@ -2649,6 +2651,7 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                 if (FX) {
                     t1m = box1 & __builtin_amdgcn_ballot_w64(!(TT.y < 1e-3f)) & __builtin_amdgcn_ballot_w64(pass1);
                     take1 = __builtin_amdgcn_inverse_ballot_w64(t1m);
+                    tprev = take1 ? TT.y : tprev;
                 } else {
                     take1 = in1 & !(TT.y < 1e-3f) & pass1;
                 }
@@ -2686,21 +2689,10 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                     // n += take0 + take1 as two v_addc (the take masks as carry-in);
                     // alpha >= +0 here, so its float maximum is the u32 maximum
                     ntk = count_lanes2(ntk, t0m, t1m);
-                    amax.x = __uint_as_float(max(__float_as_uint(amax.x), __float_as_uint(AA.x)));
-                    amax.y = __uint_as_float(max(__float_as_uint(amax.y), __float_as_uint(AA.y)));
-                    if (live_new != live) {
-                        // lanes whose T first dropped below 1e-3 in this iteration: the
-                        // value before the drop and the value after (TT.x) must lie
-                        // outside the band.  Before the drop: TT.y when the drop came at
-                        // TT.x; T0 = the iteration's starting T when it came at TT.y,
-                        // where T0 < hi is tested as TT.y < hi (1 - a0), padded by 2^-22
-                        // for the two roundings of TT.y = T0 (1 - a0).
-                        const float B = fx_band(band0, ntk, fmaxf(amax.x, amax.y));
-                        const float hi = 1e-3f * (1.0f + B), lo = 1e-3f * (1.0f - B);
-                        const float lim = TT.y < 1e-3f ? hi * (1.0f - AA.x) * (1.0f + 0x1p-22f) : hi;
-                        const bool nr = TT.y < lim || !(TT.x < lo);
-                        suspect |= __ballot(nr) & (live & ~live_new);
-                    }
+                    amax = __uint_as_float(max(max(__float_as_uint(amax), __float_as_uint(AA.x)),
+                                               __float_as_uint(AA.y)));
+                    // (the band checks of each pixel's T decisions run once, at the block's
+                    // end, on the latched T before its last composite: no per-iteration branch)
                 }
                 ++j;
                 live = live_new & (j < npairs ? ~0ull : 0ull);
@@ -2745,9 +2737,17 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
         }
     }
     if (FX) {
-        // pixels that never dropped below 1e-3 but end within the band above it
-        const float B = fx_band(band0, ntk, fmaxf(amax.x, amax.y));
-        suspect |= __ballot(!(T < 1e-3f) && T < 1e-3f * (1.0f + B));
+        // The band checks, once per pixel.  A pixel's n, m and tprev stop changing once
+        // its T drops below 1e-3 (nothing is composited after), so at the end:
+        //  - saturated: its decisive step took T from tprev (>= 1e-3) to T (< 1e-3); the
+        //    exact chain takes the same branches if both lie outside the band (every
+        //    earlier T is >= tprev: T never increases);
+        //  - unsaturated: T must lie above the band.
+        // Pixels that started saturated (outside the cover or `only`) composited nothing.
+        const float B = fx_band(band0, ntk, amax);
+        const float hi = 1e-3f * (1.0f + B), lo = 1e-3f * (1.0f - B);
+        const bool nr = (T < 1e-3f) ? (ntk != 0u) & ((tprev < hi) | !(T < lo)) : (T < hi);
+        suspect |= __ballot(nr);
     }
     if (SPLIT == 1) {
         const bool unsat = __ballot(!(T < 1e-3f)) != 0ull;
@@ -2789,7 +2789,7 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
 // publishes the count of blocks phase A left unsaturated (sp.host_st), and every
 // workgroup returns at once when that count is 0 or its own block is saturated.
 template <bool DIAG, bool STAMPS, bool FX, int SPLIT>
-__global__ __launch_bounds__(64) void k_blend_w(const uint32_t* __restrict__ idx,
+__global__ __launch_bounds__(64, 8) void k_blend_w(const uint32_t* __restrict__ idx,
                                                  const uint2* __restrict__ ranges,
                                                  const uint4* __restrict__ rec, int tiles_x, int tiles_y,
                                                  int W, int H, int cover_w, int cover_h,

@@ -379,7 +379,7 @@ struct gsr_context {
     uint32_t* cbins = nullptr;       // binning: column counts per chunk (256 x chunks)
     int64_t cbins_cap = 0;
     bool last_binned = false;        // the last sorted frame took the binning path
-    int blend_exp = 0;               // blend: 0 = gsr_blend_expf (bit-exact); 1 = fast exp with exact alpha
+    int blend_exp = 1;               // blend: 1 = fast exp, exact decisions (default); 0 = gsr_blend_expf (bit-exact)
                                      // tests and guarded T tests (re-blends what it cannot vouch for)
     int depth_split = 2;             // GSR_TUNE_DEPTH_SPLIT: 0 off, 1 on, 2 on above kLargeScene Gaussians
     int split_pm = 250;              // split point: phase A bins the nearest split_pm / 1000 of the depth order
@@ -476,10 +476,11 @@ constexpr int kSplitMinPm = 20;       // smallest split point (per mille)
 constexpr int kSplitRetry = 256;      // frames with the split turned off before it is tried again
 constexpr int kSplitRetryMax = 1 << 14;
 
-// The depth split applies to this context's frames of n Gaussians (binning path and the
-// exact blend; gsr_render / gsr_render_path decide it per frame, the stage API never).
+// The depth split applies to this context's frames of n Gaussians (binning path;
+// gsr_render / gsr_render_path decide it per frame, the stage API never).  Its two blend
+// phases always run the exact blend, whatever GSR_TUNE_BLEND_EXP says for other frames.
 bool split_enabled(const gsr_context* c, int64_t n) {
-    return n > 0 && c->blend_exp == 0 && c->blend_variant != 3 && c->split_pm < 1000 &&
+    return n > 0 && c->blend_variant != 3 && c->split_pm < 1000 &&
            (c->depth_split == 1 || (c->depth_split == 2 && n > kLargeScene));
 }
 
@@ -815,6 +816,7 @@ int ceil_log2(int64_t v) {
 extern "C" gsr_context* gsr_create(void) {
     gsr_context* c = new gsr_context();
     const char* e = std::getenv("GSR_BLEND_EXP");
+    if (e && e[0] == '0') c->blend_exp = 0;   // the exact blend (bit-identical to the oracle)
     if (e && e[0] == '1') c->blend_exp = 1;
     return c;
 }
@@ -1230,13 +1232,13 @@ static int blend_locked(gsr_context* c, float* d_out) {
         // on the device when phase A saturated every block
         const uint32_t n = (uint32_t)c->n;
         const bool key = c->frame_key;
-        if (key && (c->blend_exp != 0 || c->blend_variant == 3))
+        if (key && c->blend_variant == 3)
             return set_err(GSR_E_ARG, "gsr_blend: blend knobs changed after a depth-split frame; render it again");
         const gsr::RowSplit ra{key ? 1 : 0, c->split_na, nullptr};
-        if (c->split_rebin && c->blend_exp == 0 && c->blend_variant != 3) {
+        if (c->split_rebin && c->blend_variant != 3) {
             if (int rc = bin_locked(c, 0, key ? n : c->split_na, 1, false, &ra)) return rc;
         }
-        if (c->blend_exp == 0 && c->blend_variant != 3) {
+        if (c->blend_variant != 3) {
             // phase A; its workgroup 0 also sets the next frame's threshold from the near
             // depth order (key mode: the near part; count mode: the whole order)
             const bool spec = c->frame_spec;

@@ -290,8 +290,8 @@ int gsr_blend_take_map(gsr_context* ctx, uint64_t* out, int64_t n);
  * workgroup and LDS-capped occupancy were measured slower and removed). */
 int gsr_set_blend_variant(gsr_context* ctx, int variant);
 /* Tuning knobs for A/B experiments (all settings give bit-identical output, except
- * GSR_TUNE_BLEND_EXP 1, which is within the parity gate and composites the same
- * splats on every pixel). */
+ * GSR_TUNE_BLEND_EXP: its modes composite the same splats on every pixel and differ in
+ * the colours by < 1e-6). */
 enum {
     GSR_TUNE_BLEND_SCHEDULE = 0,     /* as gsr_set_blend_variant */
     GSR_TUNE_TILE_SORT_ITEMS = 1,    /* tile sort items per thread: 8 | 16 (default 16) */
@@ -334,12 +334,15 @@ enum {
                                         the default.  Same order, same image */
     GSR_TUNE_RANK_ATOMIC_ACTIVE = 21, /* read-only: 1 if the atomic ranks are in use (knob 20 at 1 and the
                                         self-check passed), 0 if the kernels rank with ballots */
-    GSR_TUNE_BLEND_EXP = 22,         /* blend exp: 0 (default) = gsr_blend_expf throughout (bit-exact with the
-                                        oracle).  1 (environment GSR_BLEND_EXP=1 selects it) = hardware
-                                        exp for alpha, with the alpha test exact on the exp argument and
-                                        the transmittance test guarded by a proven band; suspect pixels
-                                        are blended again exactly.  Images within 1e-6 of the exact
-                                        blend, identical take map; measured slower on config 2.
+    GSR_TUNE_BLEND_EXP = 22,         /* blend exp.  1 (default since round 4) = hardware exp for
+                                        alpha, with the alpha test exact on the exp argument and the
+                                        transmittance test guarded by a proven band; pixels whose T
+                                        decision the band cannot vouch for are blended again exactly.
+                                        Every pixel composites exactly the oracle's splats (take map
+                                        identical); colours within 1e-6 of the exact blend (measured
+                                        <= 4e-7).  0 (environment GSR_BLEND_EXP=0 selects it) =
+                                        gsr_blend_expf throughout: bit-exact with the oracle.  Depth-
+                                        split frames (GSR_TUNE_DEPTH_SPLIT) always run the exact blend.
                                         2 = test hook: 1 with a 100 % guard band, so every block
                                         in which a pixel saturates is blended again exactly. */
     GSR_TUNE_DEPTH_SPLIT = 23,       /* binning path, exact blend, gsr_render / gsr_render_path: 1 = bin

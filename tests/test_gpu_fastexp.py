@@ -23,6 +23,8 @@ import numpy as np
 import pytest
 
 from conftest import KNOB_BLEND_EXP, assert_frames, scene_soa
+
+KNOB_DEPTH_SPLIT = 23
 from test_gpu_parity import CAMS, cam_for, render_gpu
 
 pytestmark = pytest.mark.gpu
@@ -92,6 +94,10 @@ def take_parity(gpu, torch, scene, cam, W, H, want, takes_want, mode=None, rende
     r = renderer or gpu.Renderer()
     if mode is not None:
         r.set_tuning(KNOB_BLEND_EXP, mode)
+    if r.get_tuning(KNOB_BLEND_EXP) != 0:
+        # depth-split frames (scenes above 1.5M Gaussians) run the exact blend whatever the
+        # mode (tests/test_gpu_depth_split.py); here every frame must be the fast blend's
+        r.set_tuning(KNOB_DEPTH_SPLIT, 0)
     img, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r, **kw)
     r.set_diagnostics(True)
     img_d, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r, **kw)
