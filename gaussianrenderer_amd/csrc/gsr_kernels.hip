@@ -2652,7 +2652,10 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                     take0 = in0 & pass0;
                 }
                 AA.x = take0 ? al0 : 0.0f;
-                TT.y = TT.x * (1.0f - AA.x);
+                // T (1 - alpha) (render.cu:339); the fast blend folds it into one fma, T - T alpha
+                // with one rounding; the band's 4 2^-24 per composite budgets 2 roundings per
+                // chain, so 1 here and 2 in the exact chain stay inside it
+                TT.y = FX ? __builtin_fmaf(-TT.x, AA.x, TT.x) : TT.x * (1.0f - AA.x);
                 if (FX) {
                     t1m = box1 & __builtin_amdgcn_ballot_w64(!(TT.y < 1e-3f)) & __builtin_amdgcn_ballot_w64(pass1);
                     take1 = __builtin_amdgcn_inverse_ballot_w64(t1m);
@@ -2688,7 +2691,7 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                     tcount += (take0 ? 1u : 0u) + (take1 ? 1u : 0u);
                     thash += (take0 ? take_mix(g0) : 0u) + (take1 ? take_mix(g1) : 0u);
                 }
-                TT.x = TT.y * (1.0f - AA.y);
+                TT.x = FX ? __builtin_fmaf(-TT.y, AA.y, TT.y) : TT.y * (1.0f - AA.y);
                 const uint64_t live_new = __ballot(!(TT.x < 1e-3f));
                 if (FX) {
                     // n += take0 + take1 as two v_addc (the take masks as carry-in);
