@@ -2338,6 +2338,10 @@ __device__ __forceinline__ f2 fast_expf_x2(f2 x) {
 // (n = composited splats, bounded by the wave's splat-iterations) up to and including
 // the step where it first drops below 1e-3 ("Fast exp"):
 // kFxBand0 and kFxBandStep are those terms with 2 % headroom.
+// Set in the batch's last pair's second box descriptor (bit 30: above the survivor lane
+// at bits 24-29; box_mask reads bits 0-21 only).
+constexpr uint32_t kLastPair = 0x40000000u;
+
 constexpr float kFxEps3 = 6.6e-7f;
 constexpr float kFxEps2 = 4.8e-7f;
 constexpr float kFxEps1 = 4.8e-7f;
@@ -2527,6 +2531,7 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
             }
         }
         const uint64_t m = __ballot(hit);
+        const uint32_t nsurv = (uint32_t)__popcll(m);
         const bool all_fast = __ballot(hit & !fast) == 0ull;
         if (FX && !all_fast) return ~0ull;   // exact re-blend of the whole block
         if (hit) {
@@ -2548,16 +2553,18 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
             S[18 + h] = __uint_as_float(rb.w);
             if (FX) S[20 + h] = __uint_as_float(rd.x);
             // box descriptor (box_mask) | survivor lane << 24: the compositing loop reads
-            // both splats' from the slot instead of walking the survivor mask
-            S[22 + h] = __uint_as_float(dsc | ((uint32_t)lane << 24));
+            // both splats' from the slot instead of walking the survivor mask.  The last
+            // pair's second descriptor carries kLastPair (below)
+            S[22 + h] = __uint_as_float(dsc | ((uint32_t)lane << 24) | (k + 1u == nsurv && h ? kLastPair : 0u));
         }
-        const uint32_t nsurv = (uint32_t)__popcll(m);
         if ((nsurv & 1u) && lane < 11) {
             // odd count: zero the unused second half of the last slot (descriptor 0 = empty
             // box keeps it inert); second-half dwords of a slot: 1 3 5 7 9 11 13 | 16 17 |
             // 19 | 23 (arithmetic, not a table: a table load would stall the wave on memory
             // once per odd batch)
-            wP[(nsurv >> 1) * kSlot + (lane < 7 ? 2 * lane + 1 : lane < 10 ? lane + 9 + (lane == 9) : 23)] = 0.0f;
+            // (dword 23, the pair's second descriptor: kLastPair alone, an empty box)
+            wP[(nsurv >> 1) * kSlot + (lane < 7 ? 2 * lane + 1 : lane < 10 ? lane + 9 + (lane == 9) : 23)] =
+                lane == 10 ? __uint_as_float(kLastPair) : 0.0f;
         }
         if (DIAG) dg.loaded += cnt;
         const float xs_l = DIAG ? __uint_as_float(rd.x) : 0.0f;   // diagnostics: xs of record `lane`
@@ -2582,8 +2589,8 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
             TT.x = T;
             TT.y = T;
             const uint32_t npairs = (uint32_t)__builtin_amdgcn_readfirstlane((int)((nsurv + 1u) >> 1));
-            // one exit test per pair: after the batch's last pair `live` is forced to 0
-            // (the next batch recomputes it from T), so the loop stops when the block
+            // one exit test per pair: after the batch's last pair `live` is 0 (the threshold
+            // above; the next batch recomputes it from T), so the loop stops when the block
             // saturates or the batch ends
             if (npairs != 0u) {
 #pragma unroll
@@ -2612,7 +2619,7 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                 const uint32_t d1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)dd1);
                 const uint64_t box0 = box_mask(d0), box1 = box_mask(d1);
                 const bool has1 = (d1 & 0xffu) != 0u;                        // diagnostics
-                const int s0 = (int)(d0 >> 24), s1 = has1 ? (int)(d1 >> 24) : s0;
+                const int s0 = (int)(d0 >> 24), s1 = has1 ? (int)((d1 >> 24) & 63u) : s0;
                 // render.cu:329-332, same operation order and fused multiply-adds
                 // (gsr_blend_md2), both splats at once; the conic is stored pre-scaled
                 // by -0.5, so this is -0.5f * md2 exactly
@@ -2692,7 +2699,11 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                     thash += (take0 ? take_mix(g0) : 0u) + (take1 ? take_mix(g1) : 0u);
                 }
                 TT.x = FX ? __builtin_fmaf(-TT.y, AA.y, TT.y) : TT.y * (1.0f - AA.y);
-                const uint64_t live_new = __ballot(!(TT.x < 1e-3f));
+                // render.cu:328 for the next pair; after the batch's last pair the threshold
+                // is ~3.4e35 (1e-3's bits | kLastPair), so the ballot is 0 and the loop ends:
+                // the batch-end test costs two scalar instructions, not a compare of j
+                const float thr = __uint_as_float(0x3a83126fu | (d1 & kLastPair));
+                const uint64_t live_new = __ballot(!(TT.x < thr));
                 if (FX) {
                     // n += take0 + take1 as two v_addc (the take masks as carry-in);
                     // alpha >= +0 here, so its float maximum is the u32 maximum
@@ -2703,7 +2714,7 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                     // end, on the latched T before its last composite: no per-iteration branch)
                 }
                 ++j;
-                live = live_new & (j < npairs ? ~0ull : 0ull);
+                live = live_new;
                 if (live == 0ull) break;
             }
             }
