@@ -111,7 +111,8 @@ struct BlendSplit {
     Stats* host_st;                   // phase B publishes the count here (nullable)
     Stats* spec_host;                 // phase A with no phase B queued: an unsaturated block sets
                                       // spec_host->spec_miss (nullable)
-    SplitCut cut;                     // phase A: the next frame's threshold
+    SplitCut cut;                     // phase A: the next frame's threshold; phase B: nnear and na only
+                                      // (a near part short of the split point is tagged unmeasured)
     uint32_t pm;                      // phase B publishes it with the count (Stats::split_pm: the split
                                       // point | the controller's epoch << 16)
     uint32_t* fstatus;                // speculative phase A: an unsaturated block ors

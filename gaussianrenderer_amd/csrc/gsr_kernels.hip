@@ -2822,8 +2822,14 @@ __global__ __launch_bounds__(64, 8) void k_blend_w(const uint32_t* __restrict__ 
     if (SPLIT == 2) {
         const uint32_t g = *sp.gate;   // uniform
         if (vb == 0 && threadIdx.x == 0 && sp.host_st) {
+            // a frame whose near part fell short of the split point by more than 1/16 (its
+            // threshold was extrapolated from a smaller point, split_cut_update) says
+            // nothing about that point: its tag's low half 0xffff matches no split point
+            // (<= 1000), so the controller waits for a frame with a measured threshold
+            // rather than grow twice on one miss
+            const bool short_near = sp.cut.nnear && *sp.cut.nnear < sp.cut.na - sp.cut.na / 16u;
             sp.host_st->split_unsat = g;
-            sp.host_st->split_pm = sp.pm;
+            sp.host_st->split_pm = short_near ? (sp.pm | 0xffffu) : sp.pm;
             __threadfence_system();
         }
         if (g == 0u) return;

@@ -1260,7 +1260,9 @@ static int blend_locked(gsr_context* c, float* d_out) {
                 }
                 if (int rc = bin_locked(c, key ? 0 : c->split_na, key ? n : n - c->split_na, 2, false, &rb, key))
                     return rc;
-                gsr::BlendSplit b{2, c->tbuf, c->bflag, c->gate, c->hstats_dev, nullptr, {}, split_tag(c),
+                // (cut: only the near count and the split point, for the published tag)
+                const gsr::SplitCut bcut{nullptr, nullptr, nullptr, key ? c->nlive : nullptr, n, c->split_na, nullptr};
+                gsr::BlendSplit b{2, c->tbuf, c->bflag, c->gate, c->hstats_dev, nullptr, bcut, split_tag(c),
                                   nullptr};
                 HIP_TRY(gsr::launch_blend(pair_vals(c, c->pair_buf), c->ranges, c->rec, c->fr, d_out,
                                           c->diagnostics ? c->consumed : nullptr, false, c->blend_band_tiles, 0,

@@ -10,6 +10,8 @@ corrected read traffic is reported next to the raw value: x2 for streaming
 kernels, x1 for the blend (fetch_factor).
 
     python tools/summarize_prof.py gpurun_out/prof > profiles/r01_rocprof_summary.txt
+    python tools/summarize_prof.py gpurun_out/prof --pmc-json gpurun_out/pmc_TAG.json
+        (the PMC columns from the --json output, once the csv have been slimmed away)
 """
 import collections
 import csv
@@ -37,9 +39,14 @@ def short(name: str) -> str:
     return name.split("(")[0][:60]
 
 
-def main(d):
+def main(d, pmc_json=None):
     stats = list(csv.DictReader(open(os.path.join(d, "kt", "kt_kernel_stats.csv"))))
     pmc = {}
+    if pmc_json:
+        import json
+        ks = json.load(open(pmc_json))["kernels"]
+        pmc["FETCH_SIZE"] = {k: v["fetch_bytes_raw"] for k, v in ks.items() if "fetch_bytes_raw" in v}
+        pmc["WRITE_SIZE"] = {k: v["write_bytes"] for k, v in ks.items() if "write_bytes" in v}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         p = os.path.join(d, f"pmc_{c}", "pmc_counter_collection.csv")
         if not os.path.exists(p):
@@ -98,5 +105,7 @@ def write_json(d, out, config, source):
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[2] == "--json":
         write_json(sys.argv[1], sys.argv[3], int(sys.argv[4]), sys.argv[5])
+    elif len(sys.argv) > 3 and sys.argv[2] == "--pmc-json":
+        main(sys.argv[1], sys.argv[3])
     else:
         main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof")
