@@ -2334,20 +2334,22 @@ __device__ __forceinline__ f2 fast_expf_x2(f2 x) {
 //   kFxEps2  alpha > 0.5            (x >= -0.70)
 //   kFxEps1  alpha > 0.9            (x >= -0.11)
 // The transmittance of a pixel then differs from the exact chain's by a relative
-//   rho <= 207.1 kFxEps1 + 6.9078 max(3.909 kFxEps2, 1.4427 kFxEps3) + 4 2^-24 n
+//   rho <= 207.1 kFxEps1 + 6.9078 max(3.909 kFxEps2, 1.4427 kFxEps3) + 3 2^-24 n
 // (n = composited splats, bounded by the wave's splat-iterations) up to and including
 // the step where it first drops below 1e-3 ("Fast exp"):
-// kFxBand0 and kFxBandStep are those terms with 2 % headroom.
-// Set in the batch's last pair's second box descriptor (bit 30: above the survivor lane
-// at bits 24-29; box_mask reads bits 0-21 only).
-constexpr uint32_t kLastPair = 0x40000000u;
-
+// kFxBand0 and kFxBandStep are those terms with 2 % headroom.  The n term counts the
+// roundings per composite: the exact chain's two (1 - alpha, then the product) and the
+// fast chain's one (T - T alpha as one fma).
 constexpr float kFxEps3 = 6.6e-7f;
 constexpr float kFxEps2 = 4.8e-7f;
 constexpr float kFxEps1 = 4.8e-7f;
 constexpr float kFxBand0 = 1.02f * (207.1f * kFxEps1 + 6.9078f * (3.909f * kFxEps2 > 1.4427f * kFxEps3
                                                                   ? 3.909f * kFxEps2 : 1.4427f * kFxEps3));
-constexpr float kFxBandStep = 1.02f * 4.0f * 0x1p-24f;
+constexpr float kFxBandStep = 1.02f * 3.0f * 0x1p-24f;
+
+// Set in the batch's last pair's second box descriptor (bit 30: above the survivor lane
+// at bits 24-29; box_mask reads bits 0-21 only).
+constexpr uint32_t kLastPair = 0x40000000u;
 
 // n + (lane's bit of ma) + (lane's bit of mb): the wave masks are the carry-ins of two
 // v_addc_co_u32 (one VALU each; counting booleans compiles to selects and an add).
@@ -2660,8 +2662,8 @@ __device__ __forceinline__ uint64_t blend_block(const uint32_t* __restrict__ idx
                 }
                 AA.x = take0 ? al0 : 0.0f;
                 // T (1 - alpha) (render.cu:339); the fast blend folds it into one fma, T - T alpha
-                // with one rounding; the band's 4 2^-24 per composite budgets 2 roundings per
-                // chain, so 1 here and 2 in the exact chain stay inside it
+                // with one rounding (kFxBandStep: 3 2^-24 per composite, 1 here and 2 in the
+                // exact chain)
                 TT.y = FX ? __builtin_fmaf(-TT.x, AA.x, TT.x) : TT.x * (1.0f - AA.x);
                 if (FX) {
                     t1m = box1 & __builtin_amdgcn_ballot_w64(!(TT.y < 1e-3f)) & __builtin_amdgcn_ballot_w64(pass1);

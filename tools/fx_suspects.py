@@ -40,6 +40,9 @@ def main():
     lib = os.environ.get("GSR_LIBRARY", "default")
     for rk in a.ranks:
         cam = multi.orbit_camera(rk, W, H)
+        # one plain frame first: a renderer's first diagnostics frame reports no counters
+        r.render(scene, cam, W, H, out.data_ptr(), stream=stream)
+        r.sync()
         r.set_diagnostics(True)
         r.render(scene, cam, W, H, out.data_ptr(), stream=stream)
         r.sync()
