@@ -50,7 +50,7 @@ def main():
         c = r.blend_counters_ex()
         r.set_diagnostics(False)
         print(os.path.basename(lib), f"config {a.config} camera of rank {rk}:",
-              {k: c[k] for k in ("reblended_blocks", "suspect_pixels", "slow_path_iters",
+              {k: c[k] for k in ("reblended_blocks", "suspect_pixels", "slow_path_iters", "zero_taken_iters", "no_candidate_pair_iters",
                                  "wave_splat_iters", "taken_lanes")}, flush=True)
 
 
