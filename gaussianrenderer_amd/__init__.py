@@ -536,9 +536,9 @@ def exp_probe(x_lo: float, x_hi: float, x_big: float) -> tuple[int, int, float, 
     """gsr_exp_probe: (monotonicity violations of gsr_blend_expf, packed-loop exp
     mismatches, max relative fast-exp error, the same over x >= x_big) over every float
     in [x_lo, x_hi), on the GPU."""
-    v, ea, eb = (c_int64 * 2)(0, 0), ctypes.c_float(0), ctypes.c_float(0)
-    check(lib().gsr_exp_probe(x_lo, x_hi, x_big, v, byref(ea), byref(eb)), "gsr_exp_probe")
-    return int(v[0]), int(v[1]), float(ea.value), float(eb.value)
+    v, pk, ea, eb = c_int64(0), c_int64(0), ctypes.c_float(0), ctypes.c_float(0)
+    check(lib().gsr_exp_probe2(x_lo, x_hi, x_big, byref(v), byref(pk), byref(ea), byref(eb)), "gsr_exp_probe2")
+    return int(v.value), int(pk.value), float(ea.value), float(eb.value)
 
 
 def alpha_cut_probe(op: np.ndarray) -> np.ndarray:

@@ -165,6 +165,7 @@ SIGNATURES = [
     ("gsr_device_available", c_int, []),
     ("gsr_math_probe", c_int, [c_void_p, c_int, c_void_p]),
     ("gsr_exp_probe", c_int, [c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
+    ("gsr_exp_probe2", c_int, [c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gsr_alpha_cut_probe", c_int, [c_void_p, c_int, c_void_p]),
     ("gsr_rank_order_check", c_int, [POINTER(c_int64), POINTER(c_int64)]),
 ]

@@ -1485,9 +1485,15 @@ extern "C" int gsr_render_path_status(gsr_context* c, const void* scene, int lay
         if (wait_events && wait_events[i]) HIP_TRY(hipStreamWaitEvent(ls, static_cast<hipEvent_t>(wait_events[i]), 0));
         if (times) lc->time = times[i];
         else lc->time = t_saved;
+        // the frame's validity word is the lane's only while its frame is queued: the guard
+        // clears it on every exit, so a later gsr_render on this context (or an erroring
+        // frame's early return) never writes through a pointer the caller may have freed
+        struct StatusScope {
+            gsr_context* lc;
+            ~StatusScope() { lc->fstatus = nullptr; }
+        } status_scope{lc};
         lc->fstatus = d_status ? d_status[i] : nullptr;
         const int rc = render_one_locked(lc, scene, layout, n, &cams[i], W, H, nx, ny, ws, hs, k, d_outs[i], ls);
-        lc->fstatus = nullptr;
         if (rc == GSR_E_OVERFLOW) result = GSR_E_OVERFLOW;
         else if (rc != GSR_OK) return rc;
         if (record[i]) HIP_TRY(hipEventRecord(c->alias_evs[lane], ls));
@@ -1979,9 +1985,9 @@ extern "C" int gsr_math_probe(const float* host_in, int n, float* host_out) {
     return GSR_OK;
 }
 
-extern "C" int gsr_exp_probe(float x_lo, float x_hi, float x_big, int64_t* violations, float* err_all,
-                             float* err_big) {
-    if (!violations || !err_all || !err_big || !(x_lo < x_hi))
+extern "C" int gsr_exp_probe2(float x_lo, float x_hi, float x_big, int64_t* violations,
+                              int64_t* packed_mismatches, float* err_all, float* err_big) {
+    if (!violations || !packed_mismatches || !err_all || !err_big || !(x_lo < x_hi))
         return set_err(GSR_E_ARG, "gsr_exp_probe: bad argument");
     unsigned long long* dv = nullptr;
     uint32_t* de = nullptr;
@@ -1996,11 +2002,19 @@ extern "C" int gsr_exp_probe(float x_lo, float x_hi, float x_big, int64_t* viola
     HIP_TRY(hipMemcpy(e, de, sizeof e, hipMemcpyDeviceToHost));
     (void)hipFree(dv);
     (void)hipFree(de);
-    violations[0] = (int64_t)v[0];
-    violations[1] = (int64_t)v[1];
+    *violations = (int64_t)v[0];
+    *packed_mismatches = (int64_t)v[1];
     *err_all = gsr_bits_to_float(e[0]);
     *err_big = gsr_bits_to_float(e[1]);
     return GSR_OK;
+}
+
+// The round-3 signature: one int64 behind `violations` (the packed-loop count is
+// gsr_exp_probe2's).
+extern "C" int gsr_exp_probe(float x_lo, float x_hi, float x_big, int64_t* violations, float* err_all,
+                             float* err_big) {
+    int64_t packed = 0;
+    return gsr_exp_probe2(x_lo, x_hi, x_big, violations, &packed, err_all, err_big);
 }
 
 extern "C" int gsr_alpha_cut_probe(const float* host_op, int n, float* host_out) {

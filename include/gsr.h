@@ -453,13 +453,17 @@ void gsr_camera_intrinsics(const gsr_camera* cam, float* fx, float* fy);
  * bit for bit. */
 int gsr_math_probe(const float* host_in, int n, float* host_out);
 /* Exhaustive device checks of the blend's exp, over every float x in [x_lo, x_hi):
- * violations[0] = the number of x with gsr_blend_expf(x) > gsr_blend_expf(next x)
+ * *violations = the number of x with gsr_blend_expf(x) > gsr_blend_expf(next x)
  * (0: the exact exp is monotone, so the alpha test is a threshold on -md2/2);
- * violations[1] = the number of x in [-2e7, 5] (and of -x there) where the packed
- * compositing loop's exp differs from gsr_blend_expf; *err_all / *err_big = the
- * largest |fast exp / gsr_blend_expf - 1| (GSR_TUNE_BLEND_EXP 1) over the range /
- * over x >= x_big (rounded up).  violations points at two int64. */
+ * *err_all / *err_big = the largest |fast exp / gsr_blend_expf - 1|
+ * (GSR_TUNE_BLEND_EXP 1) over the range / over x >= x_big (rounded up).
+ * violations points at ONE int64 (the round-3 signature, unchanged). */
 int gsr_exp_probe(float x_lo, float x_hi, float x_big, int64_t* violations, float* err_all, float* err_big);
+/* gsr_exp_probe plus *packed_mismatches = the number of x in [-2e7, 5] (and of -x
+ * there) where the packed compositing loop's exp differs from gsr_blend_expf
+ * (0: the packed and scalar exps agree bit for bit).  Each pointer names one value. */
+int gsr_exp_probe2(float x_lo, float x_hi, float x_big, int64_t* violations, int64_t* packed_mismatches,
+                   float* err_all, float* err_big);
 /* gsr_alpha_take_min_x (gsr_detmath.h) evaluated on the device for n opacities. */
 int gsr_alpha_cut_probe(const float* host_op, int n, float* host_out);
 

@@ -1,4 +1,4 @@
-"""The fast-exp blend (GSR_TUNE_BLEND_EXP 1, opt-in) against the oracle.
+"""The fast-exp blend (GSR_TUNE_BLEND_EXP 1, the default since round 4) against the oracle.
 
 The exact blend evaluates the reference's expf (render.cu:333) as gsr_blend_expf, a
 15-VALU polynomial per pixel-splat pair, and is bit-identical to the oracle.  The

@@ -100,6 +100,7 @@ def _validity_worker(rank, world, port, ply, W, H, q):
     far_soa[2] = np.linspace(-90.0, 1.0, soa.shape[1], dtype=np.float32)   # keys need all 4 passes
     far = gsr.Scene.from_soa(far_soa)
     r = gsr.Renderer()
+    r.set_tuning(gsr.TUNE_BLEND_EXP, 0)      # exact blend: the gathered frames are checked bit for bit
     r.set_frames_in_flight(2)
     cam = multi.orbit_camera(rank, W, H)
     got, measured = [], [False]
@@ -174,7 +175,7 @@ def test_two_rank_validity_words_resend_flagged_chunk(gpu, orc, tmp_path):
                 continue
             assert (words == 0).all(), (cid, r, words)
             for row in frames[r]:
-                assert_frames(row[:npx], want[(r, int(r == 1 and cid == 2))])
+                assert_frames(row[:npx], want[(r, int(r == 1 and cid == 2))], exact=True)
 
 
 def _nccl_worker(port, ply, W, H, steps, chunk, q):

@@ -1,10 +1,11 @@
 """GPU parity: the HIP pipeline (through the C ABI) against the CPU oracle on
 the same seeded inputs.  Integer / index outputs (AABBs, pixel centres, depth
 keys, sort orders, tile ranges) must be bit-exact; the image gate is the
-north-star per-pixel L-inf <= 1e-4.  The default blend is the exact one
-(GSR_TUNE_BLEND_EXP 0, include/gsr.h) and is asserted bit-exact; the opt-in
-fast-exp blend must composite the same splats on every pixel (take maps,
-tests/test_gpu_fastexp.py)."""
+north-star per-pixel L-inf <= 1e-4.  The default blend (since round 4) is the
+fast-exp one (GSR_TUNE_BLEND_EXP 1, include/gsr.h): it must composite exactly the
+oracle's splats on every pixel (take maps, tests/test_gpu_fastexp.py) and stay within
+FX_TOL (1e-5) of the oracle; the exact blend (GSR_TUNE_BLEND_EXP 0, environment
+GSR_BLEND_EXP=0) is asserted bit-exact wherever a test selects it."""
 import ctypes
 import os
 
@@ -633,8 +634,11 @@ def test_config2_sh3_full_parity(gpu, orc, torch, tmp_path_factory):
     Scene.from_ply(sh3=True) maps them channel-major into a 59-array block and
     k_preprocess<false, true> evaluates bands 0-3.  The reference evaluates only bands
     0-2 (render.cu:506-530; consts 369-386), so this is checked against the oracle's
-    independent SH-3 restatement: colours bit-exact per visible Gaussian, image
-    bit-exact and the per-pixel take maps equal, for the exact blend."""
+    independent SH-3 restatement: colours bit-exact per visible Gaussian; for the exact
+    blend the image bit-exact, for the default fast-exp blend within FX_TOL; in both
+    modes the per-pixel take maps equal the oracle's and the shipped kernel's image
+    equals the diagnostics build's (take_parity), so the take map describes the shipped
+    composite (round-4 verdict item 6)."""
     from test_gpu_fastexp import take_parity
     path, _ = scene_soa(gpu, tmp_path_factory, 1_000_000, 2)
     W, H = 1920, 1080
@@ -647,6 +651,8 @@ def test_config2_sh3_full_parity(gpu, orc, torch, tmp_path_factory):
         want, takes_want = orc.render_takes(soa3, cam, W, H, 3.0, threads=threads)
         want_spl = orc.preprocess(soa3, cam, W, H, 3.0)
     r = gpu.Renderer()
+    linf_fast, _ = take_parity(gpu, torch, scene, cam, W, H, want, takes_want, mode=1, renderer=r)
+    print(f"SH-3 config 2: fast-exp blend L-inf {linf_fast:.3g}")
     take_parity(gpu, torch, scene, cam, W, H, want, takes_want, mode=0, renderer=r)
     vis = want_spl["status"] == 2
     assert vis.sum() > 900_000
@@ -659,9 +665,9 @@ def test_config2_sh3_full_parity(gpu, orc, torch, tmp_path_factory):
 
 
 def full_size_both_blends(gpu, orc, torch, scene, soa, cam, W, H):
-    """The default (exact) blend is bit-identical with the same take map as the oracle;
-    the opt-in fast-exp blend composites exactly the oracle's splats on every pixel
-    (take maps) within the gate."""
+    """The exact blend (mode 0) is bit-identical with the same take map as the oracle;
+    the default fast-exp blend (mode 1) composites exactly the oracle's splats on every
+    pixel (take maps, and its image equal to the diagnostics build's) within FX_TOL."""
     from test_gpu_fastexp import take_parity
     want, takes_want = orc.render_takes(soa, cam, W, H, 3.0, threads=min(16, len(os.sched_getaffinity(0))))
     take_parity(gpu, torch, scene, cam, W, H, want, takes_want, mode=0)

@@ -267,6 +267,27 @@ def test_path_status_words(gpu, orc, torch):
         assert_image_parity(o.view(3, H, W).cpu().numpy(), orc.render(soa, cam, W, H, 3.0))
 
 
+def test_path_status_word_released_after_error(gpu, orc, torch, c1):
+    """a gsr_render_path_status call that fails inside the frame (here the
+    image size is refused after the lane took the frame's validity word) must not leave
+    the word with the context: a later plain gsr_render on the same context would have
+    its column scan write the frame's overflow bits through a pointer the caller may
+    since have freed.  The old word keeps its sentinel through both calls."""
+    _, soa = c1
+    W, H = 64, 48
+    cam = cam_for(gpu, W, H)
+    scene = gpu.Scene.from_soa(soa)
+    r = gpu.Renderer()
+    word = torch.full((1,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    out = torch.empty(3 * W * H, device="cuda")
+    with pytest.raises(gpu.GsrError):
+        r.render_path(scene, [cam], 0, H, [out.data_ptr()], status=[word.data_ptr()])
+    r.render(scene, cam, W, H, out.data_ptr())
+    assert r.sync() == 0
+    assert int(word.cpu()[0]) == 0x5A5A5A5A, "a later frame wrote through the failed call's status word"
+    assert_image_parity(out.view(3, H, W).cpu().numpy(), orc.render(soa, cam, W, H, 3.0))
+
+
 def test_path_bad_arguments(gpu, torch, c1):
     r = gpu.Renderer()
     with pytest.raises(gpu.GsrError):
