@@ -72,10 +72,15 @@ def parse():
                     help="N>1: nccl (= RCCL over xGMI, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--gather", choices=("step", "end", "none"), default="step",
                     help="N>1: RCCL gather of finished frames to rank 0 every step (overlapped) or once at the end")
+    ap.add_argument("--gather-every", type=int, default=1,
+                    help="with --gather step: gather only every k-th chunk of frames to rank 0 (its inbound "
+                         "xGMI budget at 8 ranks, DESIGN.md section 8); the others stay on their rank")
     ap.add_argument("--inflight", type=int, default=4,
                     help="frames in flight per GPU (gsr_render_path lanes); 1 = one frame at a time")
     ap.add_argument("--chunk", type=int, default=8,
                     help="N>1 with --gather step: frames per render_path call (one RCCL gather per frame)")
+    ap.add_argument("--no-sh3-line", action="store_true",
+                    help="config 2: skip the SH-3 sub-measurement (the 'sh3' object of the JSON line)")
     ap.add_argument("--sh3", action="store_true",
                     help="config 2 as BASELINE states it (SH degree 3): the opt-in SH-3 mode (all 45 f_rest, "
                          "bands 0-3; the reference evaluates bands 0-2)")
@@ -102,26 +107,19 @@ def algorithmic_stage_bytes(n: int, m: int, pairs: int, ntiles: int, consumed: i
     sort);
     blend as algorithmic_blend_bytes.
     Tile binning (row_items R >= 0): depth sort passes*N*32 (upsweep read 8, downsweep
-    read 8 + 4 and write 8 + 4: item and its packed rect payload);
+    read 8 + 4 and write 8 + 4: item and its packed rect payload), or with the bucket
+    sort (depth_passes 0, GSR_TUNE_DEPTH_BUCKETS) N*56 (count read 8; scatter read 8 + 4,
+    write 8 + 4; local sort read 8 + 4, write 8 + 4);
     row pass ("emit") N*16 (4-B rects for the count, items + 4-B rects for the
     scatter) + R*8 row items; column pass ("tile_sort") R*16 (count + scatter reads)
     + P*4 values + T*8 ranges.
-    Per-tile depth order (depth_passes 0): the binning as above over Gaussians in index
-    order, then "depth_sort" = P*16 (list read, key gather, list write).
     Pair sort (R < 0): depth sort passes*N*24; emit N*40 (sorted items twice, rect
     gather, srect write/read) + P*6 (u16 key + u32 value); tile sort P*14 per
     non-final pass, P*12 for the final one (keys 2 up, 6 read, 6|4 write) + T*8."""
     out = {"preprocess": (152 + 4 * (sh_floats - 27)) * n + 64 * m + (12 if row_items >= 0 else 16) * n,
            "blend": algorithmic_blend_bytes(ntiles, consumed, W, H)}
-    if row_items >= 0 and depth_passes == 0:
-        # per-tile depth order: binning in index order (rects + items read as in the
-        # depth-ordered case), then every tile list re-read (4), its keys gathered
-        # (8-B items) and written back in depth order (4)
-        out.update({"depth_sort": 16 * pairs,
-                    "emit": 24 * n + 8 * row_items,
-                    "tile_sort": 16 * row_items + 4 * pairs + 8 * ntiles})
-    elif row_items >= 0:
-        out.update({"depth_sort": depth_passes * 32 * n,
+    if row_items >= 0:
+        out.update({"depth_sort": (depth_passes * 32 if depth_passes else 56) * n,
                     "emit": 16 * n + 8 * row_items,
                     "tile_sort": 16 * row_items + 4 * pairs + 8 * ntiles})
     else:
@@ -285,6 +283,69 @@ def gpu_telemetry(pci: str | None = None) -> dict | None:
     return cards or None
 
 
+def sh3_line(gsr, torch, multi, args, ply, cam, W, H, F, stream, n) -> dict:
+    """BASELINE config 2 as worded ("1M random Gaussians, 1920x1080, SH degree 3"): the same
+    seed-2 .ply through the SH-3 scene block (48 SH floats per Gaussian, bands 0-3), the
+    same K, warmup and camera, frames in flight and one at a time, and the preprocess
+    stage's algorithmic rate.  The headline value stays the reference's bands 0-2
+    (render.cu:506-530), the parity configuration."""
+    scene3 = gsr.Scene.from_ply(ply, sh3=True)
+    r3 = gsr.Renderer()
+    for kv in filter(None, args.tune.split(",")):
+        knob, val = kv.split("=")
+        r3.set_tuning(int(knob), int(val))
+    r3.set_frames_in_flight(F)
+    shard3 = multi.FrameShard(None, r3, scene3, cam, W, H, k=args.k, steps=args.steps, gather="none", inflight=F,
+                              chunk=args.chunk, stream=stream)
+    for i in range(max(1, args.warmup)):
+        shard3.frame(i)
+    while r3.sync() != 0:
+        shard3.frame()
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) < 0.3:          # the card stays warm (the main run just ended)
+        shard3.run(4 * F)
+        torch.cuda.synchronize()
+    r3.sync()
+    r3.set_timing(2)
+    for _ in range(STAGE_FRAMES):
+        r3.render(scene3, cam, W, H, shard3.outs[0].data_ptr(), k=args.k, stream=stream)
+    r3.sync()
+    sums, frames = r3.stage_times()
+    stages = {k: v / max(1, frames) for k, v in sums.items()}
+    r3.set_timing(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        shard3.frame(i)
+    torch.cuda.synchronize()
+    seq = time.perf_counter() - t0
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        shard3.run(args.steps)
+        shard3.drain()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if not shard3.finish("cuda"):
+            break
+    overflow = r3.sync()
+    visible = int((r3.read_splats(n)["depth_key"] != 0xFFFFFFFF).sum())
+    pre_bytes = algorithmic_stage_bytes(n, visible, 0, 1, 0, W, H, sh_floats=48)["preprocess"]
+    out = {"value": round(args.steps / el, 3), "unit": "frames/sec", "ms_per_step": round(el / args.steps * 1e3, 4),
+           "sequential": {"value": round(args.steps / seq, 3), "ms_per_frame": round(seq / args.steps * 1e3, 4)},
+           "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+           "preprocess_gbs": round(pre_bytes / (stages["preprocess"] * 1e-3) / 1e9, 1) if stages.get("preprocess")
+           else None,
+           "preprocess_algorithmic_bytes": pre_bytes, "sh_floats": 48, "frames_in_flight": F,
+           "overflow_after_timed": overflow,
+           "note": "BASELINE config 2 as worded (SH degree 3): the same .ply's 45 f_rest through the SH-3 "
+                   "scene block (bands 0-3, 48 SH floats), same K / warmup / camera; the headline value is "
+                   "the reference's bands 0-2 (render.cu:506-530)"}
+    r3.close()
+    scene3.free()
+    return out
+
+
 def frame_time(i: int) -> float:
     """Config 5: frame i renders timestep i mod 120 of [0, 1]."""
     return (i % TIMESTEPS_4D) / (TIMESTEPS_4D - 1)
@@ -367,7 +428,7 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     shard = multi.FrameShard(dist, r, scene, cam, W, H, k=args.k, steps=args.steps, gather=args.gather,
                              inflight=F, chunk=args.chunk, gloo=gloo, frame_time=frame_time if four_d else None,
-                             stream=stream, frame_cam=frame_cam)
+                             stream=stream, frame_cam=frame_cam, gather_every=args.gather_every)
     outs, frame, path = shard.outs, shard.frame, shard.path
 
     # warmup (+ grow every lane's pair buffer to the high-water mark)
@@ -575,6 +636,8 @@ def main():
         "pairs": pairs,
         "row_items": row_items,
         "depth_passes": depth_passes,
+        "depth_sort": ("bucket sort: stable scatter into depth-quantile buckets + one LDS sort per bucket "
+                       "(GSR_TUNE_DEPTH_BUCKETS)" if depth_passes == 0 else f"{depth_passes} LSD radix passes"),
         "pairs_consumed": consumed,
         "blend_exp": {1: "fast (v_exp_f32 alpha, exact alpha tests, guarded T tests, exact re-blend of "
                          "suspect pixels)", 0: "exact (gsr_blend_expf)"}[min(blend_exp, 1)],
@@ -593,6 +656,7 @@ def main():
     if dist:
         result["scene_broadcast_ms"] = round(broadcast_ms, 2)
         result["gathers_per_rank_timed"] = shard.gathers
+        result["gather_every"] = args.gather_every
     sb = algorithmic_stage_bytes(n, visible, pairs, ntiles, consumed, W, H, depth_passes=depth_passes,
                                  row_items=row_items, sh_floats=48 if args.sh3 else 27)
     result["stages_gbs"] = {k: round(sb[k] / (stages[k] * 1e-3) / 1e9, 1) for k in sb if stages.get(k)}
@@ -613,6 +677,8 @@ def main():
     if traffic is not None:
         result["roofline"]["traffic"] = traffic["bytes_per_launch"]
         result["roofline"]["traffic_source"] = traffic["source"]
+    if world == 1 and args.config == 2 and not args.sh3 and not args.no_sh3_line:
+        result["sh3"] = sh3_line(gsr, torch, multi, args, ply, cam, W, H, F, stream, n)
     if world == 1:
         result["dropin_host_fps"] = round(dropin_rate(gsr, scene, cam, W, H, args.k), 2)
     if world == 1 and not args.no_cpu_baseline:

@@ -514,6 +514,8 @@ TUNE_DEPTH_SPLIT = 23
 TUNE_DEPTH_SPLIT_PERMILLE = 24
 TUNE_DEPTH_SPLIT_UNSAT = 25
 TUNE_DEPTH_SPLIT_STATE = 26
+TUNE_DEPTH_BUCKETS = 28
+TUNE_DEPTH_BUCKETS_OVER = 29
 
 
 def rank_order_check() -> tuple[int, int]:

@@ -49,6 +49,8 @@ struct Stats {
     uint32_t spec_miss;               // depth split without phase B (speculative): a phase-A blend
                                       // left a block unsaturated, the frame is incomplete (host copy,
                                       // sticky until the host reads it)
+    unsigned int bkt_over;            // bucket depth sort: items of buckets over the local capacity,
+                                      // sorted through global memory (host copy, sticky diagnostics)
 };
 
 // Depth split (GSR_TUNE_DEPTH_SPLIT): the frame's tiles are binned over the nearest
@@ -140,6 +142,25 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
                              uint32_t* pay1 = nullptr, bool rank_atomic = false,
                              const uint32_t* base_dev = nullptr, const uint32_t* gate = nullptr,
                              const SortFilter* filter = nullptr);
+// Bucket depth sort (binning path; gsr_kernels.hip "bucket depth sort"): the stable
+// (depth key, index) order of the n items `in` (the preprocess order; rect = its packed
+// tile rects by position) into items0 with the rects into pay0; items1 / pay1 are scratch.
+// buckets: 256..4096 (a power of two); s_in: its buckets - 1 sorted splitters (the last
+// 0xFFFFFFFF); s_out: the next frame's (quantiles of this order).  hist: groups x buckets
+// u32 (groups <= kMaxBucketGroups), totals: 2 x buckets + 1 u32 (the totals, then the
+// buckets' first positions).  cap (<= kMaxBucketCap): largest bucket sorted in LDS (larger
+// ones take the global path; over_host, host-mapped and nullable, counts their items).
+constexpr int kMaxBuckets = 4096;
+constexpr uint32_t kMaxBucketCap = 2048;
+constexpr int kMaxBucketGroups = 512;    // chunks (workgroups) of the scatter; hist: groups x buckets
+hipError_t launch_bucket_sort(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int buckets,
+                              int groups, const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
+                              const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
+                              unsigned int* over_host, hipStream_t s);
+// Splitters for launch_bucket_sort from an order the LSD passes sorted (depth_sorted of
+// items0 / items1 under dstats); live_dev (nullable): its visible count.
+hipError_t launch_bkt_splitters(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,
+                                const uint32_t* live_dev, int buckets, uint32_t* s_out, hipStream_t s);
 // Pair emission in depth order: tile counts (gathering each Gaussian's rect
 // once into srect, and zeroing the tile ranges), scan, then keys (uint16_t if
 // key16 else uint32_t) + values.

@@ -1645,6 +1645,586 @@ __device__ __forceinline__ void row_range(uint32_t& base, uint32_t& n, const uin
     }
 }
 
+// ------------------------------------------------------------------ bucket depth sort
+//
+// The binning path's global depth sort in two global steps instead of three or four
+// LSD passes (GSR_TUNE_DEPTH_BUCKETS).  Stable order of (depth key, index), exactly
+// the LSD passes' order:
+//   k_bkt_count    per workgroup chunk, the histogram over B buckets: bucket(key) =
+//                  the number of splitters <= key (B - 1 sorted splitters in LDS; the
+//                  last is 0xFFFFFFFF, so bucket B - 1 holds exactly the keys equal to
+//                  0xFFFFFFFF: culled items and saturated live keys, which tie)
+//   k_bkt_scan     per bucket, exclusive scan over the chunks (a chunk-major histogram:
+//                  every access a coalesced row segment)
+//   k_bkt_scatter  stable scatter of the preprocess order into the buckets (per-wave
+//                  returning LDS atomics on packed 16-bit counters, so the rank of an
+//                  item is its order among the wave's earlier items of its bucket);
+//                  every item lands at its bucket's range, index-ordered inside it; the
+//                  tile rects ride along as payloads
+//   k_bkt_local    one workgroup per live bucket: load it (<= kBktCap items), stable
+//                  LSD in LDS over the bits (key - bucket min) spans (typically 11 on
+//                  config 2: two 8-bit passes), write it back in place.  A bucket over
+//                  capacity is sorted by the same workgroup through global memory
+//                  (stable 8-bit passes ping-ponging with the scratch buffer), so any
+//                  splitters give the exact order; they only set the speed
+// Splitters are the previous frame's quantiles: k_bkt_local writes the key at every
+// (j + 1) / (B - 1) of the live order for the next frame (double-buffered), so the
+// buckets hold about n / B items each while the camera moves smoothly.  A context's
+// first frame runs the LSD passes and k_bkt_splitters takes the quantiles from them.
+// Stability: the scatter keeps index order inside a bucket, the local passes are stable
+// and buckets are key ranges in order, so ties stay in index order — the same order as
+// render.cu's CUB SortPairs of (tile << 32 | depth) within each tile (render.cu:1099-1118).
+constexpr int kBktThreads = 256;
+constexpr int kBktItems = 8;                                  // items per thread per tile
+constexpr uint32_t kBktTile = kBktThreads * kBktItems;        // 2048
+constexpr uint32_t kBktCap = kBktTile;                        // local sort capacity (items)
+static_assert(kBktCap == kMaxBucketCap && kMaxBuckets == 4096, "gsr_internal.h bucket sort limits");
+
+// The buckets of N keys: bucket(key) = the number of the B - 1 sorted splitters s[0..B-2]
+// that are <= key.  Step by step, so each step's N LDS reads are in flight
+// together (one search per item was N x log2(B) serial LDS round trips: the count kernel
+// spent 7 of its 10 us waiting on them).
+template <int B, int N>
+__device__ __forceinline__ void bkt_of_n(const uint32_t* s, const uint32_t (&key)[N], uint32_t (&bk)[N]) {
+#pragma unroll
+    for (int k = 0; k < N; k++) bk[k] = 0;
+#pragma unroll
+    for (uint32_t st = B / 2; st >= 1; st >>= 1) {
+        uint32_t v[N];
+#pragma unroll
+        for (int k = 0; k < N; k++) v[k] = s[bk[k] + st - 1];
+#pragma unroll
+        for (int k = 0; k < N; k++) bk[k] += v[k] <= key[k] ? st : 0u;
+    }
+}
+
+template <int B>
+__device__ __forceinline__ void bkt_load_splitters(uint32_t* s_S, const uint32_t* __restrict__ splitters) {
+    for (uint32_t j = threadIdx.x; j < (uint32_t)B; j += kBktThreads)
+        s_S[j] = j < (uint32_t)B - 2u ? splitters[j] : 0xffffffffu;
+}
+
+template <int B>
+__global__ __launch_bounds__(kBktThreads) void k_bkt_count(const uint64_t* __restrict__ in, uint32_t n,
+                                                           const uint32_t* __restrict__ splitters, int groups,
+                                                           uint32_t* __restrict__ hist) {
+    GSR_GEOM_PRIO();
+    __shared__ uint32_t s_S[B], s_h[B];
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    uint64_t b, e;
+    chunk_range(n, groups, blockIdx.x, kBktTile, b, e);
+    uint32_t key[kBktItems];
+    auto load = [&](uint64_t i0) {
+#pragma unroll
+        for (int k = 0; k < kBktItems; k++) {
+            const uint64_t i = i0 + (uint64_t)k * kBktThreads + t;
+            key[k] = i < e ? (uint32_t)(in[i] >> 32) : 0xffffffffu;
+        }
+    };
+    load(b);   // the first tile's keys travel together with the splitters: one memory round trip
+    bkt_load_splitters<B>(s_S, splitters);
+    for (uint32_t j = t; j < (uint32_t)B; j += kBktThreads) s_h[j] = 0;
+    __syncthreads();
+    uint32_t dead = 0;   // culled items all share the last bucket: counted by ballots, not 64-way atomics
+    for (uint64_t i0 = b; i0 < e; i0 += kBktTile) {
+        if (i0 != b) load(i0);
+        uint32_t bk[kBktItems];
+        bkt_of_n<B>(s_S, key, bk);
+#pragma unroll
+        for (int k = 0; k < kBktItems; k++) {
+            const uint64_t i = i0 + (uint64_t)k * kBktThreads + t;
+            const bool d = key[k] == 0xffffffffu;
+            dead += (uint32_t)__popcll(__ballot(d && i < e));
+            if (!d) atomicAdd(&s_h[bk[k]], 1u);
+        }
+    }
+    if (lane == 0 && dead) atomicAdd(&s_h[B - 1], dead);
+    __syncthreads();
+    // chunk-major (hist[chunk][bucket]): this workgroup's row is one coalesced 4B-per-bucket run
+    // (bucket-major, each of its B words went to another cache line: 15 us for 1M items)
+    for (uint32_t j = t; j < (uint32_t)B; j += kBktThreads) hist[(size_t)blockIdx.x * B + j] = s_h[j];
+}
+
+// Per bucket, the exclusive scan over the chunks of the chunk-major histogram (in place)
+// and the bucket's total.  64 buckets per workgroup (one per lane), 16 waves splitting the
+// chunks: every load is a coalesced 256-B row segment.  groups <= kBktMaxGroups.
+constexpr int kBktMaxGroups = kMaxBucketGroups;
+template <int B>
+__global__ __launch_bounds__(1024) void k_bkt_scan(uint32_t* __restrict__ hist, int groups,
+                                                   uint32_t* __restrict__ totals) {
+    GSR_GEOM_PRIO();
+    constexpr int kPerMax = kBktMaxGroups / 16;
+    __shared__ uint32_t s_part[16][64];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t b = blockIdx.x * 64u + lane;
+    const uint32_t per = ((uint32_t)groups + 15u) / 16u;
+    const uint32_t g0 = w * per;
+    uint32_t v[kPerMax], sum = 0;
+#pragma unroll
+    for (int i = 0; i < kPerMax; i++) {
+        const uint32_t g = g0 + (uint32_t)i;
+        v[i] = (uint32_t)i < per && g < (uint32_t)groups ? hist[(size_t)g * B + b] : 0u;
+        sum += v[i];
+    }
+    s_part[w][lane] = sum;
+    __syncthreads();
+    uint32_t run = 0, tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++) {
+        const uint32_t p = s_part[k][lane];
+        run += k < w ? p : 0u;
+        tot += p;
+    }
+    if (w == 0) totals[b] = tot;
+#pragma unroll
+    for (int i = 0; i < kPerMax; i++) {
+        const uint32_t g = g0 + (uint32_t)i;
+        if ((uint32_t)i < per && g < (uint32_t)groups) {
+            hist[(size_t)g * B + b] = run;
+            run += v[i];
+        }
+    }
+}
+
+// 16-bit half h of the packed counter word v.
+__device__ __forceinline__ uint32_t half16(uint32_t v, uint32_t h) { return (v >> (16u * h)) & 0xffffu; }
+
+// bstart (B + 1 words): written by chunk 0's workgroup, the first position of every bucket
+// and bstart[B] = n (k_bkt_local reads its bucket's range there).
+template <int B, bool RA>
+__global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(const uint64_t* __restrict__ in,
+                                                             uint64_t* __restrict__ out, uint32_t n,
+                                                             const uint32_t* __restrict__ splitters, int groups,
+                                                             const uint32_t* __restrict__ hist,
+                                                             const uint32_t* __restrict__ totals,
+                                                             const uint32_t* __restrict__ rect,
+                                                             uint32_t* __restrict__ pay_out,
+                                                             uint32_t* __restrict__ bstart) {
+    GSR_GEOM_PRIO();
+    constexpr uint32_t kW = B / 2;                      // packed counter words per wave
+    constexpr int kPer = B / kBktThreads;               // buckets per thread (scan)
+    constexpr int kWPer = (kW + kBktThreads - 1) / kBktThreads;   // counter words per thread
+    __shared__ uint32_t s_S[B], s_gbase[B];
+    __shared__ uint32_t s_wc[4][kW];
+    __shared__ uint32_t s_scr[4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const int chunk = xcd_chunk((int)blockIdx.x, groups);   // each XCD takes a contiguous run of chunks
+    uint64_t b, e;
+    chunk_range(n, groups, chunk, kBktTile, b, e);
+    const uint32_t wbase = w * 64 * kBktItems;
+    uint64_t it[kBktItems];
+    uint32_t pv[kBktItems];
+    auto load = [&](uint64_t tb, uint32_t tn) {
+#pragma unroll
+        for (int k = 0; k < kBktItems; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            it[k] = el < tn ? in[tb + el] : ~0ull;
+            pv[k] = el < tn ? rect[tb + el] : 0u;   // the input is the preprocess order: rect by position
+        }
+    };
+    // the first tile's items and rects, the splitters, the bucket totals and this chunk's
+    // histogram row are all loaded in one memory round trip
+    load(b, (uint32_t)min((uint64_t)kBktTile, e - b));
+    bkt_load_splitters<B>(s_S, splitters);
+    {   // this chunk's first slot in every bucket: the bucket's start + the earlier chunks' items
+        uint32_t loc[kPer], hrow[kPer], sum = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            loc[k] = totals[t * kPer + k];
+            hrow[k] = hist[(size_t)chunk * B + t * kPer + k];
+            sum += loc[k];
+        }
+        uint32_t tot;
+        uint32_t run = block_exclusive_scan<uint32_t>(sum, s_scr, tot);
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const uint32_t d = t * kPer + k;
+            if (chunk == 0) bstart[d] = run;
+            s_gbase[d] = run + hrow[k];
+            run += loc[k];
+        }
+        if (chunk == 0 && t == 0) bstart[B] = n;
+    }
+    if (b >= e) return;   // uniform per workgroup, after the scan's barriers
+    for (uint64_t tb = b; tb < e; tb += kBktTile) {
+        const uint32_t tn = (uint32_t)min((uint64_t)kBktTile, e - tb);
+        for (uint32_t j = t; j < 4 * kW; j += kBktThreads) (&s_wc[0][0])[j] = 0;
+        if (tb != b) load(tb, tn);
+        __syncthreads();
+        uint32_t dg[kBktItems], rk[kBktItems], keys[kBktItems];
+#pragma unroll
+        for (int k = 0; k < kBktItems; k++) keys[k] = (uint32_t)(it[k] >> 32);
+        bkt_of_n<B>(s_S, keys, dg);   // a key 0xFFFFFFFF (culled) counts every splitter: bucket B - 1
+        // culled items (the last bucket) rank by ballot against a running wave count, so the
+        // live items' returning atomics have no LDS read between them and stay in flight together
+        uint32_t dead_run = 0;
+        uint32_t old[kBktItems];
+#pragma unroll
+        for (int k = 0; k < kBktItems; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            const bool valid = el < tn;
+            const bool dead = keys[k] == 0xffffffffu;
+            const uint32_t d = dg[k];
+            const uint64_t dm = __ballot(valid && dead);
+            uint32_t r = dead_run + (uint32_t)__popcll(dm & lt_mask);
+            dead_run += (uint32_t)__popcll(dm);
+            const uint32_t sh = 16u * (d & 1u);
+            if (RA) {
+                // every lane adds (0 when it has no live item): no branch, so the eight returning
+                // atomics are in flight together; the halves are taken after the loop
+                old[k] = atomicAdd(&s_wc[w][d >> 1], valid && !dead ? 1u << sh : 0u);
+            } else {
+                const uint64_t peers = match_peers<12>(d, valid && !dead, 12);   // every lane takes part
+                if (valid && !dead) {
+                    r = half16(s_wc[w][d >> 1], d & 1u) + (uint32_t)__popcll(peers & lt_mask);
+                    if (lane == (uint32_t)(__ffsll((unsigned long long)peers) - 1))
+                        atomicAdd(&s_wc[w][d >> 1], (uint32_t)__popcll(peers) << sh);
+                }
+            }
+            rk[k] = r;
+        }
+        if (RA) {
+#pragma unroll
+            for (int k = 0; k < kBktItems; k++)
+                if (keys[k] != 0xffffffffu) rk[k] = half16(old[k], dg[k] & 1u);
+        }
+        if (lane == 0 && dead_run) atomicAdd(&s_wc[w][(B - 1) >> 1], dead_run << 16);   // B - 1 is odd: high half
+        __syncthreads();
+        // per word (two buckets): exclusive prefix over the four waves in place, tile counts kept
+        uint32_t tc[kWPer];
+#pragma unroll
+        for (int q = 0; q < kWPer; q++) {
+            const uint32_t j = t + q * kBktThreads;
+            tc[q] = 0;
+            if (j < kW) {
+                const uint32_t c0 = s_wc[0][j], c1 = s_wc[1][j], c2 = s_wc[2][j], c3 = s_wc[3][j];
+                s_wc[0][j] = 0;
+                s_wc[1][j] = c0;
+                s_wc[2][j] = c0 + c1;          // halves <= 2048: no carry between them
+                s_wc[3][j] = c0 + c1 + c2;
+                tc[q] = c0 + c1 + c2 + c3;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kBktItems; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            if (el < tn) {
+                const uint32_t d = dg[k];
+                const uint32_t dst = s_gbase[d] + half16(s_wc[w][d >> 1], d & 1u) + rk[k];
+                out[dst] = it[k];
+                pay_out[dst] = pv[k];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kWPer; q++) {
+            const uint32_t j = t + q * kBktThreads;
+            if (j < kW) {
+                s_gbase[2 * j] += tc[q] & 0xffffu;
+                s_gbase[2 * j + 1] += tc[q] >> 16;
+            }
+        }
+        // the next tile's counter reset + barrier orders these updates before their use
+    }
+}
+
+// Next frame's splitters from this bucket's part of the sorted live order: splitter j is
+// the key at live position floor((j + 1) * live / (B - 1)), j < B - 2.  key_at(q) reads
+// the sorted key at bucket-local position q.
+template <int B, typename KeyAt>
+__device__ __forceinline__ void bkt_write_splitters(uint32_t start, uint32_t count, uint32_t live,
+                                                    uint32_t* __restrict__ s_out, KeyAt key_at) {
+    if (live == 0 || count == 0) return;
+    const uint64_t m = (uint64_t)B - 1u;
+    // positions of j in [j0, j1) fall in [start, start + count)
+    const uint64_t j0 = ((uint64_t)start * m + live - 1) / live;            // smallest j + 1 with pos >= start
+    const uint64_t j1 = ((uint64_t)(start + count) * m + live - 1) / live;  // ... with pos >= start + count
+    for (uint64_t jp = j0 + threadIdx.x; jp < j1; jp += kBktThreads) {
+        if (jp == 0 || jp > (uint64_t)B - 2u) continue;   // j = jp - 1 in [0, B - 2)
+        const uint32_t pos = (uint32_t)(jp * live / m);
+        s_out[jp - 1] = key_at(pos - start);
+    }
+}
+
+// One workgroup per live bucket (grid B - 1).  bstart: the buckets' first positions
+// (k_bkt_scatter); s_in: the splitters this frame was bucketed by, which bound the keys of
+// every bucket but the first and the last (their key span sets the passes).  cap: buckets
+// above it take the global path (kBktCap; smaller only as a test hook).  over_host
+// (host-mapped, nullable): items sorted by the global path, for the diagnostics.
+template <int B, bool RA>
+__global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict__ items, uint64_t* __restrict__ scratch,
+                                                           uint32_t* __restrict__ pay, uint32_t* __restrict__ pay_scratch,
+                                                           const uint32_t* __restrict__ bstart,
+                                                           const uint32_t* __restrict__ s_in,
+                                                           uint32_t* __restrict__ s_next, uint32_t cap,
+                                                           unsigned int* over_host) {
+    GSR_GEOM_PRIO();
+    __shared__ uint64_t s_items[kBktTile];
+    __shared__ uint32_t s_pay[kBktTile];
+    __shared__ uint32_t s_wc[4][256], s_lbase[256], s_gb[256];
+    __shared__ uint32_t s_scr[4], s_mm[2];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t bkt = blockIdx.x;
+    const uint32_t start = bstart[bkt], count = bstart[bkt + 1] - start, live = bstart[B - 1];
+    // keys of bucket b lie in [s_in[b - 1], s_in[b]) for 0 < b < B - 2
+    const bool bounded = bkt > 0 && bkt < (uint32_t)B - 2u;
+    const uint32_t klo = bounded ? s_in[bkt - 1] : 0u, khi = bounded ? s_in[bkt] : 0u;
+    if (bkt == 0 && t == 0) {
+        s_next[B - 2] = 0xffffffffu;
+        if (live == 0)
+            for (uint32_t j = 0; j < (uint32_t)B - 2u; j++) s_next[j] = 0;   // any sorted splitters will do
+    }
+    if (count == 0) return;
+    uint64_t* const seg = items + start;
+    uint32_t* const pseg = pay + start;
+    const uint32_t wbase = w * 64 * kBktItems;
+    if (count <= cap) {
+        // ---- fast path: the bucket in registers, stable 8-bit passes through LDS ----
+        uint64_t it[kBktItems];
+        uint32_t pv[kBktItems];
+#pragma unroll
+        for (int k = 0; k < kBktItems; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            it[k] = el < count ? seg[el] : ~0ull;
+            pv[k] = el < count ? pseg[el] : 0u;
+        }
+        uint32_t kmin = klo, span = khi - klo - 1u;   // bounded: keys in [klo, khi)
+        if (!bounded) {   // the open-ended first and last buckets: their own min and max
+            uint32_t mn = 0xffffffffu, mx = 0;
+#pragma unroll
+            for (int k = 0; k < kBktItems; k++)
+                if (wbase + k * 64 + lane < count) {
+                    mn = min(mn, (uint32_t)(it[k] >> 32));
+                    mx = max(mx, (uint32_t)(it[k] >> 32));
+                }
+            mn = ~wave_max_u32(~mn);
+            mx = wave_max_u32(mx);
+            if (t < 2) s_mm[t] = t ? 0u : 0xffffffffu;
+            __syncthreads();
+            if (lane == 0) {
+                atomicMin(&s_mm[0], mn);
+                atomicMax(&s_mm[1], mx);
+            }
+            __syncthreads();
+            kmin = s_mm[0];
+            span = s_mm[1] - kmin;
+        }
+        const int bits = span ? 32 - __clz((int)span) : 0;
+        for (int shift = 0; shift < bits; shift += 8) {   // uniform
+            uint32_t dig[kBktItems], pos[kBktItems];
+#pragma unroll
+            for (int k = 0; k < kBktItems; k++) dig[k] = (((uint32_t)(it[k] >> 32) - kmin) >> shift) & 0xffu;
+            (void)bin_rank_tile<kBktItems, 8, RA>(dig, count, pos, s_wc, s_lbase, s_scr);
+#pragma unroll
+            for (int k = 0; k < kBktItems; k++) {
+                const uint32_t el = wbase + k * 64 + lane;
+                if (el < count) {
+                    s_items[pos[k]] = it[k];
+                    s_pay[pos[k]] = pv[k];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kBktItems; k++) {
+                const uint32_t el = wbase + k * 64 + lane;
+                if (el < count) {
+                    it[k] = s_items[el];
+                    pv[k] = s_pay[el];
+                }
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int k = 0; k < kBktItems; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            if (el < count) {
+                seg[el] = it[k];
+                pseg[el] = pv[k];
+                s_items[el] = it[k];
+            }
+        }
+        __syncthreads();
+        if (bkt < (uint32_t)B - 1u)
+            bkt_write_splitters<B>(start, count, live, s_next,
+                                   [&](uint32_t q) { return (uint32_t)(s_items[q] >> 32); });
+        return;
+    }
+    // ---- over capacity: stable 8-bit passes through global memory, one tile at a time ----
+    if (over_host && t == 0) atomicAdd_system(over_host, count);
+    uint32_t kmin = 0xffffffffu, kmax = 0;
+    for (uint32_t i = t; i < count; i += kBktThreads) {
+        const uint32_t k = (uint32_t)(seg[i] >> 32);
+        kmin = min(kmin, k);
+        kmax = max(kmax, k);
+    }
+    kmin = ~wave_max_u32(~kmin);
+    kmax = wave_max_u32(kmax);
+    if (t < 2) s_mm[t] = t ? 0u : 0xffffffffu;
+    __syncthreads();
+    if (lane == 0) {
+        atomicMin(&s_mm[0], kmin);
+        atomicMax(&s_mm[1], kmax);
+    }
+    __syncthreads();
+    kmin = s_mm[0];
+    const uint32_t span = s_mm[1] - kmin;
+    const int bits = span ? 32 - __clz((int)span) : 0;
+    uint64_t* src = seg;
+    uint64_t* dst = scratch + start;
+    uint32_t* psrc = pseg;
+    uint32_t* pdst = pay_scratch + start;
+    int passes = 0;
+    for (int shift = 0; shift < bits; shift += 8, ++passes) {
+        auto digit = [&](uint64_t v) { return (((uint32_t)(v >> 32) - kmin) >> shift) & 0xffu; };
+        s_gb[t] = 0;
+        __syncthreads();
+        for (uint32_t i = t; i < count; i += kBktThreads) atomicAdd(&s_gb[digit(src[i])], 1u);
+        __syncthreads();
+        {
+            const uint32_t c = s_gb[t];
+            uint32_t tot;
+            const uint32_t ex = block_exclusive_scan<uint32_t>(c, s_scr, tot);
+            s_gb[t] = ex;   // every read of s_gb[t] (its own count) is done by this thread
+        }
+        for (uint32_t tb = 0; tb < count; tb += kBktTile) {
+            const uint32_t tn = min(kBktTile, count - tb);
+            uint64_t it[kBktItems];
+            uint32_t pv[kBktItems], dig[kBktItems], pos[kBktItems];
+#pragma unroll
+            for (int k = 0; k < kBktItems; k++) {
+                const uint32_t el = wbase + k * 64 + lane;
+                it[k] = el < tn ? src[tb + el] : ~0ull;
+                pv[k] = el < tn ? psrc[tb + el] : 0u;
+                dig[k] = digit(it[k]);
+            }
+            const uint32_t tcount = bin_rank_tile<kBktItems, 8, RA>(dig, tn, pos, s_wc, s_lbase, s_scr);
+#pragma unroll
+            for (int k = 0; k < kBktItems; k++) {
+                const uint32_t el = wbase + k * 64 + lane;
+                if (el < tn) {
+                    s_items[pos[k]] = it[k];
+                    s_pay[pos[k]] = pv[k];
+                }
+            }
+            __syncthreads();
+            for (uint32_t q = t; q < tn; q += kBktThreads) {
+                const uint64_t v = s_items[q];
+                const uint32_t d = digit(v);
+                const uint32_t o = s_gb[d] + (q - s_lbase[d]);
+                dst[o] = v;
+                pdst[o] = s_pay[q];
+            }
+            __syncthreads();
+            s_gb[t] += tcount;
+            // bin_rank_tile's first barrier orders this before the next tile's reads
+        }
+        __threadfence();   // the next pass (other waves of this workgroup) reads what this one wrote
+        __syncthreads();
+        uint64_t* ts = src;
+        src = dst;
+        dst = ts;
+        uint32_t* tp = psrc;
+        psrc = pdst;
+        pdst = tp;
+    }
+    if (passes & 1) {   // the result is in the scratch segment: copy it back
+        for (uint32_t i = t; i < count; i += kBktThreads) {
+            seg[i] = src[i];
+            pseg[i] = psrc[i];
+        }
+        __threadfence();
+        __syncthreads();
+    }
+    if (bkt < (uint32_t)B - 1u)
+        bkt_write_splitters<B>(start, count, live, s_next, [&](uint32_t q) { return (uint32_t)(seg[q] >> 32); });
+}
+
+// Splitters from a depth order the LSD passes sorted (a context's first frame, or the
+// first after the bucket count changed): one workgroup.  live (nullable): the visible
+// count of a partitioned sort; else the first key 0xFFFFFFFF is found by two rounds of
+// 256 probes and a last scan.
+template <int B>
+__global__ __launch_bounds__(kBktThreads) void k_bkt_splitters(const uint64_t* __restrict__ items0,
+                                                               const uint64_t* __restrict__ items1,
+                                                               const uint32_t* __restrict__ dstats, uint32_t n,
+                                                               const uint32_t* __restrict__ live_dev,
+                                                               uint32_t* __restrict__ s_out) {
+    GSR_GEOM_PRIO();
+    __shared__ uint32_t s_lo, s_hi;
+    const uint64_t* sorted = depth_sorted(items0, items1, dstats);
+    const uint32_t t = threadIdx.x;
+    uint32_t live;
+    if (live_dev) {
+        live = min(*live_dev, n);
+    } else {
+        // the first position whose key is 0xFFFFFFFF (n if none): narrow [lo, hi) by probes
+        if (t == 0) {
+            s_lo = 0;
+            s_hi = n;
+        }
+        __syncthreads();
+        for (int round = 0; round < 3; round++) {
+            const uint32_t lo = s_lo, hi = s_hi;
+            __syncthreads();
+            const uint32_t len = hi - lo;
+            if (len <= 1) break;   // uniform
+            const uint32_t step = (len + kBktThreads - 1) / kBktThreads;
+            const uint32_t p = lo + t * step;
+            const bool dead = p < hi && (uint32_t)(sorted[p] >> 32) == 0xffffffffu;
+            // the last probe that is live, then the first that is dead, bound the answer
+            if (p < hi && !dead) atomicMax(&s_lo, p + 1);
+            if (dead) atomicMin(&s_hi, p);
+            __syncthreads();
+        }
+        uint32_t lo = s_lo;
+        const uint32_t hi = s_hi;
+        __syncthreads();
+        // at most a few positions left: each thread checks one
+        if (t == 0) s_lo = hi;
+        __syncthreads();
+        for (uint32_t p = lo + t; p < hi; p += kBktThreads)
+            if ((uint32_t)(sorted[p] >> 32) == 0xffffffffu) atomicMin(&s_lo, p);
+        __syncthreads();
+        live = s_lo;
+        (void)lo;
+    }
+    // thread t takes splitters t * kPer .. + kPer - 1 and makes them non-decreasing with a
+    // running max (an order the host's pass budget left incomplete — that frame re-renders
+    // — must still give sorted splitters: the bucket search assumes them)
+    constexpr int kPer = B / kBktThreads;
+    __shared__ uint32_t s_wmax[4];
+    const uint64_t m = (uint64_t)B - 1u;
+    uint32_t v[kPer], run = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const uint32_t j = t * kPer + k;
+        v[k] = live && j < (uint32_t)B - 2u ? (uint32_t)(sorted[(uint32_t)((uint64_t)(j + 1) * live / m)] >> 32) : 0u;
+        v[k] = min(v[k], 0xfffffffeu);
+        run = max(run, v[k]);
+        v[k] = run;
+    }
+    uint32_t x = run;   // inclusive max over the wave's threads, then over earlier waves
+    const uint32_t lane = t & 63u, w = t >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (lane >= (uint32_t)o) x = max(x, y);
+    }
+    if (lane == 63) s_wmax[w] = x;
+    uint32_t before = (uint32_t)__shfl_up((int)x, 1, 64);
+    if (lane == 0) before = 0;
+    __syncthreads();
+    for (uint32_t k = 0; k < w; k++) before = max(before, s_wmax[k]);
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const uint32_t j = t * kPer + k;
+        if (j < (uint32_t)B - 2u) s_out[j] = max(before, v[k]);
+    }
+    if (t == 0) s_out[B - 2] = 0xffffffffu;
+}
+
 // Depth split, phase B: the summed-area table of the tiles phase A left unsaturated
 // (a tile counts when any of its four blocks' flags is set; the flags of a tile are
 // consecutive bytes), (tiles_y + 1) x (tiles_x + 1) words with a zero first row and
@@ -3156,6 +3736,60 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
     else
         radix_pass<16, false>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
                               rect_direct, pay0, pay1, s, sr);
+    return hipGetLastError();
+}
+
+template <int B>
+static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int groups,
+                          const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
+                          const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
+                          unsigned int* over_host, hipStream_t s) {
+    uint32_t* bstart = totals + B;   // B + 1 words after the totals
+    hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist);
+    hipLaunchKernelGGL(k_bkt_scan<B>, dim3(B / 64), dim3(1024), 0, s, hist, groups, totals);
+    if (rank_atomic) {
+        hipLaunchKernelGGL((k_bkt_scatter<B, true>), dim3(groups), dim3(kBktThreads), 0, s, in, items0, n, s_in,
+                           groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart);
+        hipLaunchKernelGGL((k_bkt_local<B, true>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0, pay1,
+                           static_cast<const uint32_t*>(bstart), s_in, s_out, cap, over_host);
+    } else {
+        hipLaunchKernelGGL((k_bkt_scatter<B, false>), dim3(groups), dim3(kBktThreads), 0, s, in, items0, n, s_in,
+                           groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart);
+        hipLaunchKernelGGL((k_bkt_local<B, false>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0, pay1,
+                           static_cast<const uint32_t*>(bstart), s_in, s_out, cap, over_host);
+    }
+}
+
+hipError_t launch_bucket_sort(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int buckets,
+                              int groups, const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
+                              const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
+                              unsigned int* over_host, hipStream_t s) {
+    if (groups < 1 || groups > kBktMaxGroups || (int64_t)groups * buckets > 256 * (int64_t)kMaxSortGroups || cap < 1 ||
+        cap > kBktCap ||
+        in == items0 || !rect || !pay0 || !pay1)   // in may be items1: the scratch is used after the scatter
+        return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    switch (buckets) {
+    case 256: bucket_sort_b<256>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s); break;
+    case 512: bucket_sort_b<512>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s); break;
+    case 1024: bucket_sort_b<1024>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s); break;
+    case 2048: bucket_sort_b<2048>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s); break;
+    case 4096: bucket_sort_b<4096>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_bkt_splitters(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,
+                                const uint32_t* live_dev, int buckets, uint32_t* s_out, hipStream_t s) {
+    switch (buckets) {
+    case 256: hipLaunchKernelGGL(k_bkt_splitters<256>, dim3(1), dim3(kBktThreads), 0, s, items0, items1, dstats, n, live_dev, s_out); break;
+    case 512: hipLaunchKernelGGL(k_bkt_splitters<512>, dim3(1), dim3(kBktThreads), 0, s, items0, items1, dstats, n, live_dev, s_out); break;
+    case 1024: hipLaunchKernelGGL(k_bkt_splitters<1024>, dim3(1), dim3(kBktThreads), 0, s, items0, items1, dstats, n, live_dev, s_out); break;
+    case 2048: hipLaunchKernelGGL(k_bkt_splitters<2048>, dim3(1), dim3(kBktThreads), 0, s, items0, items1, dstats, n, live_dev, s_out); break;
+    case 4096: hipLaunchKernelGGL(k_bkt_splitters<4096>, dim3(1), dim3(kBktThreads), 0, s, items0, items1, dstats, n, live_dev, s_out); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

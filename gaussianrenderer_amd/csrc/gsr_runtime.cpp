@@ -434,6 +434,15 @@ struct gsr_context {
                                      // (the environment's GSR_RANK_ATOMIC=0 selects 0, else 1)
     bool rank_ok = false;            // the device passed the rank-order self-check (ensure_static)
     bool overflow_seen = false;      // an overflow was reported since the last gsr_sync (which reports it again)
+    // bucket depth sort (GSR_TUNE_DEPTH_BUCKETS, gsr_kernels.hip "bucket depth sort")
+    int bucket_sort = 1;             // 0 = LSD passes; 1 = bucket sort after the context's first frame;
+                                     // 2 = test hook: as 1 with a local capacity of 64 items (most
+                                     // buckets take the global path)
+    uint32_t* bkt_split = nullptr;   // 2 x kMaxBuckets splitters (double-buffered: read one, write the other)
+    int bkt_par = 0;                 // the half the next bucket-sorted frame reads
+    int bkt_B = 0;                   // buckets the splitters were made for (0: none yet)
+    bool bds_frame = false;          // this frame's preprocess items went to items[1] for the bucket sort
+    bool last_bds = false;           // the last sorted frame was bucket-sorted (order in items[0], no pass plan)
     uint32_t* fstatus = nullptr;     // the current frame's validity word (gsr_render_path_status; device,
                                      // nullable): GSR_FRAME_* bits, written by its column scans / blend
     // frame state
@@ -482,6 +491,14 @@ constexpr int kSplitRetryMax = 1 << 14;
 bool split_enabled(const gsr_context* c, int64_t n) {
     return n > 0 && c->blend_variant != 3 && c->split_pm < 1000 &&
            (c->depth_split == 1 || (c->depth_split == 2 && n > kLargeScene));
+}
+
+// Buckets of the bucket depth sort for n items: about 1,024 items per bucket (local sorts
+// of ~930 live items at config 2 against a 2,048-item capacity), 256..kMaxBuckets.
+int bkt_count(int64_t n) {
+    int b = 256;
+    while (b < gsr::kMaxBuckets && (int64_t)b * 1024 < n) b *= 2;
+    return b;
 }
 
 int groups_for(int64_t n, int64_t per) {
@@ -541,7 +558,9 @@ int ensure_static(gsr_context* c) {
         c->rank_ok = rk.state == 1;
     }
     if (int rc = realloc_dev(&c->hist, 256 * (size_t)gsr::kMaxSortGroups)) return rc;
-    if (int rc = realloc_dev(&c->totals, 256)) return rc;
+    // LSD digit totals / bucket totals + bucket starts
+    if (int rc = realloc_dev(&c->totals, 2 * (size_t)gsr::kMaxBuckets + 1)) return rc;
+    if (int rc = realloc_dev(&c->bkt_split, 2 * (size_t)gsr::kMaxBuckets)) return rc;
     if (int rc = realloc_dev(&c->wg, (size_t)gsr::kMaxSortGroups)) return rc;
     if (int rc = realloc_dev(&c->stats, 2)) return rc;
     if (int rc = realloc_dev(&c->dstats, 4 + 4 * (size_t)gsr::kMaxSortGroups)) return rc;
@@ -924,7 +943,12 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
                    c->fr.tiles_y <= 256;
     // live partition (global depth sort on the binning path): the items go to
     // items[1] and the partition writes the visible-first order into items[0]
-    c->compact_frame = n > 0 && !c->split_key &&
+    // bucket depth sort (splitters exist for this scene size): the items go to items[1], the
+    // sort writes the order into items[0]; it keeps culled items apart itself, so it
+    // replaces the live partition
+    c->bds_frame = n > 0 && !c->split_key && c->bucket_sort && c->bkt_B == bkt_count(n) && c->tile_binning &&
+                   c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
+    c->compact_frame = n > 0 && !c->split_key && !c->bds_frame &&
                        (c->depth_compact == 1 || (c->depth_compact == 2 && layout == GSR_LAYOUT_SCENE_BLOCK_4D)) &&
                        c->tile_binning && c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
     // the binning path takes the tile rects packed to 4 B (pack_rect), the pair path 8 B;
@@ -946,7 +970,7 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     if (c->split_key) {
         if (int rc = ensure_src(c, n)) return rc;
     }
-    c->pre_out = c->split_key ? c->src_items : c->items[c->compact_frame ? 1 : 0];
+    c->pre_out = c->split_key ? c->src_items : c->items[c->compact_frame || c->bds_frame ? 1 : 0];
     HIP_TRY(gsr::launch_preprocess(arrays, stride, n, c->fr, c->rec, c->pre_out,
                                    c->rect,
                                    c->rect_packed, layout == GSR_LAYOUT_SCENE_BLOCK_4D,
@@ -986,6 +1010,27 @@ static uint32_t* pay_buf(gsr_context* c, int b) {
 // leaves them in depth order (pay_buf(c, passes run & 1)).  Result in items[passes run & 1].
 static int depth_sort_locked(gsr_context* c, bool with_rects) {
     const uint32_t n = (uint32_t)c->n;
+    // bucket depth sort: the first sort of a frame whose preprocess prepared for it (a
+    // repeated sort of the frame takes the LSD passes over the sorted items[0])
+    if (with_rects && !c->split_key && c->bds_frame && !c->have_sort && c->pre_out != c->items[0]) {
+        const int B = c->bkt_B;
+        const int G = std::min(groups_for(c->n, gsr::kMaxBucketCap), gsr::kMaxBucketGroups);
+        uint32_t* s_in = c->bkt_split + (size_t)c->bkt_par * gsr::kMaxBuckets;
+        uint32_t* s_out = c->bkt_split + (size_t)(c->bkt_par ^ 1) * gsr::kMaxBuckets;
+        HIP_TRY(gsr::launch_bucket_sort(c->pre_out, c->items[0], c->items[1], n, B, G, s_in, s_out, c->hist,
+                                        c->totals, reinterpret_cast<const uint32_t*>(c->rect), pay_buf(c, 0),
+                                        pay_buf(c, 1), rank_atomic_on(c), c->bucket_sort == 2 ? 64u : gsr::kMaxBucketCap,
+                                        c->hstats_dev ? &c->hstats_dev->bkt_over : nullptr, c->stream));
+        c->bkt_par ^= 1;
+        c->last_bds = true;
+        c->last_compact = false;
+        c->last_split_key = false;
+        c->compact_frame = false;
+        c->bds_frame = false;
+        c->passes_launched = 4;   // no pass plan on this frame: the column scan's depth check is off
+        return GSR_OK;
+    }
+    c->last_bds = false;
     // smaller tiles for the 1M-item depth sort: ~500 workgroups instead of ~250 (-2.6 %
     // frame time one at a time; in flight 8 and 16 measure within 1.5 % of each other,
     // either way round: profiles/r02_ab_depth_items.txt)
@@ -1039,6 +1084,15 @@ static int depth_sort_locked(gsr_context* c, bool with_rects) {
                                        with_rects ? pay_buf(c, 0) : nullptr,
                                        with_rects ? pay_buf(c, 1) : nullptr, rank_atomic_on(c), nullptr, nullptr,
                                        f0 ? &near : nullptr));
+    }
+    // the bucket sort's first splitters: quantiles of this whole sorted order (the next
+    // frame of this scene size is bucket-sorted)
+    if (with_rects && !key && c->bucket_sort && c->bkt_B != bkt_count(c->n)) {
+        const int B = bkt_count(c->n);
+        HIP_TRY(gsr::launch_bkt_splitters(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n,
+                                          part ? c->nlive : nullptr, B,
+                                          c->bkt_split + (size_t)c->bkt_par * gsr::kMaxBuckets, c->stream));
+        c->bkt_B = B;
     }
     return GSR_OK;
 }
@@ -1099,7 +1153,8 @@ static int bin_locked(gsr_context* c, uint32_t base, uint32_t count, int gate_mo
     const int64_t est = rs && rs->cut_mode == 1 ? std::min<int64_t>(count, std::max<int64_t>(2 * (int64_t)rs->na, 65536))
                                                 : (int64_t)count;
     const int gb = std::min(groups_for(est, 1024), gsr::kMaxSortGroups / 2);
-    uint32_t* dst = c->depth_skip ? (far ? c->dstats_far : c->dstats) : nullptr;
+    // (a bucket-sorted frame has no pass plan: its order is in items[0], its rects in pay_buf 0)
+    uint32_t* dst = c->depth_skip && !(c->last_bds && !far) ? (far ? c->dstats_far : c->dstats) : nullptr;
     HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], dst, count, pay_buf(c, 0),
                                  pay_buf(c, 1), gb,
                                  c->hist, row_items, row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items,
@@ -1137,9 +1192,10 @@ static int sort_locked(gsr_context* c, bool allow_split) {
         c->split_key = false;
         c->compact_frame = true;
     }
-    if (c->compact_frame && !bin) {   // knobs changed since gsr_preprocess
+    if ((c->compact_frame || c->bds_frame) && !bin) {   // knobs changed since gsr_preprocess
         HIP_TRY(hipMemcpyAsync(c->items[0], c->pre_out, (size_t)n * 8, hipMemcpyDeviceToDevice, c->stream));
         c->compact_frame = false;
+        c->bds_frame = false;
     }
     const bool key = split && c->split_key;
     if (!key) {   // a frame preprocessed for key mode that is not split that way: all records
@@ -1242,7 +1298,7 @@ static int blend_locked(gsr_context* c, float* d_out) {
             // phase A; its workgroup 0 also sets the next frame's threshold from the near
             // depth order (key mode: the near part; count mode: the whole order)
             const bool spec = c->frame_spec;
-            const gsr::SplitCut cut{c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr,
+            const gsr::SplitCut cut{c->items[0], c->items[1], c->depth_skip && !c->last_bds ? c->dstats : nullptr,
                                     key ? c->nlive : nullptr, n, c->split_na, c->split_rebin ? nullptr : c->kcut};
             gsr::BlendSplit a{1, c->tbuf, c->bflag, c->gate, nullptr, spec ? c->hstats_dev : nullptr, cut, 0u,
                               spec ? c->fstatus : nullptr};
@@ -1338,6 +1394,7 @@ namespace {
 void copy_settings(gsr_context* d, const gsr_context* s) {
     d->tile_items = s->tile_items;
     d->depth_items = s->depth_items;
+    d->bucket_sort = s->bucket_sort;
     d->tile_groups = s->tile_groups;
     d->tile_split_even = s->tile_split_even;
     d->depth_skip = s->depth_skip;
@@ -1619,6 +1676,10 @@ extern "C" int gsr_read_splats(gsr_context* c, void* host, int64_t n) {
 
 static int depth_passes_locked(gsr_context* c, int* passes) {
     *passes = 4;
+    if (c->last_bds) {   // bucket-sorted: no LSD passes, the order is in items[0]
+        *passes = 0;
+        return GSR_OK;
+    }
     if (!c->depth_skip) return GSR_OK;
     uint32_t st[4];   // same plan as the kernels (gsr_kernels.hip depth_pass_skipped)
     HIP_TRY(hipMemcpy(st, c->dstats, sizeof st, hipMemcpyDeviceToHost));
@@ -1797,6 +1858,13 @@ extern "C" int gsr_get_tuning(gsr_context* c, int knob, int* value) {
     case GSR_TUNE_DEPTH_SPLIT_PERMILLE: *value = c->split_pm; break;
     case GSR_TUNE_DEPTH_SPLIT_UNSAT: *value = c->hstats ? (int)((const volatile Stats*)c->hstats)->split_unsat : 0; break;
     case GSR_TUNE_DEPTH_SPLIT_STATE: *value = !c->split_frame ? 0 : !c->frame_key ? 1 : c->frame_spec ? 3 : 2; break;
+    case GSR_TUNE_DEPTH_BUCKETS: *value = c->bucket_sort; break;
+    case GSR_TUNE_DEPTH_BUCKETS_OVER: {
+        int64_t v = c->hstats ? (int64_t)((const volatile Stats*)c->hstats)->bkt_over : 0;
+        for (auto* l : c->lanes) v += l->hstats ? (int64_t)((const volatile Stats*)l->hstats)->bkt_over : 0;
+        *value = (int)std::min<int64_t>(v, INT32_MAX);
+        break;
+    }
     case GSR_TUNE_RANK_ATOMIC: *value = c->rank_atomic < 0 ? default_rank_atomic() : c->rank_atomic; break;
     case GSR_TUNE_RANK_ATOMIC_ACTIVE: {
         RankCheck rk;
@@ -1892,9 +1960,14 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         if (value != 0 && value != 1) return set_err(GSR_E_ARG, "gsr_set_tuning: rank path must be 0 or 1");
         c->rank_atomic = value;
         return GSR_OK;
+    case GSR_TUNE_DEPTH_BUCKETS:
+        if (value < 0 || value > 2) return set_err(GSR_E_ARG, "gsr_set_tuning: depth buckets must be 0, 1 or 2");
+        c->bucket_sort = value;
+        return GSR_OK;
     case GSR_TUNE_RANK_ATOMIC_ACTIVE:
     case GSR_TUNE_DEPTH_SPLIT_UNSAT:
     case GSR_TUNE_DEPTH_SPLIT_STATE:
+    case GSR_TUNE_DEPTH_BUCKETS_OVER:
         return set_err(GSR_E_ARG, "gsr_set_tuning: knob %d is read-only", knob);
     case GSR_TUNE_TILE_SORT_GROUPS:
     case GSR_TUNE_DEPTH_SORT_GROUPS:

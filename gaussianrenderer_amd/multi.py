@@ -140,7 +140,7 @@ class FrameShard:
     def __init__(self, dist, renderer, scene, cam, W: int, H: int, k: float = 3.0, steps: int = 1,
                  gather: str = "step", inflight: int = 1, chunk: int = 8, gloo: bool = False,
                  frame_time=None, stream: int = 0, overlap: bool = True, sink=None, frame_scene=None,
-                 device: str = "cuda", frame_cam=None):
+                 device: str = "cuda", frame_cam=None, gather_every: int = 1):
         import torch
         self.dist, self.r, self.scene, self.cam = dist, renderer, scene, cam
         self.W, self.H, self.k, self.stream = W, H, k, stream
@@ -151,6 +151,9 @@ class FrameShard:
         self.frame_scene = frame_scene
         self.frame_cam = frame_cam               # frame index -> camera (a moving viewer), else cam
         self.step_gather = dist is not None and gather == "step"
+        # rank 0's inbound budget: gather only every k-th chunk; the
+        # others stay on their rank, their validity words still count in finish()
+        self.gather_every = max(1, int(gather_every))
         self.chunk = max(1, chunk) if self.step_gather else max(1, steps)
         self.nsets = 2 if self.step_gather else 1
         self.per_set = self.chunk if self.step_gather else self.F
@@ -276,6 +279,20 @@ class FrameShard:
             if not self.frame_events:
                 self._deliver(s)
 
+    def keep_local(self, s: int, m: int, i0: int = 0):
+        """A chunk that is not gathered (gather_every > 1): only its validity words are
+        logged, after its frames, and the set's reuse waits on that like on a gather."""
+        if self.frame_events:
+            import torch
+            with torch.cuda.stream(self.gather_stream):
+                for j in range(max(0, m - self.F), m):
+                    self.gather_stream.wait_event(self.frame_events[s * self.per_set + j])
+                self._log_status(s, i0, m)
+                self.gathered_ev[s].record(self.gather_stream)
+                self.gathered_valid[s] = True
+        else:
+            self._log_status(s, i0, m)
+
     def frame(self, i: int = 0, b: int = 0):
         """One frame on the caller's stream (sequential: the viewer's one-at-a-time use)."""
         rc = self.r.render(self.frame_scene(i) if self.frame_scene else self.scene,
@@ -313,7 +330,10 @@ class FrameShard:
         if self.sink:
             self._deliver(s)                     # the set's previous chunk, before it is overwritten
         self.path(i0, m, [s * self.per_set + j for j in range(m)], overlap=True, first=first, wait_set=s)
-        self.gather(s, m, cid, i0)
+        if cid % self.gather_every == 0:
+            self.gather(s, m, cid, i0)
+        else:
+            self.keep_local(s, m, i0)
 
     def run(self, steps: int):
         """K frames in flight, gathered per chunk when enabled (not drained: call drain())."""

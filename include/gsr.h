@@ -365,7 +365,7 @@ enum {
                                         set value is a new starting point, 1..999) */
     GSR_TUNE_DEPTH_SPLIT_UNSAT = 25, /* read-only: 8x8 blocks the last completed split frame's phase A
                                         left unsaturated (0: its phase B did nothing); read after gsr_sync */
-    GSR_TUNE_DEPTH_SPLIT_STATE = 26  /* read-only: how the last sorted frame ran: 0 one phase; 1 split,
+    GSR_TUNE_DEPTH_SPLIT_STATE = 26, /* read-only: how the last sorted frame ran: 0 one phase; 1 split,
                                         whole depth order sorted (count mode: the first split frame);
                                         2 split by a depth threshold (near part sorted, far part sorted
                                         in phase B); 3 as 2 with no phase B queued (speculative: a frame
@@ -375,6 +375,18 @@ enum {
        histograms in 512-thread workgroups of 2048 Gaussians, pass 0 without its upsweep launch:
        preprocess 49.4 -> 60.3 us against the 5.7-us upsweep, -1.1 % one frame at a time and
        -1.2 % in flight, profiles/r04_ab_pre_hist.txt) */
+    GSR_TUNE_DEPTH_BUCKETS = 28,     /* binning path, frames not split by a depth threshold: 1 (default) =
+                                        bucket depth sort: one stable scatter of the preprocess order into
+                                        ~n/1024 depth buckets bounded by the previous frame's quantiles,
+                                        then one workgroup per bucket sorts it in LDS (buckets over 2,048
+                                        items are sorted through global memory by their workgroup).  A
+                                        context's first frame of a scene size runs the LSD passes and
+                                        takes the quantiles from them.  0 = LSD passes only; 2 = test
+                                        hook: 1 with a 64-item local capacity.  Same order, same image;
+                                        gsr_depth_passes is 0 after a bucket-sorted frame */
+    GSR_TUNE_DEPTH_BUCKETS_OVER = 29 /* read-only: items the bucket sort's global path has sorted (buckets
+                                        over the local capacity), summed over the lanes; sticky, read
+                                        after gsr_sync */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Current value of a knob (what gsr_set_tuning last set, else the default). */

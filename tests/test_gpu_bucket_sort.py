@@ -1,0 +1,270 @@
+"""The bucket depth sort (GSR_TUNE_DEPTH_BUCKETS, gsr_kernels.hip "bucket depth sort").
+
+A context's first frame of a scene size runs the LSD passes and takes depth quantiles
+from their order; every later frame scatters the preprocess order stably into ~n/1024
+buckets bounded by those quantiles and sorts each bucket in one workgroup (in LDS, or
+through global memory when the bucket is over capacity).  The order must be exactly the
+LSD passes' order: stable by depth key, ties in index order (render.cu:1099-1118, CUB
+SortPairs).  Every test renders at least two frames per context,
+so the second one is bucket-sorted, and compares the depth order with the oracle's
+(tests/_oracle.py expected_depth_order), the tile lists with the LSD path's and the
+image bit for bit with the oracle's (exact blend)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import exact_blend, scene_soa
+from test_gpu_parity import assert_image_parity, cam_for
+
+pytestmark = pytest.mark.gpu
+
+THREADS = min(16, len(os.sched_getaffinity(0)))
+
+
+@pytest.fixture(scope="module")
+def torch(gpu):
+    import torch as t
+    assert t.cuda.is_available()
+    return t
+
+
+def render_frames(gpu, torch, r, scene, cams, W, H):
+    """Render each camera on r (re-rendered after an overflow); returns the last image."""
+    out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    for cam in cams:
+        for _ in range(3):
+            r.render(scene, cam, W, H, out.data_ptr())
+            if r.sync() == 0:
+                break
+        else:
+            raise AssertionError("frame kept overflowing")
+    return out.view(3, H, W).cpu().numpy()
+
+
+def renderer(gpu, buckets=1):
+    r = exact_blend(gpu.Renderer())
+    r.set_tuning(gpu.TUNE_DEPTH_SPLIT, 0)       # whole-order lists (5M scenes split by default)
+    r.set_tuning(gpu.TUNE_DEPTH_BUCKETS, buckets)
+    return r
+
+
+def check_bucket_frame(gpu, orc, torch, scene, soa, cams, W, H, buckets=1, want_over=None):
+    """Frames over cams on a bucket-sort renderer and on an LSD-only one; the last frame
+    must be bucket-sorted on the first and equal the oracle (order, image) and the LSD
+    renderer (order, tile lists)."""
+    n = soa.shape[1]
+    r = renderer(gpu, buckets)
+    img = render_frames(gpu, torch, r, scene, cams, W, H)
+    assert r.depth_passes() == 0, "the last frame was not bucket-sorted"
+    order = r.read_depth_order(n)
+    pairs = r.read_pairs()
+    over = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER)
+    ref = renderer(gpu, 0)
+    img_lsd = render_frames(gpu, torch, ref, scene, cams[-1:], W, H)
+    assert ref.depth_passes() >= 1
+    want_spl = orc.preprocess(soa, cams[-1], W, H, 3.0)
+    assert np.array_equal(order, orc.expected_depth_order(want_spl)), "bucket-sorted depth order differs"
+    assert np.array_equal(order, ref.read_depth_order(n))
+    assert np.array_equal(pairs, ref.read_pairs()), "tile lists differ from the LSD path's"
+    want = orc.render(soa, cams[-1], W, H, 3.0, threads=THREADS)
+    assert_image_parity(img, want, exact=True)
+    assert np.array_equal(img.view(np.uint32), img_lsd.view(np.uint32))
+    if want_over is not None:
+        want_over(over)
+    r.close()
+    ref.close()
+    return order
+
+
+def no_over(o):
+    assert o == 0, f"{o} items took the global path on a fixed camera"
+
+
+def some_over(o):
+    assert o > 0, "no bucket took the global path"
+
+
+def test_bucket_sort_config1(gpu, orc, torch, tmp_path_factory):
+    """Config 1 (10k Gaussians, 640x480): 256 buckets of ~40 items."""
+    _, soa = scene_soa(gpu, tmp_path_factory, 10_000, 1)
+    W, H = 640, 480
+    cams = [cam_for(gpu, W, H)] * 2
+    check_bucket_frame(gpu, orc, torch, gpu.Scene.from_soa(soa), soa, cams, W, H, want_over=no_over)
+
+
+def test_bucket_sort_config2_full(gpu, orc, torch, tmp_path_factory):
+    """Config 2 (1M, 1920x1080): 1,024 buckets of ~930 live items, all inside the local
+    capacity on a fixed camera (no item takes the global path)."""
+    path, soa = scene_soa(gpu, tmp_path_factory, 1_000_000, 2)
+    W, H = 1920, 1080
+    cams = [cam_for(gpu, W, H)] * 3
+    check_bucket_frame(gpu, orc, torch, gpu.Scene.from_ply(path), soa, cams, W, H, want_over=no_over)
+
+
+def test_bucket_sort_moving_camera(gpu, orc, torch, tmp_path_factory):
+    """Quantiles from one view, frame from another (orbit steps of 10 and 90 degrees and a
+    zoom): the buckets are unbalanced, some may overflow into the global path; the
+    order stays exact."""
+    from gaussianrenderer_amd import multi
+    _, soa = scene_soa(gpu, tmp_path_factory, 200_000, 4)
+    W, H = 960, 540
+    cams = [multi.orbit_camera(0, W, H), multi.orbit_camera(1, W, H), multi.orbit_camera(3, W, H),
+            cam_for(gpu, W, H, pos=(0.0, 0.0, 2.5))]
+    check_bucket_frame(gpu, orc, torch, gpu.Scene.from_soa(soa), soa, cams, W, H)
+
+
+def test_bucket_sort_global_path(gpu, orc, torch, tmp_path_factory):
+    """Test hook 2: a local capacity of 64 items, so nearly every bucket of a 200k scene is
+    sorted through global memory (stable 8-bit passes ping-ponging with the scratch
+    buffer); the order and image are still exact."""
+    _, soa = scene_soa(gpu, tmp_path_factory, 200_000, 5)
+    W, H = 960, 540
+    cams = [cam_for(gpu, W, H)] * 2
+
+    def many_over(o):
+        assert o > 150_000, f"only {o} items took the global path"
+
+    check_bucket_frame(gpu, orc, torch, gpu.Scene.from_soa(soa), soa, cams, W, H, buckets=2, want_over=many_over)
+
+
+def test_bucket_sort_tie_heavy(gpu, orc, torch, tmp_path_factory):
+    """300k Gaussians on 7 depth planes: every live key is shared by ~43k Gaussians, so
+    each plane fills one bucket far over capacity (the global path with no key bits to
+    sort: the stable scatter's index order is the answer), ties in index order."""
+    _, soa = scene_soa(gpu, tmp_path_factory, 300_000, 11)
+    soa = soa.copy()
+    soa[2] = np.linspace(-0.9, 0.9, 7, dtype=np.float32)[np.arange(soa.shape[1]) % 7]
+    W, H = 1920, 1080
+    cams = [cam_for(gpu, W, H)] * 2
+    order = check_bucket_frame(gpu, orc, torch, gpu.Scene.from_soa(soa), soa, cams, W, H,
+                               want_over=some_over)
+    keys = (order >> np.uint64(32)).astype(np.uint32)
+    assert np.unique(keys[keys != 0xFFFFFFFF]).size <= 7
+
+
+def test_bucket_sort_ballot_ranks(gpu, orc, torch, tmp_path_factory):
+    """The ballot-matching rank path (GSR_TUNE_RANK_ATOMIC 0) of the scatter and the local
+    passes gives the same order."""
+    _, soa = scene_soa(gpu, tmp_path_factory, 100_000, 6)
+    W, H = 640, 480
+    n = soa.shape[1]
+    scene = gpu.Scene.from_soa(soa)
+    cams = [cam_for(gpu, W, H)] * 2
+    orders = []
+    for ra in (0, 1):
+        for hook in (1, 2):
+            r = renderer(gpu, hook)
+            r.set_tuning(gpu.TUNE_RANK_ATOMIC, ra)
+            render_frames(gpu, torch, r, scene, cams, W, H)
+            assert r.depth_passes() == 0
+            orders.append(r.read_depth_order(n))
+            r.close()
+    want = orc.expected_depth_order(orc.preprocess(soa, cams[-1], W, H, 3.0))
+    for o in orders:
+        assert np.array_equal(o, want)
+
+
+def test_bucket_sort_4d_replaces_partition(gpu, orc, torch, tmp_path_factory):
+    """4D scenes (config 5 kind) take the live partition before the LSD passes; the bucket
+    sort keeps culled items apart itself (its last bucket, index order).  Two times of a
+    100k 4D scene: the second frame is bucket-sorted; its order equals the partitioned
+    LSD path's (the temporal cull gives culled items key 0xFFFFFFFF, which the oracle's
+    3D restatement of the scene at time t does not know) and its image the oracle's."""
+    p = tmp_path_factory.mktemp("b4d") / "scene4d.ply"
+    gpu.write_synthetic_ply4d(str(p), 100_000, 5)
+    soa49 = gpu.read_ply(str(p), four_d=True)
+    scene = gpu.Scene.from_ply(str(p))
+    assert scene.is_4d
+    W, H = 960, 540
+    cam = cam_for(gpu, W, H)
+    n = soa49.shape[1]
+    got = {}
+    for buckets in (1, 0):
+        r = renderer(gpu, buckets)
+        out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+        for t in (0.0, 0.5):
+            r.render(scene, cam, W, H, out.data_ptr(), time=t)
+            assert r.sync() == 0
+        assert (r.depth_passes() == 0) == (buckets == 1)
+        got[buckets] = (r.read_depth_order(n), out.view(3, H, W).cpu().numpy(), r.read_pairs())
+        r.close()
+    order = got[1][0]
+    assert np.array_equal(order, got[0][0]), "bucket-sorted 4D order differs from the partitioned LSD order"
+    assert np.array_equal(got[1][2], got[0][2])
+    keys = (order >> np.uint64(32)).astype(np.uint32)
+    assert (keys == 0xFFFFFFFF).sum() > n // 4          # the temporal cull left many culled items
+    want = orc.render(orc.temporal(soa49, 0.5), cam, W, H, 3.0, threads=THREADS)
+    assert_image_parity(got[1][1], want, exact=True)
+
+
+def test_bucket_sort_stage_api_repeated_sort(gpu, orc, torch, tmp_path_factory):
+    """Stage API: preprocess, sort (bucket-sorted), sort again (LSD passes over the sorted
+    order), blend: the same order both times and the oracle's image."""
+    _, soa = scene_soa(gpu, tmp_path_factory, 50_000, 7)
+    W, H = 640, 480
+    cam = cam_for(gpu, W, H)
+    scene = gpu.Scene.from_soa(soa)
+    n = soa.shape[1]
+    r = renderer(gpu)
+    render_frames(gpu, torch, r, scene, [cam], W, H)      # quantiles
+    out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    r.preprocess(scene, cam, W, H)
+    r.sort()
+    assert r.depth_passes() == 0
+    first = r.read_depth_order(n)
+    r.sort()
+    assert r.depth_passes() >= 1
+    assert np.array_equal(r.read_depth_order(n), first)
+    r.blend(out.data_ptr())
+    assert r.sync() == 0
+    want_spl = orc.preprocess(soa, cam, W, H, 3.0)
+    assert np.array_equal(first, orc.expected_depth_order(want_spl))
+    assert_image_parity(out.view(3, H, W).cpu().numpy(), orc.render(soa, cam, W, H, 3.0), exact=True)
+
+
+def test_bucket_sort_frames_in_flight(gpu, orc, torch, tmp_path_factory):
+    """Four lanes over an orbit (each lane's splitters come from its own previous frame):
+    every frame equals the oracle's."""
+    from gaussianrenderer_amd import multi
+    _, soa = scene_soa(gpu, tmp_path_factory, 100_000, 8)
+    W, H = 640, 480
+    cams = [multi.orbit_camera(i % 8, W, H) for i in range(12)]
+    scene = gpu.Scene.from_soa(soa)
+    r = renderer(gpu)
+    r.set_frames_in_flight(4)
+    outs = [torch.empty(3 * W * H, device="cuda") for _ in cams]
+    for _ in range(3):
+        rc = r.render_path(scene, cams, W, H, [o.data_ptr() for o in outs])
+        if r.sync() == 0 and rc == 0:
+            break
+    for cam, o in zip(cams, outs):
+        assert_image_parity(o.view(3, H, W).cpu().numpy(), orc.render(soa, cam, W, H, 3.0), exact=True)
+
+
+def test_bucket_sort_knob(gpu):
+    r = gpu.Renderer()
+    assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS) == 1
+    with pytest.raises(gpu.GsrError):
+        r.set_tuning(gpu.TUNE_DEPTH_BUCKETS, 3)
+    with pytest.raises(gpu.GsrError):
+        r.set_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER, 0)
+    assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER) == 0
+
+
+def test_bucket_sort_all_culled_then_visible(gpu, orc, torch, tmp_path_factory):
+    """A frame with every Gaussian culled (the camera looks away: every item in the last
+    bucket, no live quantiles) between visible frames: each frame's order is exact."""
+    _, soa = scene_soa(gpu, tmp_path_factory, 20_000, 9)
+    W, H = 320, 240
+    n = soa.shape[1]
+    scene = gpu.Scene.from_soa(soa)
+    r = renderer(gpu)
+    render_frames(gpu, torch, r, scene, [cam_for(gpu, W, H)], W, H)   # the LSD frame: first quantiles
+    for cam in (cam_for(gpu, W, H), cam_for(gpu, W, H, pos=(0, 0, 40), look=(0, 0, 80)), cam_for(gpu, W, H),
+                cam_for(gpu, W, H, pos=(0, 0, 12), fov=90)):
+        img = render_frames(gpu, torch, r, scene, [cam], W, H)
+        assert r.depth_passes() == 0
+        want_spl = orc.preprocess(soa, cam, W, H, 3.0)
+        assert np.array_equal(r.read_depth_order(n), orc.expected_depth_order(want_spl))
+        assert_image_parity(img, orc.render(soa, cam, W, H, 3.0), exact=True)

@@ -101,6 +101,7 @@ def _validity_worker(rank, world, port, ply, W, H, q):
     far = gsr.Scene.from_soa(far_soa)
     r = gsr.Renderer()
     r.set_tuning(gsr.TUNE_BLEND_EXP, 0)      # exact blend: the gathered frames are checked bit for bit
+    r.set_tuning(gsr.TUNE_DEPTH_BUCKETS, 0)  # the LSD passes' budget makes the incomplete frames
     r.set_frames_in_flight(2)
     cam = multi.orbit_camera(rank, W, H)
     got, measured = [], [False]

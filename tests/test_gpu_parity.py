@@ -332,6 +332,7 @@ def test_depth_pass_plan_exact(gpu, orc, torch, c1, pos, look):
     orders = []
     for skip in (1, 0):
         r = gpu.Renderer()
+        r.set_tuning(gpu.TUNE_DEPTH_BUCKETS, 0)   # the LSD passes and their device plan
         r.set_tuning(6, skip)
         got, _ = render_gpu(gpu, torch, scene, cam, W, H, renderer=r)
         assert_image_parity(got, orc.render(soa, cam, W, H, 3.0))
@@ -400,6 +401,7 @@ def test_depth_pass_budget_adapts_and_recovers(gpu, orc, torch, c1):
     near = cam_for(gpu, W, H, pos=(0, 0, 4))
     far = cam_for(gpu, W, H, pos=(0, 0, 17.3))
     r = gpu.Renderer()
+    r.set_tuning(gpu.TUNE_DEPTH_BUCKETS, 0)       # the LSD passes' budget (the bucket sort has none)
     out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
     for i in range(8):
         r.render(scene, near, W, H, out.data_ptr())

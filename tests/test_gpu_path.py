@@ -311,6 +311,7 @@ def test_frameshard_reports_depth_budget_overflow(gpu, orc, torch, c1):
     far_soa[2] = np.linspace(-90.0, 1.0, soa.shape[1], dtype=np.float32)   # keys up to ~9.4e7 > 2^24
     far = gpu.Scene.from_soa(far_soa)
     r = gpu.Renderer()
+    r.set_tuning(gpu.TUNE_DEPTH_BUCKETS, 0)              # the LSD passes' budget (the bucket sort has none)
     r.set_frames_in_flight(F)
     cam = cam_for(gpu, W, H)
     shard = multi.FrameShard(None, r, near, cam, W, H, steps=4, gather="none", inflight=F)
