@@ -92,10 +92,13 @@ def parse():
     return ap.parse_args()
 
 
-def algorithmic_blend_bytes(ntiles: int, consumed: int, W: int, H: int) -> int:
-    """SURVEY.md 8d blend row for this design: T*8 (tile ranges) + Pc*(4 index + 48 record)
-    + 12*W*H (planar fp32 image)."""
-    return 8 * ntiles + 52 * consumed + 12 * W * H
+def algorithmic_blend_bytes(ntiles: int, consumed: int, W: int, H: int, record: int = 48) -> int:
+    """SURVEY.md 8d blend row: T*8 (tile ranges) + Pc*(4 index + 48 record) + 12*W*H
+    (planar fp32 image) -- the roofline's `achieved`.  This design's blend gathers the
+    whole 64-B splat record (4 x 16 B: conic, opacity + colour, centre + pixel box, cull
+    word; gsr_kernels.hip k_blend_w), 68 B per pair: record=64 gives that figure
+    (`algorithmic_bytes_design` beside it)."""
+    return 8 * ntiles + (4 + record) * consumed + 12 * W * H
 
 
 def algorithmic_stage_bytes(n: int, m: int, pairs: int, ntiles: int, consumed: int, W: int, H: int,
@@ -618,6 +621,8 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None, "avg_launch_ms": round(blend_avg_ms, 4),
                      "algorithmic_bytes": bytes_blend,
+                     "algorithmic_bytes_design": algorithmic_blend_bytes(ntiles, consumed, W, H, record=64),
+                     "bytes_per_pair": {"survey": 52, "design": 68},
                      "measured_on": "sequential timed segment (K frames one at a time: the kernel does not share "
                                     "the GPU); avg_launch_ms_inflight = lane 0's launches in the pipelined region",
                      "avg_launch_ms_inflight": round(blend_times_pipe["blend"] / max(1, timed_frames_pipe), 4)},

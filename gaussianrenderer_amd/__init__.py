@@ -516,6 +516,7 @@ TUNE_DEPTH_SPLIT_UNSAT = 25
 TUNE_DEPTH_SPLIT_STATE = 26
 TUNE_DEPTH_BUCKETS = 28
 TUNE_DEPTH_BUCKETS_OVER = 29
+TUNE_BUCKET_ROWS = 30
 
 
 def rank_order_check() -> tuple[int, int]:

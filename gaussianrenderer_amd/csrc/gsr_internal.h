@@ -156,7 +156,10 @@ constexpr int kMaxBucketGroups = 512;    // chunks (workgroups) of the scatter; 
 hipError_t launch_bucket_sort(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int buckets,
                               int groups, const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
                               const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
-                              unsigned int* over_host, hipStream_t s);
+                              unsigned int* over_host, hipStream_t s, int row_tiles_y = 0);
+// row_tiles_y > 0: the local kernel also writes the row pass's count histograms into hist
+// (512 x (buckets - 1) words: chunk g = bucket g, tile rows < row_tiles_y), and the row pass
+// then runs with cstart = totals + buckets (the buckets' first positions) and no count kernel.
 // Splitters for launch_bucket_sort from an order the LSD passes sorted (depth_sorted of
 // items0 / items1 under dstats); live_dev (nullable): its visible count.
 hipError_t launch_bkt_splitters(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,
@@ -202,7 +205,8 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
                            int items, hipStream_t s, const uint16_t* spans = nullptr, bool rank_atomic = false,
                            uint32_t base = 0, uint32_t* gate = nullptr, int gate_mode = 0,
-                           const uint32_t* cut = nullptr, const RowSplit* rs = nullptr);
+                           const uint32_t* cut = nullptr, const RowSplit* rs = nullptr,
+                           const uint32_t* cstart = nullptr);
 hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, const unsigned long long* row_pairs,
                            uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
                            uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,

@@ -1680,28 +1680,45 @@ constexpr uint32_t kBktTile = kBktThreads * kBktItems;        // 2048
 constexpr uint32_t kBktCap = kBktTile;                        // local sort capacity (items)
 static_assert(kBktCap == kMaxBucketCap && kMaxBuckets == 4096, "gsr_internal.h bucket sort limits");
 
-// The buckets of N keys: bucket(key) = the number of the B - 1 sorted splitters s[0..B-2]
-// that are <= key.  Step by step, so each step's N LDS reads are in flight
-// together (one search per item was N x log2(B) serial LDS round trips: the count kernel
-// spent 7 of its 10 us waiting on them).
-template <int B, int N>
-__device__ __forceinline__ void bkt_of_n(const uint32_t* s, const uint32_t (&key)[N], uint32_t (&bk)[N]) {
-#pragma unroll
-    for (int k = 0; k < N; k++) bk[k] = 0;
-#pragma unroll
-    for (uint32_t st = B / 2; st >= 1; st >>= 1) {
-        uint32_t v[N];
-#pragma unroll
-        for (int k = 0; k < N; k++) v[k] = s[bk[k] + st - 1];
-#pragma unroll
-        for (int k = 0; k < N; k++) bk[k] += v[k] <= key[k] ? st : 0u;
+// The splitters in LDS as an implicit search tree in breadth-first (Eytzinger) order:
+// node i at depth d, position p = i + 1 - 2^d holds the sorted splitter of rank
+// (2p + 1) 2^(h - 1 - d) - 1 (h = log2 B; the B - 1 splitters fill the tree exactly).  Each
+// search step reads one tree level, and a level's nodes are consecutive words.  (The plain
+// sorted array put every address of the first search steps on ONE LDS bank -- b + st - 1
+// with b a multiple of 2 st -- up to 32-way conflicts: the count kernel took 10 us.)
+template <int B>
+__device__ __forceinline__ void bkt_load_splitters(uint32_t* s_T, const uint32_t* __restrict__ splitters) {
+    constexpr int h = __builtin_ctz(B);
+    for (uint32_t i = threadIdx.x; i < (uint32_t)B; i += kBktThreads) {
+        if (i == (uint32_t)B - 1u) {
+            s_T[i] = 0xffffffffu;   // unused (the tree has B - 1 nodes)
+            continue;
+        }
+        const int d = 31 - __clz((int)(i + 1u));
+        const uint32_t p = i + 1u - (1u << d);
+        const uint32_t j = ((2u * p + 1u) << (h - 1 - d)) - 1u;   // sorted rank, <= B - 2
+        s_T[i] = j < (uint32_t)B - 2u ? splitters[j] : 0xffffffffu;
     }
 }
 
-template <int B>
-__device__ __forceinline__ void bkt_load_splitters(uint32_t* s_S, const uint32_t* __restrict__ splitters) {
-    for (uint32_t j = threadIdx.x; j < (uint32_t)B; j += kBktThreads)
-        s_S[j] = j < (uint32_t)B - 2u ? splitters[j] : 0xffffffffu;
+// The buckets of N keys: bucket(key) = the number of the B - 1 sorted splitters that are
+// <= key (the last is 0xFFFFFFFF, so a key 0xFFFFFFFF lands in bucket B - 1), by a walk
+// down the tree of bkt_load_splitters.  Level by level, so each level's N LDS reads are in
+// flight together.
+template <int B, int N>
+__device__ __forceinline__ void bkt_of_n(const uint32_t* s_T, const uint32_t (&key)[N], uint32_t (&bk)[N]) {
+#pragma unroll
+    for (int k = 0; k < N; k++) bk[k] = 0;
+#pragma unroll
+    for (int lvl = 0; lvl < __builtin_ctz(B); lvl++) {
+        uint32_t v[N];
+#pragma unroll
+        for (int k = 0; k < N; k++) v[k] = s_T[bk[k]];
+#pragma unroll
+        for (int k = 0; k < N; k++) bk[k] = 2u * bk[k] + (v[k] <= key[k] ? 2u : 1u);
+    }
+#pragma unroll
+    for (int k = 0; k < N; k++) bk[k] -= (uint32_t)B - 1u;
 }
 
 template <int B>
@@ -1948,6 +1965,46 @@ __device__ __forceinline__ void bkt_write_splitters(uint32_t start, uint32_t cou
     }
 }
 
+// Row-pass histograms of one chunk of the depth order (k_bin_rows_count's, for the chunk
+// of the bucket this workgroup sorted): per tile row the row items and the pairs of its
+// rects, as difference arrays in LDS (per wave), then a prefix over the rows.
+// hist[row][g] and hist[256 + row][g], rows < tiles_y.
+struct RowHist {
+    uint32_t* hist;      // nullptr: not fused (the row pass counts for itself)
+    int groups;          // the row pass's chunks: the live buckets (B - 1)
+    int tiles_y;
+};
+
+__device__ __forceinline__ void row_hist_add(uint32_t (*h_items)[256], uint32_t (*h_pairs)[256], uint32_t w,
+                                             uint32_t packed) {
+    const uint64_t r = unpack_rect(packed);
+    if (rect_count(r)) {
+        const uint32_t ty0 = (uint32_t)((r >> 32) & 0xffffu), ty1 = (uint32_t)(r >> 48);
+        const uint32_t cols = rect_cols(r);
+        atomicAdd(&h_items[w][ty0], 1u);
+        atomicAdd(&h_pairs[w][ty0], cols);
+        if (ty1 < 255u) {
+            atomicSub(&h_items[w][ty1 + 1], 1u);
+            atomicSub(&h_pairs[w][ty1 + 1], cols);
+        }
+    }
+}
+
+__device__ __forceinline__ void row_hist_write(const RowHist& rh, uint32_t g, uint32_t (*h_items)[256],
+                                               uint32_t (*h_pairs)[256], uint32_t* s_scr) {
+    const uint32_t t = threadIdx.x;
+    __syncthreads();
+    const uint32_t di = h_items[0][t] + h_items[1][t] + h_items[2][t] + h_items[3][t];
+    const uint32_t dp = h_pairs[0][t] + h_pairs[1][t] + h_pairs[2][t] + h_pairs[3][t];
+    uint32_t ti, tp;
+    const uint32_t ci = block_exclusive_scan<uint32_t>(di, s_scr, ti) + di;
+    const uint32_t cp = block_exclusive_scan<uint32_t>(dp, s_scr, tp) + dp;
+    if (t < (uint32_t)rh.tiles_y) {
+        rh.hist[t * (uint32_t)rh.groups + g] = ci;
+        rh.hist[(256 + t) * (uint32_t)rh.groups + g] = cp;
+    }
+}
+
 // One workgroup per live bucket (grid B - 1).  bstart: the buckets' first positions
 // (k_bkt_scatter); s_in: the splitters this frame was bucketed by, which bound the keys of
 // every bucket but the first and the last (their key span sets the passes).  cap: buckets
@@ -1959,11 +2016,12 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
                                                            const uint32_t* __restrict__ bstart,
                                                            const uint32_t* __restrict__ s_in,
                                                            uint32_t* __restrict__ s_next, uint32_t cap,
-                                                           unsigned int* over_host) {
+                                                           unsigned int* over_host, RowHist rh) {
     GSR_GEOM_PRIO();
     __shared__ uint64_t s_items[kBktTile];
     __shared__ uint32_t s_pay[kBktTile];
     __shared__ uint32_t s_wc[4][256], s_lbase[256], s_gb[256];
+    __shared__ uint32_t s_hp[4][256];   // fused row-pass count: pairs (s_wc holds the items)
     __shared__ uint32_t s_scr[4], s_mm[2];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint32_t bkt = blockIdx.x;
@@ -1976,7 +2034,20 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
         if (live == 0)
             for (uint32_t j = 0; j < (uint32_t)B - 2u; j++) s_next[j] = 0;   // any sorted splitters will do
     }
-    if (count == 0) return;
+    auto row_zero = [&]() {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            s_wc[k][t] = 0;
+            s_hp[k][t] = 0;
+        }
+    };
+    if (count == 0) {   // uniform; an empty bucket is an empty row-pass chunk
+        if (rh.hist) {
+            row_zero();
+            row_hist_write(rh, bkt, s_wc, s_hp, s_scr);
+        }
+        return;
+    }
     uint64_t* const seg = items + start;
     uint32_t* const pseg = pay + start;
     const uint32_t wbase = w * 64 * kBktItems;
@@ -2044,6 +2115,14 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
                 pseg[el] = pv[k];
                 s_items[el] = it[k];
             }
+        }
+        if (rh.hist) {   // the bucket is the row pass's chunk: its row histograms from the rects
+            row_zero();
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kBktItems; k++)
+                if (wbase + k * 64 + lane < count) row_hist_add(s_wc, s_hp, w, pv[k]);
+            row_hist_write(rh, bkt, s_wc, s_hp, s_scr);
         }
         __syncthreads();
         if (bkt < (uint32_t)B - 1u)
@@ -2136,6 +2215,12 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
         }
         __threadfence();
         __syncthreads();
+    }
+    if (rh.hist) {
+        row_zero();
+        __syncthreads();
+        for (uint32_t i = t; i < count; i += kBktThreads) row_hist_add(s_wc, s_hp, w, pseg[i]);
+        row_hist_write(rh, bkt, s_wc, s_hp, s_scr);
     }
     if (bkt < (uint32_t)B - 1u)
         bkt_write_splitters<B>(start, count, live, s_next, [&](uint32_t q) { return (uint32_t)(seg[q] >> 32); });
@@ -2405,7 +2490,8 @@ __global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(co
                                                            const uint16_t* __restrict__ spans, uint32_t base,
                                                            const uint32_t* __restrict__ gate,
                                                            const uint32_t* __restrict__ cut, int cut_mode,
-                                                           const uint32_t* __restrict__ cut_n) {
+                                                           const uint32_t* __restrict__ cut_n,
+                                                           const uint32_t* __restrict__ cstart) {
     GSR_GEOM_PRIO();
     if (gate && *gate == 0u) return;
     row_range(base, n, cut, cut_mode, cut_n);
@@ -2425,7 +2511,12 @@ __global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(co
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     uint64_t b, e;
     const int chunk = (int)blockIdx.x;
-    chunk_range(n, groups, chunk, kRowSources, b, e);
+    if (cstart) {   // the chunks are the bucket sort's buckets (k_bkt_local counted them)
+        b = min(cstart[chunk], n);
+        e = min(cstart[chunk + 1], n);
+    } else {
+        chunk_range(n, groups, chunk, kRowSources, b, e);
+    }
     const uint64_t* sorted = depth_sorted(items0, items1, dstats) + base;
     const uint32_t* srect = depth_sorted_rects(pay0, pay1, dstats) + base;
     // thread t owns sources 4t .. 4t+3 of a sub-chunk (source order): packed rect, index
@@ -3743,7 +3834,9 @@ template <int B>
 static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int groups,
                           const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
                           const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
-                          unsigned int* over_host, hipStream_t s) {
+                          unsigned int* over_host, hipStream_t s, int row_tiles_y) {
+    // fused row-pass count: the row hist overwrites the bucket hist, which only the scatter reads
+    const RowHist rh{row_tiles_y > 0 ? hist : nullptr, B - 1, row_tiles_y};
     uint32_t* bstart = totals + B;   // B + 1 words after the totals
     hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist);
     hipLaunchKernelGGL(k_bkt_scan<B>, dim3(B / 64), dim3(1024), 0, s, hist, groups, totals);
@@ -3751,30 +3844,31 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
         hipLaunchKernelGGL((k_bkt_scatter<B, true>), dim3(groups), dim3(kBktThreads), 0, s, in, items0, n, s_in,
                            groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart);
         hipLaunchKernelGGL((k_bkt_local<B, true>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0, pay1,
-                           static_cast<const uint32_t*>(bstart), s_in, s_out, cap, over_host);
+                           static_cast<const uint32_t*>(bstart), s_in, s_out, cap, over_host, rh);
     } else {
         hipLaunchKernelGGL((k_bkt_scatter<B, false>), dim3(groups), dim3(kBktThreads), 0, s, in, items0, n, s_in,
                            groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart);
         hipLaunchKernelGGL((k_bkt_local<B, false>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0, pay1,
-                           static_cast<const uint32_t*>(bstart), s_in, s_out, cap, over_host);
+                           static_cast<const uint32_t*>(bstart), s_in, s_out, cap, over_host, rh);
     }
 }
 
 hipError_t launch_bucket_sort(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int buckets,
                               int groups, const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
                               const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
-                              unsigned int* over_host, hipStream_t s) {
+                              unsigned int* over_host, hipStream_t s, int row_tiles_y) {
     if (groups < 1 || groups > kBktMaxGroups || (int64_t)groups * buckets > 256 * (int64_t)kMaxSortGroups || cap < 1 ||
         cap > kBktCap ||
         in == items0 || !rect || !pay0 || !pay1)   // in may be items1: the scratch is used after the scatter
         return hipErrorInvalidValue;
-    if (n == 0) return hipSuccess;
+    if (n == 0 || row_tiles_y > 256 || (int64_t)512 * (buckets - 1) > 256 * (int64_t)kMaxSortGroups)
+        return n == 0 ? hipSuccess : hipErrorInvalidValue;
     switch (buckets) {
-    case 256: bucket_sort_b<256>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s); break;
-    case 512: bucket_sort_b<512>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s); break;
-    case 1024: bucket_sort_b<1024>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s); break;
-    case 2048: bucket_sort_b<2048>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s); break;
-    case 4096: bucket_sort_b<4096>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s); break;
+    case 256: bucket_sort_b<256>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y); break;
+    case 512: bucket_sort_b<512>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y); break;
+    case 1024: bucket_sort_b<1024>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y); break;
+    case 2048: bucket_sort_b<2048>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y); break;
+    case 4096: bucket_sort_b<4096>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -3825,7 +3919,8 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
                            uint32_t* row_items,
                            unsigned long long* row_pairs, uint32_t pair_capacity, int tiles_y, uint64_t* rows_buf,
                            int items, hipStream_t s, const uint16_t* spans, bool rank_atomic, uint32_t base,
-                           uint32_t* gate, int gate_mode, const uint32_t* cut, const RowSplit* rs) {
+                           uint32_t* gate, int gate_mode, const uint32_t* cut, const RowSplit* rs,
+                           const uint32_t* cstart) {
     const int cut_mode = rs ? rs->cut_mode : 0;
     if (tiles_y < 1 || tiles_y > 256 || groups < 1 || groups > kMaxSortGroups / 2 ||
         (items != 4 && items != 8 && items != 16) || (gate_mode != 0 && !gate) || gate_mode < 0 || gate_mode > 2 ||
@@ -3833,8 +3928,10 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
         return hipErrorInvalidValue;
     const uint32_t* g = gate_mode == 2 ? gate : nullptr;
     const uint32_t* cut_n = rs ? rs->cut_n : nullptr;
-    hipLaunchKernelGGL(k_bin_rows_count, dim3(groups), dim3(256), 0, s, n, pay0, pay1, dstats, groups, tiles_y,
-                       hist, base, g, cut, cut_mode, cut_n);
+    if (cstart && (cut_mode != 0 || gate_mode != 0 || base != 0)) return hipErrorInvalidValue;
+    if (!cstart)   // with bucket chunks the bucket sort's local kernel wrote the counts
+        hipLaunchKernelGGL(k_bin_rows_count, dim3(groups), dim3(256), 0, s, n, pay0, pay1, dstats, groups, tiles_y,
+                           hist, base, g, cut, cut_mode, cut_n);
     hipLaunchKernelGGL(k_bin_rows_scan, dim3(256), dim3(256), 0, s, hist, groups, tiles_y, row_items, row_pairs,
                        gate, gate_mode);
     auto pick = [&](auto ra) {
@@ -3846,7 +3943,8 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
     };
     auto scatter = rank_atomic ? pick(std::true_type{}) : pick(std::false_type{});
     hipLaunchKernelGGL(scatter, dim3(groups), dim3(256), 0, s, items0, items1, dstats, pay0, pay1, n, groups, hist,
-                       row_items, row_pairs, pair_capacity, tiles_y, rows_buf, spans, base, g, cut, cut_mode, cut_n);
+                       row_items, row_pairs, pair_capacity, tiles_y, rows_buf, spans, base, g, cut, cut_mode, cut_n,
+                       cstart);
     return hipGetLastError();
 }
 

@@ -435,6 +435,7 @@ struct gsr_context {
     bool rank_ok = false;            // the device passed the rank-order self-check (ensure_static)
     bool overflow_seen = false;      // an overflow was reported since the last gsr_sync (which reports it again)
     // bucket depth sort (GSR_TUNE_DEPTH_BUCKETS, gsr_kernels.hip "bucket depth sort")
+    int fuse_rows = 1;               // GSR_TUNE_BUCKET_ROWS: the bucket sort's local kernel counts the row pass
     int bucket_sort = 1;             // 0 = LSD passes; 1 = bucket sort after the context's first frame;
                                      // 2 = test hook: as 1 with a local capacity of 64 items (most
                                      // buckets take the global path)
@@ -443,6 +444,8 @@ struct gsr_context {
     int bkt_B = 0;                   // buckets the splitters were made for (0: none yet)
     bool bds_frame = false;          // this frame's preprocess items went to items[1] for the bucket sort
     bool last_bds = false;           // the last sorted frame was bucket-sorted (order in items[0], no pass plan)
+    bool bkt_rows_fused = false;     // its local sorts wrote the row pass's counts (bucket = row chunk): the
+                                     // next binning skips its count kernel (once: the row scan consumes them)
     uint32_t* fstatus = nullptr;     // the current frame's validity word (gsr_render_path_status; device,
                                      // nullable): GSR_FRAME_* bits, written by its column scans / blend
     // frame state
@@ -1008,19 +1011,25 @@ static uint32_t* pay_buf(gsr_context* c, int b) {
 // Global stable depth sort of the preprocess items (key << 32 | index), 4 x 8-bit
 // passes with the device-side pass plan; with rects (binning) the passes carry them and
 // leaves them in depth order (pay_buf(c, passes run & 1)).  Result in items[passes run & 1].
-static int depth_sort_locked(gsr_context* c, bool with_rects) {
+static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false) {
     const uint32_t n = (uint32_t)c->n;
+    c->bkt_rows_fused = false;
     // bucket depth sort: the first sort of a frame whose preprocess prepared for it (a
     // repeated sort of the frame takes the LSD passes over the sorted items[0])
     if (with_rects && !c->split_key && c->bds_frame && !c->have_sort && c->pre_out != c->items[0]) {
         const int B = c->bkt_B;
         const int G = std::min(groups_for(c->n, gsr::kMaxBucketCap), gsr::kMaxBucketGroups);
+        // a plain frame (one binning over the whole order): the local sorts also count the
+        // row pass's items and pairs per bucket, which becomes the row pass's chunk
+        const bool fuse = plain && c->fuse_rows && (int64_t)512 * (B - 1) <= 256 * (int64_t)gsr::kMaxSortGroups;
         uint32_t* s_in = c->bkt_split + (size_t)c->bkt_par * gsr::kMaxBuckets;
         uint32_t* s_out = c->bkt_split + (size_t)(c->bkt_par ^ 1) * gsr::kMaxBuckets;
         HIP_TRY(gsr::launch_bucket_sort(c->pre_out, c->items[0], c->items[1], n, B, G, s_in, s_out, c->hist,
                                         c->totals, reinterpret_cast<const uint32_t*>(c->rect), pay_buf(c, 0),
                                         pay_buf(c, 1), rank_atomic_on(c), c->bucket_sort == 2 ? 64u : gsr::kMaxBucketCap,
-                                        c->hstats_dev ? &c->hstats_dev->bkt_over : nullptr, c->stream));
+                                        c->hstats_dev ? &c->hstats_dev->bkt_over : nullptr, c->stream,
+                                        fuse ? c->fr.tiles_y : 0));
+        c->bkt_rows_fused = fuse;
         c->bkt_par ^= 1;
         c->last_bds = true;
         c->last_compact = false;
@@ -1155,12 +1164,16 @@ static int bin_locked(gsr_context* c, uint32_t base, uint32_t count, int gate_mo
     const int gb = std::min(groups_for(est, 1024), gsr::kMaxSortGroups / 2);
     // (a bucket-sorted frame has no pass plan: its order is in items[0], its rects in pay_buf 0)
     uint32_t* dst = c->depth_skip && !(c->last_bds && !far) ? (far ? c->dstats_far : c->dstats) : nullptr;
+    // after a bucket-sorted plain frame the buckets are the row chunks and their counts exist
+    const bool fused = c->bkt_rows_fused && gate_mode == 0 && base == 0 && !rs && !far && count == (uint32_t)c->n;
+    c->bkt_rows_fused = false;
+    const uint32_t* cstart = fused ? c->totals + c->bkt_B : nullptr;
     HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], dst, count, pay_buf(c, 0),
-                                 pay_buf(c, 1), gb,
+                                 pay_buf(c, 1), fused ? c->bkt_B - 1 : gb,
                                  c->hist, row_items, row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items,
                                  c->stream, c->spans_frame ? c->spans : nullptr, rank_atomic_on(c), base,
                                  gate_mode ? c->gate : nullptr, gate_mode, rs && rs->cut_mode ? c->nlive : nullptr,
-                                 rs));
+                                 rs, cstart));
     if (marks) mark(c, GSR_STAGE_TILE_SORT);
     // column-pass workgroups: ~one 2048-item chunk each (config 3: 2048-4096 groups 12 us
     // faster than 1024; config 2: 1024 best, profiles/r02_ab_col_groups.txt)
@@ -1204,7 +1217,7 @@ static int sort_locked(gsr_context* c, bool allow_split) {
     // ---- stable depth sort of (key << 32 | index), 4 x 8 bits; for the binning
     // path the passes carry the rects, depth-ordered at the end (pay_buf) ----
     mark(c, GSR_STAGE_DEPTH_SORT);
-    if (int rc = depth_sort_locked(c, bin)) return rc;
+    if (int rc = depth_sort_locked(c, bin, bin && !split)) return rc;
     // result in items[passes run & 1] (device-side plan; emission picks it)
     if (bin) {
         // depth split: phase A bins the near part (blend_locked blends it, then sorts
@@ -1395,6 +1408,7 @@ void copy_settings(gsr_context* d, const gsr_context* s) {
     d->tile_items = s->tile_items;
     d->depth_items = s->depth_items;
     d->bucket_sort = s->bucket_sort;
+    d->fuse_rows = s->fuse_rows;
     d->tile_groups = s->tile_groups;
     d->tile_split_even = s->tile_split_even;
     d->depth_skip = s->depth_skip;
@@ -1859,6 +1873,7 @@ extern "C" int gsr_get_tuning(gsr_context* c, int knob, int* value) {
     case GSR_TUNE_DEPTH_SPLIT_UNSAT: *value = c->hstats ? (int)((const volatile Stats*)c->hstats)->split_unsat : 0; break;
     case GSR_TUNE_DEPTH_SPLIT_STATE: *value = !c->split_frame ? 0 : !c->frame_key ? 1 : c->frame_spec ? 3 : 2; break;
     case GSR_TUNE_DEPTH_BUCKETS: *value = c->bucket_sort; break;
+    case GSR_TUNE_BUCKET_ROWS: *value = c->fuse_rows; break;
     case GSR_TUNE_DEPTH_BUCKETS_OVER: {
         int64_t v = c->hstats ? (int64_t)((const volatile Stats*)c->hstats)->bkt_over : 0;
         for (auto* l : c->lanes) v += l->hstats ? (int64_t)((const volatile Stats*)l->hstats)->bkt_over : 0;
@@ -1963,6 +1978,9 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     case GSR_TUNE_DEPTH_BUCKETS:
         if (value < 0 || value > 2) return set_err(GSR_E_ARG, "gsr_set_tuning: depth buckets must be 0, 1 or 2");
         c->bucket_sort = value;
+        return GSR_OK;
+    case GSR_TUNE_BUCKET_ROWS:
+        c->fuse_rows = value != 0;
         return GSR_OK;
     case GSR_TUNE_RANK_ATOMIC_ACTIVE:
     case GSR_TUNE_DEPTH_SPLIT_UNSAT:

@@ -384,9 +384,14 @@ enum {
                                         takes the quantiles from them.  0 = LSD passes only; 2 = test
                                         hook: 1 with a 64-item local capacity.  Same order, same image;
                                         gsr_depth_passes is 0 after a bucket-sorted frame */
-    GSR_TUNE_DEPTH_BUCKETS_OVER = 29 /* read-only: items the bucket sort's global path has sorted (buckets
+    GSR_TUNE_DEPTH_BUCKETS_OVER = 29, /* read-only: items the bucket sort's global path has sorted (buckets
                                         over the local capacity), summed over the lanes; sticky, read
                                         after gsr_sync */
+    GSR_TUNE_BUCKET_ROWS = 30        /* 1 (default): on a bucket-sorted frame binned once over the whole
+                                        depth order, each bucket's workgroup also counts the row pass's
+                                        items and pairs (the bucket is the row pass's chunk), so the row
+                                        pass runs without its count kernel; 0 = the row pass counts.
+                                        Same lists, same image */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Current value of a knob (what gsr_set_tuning last set, else the default). */

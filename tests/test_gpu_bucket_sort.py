@@ -268,3 +268,29 @@ def test_bucket_sort_all_culled_then_visible(gpu, orc, torch, tmp_path_factory):
         want_spl = orc.preprocess(soa, cam, W, H, 3.0)
         assert np.array_equal(r.read_depth_order(n), orc.expected_depth_order(want_spl))
         assert_image_parity(img, orc.render(soa, cam, W, H, 3.0), exact=True)
+
+
+def test_bucket_rows_fused_matches_row_count(gpu, orc, torch, tmp_path_factory):
+    """GSR_TUNE_BUCKET_ROWS: the local sorts count the row pass per bucket (the bucket is the
+    row chunk) and the row pass skips its count kernel; with 0 the row pass counts its own
+    fixed chunks.  Same tile lists, same image, also with the global path (hook 2), whose
+    buckets are larger than a row chunk."""
+    _, soa = scene_soa(gpu, tmp_path_factory, 200_000, 12)
+    W, H = 1280, 720
+    scene = gpu.Scene.from_soa(soa)
+    cams = [cam_for(gpu, W, H)] * 2
+    got = {}
+    for hook in (1, 2):
+        for fused in (1, 0):
+            r = renderer(gpu, hook)
+            r.set_tuning(gpu.TUNE_BUCKET_ROWS, fused)
+            img = render_frames(gpu, torch, r, scene, cams, W, H)
+            assert r.depth_passes() == 0
+            got[(hook, fused)] = (img, r.read_pairs(), r.read_tile_ranges())
+            r.close()
+    base = got[(1, 0)]
+    for key, (img, pairs, ranges) in got.items():
+        assert np.array_equal(pairs, base[1]), key
+        assert np.array_equal(ranges, base[2]), key
+        assert np.array_equal(img.view(np.uint32), base[0].view(np.uint32)), key
+    assert_image_parity(base[0], orc.render(soa, cams[-1], W, H, 3.0, threads=THREADS), exact=True)

@@ -95,7 +95,7 @@ for step in ${STEPS:-suite smoke bench}; do
   ktab)
     for t in ${TUNES:-19=0 19=1}; do
       tg=$(echo "$t" | tr '=,' '__'); O=gpurun_out/kt_ab_$tg; mkdir -p $O
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 bench.py --config ${CONFIGS:-2} --steps 60 --warmup 5 --no-cpu-baseline --inflight 1 --warm-ms 200 --tune "$t" > $O/kt.log 2>&1
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 bench.py --config ${CONFIGS:-2} --steps 60 --warmup 5 --no-cpu-baseline --no-sh3-line --inflight 1 --warm-ms 200 --tune "$t" > $O/kt.log 2>&1
       rc=$?; echo "tune $t kt rc=$rc"; fatal $rc ktab; [ $rc = 0 ] || exit $rc
       python3 tools/summarize_prof.py $O > $O/summary.txt 2>&1; echo "== $t"; head -16 $O/summary.txt
     done ;;

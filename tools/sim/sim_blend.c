@@ -29,11 +29,11 @@ static inline float alpha_at(const Sp* s, int px, int py) {
 }
 
 /* out[0] = splat-slot iterations, out[1] = taken lanes, out[2] = in-box live lanes,
- * out[3] = records loaded (batches * entries) */
+ * out[3] = records loaded (batches * entries), out[4] = batches */
 void sim(const float* rec /* n x 11 */, const int* lists, const int* offs, int nblocks, const int* bxy,
          int G, int B, int pairs, int cullmode, double* out) {
-    double it = 0, taken = 0, active = 0, loaded = 0;
-#pragma omp parallel for schedule(dynamic, 64) reduction(+ : it, taken, active, loaded)
+    double it = 0, taken = 0, active = 0, loaded = 0, batches = 0;
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : it, taken, active, loaded, batches)
     for (int blk = 0; blk < nblocks; blk++) {
         const int bx = bxy[2 * blk], by = bxy[2 * blk + 1];
         float T[64];
@@ -43,6 +43,7 @@ void sim(const float* rec /* n x 11 */, const int* lists, const int* offs, int n
         for (int base = beg; base < end && alive; base += B) {
             const int cnt = end - base < B ? end - base : B;
             loaded += cnt;
+            batches += 1;
             /* per-group survivor lists (lane group g covers lanes with grp(l) == g) */
             int surv[64][256];
             int ns[64];
@@ -157,4 +158,5 @@ void sim(const float* rec /* n x 11 */, const int* lists, const int* offs, int n
     out[1] = taken;
     out[2] = active;
     out[3] = loaded;
+    out[4] = batches;
 }
