@@ -564,6 +564,7 @@ def main():
         elapsed, blend_times_pipe, timed_frames_pipe = seq_elapsed, blend_times, timed_frames
     overflow = r.sync() or seq_overflow
     split_after = (r.get_tuning(26), r.get_tuning(24))   # depth split state and point after the timed frames
+    bucket_over = r.get_tuning(29)   # items the bucket sort's global path sorted so far (all lanes, sticky)
     telemetry_after = gpu_telemetry(pci) if rank == 0 else None
 
     max_elapsed = multi.max_over_ranks(dist, elapsed, "cpu" if gloo else "cuda")
@@ -643,6 +644,7 @@ def main():
         "depth_passes": depth_passes,
         "depth_sort": ("bucket sort: stable scatter into depth-quantile buckets + one LDS sort per bucket "
                        "(GSR_TUNE_DEPTH_BUCKETS)" if depth_passes == 0 else f"{depth_passes} LSD radix passes"),
+        "depth_bucket_global_items": bucket_over,
         "pairs_consumed": consumed,
         "blend_exp": {1: "fast (v_exp_f32 alpha, exact alpha tests, guarded T tests, exact re-blend of "
                          "suspect pixels)", 0: "exact (gsr_blend_expf)"}[min(blend_exp, 1)],

@@ -504,6 +504,13 @@ int bkt_count(int64_t n) {
     return b;
 }
 
+// The bucket sort pays up to 2,048 buckets (n <= 2M: config 2 one frame at a time +7.7 %,
+// config 5 +9.7 %).  At 5M Gaussians (config 3) its scatter runs ~10K items per workgroup
+// through five serial tiles (the histogram caps the workgroups at 512) and measured 244 us
+// against the LSD passes' 186 (profiles/r05_kt_c3_orbit.txt): the LSD passes stay there.
+constexpr int64_t kBucketSortMaxN = (int64_t)2048 * 1024;
+bool bkt_applies(int64_t n) { return n > 0 && n <= kBucketSortMaxN; }
+
 int groups_for(int64_t n, int64_t per) {
     int64_t g = (n + per - 1) / per;
     return (int)std::max<int64_t>(1, std::min<int64_t>(g, gsr::kMaxSortGroups));
@@ -949,7 +956,7 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     // bucket depth sort (splitters exist for this scene size): the items go to items[1], the
     // sort writes the order into items[0]; it keeps culled items apart itself, so it
     // replaces the live partition
-    c->bds_frame = n > 0 && !c->split_key && c->bucket_sort && c->bkt_B == bkt_count(n) && c->tile_binning &&
+    c->bds_frame = bkt_applies(n) && !c->split_key && c->bucket_sort && c->bkt_B == bkt_count(n) && c->tile_binning &&
                    c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
     c->compact_frame = n > 0 && !c->split_key && !c->bds_frame &&
                        (c->depth_compact == 1 || (c->depth_compact == 2 && layout == GSR_LAYOUT_SCENE_BLOCK_4D)) &&
@@ -1096,7 +1103,7 @@ static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false
     }
     // the bucket sort's first splitters: quantiles of this whole sorted order (the next
     // frame of this scene size is bucket-sorted)
-    if (with_rects && !key && c->bucket_sort && c->bkt_B != bkt_count(c->n)) {
+    if (with_rects && !key && c->bucket_sort && bkt_applies(c->n) && c->bkt_B != bkt_count(c->n)) {
         const int B = bkt_count(c->n);
         HIP_TRY(gsr::launch_bkt_splitters(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n,
                                           part ? c->nlive : nullptr, B,

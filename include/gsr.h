@@ -375,7 +375,8 @@ enum {
        histograms in 512-thread workgroups of 2048 Gaussians, pass 0 without its upsweep launch:
        preprocess 49.4 -> 60.3 us against the 5.7-us upsweep, -1.1 % one frame at a time and
        -1.2 % in flight, profiles/r04_ab_pre_hist.txt) */
-    GSR_TUNE_DEPTH_BUCKETS = 28,     /* binning path, frames not split by a depth threshold: 1 (default) =
+    GSR_TUNE_DEPTH_BUCKETS = 28,     /* binning path, frames not split by a depth threshold, scenes of at
+                                        most 2,097,152 Gaussians (larger ones keep the LSD passes): 1 (default) =
                                         bucket depth sort: one stable scatter of the preprocess order into
                                         ~n/1024 depth buckets bounded by the previous frame's quantiles,
                                         then one workgroup per bucket sorts it in LDS (buckets over 2,048

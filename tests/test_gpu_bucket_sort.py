@@ -294,3 +294,14 @@ def test_bucket_rows_fused_matches_row_count(gpu, orc, torch, tmp_path_factory):
         assert np.array_equal(ranges, base[2]), key
         assert np.array_equal(img.view(np.uint32), base[0].view(np.uint32)), key
     assert_image_parity(base[0], orc.render(soa, cams[-1], W, H, 3.0, threads=THREADS), exact=True)
+
+
+def test_bucket_sort_limited_to_2m(gpu, torch, tmp_path_factory):
+    """Above 2,097,152 Gaussians (config 3's 5M) the LSD passes stay: the bucket sort's
+    scatter measured slower there (profiles/r05_kt_c3_orbit.txt)."""
+    _, soa = scene_soa(gpu, tmp_path_factory, 2_100_000, 13)
+    W, H = 320, 240
+    scene = gpu.Scene.from_soa(soa)
+    r = renderer(gpu)
+    render_frames(gpu, torch, r, scene, [cam_for(gpu, W, H)] * 2, W, H)
+    assert r.depth_passes() >= 1
