@@ -1688,17 +1688,23 @@ static_assert(kBktCap == kMaxBucketCap && kMaxBuckets == 4096, "gsr_internal.h b
 // with b a multiple of 2 st -- up to 32-way conflicts: the count kernel took 10 us.)
 template <int B>
 __device__ __forceinline__ void bkt_load_splitters(uint32_t* s_T, const uint32_t* __restrict__ splitters) {
+    // B / 256 nodes per thread, every load issued before the first LDS write: a rolled
+    // loop waited for each load in turn (four serial memory round trips at B = 1,024)
     constexpr int h = __builtin_ctz(B);
-    for (uint32_t i = threadIdx.x; i < (uint32_t)B; i += kBktThreads) {
-        if (i == (uint32_t)B - 1u) {
-            s_T[i] = 0xffffffffu;   // unused (the tree has B - 1 nodes)
-            continue;
-        }
+    constexpr int kPer = B / kBktThreads;
+    uint32_t v[kPer], jj[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const uint32_t i = threadIdx.x + (uint32_t)k * kBktThreads;
         const int d = 31 - __clz((int)(i + 1u));
         const uint32_t p = i + 1u - (1u << d);
-        const uint32_t j = ((2u * p + 1u) << (h - 1 - d)) - 1u;   // sorted rank, <= B - 2
-        s_T[i] = j < (uint32_t)B - 2u ? splitters[j] : 0xffffffffu;
+        const int sh = h - 1 - d;                               // < 0 only for i = B - 1 (no node)
+        jj[k] = sh >= 0 ? ((2u * p + 1u) << sh) - 1u : (uint32_t)B - 2u;   // sorted rank
+        v[k] = splitters[min(jj[k], (uint32_t)B - 3u)];
     }
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+        s_T[threadIdx.x + (uint32_t)k * kBktThreads] = jj[k] < (uint32_t)B - 2u ? v[k] : 0xffffffffu;
 }
 
 // The buckets of N keys: bucket(key) = the number of the B - 1 sorted splitters that are
