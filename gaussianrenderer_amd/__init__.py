@@ -505,6 +505,8 @@ def device_available() -> bool:
 
 
 # gsr_set_tuning knobs used by the tests and tools (include/gsr.h lists them all)
+TUNE_DEPTH_SORT_ITEMS = 2
+TUNE_DEPTH_SORT_GROUPS = 4
 TUNE_TILE_BINNING = 7
 TUNE_TILE_SPANS = 19
 TUNE_RANK_ATOMIC = 20

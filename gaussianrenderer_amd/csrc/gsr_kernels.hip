@@ -1005,19 +1005,23 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
         uint32_t rk[ITEMS], pv[ITEMS];
         bool kp[ITEMS];   // in the tile and kept (a filtered pass 0 drops the other part)
         const uint32_t wbase = w * 64 * ITEMS;
+        // tile-relative 32-bit offsets from a uniform base: one address VGPR for all ITEMS
+        // loads (64-bit per-item addresses had the 16-item kernel at 164+ VGPRs)
+        const uint64_t* __restrict__ in_t = in + tb;
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
             const uint32_t el = wbase + k * 64 + lane;
-            it[k] = (el < tn) ? in[tb + el] : 0ull;
+            it[k] = (el < tn) ? in_t[el] : 0ull;
         }
-        if (carry) {
+        auto load_pay = [&]() {
+            if (!carry) return;
             // uniform branches: the position-indexed reads must not wait for the item loads
-            const uint32_t* src = pay_in ? pay_in : rect;
+            const uint32_t* src = (pay_in ? pay_in : rect) + tb;
             if (pay_in || rect_direct) {
 #pragma unroll
                 for (int k = 0; k < ITEMS; k++) {
                     const uint32_t el = wbase + k * 64 + lane;
-                    pv[k] = (el < tn) ? src[tb + el] : 0u;
+                    pv[k] = (el < tn) ? src[el] : 0u;
                 }
             } else {
 #pragma unroll
@@ -1026,29 +1030,41 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
                     pv[k] = (el < tn) ? rect[(uint32_t)it[k]] : 0u;
                 }
             }
-        }
+        };
+        // a filtered pass 0 ranks by the payloads; otherwise they are loaded after the
+        // ranking (their latency hides behind the tile scan, and the ranking holds 16 fewer
+        // VGPRs at 16 items per thread)
+        if (FILT) load_pay();
+        uint32_t before[ITEMS];
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             const bool valid = el < tn && (!FILT || sort_keep(sr, K, it[k], pv[k]));
             kp[k] = valid;
             const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
-            uint32_t r = 0;
             // returning atomics at 4-8 items per thread; at 16 (4M+ items) ballot matching
-            // measured faster (config 3 depth sort 163 vs 171 us)
             if (RA && ITEMS < 16) {
-                if (valid) r = atomicAdd(&s_wc[w][d], 1u);
+                rk[k] = valid ? atomicAdd(&s_wc[w][d], 1u) : 0u;
+                before[k] = 0;
             } else {
-                const uint64_t peers = match_peers<8>(d, valid, bits);
-                if (valid) {
-                    const uint32_t before = s_wc[w][d];
-                    r = before + (uint32_t)__popcll(peers & lt_mask);
-                    if ((uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
-                        s_wc[w][d] = before + (uint32_t)__popcll(peers);
-                }
+                // every lane reads its digit's running count and the digit's leader adds the
+                // slot's count without a return: a wave's LDS ops execute in issue order, so
+                // slot k's read sees slots < k and no read is waited on before the next slot
+                // (reading, waiting and writing back per slot serialised 16 LDS round trips)
+                // (digits of fewer than 8 bits are masked: their high ballots match all)
+                const uint64_t peers = match_peers<8>(d, valid, 8);
+                rk[k] = (uint32_t)__popcll(peers & lt_mask);
+                before[k] = s_wc[w][d];
+                if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
+                    atomicAdd(&s_wc[w][d], (uint32_t)__popcll(peers));
+                // the reads are folded in every 4 slots: 16 reads in flight held 16 more
+                // VGPRs (the 16-item kernel at 207, two waves per SIMD)
+                if ((k & 3) == 3)
+#pragma unroll
+                    for (int j = k - 3; j <= k; j++) rk[j] += before[j];
             }
-            rk[k] = r;
         }
+        if (!FILT) load_pay();
         __syncthreads();
         // per digit t: exclusive prefix over the four waves, tile count, tile-local base
         uint32_t tcount, tv;   // tv: the tile's kept items (tn unless filtered)
@@ -1069,10 +1085,16 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
                 const uint32_t slot = s_lbase[d] + s_wc[w][d] + rk[k];
                 s_items[slot] = it[k];
                 if (kPaySlots && carry) s_payd[slot] = pv[k];
+                rk[k] = slot;   // the payload round's slot (the items die here)
             }
         }
         __syncthreads();
-        uint32_t dq[ITEMS];
+        // the digits of the items this thread wrote, four per word: the payload round
+        // rebuilds their destinations from them (16 destinations held across the round
+        // took the 16-item kernel to 179 VGPRs, two workgroups per CU)
+        uint32_t dpk[(ITEMS + 3) / 4];
+#pragma unroll
+        for (int k = 0; k < (ITEMS + 3) / 4; k++) dpk[k] = 0;
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
             const uint32_t q = t + k * kSortThreads;
@@ -1082,7 +1104,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
                 const uint32_t dst = s_gbase[d] + (q - s_lbase[d]);
                 out[dst] = v;
                 if (kPaySlots && carry) pay_out[dst] = s_payd[q];
-                dq[k] = dst;
+                dpk[k / 4] |= d << (8 * (k % 4));
                 if (ranges) {
                     // final pass of the tile sort: the LDS tile is fully sorted, so each
                     // run of one tile key is contiguous; record its global [start, end)
@@ -1100,19 +1122,20 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
             uint32_t* s_pay = reinterpret_cast<uint32_t*>(s_items);
             __syncthreads();
 #pragma unroll
-            for (int k = 0; k < ITEMS; k++) {
-                if (kp[k]) {
-                    const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
-                    s_pay[s_lbase[d] + s_wc[w][d] + rk[k]] = pv[k];
-                }
-            }
+            for (int k = 0; k < ITEMS; k++)
+                if (kp[k]) s_pay[rk[k]] = pv[k];
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < ITEMS; k++) {
                 const uint32_t q = t + k * kSortThreads;
-                if (q < tv) pay_out[dq[k]] = s_pay[q];
+                const uint32_t d = (dpk[k / 4] >> (8 * (k % 4))) & 0xffu;
+                if (q < tv) pay_out[s_gbase[d] + (q - s_lbase[d])] = s_pay[q];
             }
         }
+        // 16 items per thread: one tile per workgroup (launch_radix_pass checks the grid),
+        // so the loop is straight-line code and nothing is hoisted across tiles (the
+        // loop-invariant slot offsets of the write-back held 15 VGPRs for the whole kernel)
+        if (ITEMS == 16) break;
         __syncthreads();
         s_gbase[t] += tcount;
         // next iteration's first barrier orders this update before its use
@@ -3817,7 +3840,9 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
     const SortRange sr{base_dev, gate, filter ? f->kcut : nullptr, filter, filter ? f->count_out : nullptr,
                        filter == 1 ? f->kcut_copy : nullptr, filter == 2 ? f->sat : nullptr, f ? f->sat_w : 0,
                        filter == 2 && f->sat ? rect : nullptr, f && !filter ? f->count : nullptr};
-    // 16 items per thread always rank with ballots (k_radix_downsweep)
+    // 16 items per thread always rank with ballots, one tile per workgroup
+    // (k_radix_downsweep): a grid too small for that sorts 8 per thread
+    if (items == 16 && (uint64_t)groups * kSortTile < (uint64_t)n_host) items = 8;
     if (items == 4 && rank_atomic)
         radix_pass<4, true>(in, out, n_dev, n_host, shift, bits, groups, hist, totals, ranges, dstats, pass, rect,
                             rect_direct, pay0, pay1, s, sr);

@@ -110,3 +110,39 @@ def test_rank_paths_tie_heavy(gpu, orc, torch, tmp_path_factory):
     assert np.unique(live).size <= 7 and live.size > 200_000
     want = orc.render(soa, cam, W, H, 3.0, threads=min(16, os.cpu_count() or 1))
     check_paths(out, want)
+
+
+def test_depth_sort_16_items_one_tile_per_workgroup(gpu, orc, torch, tmp_path_factory):
+    """The 16-items-per-thread downsweep sorts exactly one 4,096-item tile per workgroup
+    (a straight-line kernel: 147 VGPRs instead of 207); launch_radix_pass sorts 8 per
+    thread when the grid is too small for that (GSR_TUNE_DEPTH_SORT_GROUPS caps it).
+    700k Gaussians (the last tile partial) with 16 per thread, 16 with the grid capped at
+    64 workgroups (the 8-item fallback, several tiles per workgroup) and 8 per thread: the
+    same depth order, ties by index, and the image bit-exact against the oracle."""
+    path, soa = scene_soa(gpu, tmp_path_factory, 700_000, 5)
+    n = soa.shape[1]
+    W, H = 1280, 720
+    cam = cam_for(gpu, W, H)
+    scene = gpu.Scene.from_ply(path)
+    want = orc.render(soa, cam, W, H, 3.0, threads=min(16, os.cpu_count() or 1))
+    orders = []
+    for knobs in ({gpu.TUNE_DEPTH_SORT_ITEMS: 16}, {gpu.TUNE_DEPTH_SORT_ITEMS: 16, gpu.TUNE_DEPTH_SORT_GROUPS: 64},
+                  {gpu.TUNE_DEPTH_SORT_ITEMS: 8}):
+        r = exact_blend(gpu.Renderer())
+        r.set_tuning(gpu.TUNE_DEPTH_SPLIT, 0)
+        r.set_tuning(gpu.TUNE_DEPTH_BUCKETS, 0)            # the LSD passes on every frame
+        for k, v in knobs.items():
+            r.set_tuning(k, v)
+        img = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+        for _ in range(3):
+            r.render(scene, cam, W, H, img.data_ptr())
+            if r.sync() == 0:
+                break
+        orders.append(r.read_depth_order(n))
+        assert_image_parity(img.view(3, H, W).cpu().numpy(), want, exact=True)
+        r.close()
+    assert all(np.array_equal(orders[0], o) for o in orders[1:])
+    keys = (orders[0] >> np.uint64(32)).astype(np.uint32)
+    idx = (orders[0] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    tie = keys[1:] == keys[:-1]
+    assert (keys[1:] >= keys[:-1]).all() and (idx[1:][tie] > idx[:-1][tie]).all()
