@@ -55,18 +55,58 @@ __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
 // ------------------------------------------------------------------ helpers
 
+// Cross-lane moves on the DPP path (VALU) instead of ds_bpermute (the LDS crossbar,
+// one LDS round trip per step): a wave64 scan is six dependent VALU ops.  CDNA4 is a
+// GFX9 core, so row_bcast:15 / :31 and wave_shr:1 exist.  Lanes a control does not
+// reach (row start for row_shr, rows outside row_mask) read 0, the identity of every
+// scan below (add, unsigned max, or).
+template <int CTRL, int ROWM, bool BC>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWM, 0xf, BC);
+}
+template <int CTRL, int ROWM, bool BC, typename T>
+__device__ __forceinline__ T dpp_mov(T x) {
+    if constexpr (sizeof(T) == 4) {
+        return (T)dpp_u32<CTRL, ROWM, BC>((uint32_t)x);
+    } else {
+        const uint64_t u = (uint64_t)x;
+        const uint32_t lo = dpp_u32<CTRL, ROWM, BC>((uint32_t)u), hi = dpp_u32<CTRL, ROWM, BC>((uint32_t)(u >> 32));
+        return (T)(((uint64_t)hi << 32) | lo);
+    }
+}
+struct OpAdd {
+    template <typename T>
+    __device__ T operator()(T a, T b) const { return a + b; }
+};
+struct OpMax {
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return max(a, b); }
+};
+struct OpOr {
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; }
+};
+// Inclusive wave64 scan: Hillis-Steele inside each row of 16 lanes (row_shr 1, 2, 4, 8),
+// then row 0's total into row 1 and row 2's into row 3 (row_bcast:15), then rows 0-1's
+// into rows 2-3 (row_bcast:31).
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_incl_scan(T x, Op op) {
+    x = op(x, dpp_mov<0x111, 0xf, true>(x));
+    x = op(x, dpp_mov<0x112, 0xf, true>(x));
+    x = op(x, dpp_mov<0x114, 0xf, true>(x));
+    x = op(x, dpp_mov<0x118, 0xf, true>(x));
+    x = op(x, dpp_mov<0x142, 0xa, false>(x));
+    x = op(x, dpp_mov<0x143, 0xc, false>(x));
+    return x;
+}
+// The value of the lane below (0 at lane 0): wave_shr:1.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x) { return dpp_u32<0x138, 0xf, true>(x); }
+
 // Exclusive scan across a 256-thread workgroup (4 waves).  `scratch` holds 4
 // entries.  Contains two barriers; every thread of the block must call it.
 template <typename T>
 __device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
     const uint32_t lane = lane_id();
     const uint32_t w = threadIdx.x >> 6;
-    T x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        T y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
-    }
+    const T x = wave_incl_scan(v, OpAdd{});
     if (lane == 63) scratch[w] = x;
     __syncthreads();
     T pre = 0, tot = 0;
@@ -81,16 +121,12 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
     return pre + x - v;
 }
 
-// Wave64-wide max / or (every lane gets the result).
+// Wave64-wide max / or (every lane gets the result: lane 63 of the inclusive scan).
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v, OpMax{}), 63);
 }
 __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
-    return v;
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v, OpOr{}), 63);
 }
 
 // [begin, end) of workgroup g when n items are split over `groups` workgroups in
@@ -1426,13 +1462,8 @@ __global__ __launch_bounds__(256) void k_emit_pairs(const uint64_t* __restrict__
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             // inclusive prefix of the round's counts
-            uint32_t incl = cnt[k];
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o, 64);
-                if (lane >= (uint32_t)o) incl += y;
-            }
-            const uint32_t rtot = __shfl(incl, 63, 64);
+            const uint32_t incl = wave_incl_scan(cnt[k], OpAdd{});
+            const uint32_t rtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
             s_incl[w][lane] = incl;
             s_idx[w][lane] = gi[k];
             s_rect[w][lane] = r[k];
@@ -1597,15 +1628,9 @@ __device__ __forceinline__ void bin_tile_owners(const uint32_t (&cnt)[PER], cons
         v[i] = run;
     }
     // exclusive max over the earlier lanes of the wave, then over earlier waves
-    uint32_t x = run;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x = max(x, y);
-    }
+    const uint32_t x = wave_incl_scan(run, OpMax{});
     if (lane == 63) s_wmax[w] = x;
-    uint32_t before = __shfl_up(x, 1, 64);
-    if (lane == 0) before = 0;
+    const uint32_t before = wave_shr1(x);
     __syncthreads();
     uint32_t cin = carry;
     for (uint32_t k = 0; k < w; k++) cin = max(cin, s_wmax[k]);
@@ -2319,16 +2344,11 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_splitters(const uint64_t* _
         run = max(run, v[k]);
         v[k] = run;
     }
-    uint32_t x = run;   // inclusive max over the wave's threads, then over earlier waves
+    // inclusive max over the wave's threads, then over earlier waves
     const uint32_t lane = t & 63u, w = t >> 6;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-        if (lane >= (uint32_t)o) x = max(x, y);
-    }
+    const uint32_t x = wave_incl_scan(run, OpMax{});
     if (lane == 63) s_wmax[w] = x;
-    uint32_t before = (uint32_t)__shfl_up((int)x, 1, 64);
-    if (lane == 0) before = 0;
+    uint32_t before = wave_shr1(x);
     __syncthreads();
     for (uint32_t k = 0; k < w; k++) before = max(before, s_wmax[k]);
 #pragma unroll
