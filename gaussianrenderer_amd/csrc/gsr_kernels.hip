@@ -1582,12 +1582,14 @@ __device__ __forceinline__ uint32_t bin_rank_tile(const uint32_t (&dig)[ITEMS], 
     return tcount;
 }
 
-// Inclusive prefix (in source order) of per-source counts cnt[] (thread t owns
-// sources PER*t .. PER*t + PER-1): writes s_pref, returns each owned source's
-// exclusive start in start[] and the total.  Two barriers.
+// Exclusive starts (in source order) of per-source counts cnt[] (thread t owns sources
+// PER*t .. PER*t + PER-1): returns them in start[] and the total, and writes each with
+// an 8-bit tag (the source's first row or column) to s_ft[s] = start << 8 | tag, so an
+// element reads one word for both (starts stay below 2^24: <= 2,048 sources x 256
+// digits).  Two barriers.
 template <int PER>
-__device__ __forceinline__ uint32_t bin_source_prefix(const uint32_t (&cnt)[PER], uint32_t (&start)[PER],
-                                                      uint32_t* s_pref, uint32_t* s_scr) {
+__device__ __forceinline__ uint32_t bin_source_starts(const uint32_t (&cnt)[PER], uint32_t (&start)[PER],
+                                                      const uint32_t (&tag)[PER], uint32_t* s_ft, uint32_t* s_scr) {
     const uint32_t t = threadIdx.x;
     uint32_t loc = 0;
 #pragma unroll
@@ -1597,8 +1599,8 @@ __device__ __forceinline__ uint32_t bin_source_prefix(const uint32_t (&cnt)[PER]
 #pragma unroll
     for (int i = 0; i < PER; i++) {
         start[i] = run;
+        s_ft[PER * t + i] = (run << 8) | tag[i];
         run += cnt[i];
-        s_pref[PER * t + i] = run;
     }
     return tot;
 }
@@ -2545,17 +2547,18 @@ __global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(co
     if (gate && *gate == 0u) return;
     row_range(base, n, cut, cut_mode, cut_n);
     constexpr uint32_t kTile = 256u * ITEMS;
-    __shared__ uint32_t s_pref[kRowSources], s_idx[kRowSources];
+    // per source: exclusive start << 8 | first tile row; index
+    __shared__ uint32_t s_ft[kRowSources], s_idx[kRowSources];
     // per source: packed rect (pack_rect) | tile row spans << 32 (no LDS beyond the
     // 8 B per source it always had: 6 workgroups per CU)
     __shared__ uint64_t s_rect[kRowSources];
-    // s_own (source owners, read by the generation) and s_l (source slots of the
-    // ranked tile, written after the ranking) share storage: their lives do not overlap
-    __shared__ uint16_t s_own[kTile];
-    uint16_t* const s_l = s_own;
+    // s_own (source owners, read by the generation) and s_dl (the ranked tile: source
+    // slot << 8 | row, written after the ranking) share storage: their lives do not overlap
+    __shared__ uint32_t s_dl[kTile];
+    uint16_t* const s_own = reinterpret_cast<uint16_t*>(s_dl);
     __shared__ uint32_t s_wmax[4];
-    __shared__ uint8_t s_dig[kTile];
-    __shared__ uint32_t s_wc[4][256], s_gbase[256], s_lbase[256], s_scr[4];
+    // s_dbase[d]: global position of the tile's first item of row d minus its tile slot
+    __shared__ uint32_t s_wc[4][256], s_dbase[256], s_lbase[256], s_scr[4];
     __shared__ unsigned long long s_scr64[4];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     uint64_t b, e;
@@ -2584,25 +2587,27 @@ __global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(co
         for (int i = 0; i < 4; i++) spv[i] = spans && rect_rows(unpack_rect(prc[i])) ? spans[gix[i]] : 0u;
     };
     load_sources(b);
+    uint32_t gb;   // row t's running global position (thread t owns row t)
     {
         uint32_t tot;
-        s_gbase[t] = block_exclusive_scan<uint32_t>(row_items[t], s_scr, tot) +
-                     (t < (uint32_t)tiles_y ? hist[t * (uint32_t)groups + chunk] : 0u);
+        gb = block_exclusive_scan<uint32_t>(row_items[t], s_scr, tot) +
+             (t < (uint32_t)tiles_y ? hist[t * (uint32_t)groups + chunk] : 0u);
         unsigned long long ptot;
         block_exclusive_scan<unsigned long long>(row_pairs[t], s_scr64, ptot);
         if (ptot > cap || b >= e) return;   // uniform: overflow frames stop here
     }
     for (uint64_t c0 = b; c0 < e; c0 += kRowSources) {
         if (c0 != b) load_sources(c0);
-        uint32_t cnt[4], start[4];
+        uint32_t cnt[4], start[4], ty0v[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             s_idx[4 * t + i] = gix[i];
             cnt[i] = rect_rows(unpack_rect(prc[i]));
+            ty0v[i] = (prc[i] >> 16) & 0xffu;
         }
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) s_own[t * ITEMS + i] = 0;
-        const uint32_t total = bin_source_prefix<4>(cnt, start, s_pref, s_scr);
+        const uint32_t total = bin_source_starts<4>(cnt, start, ty0v, s_ft, s_scr);
 #pragma unroll
         for (int i = 0; i < 4; i++)   // read after bin_tile_owners' barriers
             s_rect[4 * t + i] = (uint64_t)prc[i] | ((uint64_t)spv[i] << 32);
@@ -2616,25 +2621,24 @@ __global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(co
                 const uint32_t el = min(w * 64 * ITEMS + k * 64 + lane, tn - 1);
                 const uint32_t l = (uint32_t)s_own[el] - 1u;
                 src[k] = l;
-                const uint32_t first = l ? s_pref[l - 1] : 0u;
-                dig[k] = (uint32_t)((s_rect[l] >> 16) & 0xffu) + (tb + el - first);   // ty0 + row
+                const uint32_t ft = s_ft[l];
+                dig[k] = (ft & 0xffu) + (tb + el - (ft >> 8));   // ty0 + row
             }
             const uint32_t tcount = bin_rank_tile<ITEMS, BITS, RA>(dig, tn, pos, s_wc, s_lbase, s_scr);
+            s_dbase[t] = gb - s_lbase[t];   // this thread's own scan output
 #pragma unroll
             for (int k = 0; k < ITEMS; k++) {
                 const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
-                if (el < tn) {
-                    s_dig[pos[k]] = (uint8_t)dig[k];
-                    s_l[pos[k]] = (uint16_t)src[k];
-                }
+                if (el < tn) s_dl[pos[k]] = (src[k] << 8) | dig[k];
             }
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < ITEMS; k++) {
                 const uint32_t q = t + 256 * k;
                 const uint32_t qc = min(q, tn - 1);
-                const uint32_t d = s_dig[qc], l = s_l[qc];
-                const uint32_t dst = s_gbase[d] + (qc - s_lbase[d]);
+                const uint32_t x = s_dl[qc];
+                const uint32_t d = x & 0xffu, l = x >> 8;
+                const uint32_t dst = s_dbase[d] + qc;
                 const uint64_t r = s_rect[l];
                 uint32_t x0 = (uint32_t)(r & 0xffu), x1 = (uint32_t)((r >> 8) & 0xffu);
                 const uint32_t ro = d - (uint32_t)((r >> 16) & 0xffu);   // row within the rect
@@ -2649,7 +2653,7 @@ __global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(co
                 if (q < tn && dst < cap) rows_out[dst] = (uint64_t)s_idx[l] | ((uint64_t)x0 << 32) | ((uint64_t)x1 << 48);
             }
             __syncthreads();
-            s_gbase[t] += tcount;
+            gb += tcount;
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) s_own[t * ITEMS + i] = 0;   // owners of the next tile start cleared
             __syncthreads();
@@ -2801,12 +2805,13 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
     if (gate && *gate == 0u) return;
     constexpr uint32_t kTile = 256u * ITEMS;
     __shared__ ColPlan<false> pl;
-    __shared__ uint32_t s_pref[kColChunk], s_idx[kColChunk];
-    __shared__ uint8_t s_tx0[kColChunk];
-    __shared__ uint16_t s_l[kTile], s_own[kTile];
+    // per source (row item of the chunk): exclusive start << 8 | first column; index
+    __shared__ uint32_t s_ft[kColChunk], s_idx[kColChunk];
+    __shared__ uint16_t s_own[kTile];
+    __shared__ uint32_t s_dl[kTile];   // the ranked tile: source slot << 8 | column
     __shared__ uint32_t s_wmax[4];
-    __shared__ uint8_t s_dig[kTile];
-    __shared__ uint32_t s_wc[4][256], s_gbase[256], s_lbase[256], s_scr[4];
+    // s_dbase[d]: global position of the tile's first value of column d minus its tile slot
+    __shared__ uint32_t s_wc[4][256], s_dbase[256], s_lbase[256], s_scr[4];
     __shared__ unsigned long long s_scr64[4];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     if (col_plan(row_items, row_pairs, pl, s_scr, s_scr64) > cap) return;
@@ -2815,22 +2820,23 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
         const uint32_t r = col_chunk_row(pl, c);
         const uint32_t ib = pl.rbase[r] + (c - pl.chbase[r]) * kColChunk;
         const uint32_t m = min(kColChunk, pl.rbase[r] + pl.rcnt[r] - ib);
-        s_gbase[t] = t < (uint32_t)tiles_x ? ~ranges[r * (uint32_t)tiles_x + t].x + cbins[(size_t)c * 256 + t] : 0u;
+        // column t's running global position (thread t owns column t)
+        uint32_t gb = t < (uint32_t)tiles_x ? ~ranges[r * (uint32_t)tiles_x + t].x + cbins[(size_t)c * 256 + t] : 0u;
         // thread t owns row items PER*t .. PER*t + PER-1 of the chunk (source order)
         constexpr int PER = kColChunk / 256;
-        uint32_t cnt[PER], start[PER];
+        uint32_t cnt[PER], start[PER], tx0v[PER];
 #pragma unroll
         for (int i = 0; i < PER; i++) {
             const uint32_t j = PER * t + i;
             const uint64_t it = j < m ? rows_in[ib + j] : 0ull;
             const uint32_t tx0 = (uint32_t)((it >> 32) & 0xffffu);
             cnt[i] = j < m ? (uint32_t)(it >> 48) - tx0 + 1u : 0u;
+            tx0v[i] = tx0 & 0xffu;
             s_idx[j] = (uint32_t)it;
-            s_tx0[j] = (uint8_t)tx0;
         }
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) s_own[t * ITEMS + i] = 0;
-        const uint32_t total = bin_source_prefix<PER>(cnt, start, s_pref, s_scr);
+        const uint32_t total = bin_source_starts<PER>(cnt, start, tx0v, s_ft, s_scr);
         uint32_t carry = 0;
         for (uint32_t tb = 0; tb < total; tb += kTile) {
             const uint32_t tn = min(kTile, total - tb);
@@ -2841,32 +2847,30 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
                 const uint32_t el = min(w * 64 * ITEMS + k * 64 + lane, tn - 1);
                 const uint32_t l = (uint32_t)s_own[el] - 1u;
                 src[k] = l;
-                const uint32_t first = l ? s_pref[l - 1] : 0u;
-                dig[k] = (uint32_t)s_tx0[l] + (tb + el - first);
+                const uint32_t ft = s_ft[l];
+                dig[k] = (ft & 0xffu) + (tb + el - (ft >> 8));
             }
             const uint32_t tcount = bin_rank_tile<ITEMS, BITS, RA>(dig, tn, pos, s_wc, s_lbase, s_scr);
+            s_dbase[t] = gb - s_lbase[t];   // this thread's own scan output
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) s_own[t * ITEMS + i] = 0;   // for the next tile (rank barriers passed)
 #pragma unroll
             for (int k = 0; k < ITEMS; k++) {
                 const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
-                if (el < tn) {
-                    s_dig[pos[k]] = (uint8_t)dig[k];
-                    s_l[pos[k]] = (uint16_t)src[k];
-                }
+                if (el < tn) s_dl[pos[k]] = (src[k] << 8) | dig[k];
             }
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < ITEMS; k++) {
                 const uint32_t q = t + 256 * k;
                 const uint32_t qc = min(q, tn - 1);
-                const uint32_t d = s_dig[qc];
-                const uint32_t v = s_idx[s_l[qc]];
-                const uint32_t dst = s_gbase[d] + (qc - s_lbase[d]);
+                const uint32_t x = s_dl[qc];
+                const uint32_t v = s_idx[x >> 8];
+                const uint32_t dst = s_dbase[x & 0xffu] + qc;
                 if (q < tn) vals[dst] = v;
             }
             __syncthreads();
-            s_gbase[t] += tcount;
+            gb += tcount;
         }
         __syncthreads();
     }
