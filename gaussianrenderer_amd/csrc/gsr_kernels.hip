@@ -954,16 +954,22 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
     uint32_t* row = hist + (size_t)blockIdx.x * groups;
     const int per = (groups + 255) / 256;
     const int b = threadIdx.x * per;
-    uint32_t local = 0;
-    for (int k = 0; k < per; k++)
-        if (b + k < groups) local += row[b + k];
+    // every load of the thread's segment in flight at once (a loop over `per` waited for
+    // each in turn: 5 round trips at 5M items, 20 for the row scan below)
+    constexpr int kPerMax = kMaxSortGroups / 256;
+    uint32_t v[kPerMax], local = 0;
+#pragma unroll
+    for (int k = 0; k < kPerMax; k++) {
+        v[k] = k < per && b + k < groups ? row[b + k] : 0u;
+        local += v[k];
+    }
     uint32_t total;
     uint32_t run = block_exclusive_scan<uint32_t>(local, scratch, total);
-    for (int k = 0; k < per; k++)
-        if (b + k < groups) {
-            const uint32_t v = row[b + k];
+#pragma unroll
+    for (int k = 0; k < kPerMax; k++)
+        if (k < per && b + k < groups) {
             row[b + k] = run;
-            run += v;
+            run += v[k];
         }
     if (threadIdx.x == 0) totals[blockIdx.x] = total;
 }
@@ -2500,22 +2506,26 @@ __global__ __launch_bounds__(256) void k_bin_rows_scan(uint32_t* __restrict__ hi
     const uint32_t* hp = hist + (size_t)(256 + r) * (uint32_t)groups;
     const int per = (groups + 255) / 256;
     const int b = (int)t * per;
-    uint32_t local = 0;
+    // all loads of the segment issued together (k_radix_scan)
+    constexpr int kPerMax = kMaxSortGroups / 256;
+    uint32_t v[kPerMax], local = 0;
     unsigned long long lp = 0;
-    for (int k = 0; k < per; k++)
-        if (b + k < groups) {
-            local += hi[b + k];
-            lp += hp[b + k];
-        }
+#pragma unroll
+    for (int k = 0; k < kPerMax; k++) {
+        const bool in = k < per && b + k < groups;
+        v[k] = in ? hi[b + k] : 0u;
+        lp += in ? hp[b + k] : 0u;
+        local += v[k];
+    }
     uint32_t tot;
     uint32_t run = block_exclusive_scan<uint32_t>(local, scr, tot);
     unsigned long long ptot;
     block_exclusive_scan<unsigned long long>(lp, scr64, ptot);
-    for (int k = 0; k < per; k++)
-        if (b + k < groups) {
-            const uint32_t v = hi[b + k];
+#pragma unroll
+    for (int k = 0; k < kPerMax; k++)
+        if (k < per && b + k < groups) {
             hi[b + k] = run;
-            run += v;
+            run += v[k];
         }
     if (t == 0) {
         row_items[r] = tot;
