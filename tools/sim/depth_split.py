@@ -1,4 +1,4 @@
-"""Depth-split analysis (analysis only): how many (tile, splat) pairs and row items a
+"""Depth-split analysis (analysis only; AZ = orbit azimuth in degrees): how many (tile, splat) pairs and row items a
 two-phase binning would list if phase A bins only the nearest fraction f of the
 depth-ordered visible splats and phase B bins the rest for the tiles that phase A
 did not saturate (every pixel's transmittance below 1e-3).  Oracle records, AABB
@@ -28,6 +28,9 @@ soa = gsr.read_ply(ply, four_d=four_d)
 if four_d:
     soa = orc.temporal(soa, float(os.environ.get("T", 0.5)))
 cam = gsr.make_camera(position=(0, 0, 4), fov_y=50, aspect=W / H)
+az = float(os.environ.get("AZ", 0))   # Camera::orbit azimuth (bench.py --orbit-step: frame i at i * step)
+if az:
+    gsr.orbit(cam, az)
 t0 = time.time()
 sp = orc.preprocess(soa, cam, W, H, 3.0)
 vis = np.nonzero(sp["status"] == 2)[0]
