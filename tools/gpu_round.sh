@@ -68,7 +68,7 @@ for step in ${STEPS:-suite smoke bench}; do
       PMC_GROUPS=${PMC_GROUPS:-"FETCH_SIZE;WRITE_SIZE;SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_INSTS_SALU"} \
       bash tools/profile.sh
     rc=$?; fatal $rc pmc; [ $rc = 0 ] || exit $rc
-    python3 tools/summarize_prof.py gpurun_out/prof_$TAG --json gpurun_out/pmc_$TAG.json ${CONFIGS:-2} \
+    python3 tools/summarize_prof.py gpurun_out/prof_$TAG --json gpurun_out/pmc_$TAG.json ${PMC_CONFIG:-2} \
       "rocprofv3 --pmc, separate passes, bench.py --steps 50 ${BENCH_ARGS:---inflight 1}, $TAG"
     python3 tools/pmc_agg.py gpurun_out/prof_$TAG k_ > gpurun_out/prof_$TAG/pmc_means.txt 2>&1
     # with a kernel trace of the same TAG already there: the table with the PMC columns
