@@ -100,9 +100,10 @@ __device__ __forceinline__ T wave_incl_scan(T x, Op op) {
 // The value of the lane below (0 at lane 0): wave_shr:1.
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t x) { return dpp_u32<0x138, 0xf, true>(x); }
 
-// Exclusive scan across a 256-thread workgroup (4 waves).  `scratch` holds 4
-// entries.  Contains two barriers; every thread of the block must call it.
-template <typename T>
+// Exclusive scan across a workgroup of NW waves (256 threads unless NW says otherwise).
+// Contains two barriers; every thread of the block must call it.
+// (NW: waves of the workgroup, 4 unless a kernel says otherwise; scratch holds NW.)
+template <typename T, int NW = 4>
 __device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
     const uint32_t lane = lane_id();
     const uint32_t w = threadIdx.x >> 6;
@@ -111,7 +112,7 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
     __syncthreads();
     T pre = 0, tot = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < NW; k++) {
         const T s = scratch[k];
         if ((uint32_t)k < w) pre += s;
         tot += s;
@@ -1742,16 +1743,17 @@ static_assert(kBktCap == kMaxBucketCap && kMaxBuckets == 4096, "gsr_internal.h b
 // search step reads one tree level, and a level's nodes are consecutive words.  (The plain
 // sorted array put every address of the first search steps on ONE LDS bank -- b + st - 1
 // with b a multiple of 2 st -- up to 32-way conflicts: the count kernel took 10 us.)
-template <int B>
+template <int B, int TH = kBktThreads>
 __device__ __forceinline__ void bkt_load_splitters(uint32_t* s_T, const uint32_t* __restrict__ splitters) {
-    // B / 256 nodes per thread, every load issued before the first LDS write: a rolled
+    // B / TH nodes per thread, every load issued before the first LDS write: a rolled
     // loop waited for each load in turn (four serial memory round trips at B = 1,024)
+    static_assert(B >= TH, "one node per thread at least");
     constexpr int h = __builtin_ctz(B);
-    constexpr int kPer = B / kBktThreads;
+    constexpr int kPer = B / TH;
     uint32_t v[kPer], jj[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
-        const uint32_t i = threadIdx.x + (uint32_t)k * kBktThreads;
+        const uint32_t i = threadIdx.x + (uint32_t)k * TH;
         const int d = 31 - __clz((int)(i + 1u));
         const uint32_t p = i + 1u - (1u << d);
         const int sh = h - 1 - d;                               // < 0 only for i = B - 1 (no node)
@@ -1760,7 +1762,7 @@ __device__ __forceinline__ void bkt_load_splitters(uint32_t* s_T, const uint32_t
     }
 #pragma unroll
     for (int k = 0; k < kPer; k++)
-        s_T[threadIdx.x + (uint32_t)k * kBktThreads] = jj[k] < (uint32_t)B - 2u ? v[k] : 0xffffffffu;
+        s_T[threadIdx.x + (uint32_t)k * TH] = jj[k] < (uint32_t)B - 2u ? v[k] : 0xffffffffu;
 }
 
 // The buckets of N keys: bucket(key) = the number of the B - 1 sorted splitters that are
@@ -1870,8 +1872,10 @@ __device__ __forceinline__ uint32_t half16(uint32_t v, uint32_t h) { return (v >
 
 // bstart (B + 1 words): written by chunk 0's workgroup, the first position of every bucket
 // and bstart[B] = n (k_bkt_local reads its bucket's range there).
-template <int B, bool RA>
-__global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(const uint64_t* __restrict__ in,
+// TH threads (512 from 512 buckets up: twice the waves of 256, half the items per wave, so
+// each wave's latency chain is half as long; the grid is only ~n / 2,048 workgroups).
+template <int B, bool RA, int TH>
+__global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__ in,
                                                              uint64_t* __restrict__ out, uint32_t n,
                                                              const uint32_t* __restrict__ splitters, int groups,
                                                              const uint32_t* __restrict__ hist,
@@ -1880,23 +1884,25 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(const uint64_t* __r
                                                              uint32_t* __restrict__ pay_out,
                                                              uint32_t* __restrict__ bstart) {
     GSR_GEOM_PRIO();
+    constexpr int NW = TH / 64, kIt = kBktTile / TH;  // waves; items per thread
     constexpr uint32_t kW = B / 2;                      // packed counter words per wave
-    constexpr int kPer = B / kBktThreads;               // buckets per thread (scan)
-    constexpr int kWPer = (kW + kBktThreads - 1) / kBktThreads;   // counter words per thread
+    constexpr int kPer = B / TH;                        // buckets per thread (scan)
+    constexpr int kWPer = (kW + TH - 1) / TH;           // counter words per thread
+    static_assert(kPer >= 1 && kIt * TH == kBktTile, "bucket / thread split");
     __shared__ uint32_t s_S[B], s_gbase[B];
-    __shared__ uint32_t s_wc[4][kW];
-    __shared__ uint32_t s_scr[4];
+    __shared__ uint32_t s_wc[NW][kW];
+    __shared__ uint32_t s_scr[NW];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const int chunk = xcd_chunk((int)blockIdx.x, groups);   // each XCD takes a contiguous run of chunks
     uint64_t b, e;
     chunk_range(n, groups, chunk, kBktTile, b, e);
-    const uint32_t wbase = w * 64 * kBktItems;
-    uint64_t it[kBktItems];
-    uint32_t pv[kBktItems];
+    const uint32_t wbase = w * 64 * kIt;
+    uint64_t it[kIt];
+    uint32_t pv[kIt];
     auto load = [&](uint64_t tb, uint32_t tn) {
 #pragma unroll
-        for (int k = 0; k < kBktItems; k++) {
+        for (int k = 0; k < kIt; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             it[k] = el < tn ? in[tb + el] : ~0ull;
             pv[k] = el < tn ? rect[tb + el] : 0u;   // the input is the preprocess order: rect by position
@@ -1905,7 +1911,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(const uint64_t* __r
     // the first tile's items and rects, the splitters, the bucket totals and this chunk's
     // histogram row are all loaded in one memory round trip
     load(b, (uint32_t)min((uint64_t)kBktTile, e - b));
-    bkt_load_splitters<B>(s_S, splitters);
+    bkt_load_splitters<B, TH>(s_S, splitters);
     {   // this chunk's first slot in every bucket: the bucket's start + the earlier chunks' items
         uint32_t loc[kPer], hrow[kPer], sum = 0;
 #pragma unroll
@@ -1915,7 +1921,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(const uint64_t* __r
             sum += loc[k];
         }
         uint32_t tot;
-        uint32_t run = block_exclusive_scan<uint32_t>(sum, s_scr, tot);
+        uint32_t run = block_exclusive_scan<uint32_t, NW>(sum, s_scr, tot);
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             const uint32_t d = t * kPer + k;
@@ -1928,19 +1934,19 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(const uint64_t* __r
     if (b >= e) return;   // uniform per workgroup, after the scan's barriers
     for (uint64_t tb = b; tb < e; tb += kBktTile) {
         const uint32_t tn = (uint32_t)min((uint64_t)kBktTile, e - tb);
-        for (uint32_t j = t; j < 4 * kW; j += kBktThreads) (&s_wc[0][0])[j] = 0;
+        for (uint32_t j = t; j < NW * kW; j += TH) (&s_wc[0][0])[j] = 0;
         if (tb != b) load(tb, tn);
         __syncthreads();
-        uint32_t dg[kBktItems], rk[kBktItems], keys[kBktItems];
+        uint32_t dg[kIt], rk[kIt], keys[kIt];
 #pragma unroll
-        for (int k = 0; k < kBktItems; k++) keys[k] = (uint32_t)(it[k] >> 32);
+        for (int k = 0; k < kIt; k++) keys[k] = (uint32_t)(it[k] >> 32);
         bkt_of_n<B>(s_S, keys, dg);   // a key 0xFFFFFFFF (culled) counts every splitter: bucket B - 1
         // culled items (the last bucket) rank by ballot against a running wave count, so the
         // live items' returning atomics have no LDS read between them and stay in flight together
         uint32_t dead_run = 0;
-        uint32_t old[kBktItems];
+        uint32_t old[kIt];
 #pragma unroll
-        for (int k = 0; k < kBktItems; k++) {
+        for (int k = 0; k < kIt; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             const bool valid = el < tn;
             const bool dead = keys[k] == 0xffffffffu;
@@ -1965,29 +1971,34 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(const uint64_t* __r
         }
         if (RA) {
 #pragma unroll
-            for (int k = 0; k < kBktItems; k++)
+            for (int k = 0; k < kIt; k++)
                 if (keys[k] != 0xffffffffu) rk[k] = half16(old[k], dg[k] & 1u);
         }
         if (lane == 0 && dead_run) atomicAdd(&s_wc[w][(B - 1) >> 1], dead_run << 16);   // B - 1 is odd: high half
         __syncthreads();
-        // per word (two buckets): exclusive prefix over the four waves in place, tile counts kept
+        // per word (two buckets): exclusive prefix over the waves in place, tile counts kept
+        // (halves <= 2,048: no carry between them)
         uint32_t tc[kWPer];
 #pragma unroll
         for (int q = 0; q < kWPer; q++) {
-            const uint32_t j = t + q * kBktThreads;
+            const uint32_t j = t + q * TH;
             tc[q] = 0;
             if (j < kW) {
-                const uint32_t c0 = s_wc[0][j], c1 = s_wc[1][j], c2 = s_wc[2][j], c3 = s_wc[3][j];
-                s_wc[0][j] = 0;
-                s_wc[1][j] = c0;
-                s_wc[2][j] = c0 + c1;          // halves <= 2048: no carry between them
-                s_wc[3][j] = c0 + c1 + c2;
-                tc[q] = c0 + c1 + c2 + c3;
+                uint32_t c[NW];
+#pragma unroll
+                for (int v = 0; v < NW; v++) c[v] = s_wc[v][j];
+                uint32_t run = 0;
+#pragma unroll
+                for (int v = 0; v < NW; v++) {
+                    s_wc[v][j] = run;
+                    run += c[v];
+                }
+                tc[q] = run;
             }
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kBktItems; k++) {
+        for (int k = 0; k < kIt; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             if (el < tn) {
                 const uint32_t d = dg[k];
@@ -1999,7 +2010,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(const uint64_t* __r
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < kWPer; q++) {
-            const uint32_t j = t + q * kBktThreads;
+            const uint32_t j = t + q * TH;
             if (j < kW) {
                 s_gbase[2 * j] += tc[q] & 0xffffu;
                 s_gbase[2 * j + 1] += tc[q] >> 16;
@@ -3905,13 +3916,14 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
     uint32_t* bstart = totals + B;   // B + 1 words after the totals
     hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist);
     hipLaunchKernelGGL(k_bkt_scan<B>, dim3(B / 64), dim3(1024), 0, s, hist, groups, totals);
+    constexpr int kScTh = B >= 512 ? 512 : kBktThreads;   // k_bkt_scatter's workgroup size
     if (rank_atomic) {
-        hipLaunchKernelGGL((k_bkt_scatter<B, true>), dim3(groups), dim3(kBktThreads), 0, s, in, items0, n, s_in,
+        hipLaunchKernelGGL((k_bkt_scatter<B, true, kScTh>), dim3(groups), dim3(kScTh), 0, s, in, items0, n, s_in,
                            groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart);
         hipLaunchKernelGGL((k_bkt_local<B, true>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0, pay1,
                            static_cast<const uint32_t*>(bstart), s_in, s_out, cap, over_host, rh);
     } else {
-        hipLaunchKernelGGL((k_bkt_scatter<B, false>), dim3(groups), dim3(kBktThreads), 0, s, in, items0, n, s_in,
+        hipLaunchKernelGGL((k_bkt_scatter<B, false, kScTh>), dim3(groups), dim3(kScTh), 0, s, in, items0, n, s_in,
                            groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart);
         hipLaunchKernelGGL((k_bkt_local<B, false>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0, pay1,
                            static_cast<const uint32_t*>(bstart), s_in, s_out, cap, over_host, rh);
