@@ -295,7 +295,9 @@ int gsr_set_blend_variant(gsr_context* ctx, int variant);
 enum {
     GSR_TUNE_BLEND_SCHEDULE = 0,     /* as gsr_set_blend_variant */
     GSR_TUNE_TILE_SORT_ITEMS = 1,    /* tile sort items per thread: 8 | 16 (default 16) */
-    GSR_TUNE_DEPTH_SORT_ITEMS = 2,   /* depth sort items per thread: 0 = by size | 8 | 16 */
+    GSR_TUNE_DEPTH_SORT_ITEMS = 2,   /* depth sort items per thread: 0 = by size | 8 | 16 (16 sorts one
+                                        4,096-item tile per workgroup: a grid too small for that, e.g.
+                                        capped by knob 4, sorts 8 per thread) */
     GSR_TUNE_TILE_SORT_GROUPS = 3,   /* tile sort workgroup cap (default 1024; 0 = one per tile of items) */
     GSR_TUNE_DEPTH_SORT_GROUPS = 4,  /* depth sort workgroup cap (0 = one per tile of items) */
     GSR_TUNE_TILE_SORT_SPLIT = 5,    /* tile sort digits: 1 = split evenly (default), 0 = 8 bits first */
