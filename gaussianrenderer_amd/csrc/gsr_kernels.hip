@@ -861,8 +861,11 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
     const uint32_t base = sr.base ? *sr.base : 0u;
     if (!FILT) in += base;
     const uint64_t n = FILT ? (uint64_t)n_host : sort_len(sr, n_dev, n_host);
+    // (XCD-contiguous chunks, so that a histogram row's 64-B lines merge in one L2, measured
+    // slower: config 3 upsweep 11.5 -> 16.5 us, profiles/r05_kt_xcd_hist.txt)
+    const int chunk = (int)blockIdx.x;
     uint64_t b, e;
-    chunk_range(n, groups, blockIdx.x, kSortThreads * ITEMS, b, e);
+    chunk_range(n, groups, chunk, kSortThreads * ITEMS, b, e);
     const bool masked = FILT && sr.sat;   // the far pass 0's rect test reads rect[position]
     // the digit's counter, or the drop counter for an item a filtered pass 0 does not keep
     auto dig = [&](uint64_t v, uint64_t i) {
@@ -911,7 +914,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const uint64_t* 
         }
     }
     __syncthreads();
-    hist[t * (uint32_t)groups + blockIdx.x] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
+    hist[t * (uint32_t)groups + chunk] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
     // per-workgroup plan words after the 4 final ones; pass 0's scan kernel
     // reduces them (plain stores: ~500 device atomics on 4 addresses serialise)
     if (plan && t < 4) dstats[4 + 4 * blockIdx.x + t] = s_st[t];
@@ -2097,7 +2100,10 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
     __shared__ uint32_t s_hp[4][256];   // fused row-pass count: pairs (s_wc holds the items)
     __shared__ uint32_t s_scr[4], s_mm[2];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    const uint32_t bkt = blockIdx.x;
+    // XCD-contiguous buckets: the fused row count's histogram lines (16 consecutive
+    // buckets of a row) merge in one L2 (12.4 -> 11.95 us at config 2,
+    // profiles/r05_kt_xcd_hist.txt)
+    const uint32_t bkt = (uint32_t)xcd_chunk((int)blockIdx.x, B - 1);
     const uint32_t start = bstart[bkt], count = bstart[bkt + 1] - start, live = bstart[B - 1];
     // keys of bucket b lie in [s_in[b - 1], s_in[b]) for 0 < b < B - 2
     const bool bounded = bkt > 0 && bkt < (uint32_t)B - 2u;
@@ -2430,8 +2436,9 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint32
     }
     __syncthreads();
     const uint32_t* srect = depth_sorted_rects(pay0, pay1, dstats) + base;
+    const int chunk = (int)blockIdx.x;   // (XCD-contiguous chunks: 16.2 -> 18.7 us at config 3)
     uint64_t b, e;
-    chunk_range(n, groups, blockIdx.x, kRowSources, b, e);
+    chunk_range(n, groups, chunk, kRowSources, b, e);
     for (uint64_t c0 = b; c0 < e; c0 += 1024) {
         uint64_t r[4];
 #pragma unroll
@@ -2463,8 +2470,8 @@ __global__ __launch_bounds__(256) void k_bin_rows_count(uint32_t n, const uint32
     const uint32_t ci = block_exclusive_scan<uint32_t>(di, scr, ti) + di;
     const uint32_t cp = block_exclusive_scan<uint32_t>(dp, scr, tp) + dp;
     if (t < (uint32_t)tiles_y) {   // rows past the grid hold nothing: no scattered writes for them
-        hist[t * (uint32_t)groups + blockIdx.x] = ci;
-        hist[(256 + t) * (uint32_t)groups + blockIdx.x] = cp;
+        hist[t * (uint32_t)groups + chunk] = ci;
+        hist[(256 + t) * (uint32_t)groups + chunk] = cp;
     }
 }
 
