@@ -27,6 +27,8 @@
 
 #include <algorithm>
 
+#include <type_traits>
+
 #include "gsr_detmath.h"
 #include "gsr.h"
 #include "gsr_internal.h"
@@ -2129,13 +2131,17 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
     }
     uint64_t* const seg = items + start;
     uint32_t* const pseg = pay + start;
-    const uint32_t wbase = w * 64 * kBktItems;
-    if (count <= cap) {
-        // ---- fast path: the bucket in registers, stable 8-bit passes through LDS ----
-        uint64_t it[kBktItems];
-        uint32_t pv[kBktItems];
+    // ---- fast path: the bucket in registers, stable 8-bit passes through LDS.  IT items per
+    // thread: 4 for buckets of up to 1,024 (the usual ~n / B: every wave holds a quarter of
+    // the bucket), 8 up to the capacity (at 8, buckets under 1,024 left waves 2 and 3 idle
+    // and waves 0 and 1 with twice the slots) ----
+    auto fast = [&](auto it_c) {
+        constexpr int IT = decltype(it_c)::value;
+        const uint32_t wbase = w * 64 * IT;
+        uint64_t it[IT];
+        uint32_t pv[IT];
 #pragma unroll
-        for (int k = 0; k < kBktItems; k++) {
+        for (int k = 0; k < IT; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             it[k] = el < count ? seg[el] : ~0ull;
             pv[k] = el < count ? pseg[el] : 0u;
@@ -2144,7 +2150,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
         if (!bounded) {   // the open-ended first and last buckets: their own min and max
             uint32_t mn = 0xffffffffu, mx = 0;
 #pragma unroll
-            for (int k = 0; k < kBktItems; k++)
+            for (int k = 0; k < IT; k++)
                 if (wbase + k * 64 + lane < count) {
                     mn = min(mn, (uint32_t)(it[k] >> 32));
                     mx = max(mx, (uint32_t)(it[k] >> 32));
@@ -2163,12 +2169,12 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
         }
         const int bits = span ? 32 - __clz((int)span) : 0;
         for (int shift = 0; shift < bits; shift += 8) {   // uniform
-            uint32_t dig[kBktItems], pos[kBktItems];
+            uint32_t dig[IT], pos[IT];
 #pragma unroll
-            for (int k = 0; k < kBktItems; k++) dig[k] = (((uint32_t)(it[k] >> 32) - kmin) >> shift) & 0xffu;
-            (void)bin_rank_tile<kBktItems, 8, RA>(dig, count, pos, s_wc, s_lbase, s_scr);
+            for (int k = 0; k < IT; k++) dig[k] = (((uint32_t)(it[k] >> 32) - kmin) >> shift) & 0xffu;
+            (void)bin_rank_tile<IT, 8, RA>(dig, count, pos, s_wc, s_lbase, s_scr);
 #pragma unroll
-            for (int k = 0; k < kBktItems; k++) {
+            for (int k = 0; k < IT; k++) {
                 const uint32_t el = wbase + k * 64 + lane;
                 if (el < count) {
                     s_items[pos[k]] = it[k];
@@ -2177,7 +2183,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
             }
             __syncthreads();
 #pragma unroll
-            for (int k = 0; k < kBktItems; k++) {
+            for (int k = 0; k < IT; k++) {
                 const uint32_t el = wbase + k * 64 + lane;
                 if (el < count) {
                     it[k] = s_items[el];
@@ -2187,7 +2193,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
             __syncthreads();
         }
 #pragma unroll
-        for (int k = 0; k < kBktItems; k++) {
+        for (int k = 0; k < IT; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             if (el < count) {
                 seg[el] = it[k];
@@ -2199,7 +2205,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
             row_zero();
             __syncthreads();
 #pragma unroll
-            for (int k = 0; k < kBktItems; k++)
+            for (int k = 0; k < IT; k++)
                 if (wbase + k * 64 + lane < count) row_hist_add(s_wc, s_hp, w, pv[k]);
             row_hist_write(rh, bkt, s_wc, s_hp, s_scr);
         }
@@ -2207,8 +2213,16 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
         if (bkt < (uint32_t)B - 1u)
             bkt_write_splitters<B>(start, count, live, s_next,
                                    [&](uint32_t q) { return (uint32_t)(s_items[q] >> 32); });
+    };
+    if (count <= min(cap, (uint32_t)kBktThreads * 4u)) {
+        fast(std::integral_constant<int, 4>{});
         return;
     }
+    if (count <= cap) {
+        fast(std::integral_constant<int, 8>{});
+        return;
+    }
+    const uint32_t wbase = w * 64 * kBktItems;
     // ---- over capacity: stable 8-bit passes through global memory, one tile at a time ----
     if (over_host && t == 0) atomicAdd_system(over_host, count);
     uint32_t kmin = 0xffffffffu, kmax = 0;
