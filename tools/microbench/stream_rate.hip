@@ -54,6 +54,52 @@ __global__ __launch_bounds__(256) void k_soa38(const float* __restrict__ a, size
     rec[i] = make_float4(s0, s1, s2, s3);
 }
 
+// The same bytes with 16 B per lane: each thread loads a float4 of every array (4 elements)
+// and writes four 16-B words -- the access shape an LDS-staged preprocess would have.
+__global__ __launch_bounds__(256) void k_soa38_v4(const float* __restrict__ a, size_t stride, size_t n,
+                                                  float4* __restrict__ rec) {
+    const size_t i4 = blockIdx.x * 256ull + threadIdx.x;   // float4 index
+    if (4 * i4 >= n) return;
+    float4 s = make_float4(0, 0, 0, 0);
+    float4 v[38];
+#pragma unroll
+    for (int k = 0; k < 38; k++) v[k] = reinterpret_cast<const float4*>(a + k * stride)[i4];
+#pragma unroll
+    for (int k = 0; k < 38; k++) {
+        s.x += v[k].x;
+        s.y += v[k].y;
+        s.z += v[k].z;
+        s.w += v[k].w;
+    }
+    rec[4 * i4] = s;
+    rec[4 * i4 + 1] = s;
+    rec[4 * i4 + 2] = s;
+    rec[4 * i4 + 3] = s;
+}
+
+// 38 arrays staged through LDS by float4 loads (wave w loads arrays w, w + 4, ...), then one
+// element per thread read from LDS: the preprocess's one-thread-per-Gaussian shape with
+// 16-B-per-lane global loads.
+__global__ __launch_bounds__(256) void k_soa38_lds(const float* __restrict__ a, size_t stride, size_t n,
+                                                   float4* __restrict__ rec) {
+    __shared__ float4 s_v[38][64];   // 38 arrays x 256 elements
+    const size_t i0 = blockIdx.x * 256ull;
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    for (int k = (int)w; k < 38; k += 4)
+        s_v[k][lane] = reinterpret_cast<const float4*>(a + k * stride + i0)[lane];
+    __syncthreads();
+    const float* sf = reinterpret_cast<const float*>(s_v);
+    float s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+    for (int k = 0; k < 38; k += 4) {
+        s0 += sf[k * 256 + t];
+        if (k + 1 < 38) s1 += sf[(k + 1) * 256 + t];
+        if (k + 2 < 38) s2 += sf[(k + 2) * 256 + t];
+        if (k + 3 < 38) s3 += sf[(k + 3) * 256 + t];
+    }
+    if (i0 + t < n) rec[i0 + t] = make_float4(s0, s1, s2, s3);
+}
+
 int main() {
     const size_t bytes = 1ull << 30, n4 = bytes / 16;
     float4 *a, *b;
@@ -101,5 +147,27 @@ int main() {
     const double mb = (38.0 * 4 * n + 16.0 * n) / 1e6;
     printf("38-array SoA read + 16-B write, 5M elements (%.0f MB): %.1f us, %.0f GB/s\n", mb, best * 1e3,
            mb / (best * 1e3) * 1e3);
+    for (int variant = 0; variant < 2; variant++) {
+        float bv = 1e9f;
+        for (int rep = 0; rep < 5; rep++) {
+            CHECK(hipEventRecord(e0));
+            if (variant == 0)
+                hipLaunchKernelGGL(k_soa38_v4, dim3((n / 4 + 255) / 256), dim3(256), 0, 0,
+                                   reinterpret_cast<const float*>(a), stride, n, b);
+            else
+                hipLaunchKernelGGL(k_soa38_lds, dim3((n + 255) / 256), dim3(256), 0, 0,
+                                   reinterpret_cast<const float*>(a), stride, n, b);
+            CHECK(hipEventRecord(e1));
+            CHECK(hipEventSynchronize(e1));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, e0, e1));
+            if (ms < bv) bv = ms;
+        }
+        const double mbv = variant == 0 ? (38.0 * 4 * n + 64.0 * n) / 1e6 : mb;
+        printf("%s: %.1f us, %.0f GB/s\n",
+               variant == 0 ? "38-array SoA read, float4 per lane + 64-B writes per 4 elements"
+                            : "38-array SoA read staged through LDS by float4 loads + 16-B write",
+               bv * 1e3, mbv / (bv * 1e3) * 1e3);
+    }
     return 0;
 }
