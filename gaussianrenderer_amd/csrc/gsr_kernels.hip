@@ -102,9 +102,9 @@ __device__ __forceinline__ T wave_incl_scan(T x, Op op) {
 // The value of the lane below (0 at lane 0): wave_shr:1.
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t x) { return dpp_u32<0x138, 0xf, true>(x); }
 
-// Exclusive scan across a workgroup of NW waves (256 threads unless NW says otherwise).
-// Contains two barriers; every thread of the block must call it.
-// (NW: waves of the workgroup, 4 unless a kernel says otherwise; scratch holds NW.)
+// Exclusive scan across a workgroup of NW waves (4 = 256 threads unless a kernel says
+// otherwise); `scratch` holds NW entries.  Contains two barriers; every thread of the
+// block must call it.
 template <typename T, int NW = 4>
 __device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
     const uint32_t lane = lane_id();
@@ -1105,8 +1105,8 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
                 before[k] = s_wc[w][d];
                 if (valid && (uint32_t)(__ffsll((unsigned long long)peers) - 1) == lane)
                     atomicAdd(&s_wc[w][d], (uint32_t)__popcll(peers));
-                // the reads are folded in every 4 slots: 16 reads in flight held 16 more
-                // VGPRs (the 16-item kernel at 207, two waves per SIMD)
+                // the reads fold into the ranks every 4 slots (the compiler places the waits
+                // for them; the VGPR peak came from hoisted loop invariants, see below)
                 if ((k & 3) == 3)
 #pragma unroll
                     for (int j = k - 3; j <= k; j++) rk[j] += before[j];
@@ -1878,7 +1878,8 @@ __device__ __forceinline__ uint32_t half16(uint32_t v, uint32_t h) { return (v >
 // bstart (B + 1 words): written by chunk 0's workgroup, the first position of every bucket
 // and bstart[B] = n (k_bkt_local reads its bucket's range there).
 // TH threads (512 from 512 buckets up: twice the waves of 256, half the items per wave, so
-// each wave's latency chain is half as long; the grid is only ~n / 2,048 workgroups).
+// each wave's latency chain is half as long; the grid is only ~n / 2,048 workgroups:
+// 16.3-16.8 -> 15.6-15.8 us at config 2, profiles/r05_kt_bkt_scatter512.txt).
 template <int B, bool RA, int TH>
 __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__ in,
                                                              uint64_t* __restrict__ out, uint32_t n,
