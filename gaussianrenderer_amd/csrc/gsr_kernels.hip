@@ -1014,9 +1014,8 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     }
     const uint32_t K = FILT ? *sr.kcut : 0u;
     const bool carry = pay_out != nullptr;
-    __shared__ uint32_t s_wc[4][256];           // per-wave digit counters, then wave bases
-    __shared__ uint32_t s_gbase[256];           // running global offset per digit
-    __shared__ uint32_t s_lbase[256];           // tile-local exclusive base per digit
+    __shared__ uint32_t s_wc[4][256];           // per-wave digit counters, then wave slot bases
+    __shared__ uint32_t s_gd[256];              // per digit: global offset minus tile slot
     __shared__ uint32_t s_scr[4];
     // up to 8 items per thread the payloads get slots of their own (+8 KB of LDS, no
     // occupancy change) and travel with the items; at 16 the LDS is the occupancy
@@ -1034,10 +1033,11 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
 
     // global base of each digit for this workgroup (a filtered pass 0: the kept count is
     // the sum of the digit totals)
+    uint32_t gb;   // digit t's running global offset (thread t owns digit t)
     {
         uint32_t tot;
         const uint32_t dig_excl = block_exclusive_scan<uint32_t>(totals[t], s_scr, tot);
-        s_gbase[t] = dig_excl + hist[t * (uint32_t)groups + chunk];
+        gb = dig_excl + hist[t * (uint32_t)groups + chunk];
         if (FILT && sr.count_out && blockIdx.x == 0 && t == 0) *sr.count_out = tot;
     }
     if (b >= e) return;                          // uniform per workgroup
@@ -1114,23 +1114,26 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
         }
         if (!FILT) load_pay();
         __syncthreads();
-        // per digit t: exclusive prefix over the four waves, tile count, tile-local base
+        // per digit t: tile count, tile-local base, and each wave's first slot (tile base
+        // included, so an item reads one word for its slot); the write-back's base is kept
+        // as global offset minus tile slot (one word per item there too)
         uint32_t tcount, tv;   // tv: the tile's kept items (tn unless filtered)
         {
             const uint32_t c0 = s_wc[0][t], c1 = s_wc[1][t], c2 = s_wc[2][t], c3 = s_wc[3][t];
-            s_wc[0][t] = 0;
-            s_wc[1][t] = c0;
-            s_wc[2][t] = c0 + c1;
-            s_wc[3][t] = c0 + c1 + c2;
             tcount = c0 + c1 + c2 + c3;
-            s_lbase[t] = block_exclusive_scan<uint32_t>(tcount, s_scr, tv);
+            const uint32_t lb = block_exclusive_scan<uint32_t>(tcount, s_scr, tv);   // barriers: reads done
+            s_wc[0][t] = lb;
+            s_wc[1][t] = lb + c0;
+            s_wc[2][t] = lb + c0 + c1;
+            s_wc[3][t] = lb + c0 + c1 + c2;
+            s_gd[t] = gb - lb;
         }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < ITEMS; k++) {
             if (kp[k]) {
                 const uint32_t d = (uint32_t)(it[k] >> shift) & mask;
-                const uint32_t slot = s_lbase[d] + s_wc[w][d] + rk[k];
+                const uint32_t slot = s_wc[w][d] + rk[k];
                 s_items[slot] = it[k];
                 if (kPaySlots && carry) s_payd[slot] = pv[k];
                 rk[k] = slot;   // the payload round's slot (the items die here)
@@ -1149,7 +1152,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
             if (q < tv) {
                 const uint64_t v = s_items[q];
                 const uint32_t d = (uint32_t)(v >> shift) & mask;
-                const uint32_t dst = s_gbase[d] + (q - s_lbase[d]);
+                const uint32_t dst = s_gd[d] + q;
                 out[dst] = v;
                 if (kPaySlots && carry) pay_out[dst] = s_payd[q];
                 dpk[k / 4] |= d << (8 * (k % 4));
@@ -1177,16 +1180,15 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
             for (int k = 0; k < ITEMS; k++) {
                 const uint32_t q = t + k * kSortThreads;
                 const uint32_t d = (dpk[k / 4] >> (8 * (k % 4))) & 0xffu;
-                if (q < tv) pay_out[s_gbase[d] + (q - s_lbase[d])] = s_pay[q];
+                if (q < tv) pay_out[s_gd[d] + q] = s_pay[q];
             }
         }
         // 16 items per thread: one tile per workgroup (launch_radix_pass checks the grid),
         // so the loop is straight-line code and nothing is hoisted across tiles (the
         // loop-invariant slot offsets of the write-back held 15 VGPRs for the whole kernel)
         if (ITEMS == 16) break;
-        __syncthreads();
-        s_gbase[t] += tcount;
-        // next iteration's first barrier orders this update before its use
+        __syncthreads();   // every read of s_gd / s_wc done before the next tile's writes
+        gb += tcount;
     }
 }
 
@@ -1576,20 +1578,23 @@ __device__ __forceinline__ uint32_t bin_rank_tile(const uint32_t (&dig)[ITEMS], 
     __syncthreads();
     uint32_t tcount;
     {
+        // each wave's first slot of digit t, tile base included (s_wc[w][t] = s_lbase[t] +
+        // the earlier waves' counts), so an item reads one word for its slot, not two
         const uint32_t c0 = s_wc[0][t], c1 = s_wc[1][t], c2 = s_wc[2][t], c3 = s_wc[3][t];
-        s_wc[0][t] = 0;
-        s_wc[1][t] = c0;
-        s_wc[2][t] = c0 + c1;
-        s_wc[3][t] = c0 + c1 + c2;
         tcount = c0 + c1 + c2 + c3;
         uint32_t tot;
-        s_lbase[t] = block_exclusive_scan<uint32_t>(tcount, s_scr, tot);
+        const uint32_t lb = block_exclusive_scan<uint32_t>(tcount, s_scr, tot);   // barriers: reads done
+        s_lbase[t] = lb;
+        s_wc[0][t] = lb;
+        s_wc[1][t] = lb + c0;
+        s_wc[2][t] = lb + c0 + c1;
+        s_wc[3][t] = lb + c0 + c1 + c2;
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < ITEMS; k++) {
         const uint32_t el = w * 64 * ITEMS + k * 64 + lane;
-        if (el < tn) pos[k] += s_lbase[dig[k]] + s_wc[w][dig[k]];
+        if (el < tn) pos[k] += s_wc[w][dig[k]];
     }
     return tcount;
 }
