@@ -519,6 +519,7 @@ TUNE_DEPTH_SPLIT_STATE = 26
 TUNE_DEPTH_BUCKETS = 28
 TUNE_DEPTH_BUCKETS_OVER = 29
 TUNE_BUCKET_ROWS = 30
+TUNE_COL_CHUNK = 31
 
 
 def rank_order_check() -> tuple[int, int]:

@@ -211,7 +211,8 @@ hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, 
                            uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
                            uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,
                            hipStream_t s, const uint32_t* dstats = nullptr, int passes_launched = 4,
-                           bool rank_atomic = false, const uint32_t* gate = nullptr, uint32_t* fstatus = nullptr);
+                           bool rank_atomic = false, const uint32_t* gate = nullptr, uint32_t* fstatus = nullptr,
+                           int chunk = 2048);   // row items per column-pass chunk: 1024 or 2048
 uint32_t bin_col_chunks_max(uint32_t pair_capacity, int tiles_y);
 // Standalone sort ABI helpers (oneSweepSort / oneSweep3DGaussianSort).
 hipError_t launch_items_from_keys(const int* keys, uint32_t n, uint64_t* items, hipStream_t s);

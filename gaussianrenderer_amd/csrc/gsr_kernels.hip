@@ -1524,10 +1524,12 @@ __global__ __launch_bounds__(256) void k_emit_pairs(const uint64_t* __restrict__
 // the same stable order as the pair sort [render.cu:788-857].
 
 constexpr uint32_t kRowSources = 1024;              // Gaussians per row-pass sub-chunk
-#ifndef GSR_COL_CHUNK
-#define GSR_COL_CHUNK 2048
-#endif
-constexpr uint32_t kColChunk = GSR_COL_CHUNK;       // row items per column-pass chunk (inside one row)
+// Row items per column-pass chunk (a chunk never crosses a row): 1,024 or 2,048, chosen
+// per frame by the runtime (GSR_TUNE_COL_CHUNK).  Smaller chunks halve the scatter's
+// per-chunk LDS (config 2: column scatter 26.0 -> 21.6 us); on config 3's ~9M row items
+// the doubled chunk count costs the count and scan more (+10 us), so 2,048 stays there
+// (profiles/r05_ab_col_chunk.txt).
+constexpr uint32_t kColChunkMin = 1024, kColChunkMax = 2048;
 
 __device__ __forceinline__ uint32_t rect_rows(uint64_t r) {
     return rect_count(r) ? (uint32_t)((r >> 48) - ((r >> 32) & 0xffffu) + 1u) : 0u;
@@ -2711,7 +2713,7 @@ __global__ __launch_bounds__(256, ITEMS == 4 ? 6 : 1) void k_bin_rows_scatter(co
 
 // Row geometry of the column pass, rebuilt by each workgroup from the row
 // totals: item base and count per row, first chunk per row (chunks of
-// kColChunk items never cross a row), chunk total, pair base per row, P.
+// CH items never cross a row), chunk total, pair base per row, P.
 // (PB: also the pair base per row — only the column scan needs it.)
 template <bool PB>
 struct ColPlan {
@@ -2719,7 +2721,7 @@ struct ColPlan {
     unsigned long long pbase[PB ? 256 : 1];
 };
 
-template <bool PB>
+template <uint32_t CH, bool PB>
 __device__ __forceinline__ unsigned long long col_plan(const uint32_t* __restrict__ row_items,
                                                        const unsigned long long* __restrict__ row_pairs,
                                                        ColPlan<PB>& pl, uint32_t* s_scr,
@@ -2729,7 +2731,7 @@ __device__ __forceinline__ unsigned long long col_plan(const uint32_t* __restric
     uint32_t tot;
     pl.rbase[t] = block_exclusive_scan<uint32_t>(cnt, s_scr, tot);
     pl.rcnt[t] = cnt;
-    pl.chbase[t] = block_exclusive_scan<uint32_t>((cnt + kColChunk - 1) / kColChunk, s_scr, tot);
+    pl.chbase[t] = block_exclusive_scan<uint32_t>((cnt + CH - 1) / CH, s_scr, tot);
     if (t == 255) pl.chbase[256] = tot;
     unsigned long long ptot;
     const unsigned long long pb = block_exclusive_scan<unsigned long long>(row_pairs[t], s_scr64, ptot);
@@ -2749,6 +2751,7 @@ __device__ __forceinline__ uint32_t col_chunk_row(const ColPlan<PB>& pl, uint32_
 }
 
 // Column pass, count: per chunk, pairs per tile column -> cbins[chunk][col].
+template <uint32_t CH>
 __global__ __launch_bounds__(256) void k_bin_cols_count(const uint64_t* __restrict__ rows_in,
                                                          const uint32_t* __restrict__ row_items,
                                                          const unsigned long long* __restrict__ row_pairs,
@@ -2760,18 +2763,18 @@ __global__ __launch_bounds__(256) void k_bin_cols_count(const uint64_t* __restri
     __shared__ uint32_t h[4][256], s_scr[4];
     __shared__ unsigned long long s_scr64[4];
     const uint32_t t = threadIdx.x, w = t >> 6;
-    if (col_plan(row_items, row_pairs, pl, s_scr, s_scr64) > cap) return;
+    if (col_plan<CH>(row_items, row_pairs, pl, s_scr, s_scr64) > cap) return;
     const uint32_t nch = pl.chbase[256];
     for (uint32_t c = blockIdx.x; c < nch; c += gridDim.x) {
 #pragma unroll
         for (int k = 0; k < 4; k++) h[k][t] = 0;
         __syncthreads();
         const uint32_t r = col_chunk_row(pl, c);
-        const uint32_t ib = pl.rbase[r] + (c - pl.chbase[r]) * kColChunk;
-        const uint32_t ie = min(ib + kColChunk, pl.rbase[r] + pl.rcnt[r]);
+        const uint32_t ib = pl.rbase[r] + (c - pl.chbase[r]) * CH;
+        const uint32_t ie = min(ib + CH, pl.rbase[r] + pl.rcnt[r]);
         // difference arrays: +1 at the first column, -1 past the last (all of a thread's
         // loads issued before its first LDS update)
-        constexpr int PER = kColChunk / 256;
+        constexpr int PER = CH / 256;
         uint64_t its[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) its[k] = ib + t + 256 * k < ie ? rows_in[ib + t + 256 * k] : 0ull;
@@ -2795,6 +2798,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_count(const uint64_t* __restri
 // row pair base + exclusive scan over columns; ranges = {~start, end} (zero =
 // empty).  Overflowed frames (P > cap) get empty ranges.  Workgroup 0 publishes
 // the frame's pair statistics.
+template <uint32_t CH>
 __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restrict__ row_items,
                                                         const unsigned long long* __restrict__ row_pairs,
                                                         uint32_t cap, int tiles_x, uint32_t* __restrict__ cbins,
@@ -2808,7 +2812,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restric
     __shared__ uint32_t s_scr[4];
     __shared__ unsigned long long s_scr64[4];
     const uint32_t t = threadIdx.x, r = blockIdx.x;
-    const unsigned long long P = col_plan(row_items, row_pairs, pl, s_scr, s_scr64);
+    const unsigned long long P = col_plan<CH>(row_items, row_pairs, pl, s_scr, s_scr64);
     if (r == 0 && t == 0)
         publish_pair_stats(P, cap, st, host_st, dstats ? (uint32_t)depth_passes_run(dstats) : 0u,
                            (uint32_t)passes_launched, fstatus, gate == nullptr);
@@ -2840,7 +2844,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_scan(const uint32_t* __restric
 // Column pass, scatter: per chunk, its row items expand into one value per
 // covered column; tiles of 256*ITEMS values are ranked by column and written in
 // column runs at tile start + chunk offset.
-template <int ITEMS, int BITS, bool RA>
+template <int ITEMS, int BITS, bool RA, uint32_t CH>
 __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __restrict__ rows_in,
                                                            const uint32_t* __restrict__ row_items,
                                                            const unsigned long long* __restrict__ row_pairs,
@@ -2854,7 +2858,7 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
     constexpr uint32_t kTile = 256u * ITEMS;
     __shared__ ColPlan<false> pl;
     // per source (row item of the chunk): exclusive start << 8 | first column; index
-    __shared__ uint32_t s_ft[kColChunk], s_idx[kColChunk];
+    __shared__ uint32_t s_ft[CH], s_idx[CH];
     __shared__ uint16_t s_own[kTile];
     __shared__ uint32_t s_dl[kTile];   // the ranked tile: source slot << 8 | column
     __shared__ uint32_t s_wmax[4];
@@ -2862,16 +2866,16 @@ __global__ __launch_bounds__(256) void k_bin_cols_scatter(const uint64_t* __rest
     __shared__ uint32_t s_wc[4][256], s_dbase[256], s_lbase[256], s_scr[4];
     __shared__ unsigned long long s_scr64[4];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    if (col_plan(row_items, row_pairs, pl, s_scr, s_scr64) > cap) return;
+    if (col_plan<CH>(row_items, row_pairs, pl, s_scr, s_scr64) > cap) return;
     const uint32_t nch = pl.chbase[256];
     for (uint32_t c = blockIdx.x; c < nch; c += gridDim.x) {
         const uint32_t r = col_chunk_row(pl, c);
-        const uint32_t ib = pl.rbase[r] + (c - pl.chbase[r]) * kColChunk;
-        const uint32_t m = min(kColChunk, pl.rbase[r] + pl.rcnt[r] - ib);
+        const uint32_t ib = pl.rbase[r] + (c - pl.chbase[r]) * CH;
+        const uint32_t m = min(CH, pl.rbase[r] + pl.rcnt[r] - ib);
         // column t's running global position (thread t owns column t)
         uint32_t gb = t < (uint32_t)tiles_x ? ~ranges[r * (uint32_t)tiles_x + t].x + cbins[(size_t)c * 256 + t] : 0u;
         // thread t owns row items PER*t .. PER*t + PER-1 of the chunk (source order)
-        constexpr int PER = kColChunk / 256;
+        constexpr int PER = CH / 256;
         uint32_t cnt[PER], start[PER], tx0v[PER];
 #pragma unroll
         for (int i = 0; i < PER; i++) {
@@ -4056,29 +4060,41 @@ hipError_t launch_bin_cols(const uint64_t* rows_buf, const uint32_t* row_items, 
                            uint32_t* cbins, int col_groups, uint32_t pair_capacity, int tiles_x, int tiles_y,
                            uint32_t* vals, uint2* ranges, Stats* stats, Stats* host_mapped_stats, int items,
                            hipStream_t s, const uint32_t* dstats, int passes_launched, bool rank_atomic,
-                           const uint32_t* gate, uint32_t* fstatus) {
+                           const uint32_t* gate, uint32_t* fstatus, int chunk) {
     if (tiles_x < 1 || tiles_x > 256 || tiles_y < 1 || tiles_y > 256 || col_groups < 1 ||
-        (items != 4 && items != 8 && items != 16))
+        (items != 4 && items != 8 && items != 16) || (chunk != (int)kColChunkMin && chunk != (int)kColChunkMax))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_bin_cols_count, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs,
-                       pair_capacity, tiles_x, cbins, gate);
-    hipLaunchKernelGGL(k_bin_cols_scan, dim3(tiles_y), dim3(256), 0, s, row_items, row_pairs, pair_capacity, tiles_x,
-                       cbins, ranges, stats, host_mapped_stats, dstats, passes_launched, gate, fstatus);
-    auto pick = [&](auto ra) {
-        constexpr bool RA = decltype(ra)::value;
-        return tiles_x <= 128 ? (items == 4 ? k_bin_cols_scatter<4, 7, RA> : items == 8 ? k_bin_cols_scatter<8, 7, RA>
-                                                                                     : k_bin_cols_scatter<16, 7, RA>)
-                              : (items == 4 ? k_bin_cols_scatter<4, 8, RA> : items == 8 ? k_bin_cols_scatter<8, 8, RA>
-                                                                                     : k_bin_cols_scatter<16, 8, RA>);
+    auto run = [&](auto ch) {
+        constexpr uint32_t CH = decltype(ch)::value;
+        hipLaunchKernelGGL(k_bin_cols_count<CH>, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs,
+                           pair_capacity, tiles_x, cbins, gate);
+        hipLaunchKernelGGL(k_bin_cols_scan<CH>, dim3(tiles_y), dim3(256), 0, s, row_items, row_pairs, pair_capacity,
+                           tiles_x, cbins, ranges, stats, host_mapped_stats, dstats, passes_launched, gate, fstatus);
+        auto pick = [&](auto ra) {
+            constexpr bool RA = decltype(ra)::value;
+            return tiles_x <= 128
+                       ? (items == 4   ? k_bin_cols_scatter<4, 7, RA, CH>
+                          : items == 8 ? k_bin_cols_scatter<8, 7, RA, CH>
+                                       : k_bin_cols_scatter<16, 7, RA, CH>)
+                       : (items == 4   ? k_bin_cols_scatter<4, 8, RA, CH>
+                          : items == 8 ? k_bin_cols_scatter<8, 8, RA, CH>
+                                       : k_bin_cols_scatter<16, 8, RA, CH>);
+        };
+        auto scatter = rank_atomic ? pick(std::true_type{}) : pick(std::false_type{});
+        hipLaunchKernelGGL(scatter, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs, pair_capacity,
+                           tiles_x, cbins, ranges, vals, gate);
     };
-    auto scatter = rank_atomic ? pick(std::true_type{}) : pick(std::false_type{});
-    hipLaunchKernelGGL(scatter, dim3(col_groups), dim3(256), 0, s, rows_buf, row_items, row_pairs, pair_capacity,
-                       tiles_x, cbins, ranges, vals, gate);
+    if (chunk == (int)kColChunkMin)
+        run(std::integral_constant<uint32_t, kColChunkMin>{});
+    else
+        run(std::integral_constant<uint32_t, kColChunkMax>{});
     return hipGetLastError();
 }
 
+// cbins rows for either chunk size: a row's chunks <= its items / chunk + 1, and every row
+// item holds at least one pair
 uint32_t bin_col_chunks_max(uint32_t pair_capacity, int tiles_y) {
-    return pair_capacity / kColChunk + (uint32_t)tiles_y + 1u;
+    return pair_capacity / kColChunkMin + (uint32_t)tiles_y + 1u;
 }
 
 template <typename K, int ITEMS>

@@ -436,6 +436,7 @@ struct gsr_context {
     bool overflow_seen = false;      // an overflow was reported since the last gsr_sync (which reports it again)
     // bucket depth sort (GSR_TUNE_DEPTH_BUCKETS, gsr_kernels.hip "bucket depth sort")
     int fuse_rows = 1;               // GSR_TUNE_BUCKET_ROWS: the bucket sort's local kernel counts the row pass
+    int col_chunk = 0;               // GSR_TUNE_COL_CHUNK: 0 = by scene size (col_chunk_for), 1024, 2048
     int bucket_sort = 1;             // 0 = LSD passes; 1 = bucket sort after the context's first frame;
                                      // 2 = test hook: as 1 with a local capacity of 64 items (most
                                      // buckets take the global path)
@@ -510,6 +511,13 @@ int bkt_count(int64_t n) {
 // against the LSD passes' 186 (profiles/r05_kt_c3_orbit.txt): the LSD passes stay there.
 constexpr int64_t kBucketSortMaxN = (int64_t)2048 * 1024;
 bool bkt_applies(int64_t n) { return n > 0 && n <= kBucketSortMaxN; }
+
+// Row items per column-pass chunk (GSR_TUNE_COL_CHUNK 0): 1,024 up to the same 2M
+// Gaussians (config 2: column scatter 26.0 -> 21.6 us, chain -2 us), 2,048 above (config 3:
+// the doubled chunk count costs the count and scan +10 us), profiles/r05_ab_col_chunk.txt.
+int col_chunk_for(const gsr_context* c) {
+    return c->col_chunk ? c->col_chunk : (c->n <= kBucketSortMaxN ? 1024 : 2048);
+}
 
 int groups_for(int64_t n, int64_t per) {
     int64_t g = (n + per - 1) / per;
@@ -1190,7 +1198,7 @@ static int bin_locked(gsr_context* c, uint32_t base, uint32_t count, int gate_mo
                                  c->fr.tiles_x, c->fr.tiles_y, pair_vals(c, 1), c->ranges, c->stats,
                                  c->hstats_dev, c->bin_col_items, c->stream,
                                  dst, far ? c->far_launched : c->passes_launched, rank_atomic_on(c),
-                                 gate_mode == 2 ? c->gate : nullptr, c->fstatus));
+                                 gate_mode == 2 ? c->gate : nullptr, c->fstatus, col_chunk_for(c)));
     c->pair_buf = 1;
     return GSR_OK;
 }
@@ -1416,6 +1424,7 @@ void copy_settings(gsr_context* d, const gsr_context* s) {
     d->depth_items = s->depth_items;
     d->bucket_sort = s->bucket_sort;
     d->fuse_rows = s->fuse_rows;
+    d->col_chunk = s->col_chunk;
     d->tile_groups = s->tile_groups;
     d->tile_split_even = s->tile_split_even;
     d->depth_skip = s->depth_skip;
@@ -1881,6 +1890,7 @@ extern "C" int gsr_get_tuning(gsr_context* c, int knob, int* value) {
     case GSR_TUNE_DEPTH_SPLIT_STATE: *value = !c->split_frame ? 0 : !c->frame_key ? 1 : c->frame_spec ? 3 : 2; break;
     case GSR_TUNE_DEPTH_BUCKETS: *value = c->bucket_sort; break;
     case GSR_TUNE_BUCKET_ROWS: *value = c->fuse_rows; break;
+    case GSR_TUNE_COL_CHUNK: *value = c->col_chunk; break;
     case GSR_TUNE_DEPTH_BUCKETS_OVER: {
         int64_t v = c->hstats ? (int64_t)((const volatile Stats*)c->hstats)->bkt_over : 0;
         for (auto* l : c->lanes) v += l->hstats ? (int64_t)((const volatile Stats*)l->hstats)->bkt_over : 0;
@@ -1985,6 +1995,11 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     case GSR_TUNE_DEPTH_BUCKETS:
         if (value < 0 || value > 2) return set_err(GSR_E_ARG, "gsr_set_tuning: depth buckets must be 0, 1 or 2");
         c->bucket_sort = value;
+        return GSR_OK;
+    case GSR_TUNE_COL_CHUNK:
+        if (value != 0 && value != 1024 && value != 2048)
+            return set_err(GSR_E_ARG, "gsr_set_tuning: column chunk must be 0, 1024 or 2048");
+        c->col_chunk = value;
         return GSR_OK;
     case GSR_TUNE_BUCKET_ROWS:
         c->fuse_rows = value != 0;

@@ -390,11 +390,14 @@ enum {
     GSR_TUNE_DEPTH_BUCKETS_OVER = 29, /* read-only: items the bucket sort's global path has sorted (buckets
                                         over the local capacity), summed over the lanes; sticky, read
                                         after gsr_sync */
-    GSR_TUNE_BUCKET_ROWS = 30        /* 1 (default): on a bucket-sorted frame binned once over the whole
+    GSR_TUNE_BUCKET_ROWS = 30,       /* 1 (default): on a bucket-sorted frame binned once over the whole
                                         depth order, each bucket's workgroup also counts the row pass's
                                         items and pairs (the bucket is the row pass's chunk), so the row
                                         pass runs without its count kernel; 0 = the row pass counts.
                                         Same lists, same image */
+    GSR_TUNE_COL_CHUNK = 31          /* binning path: row items per column-pass chunk.  0 (default) =
+                                        1024 for scenes of at most 2,097,152 Gaussians, else 2048;
+                                        1024 or 2048 forces it.  Same lists, same image */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Current value of a knob (what gsr_set_tuning last set, else the default). */

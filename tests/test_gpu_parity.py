@@ -252,13 +252,15 @@ def test_blend_block_mappings_parity(gpu, orc, torch, c1, knobs):
             r.set_blend_variant(v)
 
 
-@pytest.mark.parametrize("knobs", [{}, {8: 4, 9: 16}, {8: 16, 9: 4, 10: 7}])
+@pytest.mark.parametrize("knobs", [{}, {8: 4, 9: 16}, {8: 16, 9: 4, 10: 7}, {31: 2048}, {31: 2048, 10: 7},
+                                   {31: 1024, 9: 16, 10: 7}])
 def test_tile_binning_matches_pair_sort(gpu, orc, torch, c1, knobs):
     """Row + column binning (default for grids <= 256 x 256 tiles) gives the same
     tile lists as pair emission + the key-value tile sort: identical (tile,
     Gaussian) pairs in identical order, identical images, both equal to the
     oracle.  Knobs 8/9: items per thread of the row / column tiles (4, 16);
-    10: column-pass workgroups (7 forces the grid-stride chunk loop)."""
+    10: column-pass workgroups (7 forces the grid-stride chunk loop); 31: row items
+    per column-pass chunk (1024, the default at this size, or 2048)."""
     path, soa = c1
     W, H = 1000, 700
     scene = gpu.Scene.from_soa(soa)
@@ -381,11 +383,15 @@ def test_tuning_defaults_read_back(gpu):
     gsr_set_tuning set; unknown knobs are refused."""
     r = gpu.Renderer()
     defaults = {1: 16, 2: 0, 3: 1024, 4: 0, 5: 1, 6: 1, 7: 1, 8: 4, 9: 8, 10: 0, 11: 1, 13: 4, 18: 2, 19: 2,
-                23: 2, 24: 250}
+                23: 2, 24: 250, 31: 0}
     for kn, v in defaults.items():
         assert r.get_tuning(kn) == v, kn
     r.set_tuning(9, 16)
     assert r.get_tuning(9) == 16
+    r.set_tuning(31, 2048)
+    assert r.get_tuning(31) == 2048
+    with pytest.raises(gpu.GsrError):
+        r.set_tuning(31, 512)
     with pytest.raises(gpu.GsrError):
         r.get_tuning(12)
 
