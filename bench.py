@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--sh3", action="store_true",
                     help="config 2 as BASELINE states it (SH degree 3): the opt-in SH-3 mode (all 45 f_rest, "
                          "bands 0-3; the reference evaluates bands 0-2)")
+    ap.add_argument("--no-orbit-line", action="store_true",
+                    help="config 2: skip the moving-camera sub-measurement (the 'orbit' object of the JSON line)")
     ap.add_argument("--orbit-step", type=float, default=0.0,
                     help="degrees of Camera::orbit per frame (a moving viewer: frame i at azimuth i * step); "
                          "0 = the fixed camera")
@@ -349,6 +351,113 @@ def sh3_line(gsr, torch, multi, args, ply, cam, W, H, F, stream, n) -> dict:
     return out
 
 
+ORBIT_LINE_STEP_DEG = 0.25    # the moving viewer of the 'orbit' object: Camera::orbit per frame
+ORBIT_STATS_FRAMES = 40       # untimed frames whose bucket sizes give the splitter imbalance
+
+
+def orbit_line(gsr, torch, multi, args, scene, W, H, F, stream) -> dict:
+    """Config 2 on a moving camera: the same seed-2 scene, frame i orbited
+    by 0.25 deg * i (Camera::orbit, camera.cpp:130-158; the orbit continues across every
+    region below, so no frame repeats a view), K frames in flight and one at a time after
+    the same warmup.  The headline repeats one camera, the best case of every temporal cache
+    in the path (the bucket splitters are the previous frame's depth quantiles, the depth
+    pass budget, the depth split's speculation); this object reports the moving viewer's
+    rate beside it, the items the bucket sort sent through its global path (buckets over
+    the 2,048-item local capacity) in the timed frames, and the splitter imbalance (the
+    largest live bucket / the mean) of ORBIT_STATS_FRAMES more frames."""
+    import numpy as np
+    pos = [0]
+    cache = {}
+
+    def cam_at(i):
+        j = pos[0] + i
+        if j not in cache:
+            c = gsr.make_camera(position=(0, 0, 4), fov_y=50, aspect=W / H)
+            gsr.orbit(c, ORBIT_LINE_STEP_DEG * j, 0.0)
+            cache[j] = c
+        return cache[j]
+
+    ro = gsr.Renderer()
+    for kv in filter(None, args.tune.split(",")):
+        knob, val = kv.split("=")
+        ro.set_tuning(int(knob), int(val))
+    ro.set_frames_in_flight(F)
+    sh = multi.FrameShard(None, ro, scene, cam_at(0), W, H, k=args.k, steps=args.steps, gather="none", inflight=F,
+                          chunk=args.chunk, stream=stream, frame_cam=cam_at)
+    for i in range(max(1, args.warmup)):
+        sh.frame(i)
+    pos[0] += max(1, args.warmup)
+    while ro.sync() != 0:
+        sh.frame(0)
+        pos[0] += 1
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) < 0.3:          # the card stays warm, the orbit keeps moving
+        sh.run(4 * F)
+        pos[0] += 4 * F
+        torch.cuda.synchronize()
+    ro.sync()
+    over0 = ro.get_tuning(29)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        sh.frame(i)
+    torch.cuda.synchronize()
+    seq = time.perf_counter() - t0
+    pos[0] += args.steps
+    seq_rc = ro.sync()
+    timed_frames = args.steps
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sh.run(args.steps)
+        sh.drain()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        pos[0] += args.steps
+        timed_frames += args.steps
+        if not sh.finish("cuda"):
+            break
+    over_timed = ro.get_tuning(29) - over0
+    # untimed: frames one at a time on lane 0 (its bucket totals after each), the orbit
+    # continuing, with the per-stage events
+    imb, glob, lsd = [], [], 0
+    ro.set_timing(2)
+    for i in range(ORBIT_STATS_FRAMES):
+        o0 = ro.get_tuning(29)
+        sh.frame(i)
+        ro.sync()
+        sizes = ro.bucket_sizes()
+        if sizes is None:
+            lsd += 1
+            continue
+        live = sizes[:-1].astype(np.float64)
+        if live.sum() > 0:
+            imb.append(float(live.max() / live.mean()))
+        glob.append(ro.get_tuning(29) - o0)
+    sums, frames = ro.stage_times()
+    ro.set_timing(0)
+    pos[0] += ORBIT_STATS_FRAMES
+    ro.close()
+    return {"value": round(args.steps / el, 3), "unit": "frames/sec", "ms_per_step": round(el / args.steps * 1e3, 4),
+            "sequential": {"value": round(args.steps / seq, 3), "ms_per_frame": round(seq / args.steps * 1e3, 4)},
+            "orbit_step_deg": ORBIT_LINE_STEP_DEG, "frames_in_flight": F,
+            "depth_bucket_global_items": int(over_timed),
+            "depth_bucket_global_items_per_frame": round(over_timed / max(1, timed_frames), 1),
+            "splitter_imbalance": {"mean": round(float(np.mean(imb)), 3) if imb else None,
+                                   "max": round(float(np.max(imb)), 3) if imb else None,
+                                   "frames": len(imb),
+                                   "global_items_per_frame": round(float(np.mean(glob)), 1) if glob else None,
+                                   "lsd_frames": lsd,
+                                   "note": "largest live bucket / mean live bucket of each bucket-sorted frame "
+                                           "(gsr_bucket_sizes), ORBIT_STATS_FRAMES untimed frames one at a time "
+                                           "after the timed ones"},
+            "stages_ms": {k: round(v / max(1, frames), 4) for k, v in sums.items()},
+            "overflow_after_timed": seq_rc,
+            "note": "config 2 on a moving camera: frame i orbited by 0.25 deg * i around the scene (camera.cpp "
+                    "Camera::orbit), the orbit continuing through warmup, the one-at-a-time and the in-flight "
+                    "regions; same scene, K, warmup as the headline"}
+
+
 def frame_time(i: int) -> float:
     """Config 5: frame i renders timestep i mod 120 of [0, 1]."""
     return (i % TIMESTEPS_4D) / (TIMESTEPS_4D - 1)
@@ -538,6 +647,7 @@ def main():
     # collective); a region with one is timed again, once, on the grown buffers.
     dev_kind = "cpu" if gloo else "cuda"
     reruns = 0
+    shard.time_gathers = dist is not None   # N > 1: per-chunk gather times for the 'scale' object
     if shard.validity:
         # per-step gathers carry each frame's validity word: the timed region includes
         # re-rendering and re-gathering exactly the chunks some rank got incomplete
@@ -569,6 +679,28 @@ def main():
 
     max_elapsed = multi.max_over_ranks(dist, elapsed, "cpu" if gloo else "cuda")
     max_seq = multi.max_over_ranks(dist, seq_elapsed, "cpu" if gloo else "cuda")
+    scale = None
+    if dist:
+        # what each rank renders with no gathers (a short region after the
+        # headline, not part of it) and what the gathers cost, so the first SCALE record
+        # can be read against DESIGN.md section 8's prediction
+        gms = shard.gather_ms()
+        shard.time_gathers = False
+        ro = multi.FrameShard(dist, r, scene, cam, W, H, k=args.k, steps=args.steps, gather="none", inflight=F,
+                              chunk=args.chunk, gloo=gloo, frame_time=frame_time if four_d else None,
+                              stream=stream, frame_cam=frame_cam)
+        ro.run(args.steps)               # warm: the lanes leave the gathered loop's rhythm
+        torch.cuda.synchronize()
+        r.sync()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ro.run(args.steps)
+        torch.cuda.synchronize()
+        render_el = time.perf_counter() - t0
+        r.sync()
+        scale = multi.scale_report(dist, render_el, args.steps, gms, world * args.steps / max_elapsed,
+                                   "cpu" if gloo else "cuda")
     gather_ms = None
     if dist and args.gather == "end":
         torch.cuda.synchronize()
@@ -660,6 +792,8 @@ def main():
     result["sustained_warmup"] = {"frames": warm_frames, "min_ms": args.warm_ms}
     if gather_ms is not None:
         result["gather_ms"] = round(gather_ms, 3)
+    if scale is not None:
+        result["scale"] = scale
     if dist:
         result["scene_broadcast_ms"] = round(broadcast_ms, 2)
         result["gathers_per_rank_timed"] = shard.gathers
@@ -686,6 +820,8 @@ def main():
         result["roofline"]["traffic_source"] = traffic["source"]
     if world == 1 and args.config == 2 and not args.sh3 and not args.no_sh3_line:
         result["sh3"] = sh3_line(gsr, torch, multi, args, ply, cam, W, H, F, stream, n)
+    if world == 1 and args.config == 2 and not args.sh3 and not args.orbit_step and not args.no_orbit_line:
+        result["orbit"] = orbit_line(gsr, torch, multi, args, scene, W, H, F, stream)
     if world == 1:
         result["dropin_host_fps"] = round(dropin_rate(gsr, scene, cam, W, H, args.k), 2)
     if world == 1 and not args.no_cpu_baseline:

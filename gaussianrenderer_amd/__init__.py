@@ -485,6 +485,15 @@ class Renderer:
             raise GsrError(rc, "gsr_depth_passes")
         return rc
 
+    def bucket_sizes(self):
+        """gsr_bucket_sizes: per-bucket item counts of the last frame when it was
+        bucket-sorted (the last bucket: key 0xFFFFFFFF, the culled items), else None."""
+        out = np.zeros(MAX_BUCKETS, dtype=np.uint32)
+        rc = lib().gsr_bucket_sizes(self.ctx, out.ctypes.data, out.size)
+        if rc < 0:
+            raise GsrError(rc, "gsr_bucket_sizes")
+        return out[:rc] if rc else None
+
     def blend_stamps(self, n_groups: int) -> np.ndarray:
         """{start, end} s_memrealtime stamps (100 MHz) per blend workgroup of the
         last diagnostics frame rendered with schedule 2 (one per tile) or 3 (one
@@ -520,6 +529,8 @@ TUNE_DEPTH_BUCKETS = 28
 TUNE_DEPTH_BUCKETS_OVER = 29
 TUNE_BUCKET_ROWS = 30
 TUNE_COL_CHUNK = 31
+TUNE_FAIL_FRAME = 32
+MAX_BUCKETS = 4096             # gsr_internal.h kMaxBuckets: the bucket sort's largest bucket count
 
 
 def rank_order_check() -> tuple[int, int]:

@@ -143,6 +143,7 @@ SIGNATURES = [
     ("gsr_get_tuning", c_int, [c_void_p, c_int, c_void_p]),
     ("gsr_set_timing_stride", c_int, [c_void_p, c_int, c_int]),
     ("gsr_depth_passes", c_int, [c_void_p]),
+    ("gsr_bucket_sizes", c_int, [c_void_p, c_void_p, c_int]),
     ("gsr_scene_upload", c_void_p, [c_void_p, c_int64]),
     ("gsr_scene_upload_ex", c_void_p, [c_void_p, c_int, c_int64]),
     ("gsr_set_time", c_int, [c_void_p, c_float]),

@@ -147,8 +147,8 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
 // tile rects by position) into items0 with the rects into pay0; items1 / pay1 are scratch.
 // buckets: 256..4096 (a power of two); s_in: its buckets - 1 sorted splitters (the last
 // 0xFFFFFFFF); s_out: the next frame's (quantiles of this order).  hist: groups x buckets
-// u32 (groups <= kMaxBucketGroups), totals: 2 x buckets + 1 u32 (the totals, then the
-// buckets' first positions).  cap (<= kMaxBucketCap): largest bucket sorted in LDS (larger
+// u32 (groups <= kMaxBucketGroups), totals: 2 x buckets + 2 u32 (the totals, then the
+// buckets' first positions and n, then a word raised when a live item has key 0xFFFFFFFF).  cap (<= kMaxBucketCap): largest bucket sorted in LDS (larger
 // ones take the global path; over_host, host-mapped and nullable, counts their items).
 constexpr int kMaxBuckets = 4096;
 constexpr uint32_t kMaxBucketCap = 2048;
@@ -158,8 +158,10 @@ hipError_t launch_bucket_sort(const uint64_t* in, uint64_t* items0, uint64_t* it
                               const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
                               unsigned int* over_host, hipStream_t s, int row_tiles_y = 0);
 // row_tiles_y > 0: the local kernel also writes the row pass's count histograms into hist
-// (512 x (buckets - 1) words: chunk g = bucket g, tile rows < row_tiles_y), and the row pass
-// then runs with cstart = totals + buckets (the buckets' first positions) and no count kernel.
+// (512 x buckets words: chunk g = bucket g, tile rows < row_tiles_y; the last bucket's chunk
+// is empty unless a live item's key saturated to 0xFFFFFFFF), and the row pass then runs
+// with buckets chunks, cstart = totals + buckets (the buckets' first positions) and no count
+// kernel.
 // Splitters for launch_bucket_sort from an order the LSD passes sorted (depth_sorted of
 // items0 / items1 under dstats); live_dev (nullable): its visible count.
 hipError_t launch_bkt_splitters(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,

@@ -1869,6 +1869,8 @@ __global__ __launch_bounds__(1024) void k_bkt_scan(uint32_t* __restrict__ hist, 
         tot += p;
     }
     if (w == 0) totals[b] = tot;
+    // the frame's "a live item has key 0xFFFFFFFF" word (bkt_sat_word), raised by the scatter
+    if (blockIdx.x == 0 && t == 0) totals[2 * B + 1] = 0u;
 #pragma unroll
     for (int i = 0; i < kPerMax; i++) {
         const uint32_t g = g0 + (uint32_t)i;
@@ -1882,8 +1884,9 @@ __global__ __launch_bounds__(1024) void k_bkt_scan(uint32_t* __restrict__ hist, 
 // 16-bit half h of the packed counter word v.
 __device__ __forceinline__ uint32_t half16(uint32_t v, uint32_t h) { return (v >> (16u * h)) & 0xffffu; }
 
-// bstart (B + 1 words): written by chunk 0's workgroup, the first position of every bucket
-// and bstart[B] = n (k_bkt_local reads its bucket's range there).
+// bstart (B + 2 words): written by chunk 0's workgroup, the first position of every bucket
+// and bstart[B] = n (k_bkt_local reads its bucket's range there); bstart[B + 1] (cleared by
+// k_bkt_scan) is raised when a live item (a tile rect that covers tiles) has key 0xFFFFFFFF.
 // TH threads (512 from 512 buckets up: twice the waves of 256, half the items per wave, so
 // each wave's latency chain is half as long; the grid is only ~n / 2,048 workgroups:
 // 16.3-16.8 -> 15.6-15.8 us at config 2, profiles/r05_kt_bkt_scatter512.txt).
@@ -1964,6 +1967,10 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
             const bool valid = el < tn;
             const bool dead = keys[k] == 0xffffffffu;
             const uint32_t d = dg[k];
+            // a live Gaussian whose key saturated (depth >= ~4295 under a far clip that keeps
+            // it) shares the last bucket with the culled items: k_bkt_local's fused row count
+            // must then bin that bucket too (rare: a plain vector store of 1)
+            if (valid && dead && rect_count(unpack_rect(pv[k]))) bstart[B + 1] = 1u;
             const uint64_t dm = __ballot(valid && dead);
             uint32_t r = dead_run + (uint32_t)__popcll(dm & lt_mask);
             dead_run += (uint32_t)__popcll(dm);
@@ -2091,7 +2098,8 @@ __device__ __forceinline__ void row_hist_write(const RowHist& rh, uint32_t g, ui
     }
 }
 
-// One workgroup per live bucket (grid B - 1).  bstart: the buckets' first positions
+// One workgroup per live bucket (grid B - 1; B with the fused row count, whose last
+// workgroup only counts the last bucket's rows).  bstart: the buckets' first positions
 // (k_bkt_scatter); s_in: the splitters this frame was bucketed by, which bound the keys of
 // every bucket but the first and the last (their key span sets the passes).  cap: buckets
 // above it take the global path (kBktCap; smaller only as a test hook).  over_host
@@ -2099,7 +2107,7 @@ __device__ __forceinline__ void row_hist_write(const RowHist& rh, uint32_t g, ui
 template <int B, bool RA>
 __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict__ items, uint64_t* __restrict__ scratch,
                                                            uint32_t* __restrict__ pay, uint32_t* __restrict__ pay_scratch,
-                                                           const uint32_t* __restrict__ bstart,
+                                                           uint32_t* __restrict__ bstart,
                                                            const uint32_t* __restrict__ s_in,
                                                            uint32_t* __restrict__ s_next, uint32_t cap,
                                                            unsigned int* over_host, RowHist rh) {
@@ -2110,6 +2118,39 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
     __shared__ uint32_t s_hp[4][256];   // fused row-pass count: pairs (s_wc holds the items)
     __shared__ uint32_t s_scr[4], s_mm[2];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    auto row_zero = [&]() {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            s_wc[k][t] = 0;
+            s_hp[k][t] = 0;
+        }
+    };
+    if (blockIdx.x == (uint32_t)B - 1u) {
+        // fused row count only (grid B): the last bucket (key 0xFFFFFFFF, index order, never
+        // sorted) is the row pass's last chunk.  It holds culled items only unless the scatter
+        // raised bstart[B + 1]; then its rects are counted (every live one binned, as the LSD
+        // path and render.cu do), else the chunk is emptied (bstart[B] = its start: the
+        // row pass reads nothing there).  Only this workgroup reads bstart[B].
+        const uint32_t start = bstart[B - 1], end = bstart[B];
+        const bool sat = bstart[B + 1] != 0u;
+        row_zero();
+        __syncthreads();
+        if (sat) {
+            for (uint32_t i = start + t; i < end; i += 4u * kBktThreads) {
+                uint32_t p[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t j = i + (uint32_t)k * kBktThreads;
+                    p[k] = j < end ? pay[j] : pack_rect(kDeadRect);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) row_hist_add(s_wc, s_hp, w, p[k]);
+            }
+        }
+        row_hist_write(rh, (uint32_t)B - 1u, s_wc, s_hp, s_scr);
+        if (!sat && t == 0) bstart[B] = start;
+        return;
+    }
     // XCD-contiguous buckets: the fused row count's histogram lines (16 consecutive
     // buckets of a row) merge in one L2 (12.4 -> 11.95 us at config 2,
     // profiles/r05_kt_xcd_hist.txt)
@@ -2123,13 +2164,6 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
         if (live == 0)
             for (uint32_t j = 0; j < (uint32_t)B - 2u; j++) s_next[j] = 0;   // any sorted splitters will do
     }
-    auto row_zero = [&]() {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            s_wc[k][t] = 0;
-            s_hp[k][t] = 0;
-        }
-    };
     if (count == 0) {   // uniform; an empty bucket is an empty row-pass chunk
         if (rh.hist) {
             row_zero();
@@ -3943,21 +3977,23 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
                           const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
                           unsigned int* over_host, hipStream_t s, int row_tiles_y) {
     // fused row-pass count: the row hist overwrites the bucket hist, which only the scatter reads
-    const RowHist rh{row_tiles_y > 0 ? hist : nullptr, B - 1, row_tiles_y};
-    uint32_t* bstart = totals + B;   // B + 1 words after the totals
+    // (grid B with it: the last bucket is the row pass's last chunk, k_bkt_local)
+    const RowHist rh{row_tiles_y > 0 ? hist : nullptr, B, row_tiles_y};
+    const int local_grid = row_tiles_y > 0 ? B : B - 1;
+    uint32_t* bstart = totals + B;   // B + 2 words after the totals
     hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist);
     hipLaunchKernelGGL(k_bkt_scan<B>, dim3(B / 64), dim3(1024), 0, s, hist, groups, totals);
     constexpr int kScTh = B >= 512 ? 512 : kBktThreads;   // k_bkt_scatter's workgroup size
     if (rank_atomic) {
         hipLaunchKernelGGL((k_bkt_scatter<B, true, kScTh>), dim3(groups), dim3(kScTh), 0, s, in, items0, n, s_in,
                            groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart);
-        hipLaunchKernelGGL((k_bkt_local<B, true>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0, pay1,
-                           static_cast<const uint32_t*>(bstart), s_in, s_out, cap, over_host, rh);
+        hipLaunchKernelGGL((k_bkt_local<B, true>), dim3(local_grid), dim3(kBktThreads), 0, s, items0, items1, pay0,
+                           pay1, bstart, s_in, s_out, cap, over_host, rh);
     } else {
         hipLaunchKernelGGL((k_bkt_scatter<B, false, kScTh>), dim3(groups), dim3(kScTh), 0, s, in, items0, n, s_in,
                            groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart);
-        hipLaunchKernelGGL((k_bkt_local<B, false>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0, pay1,
-                           static_cast<const uint32_t*>(bstart), s_in, s_out, cap, over_host, rh);
+        hipLaunchKernelGGL((k_bkt_local<B, false>), dim3(local_grid), dim3(kBktThreads), 0, s, items0, items1, pay0,
+                           pay1, bstart, s_in, s_out, cap, over_host, rh);
     }
 }
 
@@ -3969,7 +4005,7 @@ hipError_t launch_bucket_sort(const uint64_t* in, uint64_t* items0, uint64_t* it
         cap > kBktCap ||
         in == items0 || !rect || !pay0 || !pay1)   // in may be items1: the scratch is used after the scatter
         return hipErrorInvalidValue;
-    if (n == 0 || row_tiles_y > 256 || (int64_t)512 * (buckets - 1) > 256 * (int64_t)kMaxSortGroups)
+    if (n == 0 || row_tiles_y > 256 || (int64_t)512 * buckets > 256 * (int64_t)kMaxSortGroups)
         return n == 0 ? hipSuccess : hipErrorInvalidValue;
     switch (buckets) {
     case 256: bucket_sort_b<256>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y); break;

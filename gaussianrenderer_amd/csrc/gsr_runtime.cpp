@@ -418,6 +418,7 @@ struct gsr_context {
     uint64_t* pre_out = nullptr;     // where the preprocess wrote its items
     bool records_partial = false;    // the preprocess wrote only the near Gaussians' records
     const float* pre_arrays = nullptr;   // the preprocessed scene arrays (the far record pass re-reads them)
+    const void* pre_scene = nullptr;     // the scene pointer gsr_preprocess was given
     int64_t pre_stride = 0;
     int pre_layout = 0;
     uint32_t* dstats_far = nullptr;  // depth split: the far sort's pass plan
@@ -443,10 +444,13 @@ struct gsr_context {
     uint32_t* bkt_split = nullptr;   // 2 x kMaxBuckets splitters (double-buffered: read one, write the other)
     int bkt_par = 0;                 // the half the next bucket-sorted frame reads
     int bkt_B = 0;                   // buckets the splitters were made for (0: none yet)
+    const void* bkt_scene = nullptr; // the scene they were made from (another scene reseeds them)
+    unsigned int bkt_over_seen = 0;  // hstats->bkt_over when the last frame was prepared
     bool bds_frame = false;          // this frame's preprocess items went to items[1] for the bucket sort
     bool last_bds = false;           // the last sorted frame was bucket-sorted (order in items[0], no pass plan)
     bool bkt_rows_fused = false;     // its local sorts wrote the row pass's counts (bucket = row chunk): the
                                      // next binning skips its count kernel (once: the row scan consumes them)
+    int fail_frame = 0;              // GSR_TUNE_FAIL_FRAME: gsr_render_path fails this frame (> 0) once
     uint32_t* fstatus = nullptr;     // the current frame's validity word (gsr_render_path_status; device,
                                      // nullable): GSR_FRAME_* bits, written by its column scans / blend
     // frame state
@@ -577,7 +581,7 @@ int ensure_static(gsr_context* c) {
     }
     if (int rc = realloc_dev(&c->hist, 256 * (size_t)gsr::kMaxSortGroups)) return rc;
     // LSD digit totals / bucket totals + bucket starts
-    if (int rc = realloc_dev(&c->totals, 2 * (size_t)gsr::kMaxBuckets + 1)) return rc;
+    if (int rc = realloc_dev(&c->totals, 2 * (size_t)gsr::kMaxBuckets + 2)) return rc;
     if (int rc = realloc_dev(&c->bkt_split, 2 * (size_t)gsr::kMaxBuckets)) return rc;
     if (int rc = realloc_dev(&c->wg, (size_t)gsr::kMaxSortGroups)) return rc;
     if (int rc = realloc_dev(&c->stats, 2)) return rc;
@@ -964,6 +968,17 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     // bucket depth sort (splitters exist for this scene size): the items go to items[1], the
     // sort writes the order into items[0]; it keeps culled items apart itself, so it
     // replaces the live partition
+    // the splitters are this scene's and did not just fail: a frame that sent more than an
+    // eighth of the scene through the global path (a camera cut, a zoom) makes the next one
+    // reseed them from the LSD passes (a camera jump could put most of a 2M scene
+    // into one bucket, sorted by one workgroup, a frame of tens of ms).  bkt_over is
+    // host-mapped and lags by the frames in flight; the test hook 2 (capacity 64) keeps them.
+    {
+        const unsigned int over = c->hstats ? ((const volatile Stats*)c->hstats)->bkt_over : 0u;
+        const bool spike = c->bucket_sort == 1 && (int64_t)(over - c->bkt_over_seen) > n / 8;
+        c->bkt_over_seen = over;
+        if (c->bkt_B && (spike || c->bkt_scene != scene)) c->bkt_B = 0;
+    }
     c->bds_frame = bkt_applies(n) && !c->split_key && c->bucket_sort && c->bkt_B == bkt_count(n) && c->tile_binning &&
                    c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
     c->compact_frame = n > 0 && !c->split_key && !c->bds_frame &&
@@ -982,6 +997,7 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     // (speculative frames only: a frame that queues phase B needs every record there)
     c->records_partial = c->split_key && c->split_spec && !c->spans_frame;
     c->pre_arrays = arrays;
+    c->pre_scene = scene;
     c->pre_stride = stride;
     c->pre_layout = layout;
     const gsr::RecSplit rsp{c->records_partial ? 1 : 0, c->kcut, c->kcut_frame, nullptr};
@@ -1036,7 +1052,7 @@ static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false
         const int G = std::min(groups_for(c->n, gsr::kMaxBucketCap), gsr::kMaxBucketGroups);
         // a plain frame (one binning over the whole order): the local sorts also count the
         // row pass's items and pairs per bucket, which becomes the row pass's chunk
-        const bool fuse = plain && c->fuse_rows && (int64_t)512 * (B - 1) <= 256 * (int64_t)gsr::kMaxSortGroups;
+        const bool fuse = plain && c->fuse_rows && (int64_t)512 * B <= 256 * (int64_t)gsr::kMaxSortGroups;
         uint32_t* s_in = c->bkt_split + (size_t)c->bkt_par * gsr::kMaxBuckets;
         uint32_t* s_out = c->bkt_split + (size_t)(c->bkt_par ^ 1) * gsr::kMaxBuckets;
         HIP_TRY(gsr::launch_bucket_sort(c->pre_out, c->items[0], c->items[1], n, B, G, s_in, s_out, c->hist,
@@ -1117,6 +1133,7 @@ static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false
                                           part ? c->nlive : nullptr, B,
                                           c->bkt_split + (size_t)c->bkt_par * gsr::kMaxBuckets, c->stream));
         c->bkt_B = B;
+        c->bkt_scene = c->pre_scene;
     }
     return GSR_OK;
 }
@@ -1184,7 +1201,7 @@ static int bin_locked(gsr_context* c, uint32_t base, uint32_t count, int gate_mo
     c->bkt_rows_fused = false;
     const uint32_t* cstart = fused ? c->totals + c->bkt_B : nullptr;
     HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], dst, count, pay_buf(c, 0),
-                                 pay_buf(c, 1), fused ? c->bkt_B - 1 : gb,
+                                 pay_buf(c, 1), fused ? c->bkt_B : gb,
                                  c->hist, row_items, row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items,
                                  c->stream, c->spans_frame ? c->spans : nullptr, rank_atomic_on(c), base,
                                  gate_mode ? c->gate : nullptr, gate_mode, rs && rs->cut_mode ? c->nlive : nullptr,
@@ -1563,13 +1580,27 @@ extern "C" int gsr_render_path_status(gsr_context* c, const void* scene, int lay
         }
     }
     int result = GSR_OK;
+    int err = GSR_OK;   // the first error; the frames queued before it are still joined below
     const float t_saved = c->time;
-    for (int i = 0; i < nframes; i++) {
+    auto hip_fail = [&](hipError_t e, const char* what) {
+        return set_err(GSR_E_HIP, "gsr_render_path: %s: %s", what, hipGetErrorString(e));
+    };
+    for (int i = 0; i < nframes && err == GSR_OK; i++) {
         const int lane = i % F;
         gsr_context* lc = lane == 0 ? c : c->lanes[lane - 1];
         const hipStream_t ls = lane == 0 ? S : c->lane_streams[lane - 1];
-        if (prev[i] >= 0 && prev[i] % F != lane) HIP_TRY(hipStreamWaitEvent(ls, c->alias_evs[prev[i] % F], 0));
-        if (wait_events && wait_events[i]) HIP_TRY(hipStreamWaitEvent(ls, static_cast<hipEvent_t>(wait_events[i]), 0));
+        if (prev[i] >= 0 && prev[i] % F != lane) {
+            if (hipError_t e = hipStreamWaitEvent(ls, c->alias_evs[prev[i] % F], 0)) {
+                err = hip_fail(e, "output reuse wait");
+                break;
+            }
+        }
+        if (wait_events && wait_events[i]) {
+            if (hipError_t e = hipStreamWaitEvent(ls, static_cast<hipEvent_t>(wait_events[i]), 0)) {
+                err = hip_fail(e, "wait event");
+                break;
+            }
+        }
         if (times) lc->time = times[i];
         else lc->time = t_saved;
         // the frame's validity word is the lane's only while its frame is queued: the guard
@@ -1580,20 +1611,40 @@ extern "C" int gsr_render_path_status(gsr_context* c, const void* scene, int lay
             ~StatusScope() { lc->fstatus = nullptr; }
         } status_scope{lc};
         lc->fstatus = d_status ? d_status[i] : nullptr;
-        const int rc = render_one_locked(lc, scene, layout, n, &cams[i], W, H, nx, ny, ws, hs, k, d_outs[i], ls);
-        if (rc == GSR_E_OVERFLOW) result = GSR_E_OVERFLOW;
-        else if (rc != GSR_OK) return rc;
-        if (record[i]) HIP_TRY(hipEventRecord(c->alias_evs[lane], ls));
-        if (frame_events && frame_events[i]) HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(frame_events[i]), ls));
+        int rc;
+        if (c->fail_frame > 0 && i == c->fail_frame) {   // GSR_TUNE_FAIL_FRAME (test hook, once)
+            c->fail_frame = 0;
+            rc = set_err(GSR_E_ARG, "gsr_render_path: frame %d failed (GSR_TUNE_FAIL_FRAME test hook)", i);
+        } else {
+            rc = render_one_locked(lc, scene, layout, n, &cams[i], W, H, nx, ny, ws, hs, k, d_outs[i], ls);
+        }
+        if (rc == GSR_E_OVERFLOW) {
+            result = GSR_E_OVERFLOW;
+        } else if (rc != GSR_OK) {
+            err = rc;
+            break;
+        }
+        if (record[i]) {
+            if (hipError_t e = hipEventRecord(c->alias_evs[lane], ls)) err = hip_fail(e, "output reuse event");
+        }
+        if (err == GSR_OK && frame_events && frame_events[i]) {
+            if (hipError_t e = hipEventRecord(static_cast<hipEvent_t>(frame_events[i]), ls))
+                err = hip_fail(e, "frame event");
+        }
     }
+    // on every exit after the fork, errors included (render.cu:914-923 reports a failed
+    // step and the caller's frame loop goes on): the time knob is restored, the caller's
+    // stream is the context's again, and work queued on it afterwards sees every frame the
+    // lanes took (a caller that frees or reuses an output after an error must not race a
+    // lane still writing it).  A join failure after an earlier error keeps the first message.
     c->time = t_saved;
-    // join: work queued on the caller's stream afterwards sees every frame
-    for (int l = 0; l < F - 1 && l + 1 < nframes && !(flags & GSR_PATH_NO_JOIN); l++) {
-        HIP_TRY(hipEventRecord(c->join_evs[l], c->lane_streams[l]));
-        HIP_TRY(hipStreamWaitEvent(S, c->join_evs[l], 0));
-    }
     c->stream = S;
-    return result;
+    for (int l = 0; l < F - 1 && l + 1 < nframes && !(flags & GSR_PATH_NO_JOIN); l++) {
+        hipError_t e = hipEventRecord(c->join_evs[l], c->lane_streams[l]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(S, c->join_evs[l], 0);
+        if (e != hipSuccess && err == GSR_OK) err = hip_fail(e, "join");
+    }
+    return err != GSR_OK ? err : result;
 }
 
 extern "C" int gsr_sync(gsr_context* c) {
@@ -1750,6 +1801,18 @@ extern "C" int gsr_depth_passes(gsr_context* c) {
     return p;
 }
 
+extern "C" int gsr_bucket_sizes(gsr_context* c, uint32_t* sizes, int cap) {
+    if (!c || cap < 0 || (cap > 0 && !sizes)) return set_err(GSR_E_ARG, "gsr_bucket_sizes: bad argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->have_sort || !c->last_bds || !c->bkt_B || !c->totals) return 0;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    // k_bkt_scan's bucket totals (totals[0 .. B)), which a bucket-sorted frame's later
+    // kernels only read
+    const int m = std::min(cap, c->bkt_B);
+    if (m) HIP_TRY(hipMemcpy(sizes, c->totals, (size_t)m * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return c->bkt_B;
+}
+
 extern "C" int gsr_read_depth_order(gsr_context* c, uint64_t* host, int64_t n) {
     if (!c || !host || n < 0 || n > c->n || !c->have_sort) return set_err(GSR_E_ARG, "gsr_read_depth_order: bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
@@ -1891,6 +1954,7 @@ extern "C" int gsr_get_tuning(gsr_context* c, int knob, int* value) {
     case GSR_TUNE_DEPTH_BUCKETS: *value = c->bucket_sort; break;
     case GSR_TUNE_BUCKET_ROWS: *value = c->fuse_rows; break;
     case GSR_TUNE_COL_CHUNK: *value = c->col_chunk; break;
+    case GSR_TUNE_FAIL_FRAME: *value = c->fail_frame; break;
     case GSR_TUNE_DEPTH_BUCKETS_OVER: {
         int64_t v = c->hstats ? (int64_t)((const volatile Stats*)c->hstats)->bkt_over : 0;
         for (auto* l : c->lanes) v += l->hstats ? (int64_t)((const volatile Stats*)l->hstats)->bkt_over : 0;
@@ -2003,6 +2067,10 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         return GSR_OK;
     case GSR_TUNE_BUCKET_ROWS:
         c->fuse_rows = value != 0;
+        return GSR_OK;
+    case GSR_TUNE_FAIL_FRAME:
+        if (value < 0) return set_err(GSR_E_ARG, "gsr_set_tuning: fail frame must be >= 0");
+        c->fail_frame = value;
         return GSR_OK;
     case GSR_TUNE_RANK_ATOMIC_ACTIVE:
     case GSR_TUNE_DEPTH_SPLIT_UNSAT:

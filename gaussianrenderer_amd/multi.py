@@ -103,6 +103,59 @@ def broadcast_scene(dist, scene, gloo: bool = False):
     return out
 
 
+# DESIGN.md section 8's prediction of the N-GPU rate: the per-chunk gathers cost one GPU
+# 3.8 % at world 1 (profiles/r03_reh_chunks.txt), and rank 0's receive kernels beside its
+# own render are budgeted at 5 %.
+GATHER_COST_WORLD1 = 0.038
+RANK0_RECEIVE_BUDGET = 0.95
+
+
+def scale_report(dist, render_elapsed: float, render_steps: int, gather_ms, value: float, device) -> dict | None:
+    """The self-explaining part of an N > 1 bench line (a collective: every rank calls it;
+    rank 0 gets the dict, the others None).
+
+    render_elapsed: this rank's wall time for render_steps frames in flight with no
+    gathers (its render-only rate); gather_ms: this rank's per-chunk gather durations on
+    the side stream during the headline region (from the frames being done to the gather's
+    completion: the wire time plus the wait for the slowest rank); value: the headline
+    whole-job rate.  Reports the per-rank render-only rates (min / max), the gather time
+    per chunk, and DESIGN.md section 8's predicted rate from the slowest rank's render-only
+    rate: world * R1 * 0.95 with R1 = that rate * (1 - 0.038)."""
+    import torch
+    world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
+    rank = dist.get_rank() if world > 1 else 0
+    fps = render_steps / render_elapsed if render_elapsed > 0 else 0.0
+    g = [float(x) for x in (gather_ms or [])]
+    t = torch.tensor([fps, sum(g) / len(g) if g else 0.0, max(g) if g else 0.0, float(len(g))],
+                     dtype=torch.float64, device=device)
+    rows = [t]
+    if world > 1:
+        rows = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(rows, t)
+    if rank != 0:
+        return None
+    per = [r.tolist() for r in rows]
+    fmin = min(r[0] for r in per)
+    r1 = fmin * (1.0 - GATHER_COST_WORLD1)
+    predicted = world * r1 * RANK0_RECEIVE_BUDGET
+    return {
+        "per_rank_render_fps": {"min": round(fmin, 3), "max": round(max(r[0] for r in per), 3),
+                                "per_rank": [round(r[0], 3) for r in per], "frames_per_rank": render_steps,
+                                "note": "frames in flight with no gathers, untimed for the headline, after it"},
+        "gather_ms_per_chunk": {"mean": round(sum(r[1] * r[3] for r in per) / max(1.0, sum(r[3] for r in per)), 4),
+                                "max": round(max(r[2] for r in per), 4),
+                                "per_rank_mean": [round(r[1], 4) for r in per],
+                                "chunks_per_rank": [int(r[3]) for r in per],
+                                "note": "side stream, from the chunk's frames done to its gather complete (wire "
+                                        "time + the wait for the slowest rank), headline region"},
+        "render_bound_fps": round(world * fmin, 3),
+        "value_over_render_bound": round(value / (world * fmin), 4) if fmin > 0 else None,
+        "predicted_fps": round(predicted, 1),
+        "predicted_formula": (f"world * R1 * {RANK0_RECEIVE_BUDGET} with R1 = min per-rank render fps * "
+                              f"(1 - {GATHER_COST_WORLD1}) (DESIGN.md section 8)"),
+    }
+
+
 # Floats after each image in a FrameShard buffer: word 0 is the frame's validity word
 # (gsr_render_path_status: 0 complete, else GSR_FRAME_* bits); the pad keeps the next
 # image 256-B aligned when the image is.
@@ -195,6 +248,10 @@ class FrameShard:
         self.overflowed = False
         self.gathers = 0
         self.repaired = 0
+        # per-chunk gather timing (time_gathers): (start, end) timing events on the side
+        # stream (RCCL), or host milliseconds (synchronous gloo gathers)
+        self.time_gathers = False
+        self.gather_marks = []
 
     def _times(self, i0: int, m: int):
         return [self.frame_time(i0 + j) for j in range(m)] if self.frame_time else None
@@ -228,6 +285,17 @@ class FrameShard:
             self.wait_pending(s)
         cid, i0, m = u
         self.sink(cid, i0, [t[:m] for t in self.recv[s]])
+
+    def gather_ms(self) -> list:
+        """Milliseconds of every timed gather since time_gathers was set (synchronizes)."""
+        out = []
+        for m in self.gather_marks:
+            if isinstance(m, tuple):
+                m[1].synchronize()
+                out.append(m[0].elapsed_time(m[1]))
+            else:
+                out.append(m)
+        return out
 
     def drain(self):
         for s in range(self.nsets):
@@ -264,16 +332,26 @@ class FrameShard:
                 for j in range(max(0, m - self.F), m):
                     self.gather_stream.wait_event(self.frame_events[s * self.per_set + j])
                 self._log_status(s, i0, m)
+                if self.time_gathers:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(self.gather_stream)
                 self.pending[s] = self.dist.gather(src, dst, dst=0, async_op=True)
                 self.pending[s].wait()                       # side stream: after the gather
+                if self.time_gathers:
+                    e1.record(self.gather_stream)
+                    self.gather_marks.append((e0, e1))
                 self.gathered_ev[s].record(self.gather_stream)
                 self.gathered_valid[s] = True
         else:
             self._log_status(s, i0, m)
+            import time
+            t0 = time.perf_counter()
             if self.gloo:
                 self.pending[s] = self.dist.gather(src.cpu(), dst, dst=0)
             else:
                 self.pending[s] = self.dist.gather(src, dst, dst=0, async_op=True)
+            if self.time_gathers and self.gloo:
+                self.gather_marks.append((time.perf_counter() - t0) * 1e3)
         if self.sink:
             self.undelivered[s] = (cid, i0, m)
             if not self.frame_events:

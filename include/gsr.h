@@ -384,8 +384,11 @@ enum {
                                         then one workgroup per bucket sorts it in LDS (buckets over 2,048
                                         items are sorted through global memory by their workgroup).  A
                                         context's first frame of a scene size runs the LSD passes and
-                                        takes the quantiles from them.  0 = LSD passes only; 2 = test
-                                        hook: 1 with a 64-item local capacity.  Same order, same image;
+                                        takes the quantiles from them, and so does the first frame of
+                                        another scene pointer, and the frame after one that sent more
+                                        than n/8 items through the global path (a camera cut).  0 = LSD
+                                        passes only; 2 = test hook: 1 with a 64-item local capacity
+                                        (no reseeding on overflow).  Same order, same image;
                                         gsr_depth_passes is 0 after a bucket-sorted frame */
     GSR_TUNE_DEPTH_BUCKETS_OVER = 29, /* read-only: items the bucket sort's global path has sorted (buckets
                                         over the local capacity), summed over the lanes; sticky, read
@@ -395,9 +398,13 @@ enum {
                                         items and pairs (the bucket is the row pass's chunk), so the row
                                         pass runs without its count kernel; 0 = the row pass counts.
                                         Same lists, same image */
-    GSR_TUNE_COL_CHUNK = 31          /* binning path: row items per column-pass chunk.  0 (default) =
+    GSR_TUNE_COL_CHUNK = 31,         /* binning path: row items per column-pass chunk.  0 (default) =
                                         1024 for scenes of at most 2,097,152 Gaussians, else 2048;
                                         1024 or 2048 forces it.  Same lists, same image */
+    GSR_TUNE_FAIL_FRAME = 32         /* test hook: v > 0 makes the next gsr_render_path* call fail its
+                                        frame v with GSR_E_ARG (once; 0 = off, the default).  The
+                                        frames queued before it are still joined to the caller's
+                                        stream */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Current value of a knob (what gsr_set_tuning last set, else the default). */
@@ -413,6 +420,11 @@ int gsr_rank_order_check(int64_t* lane_ops, int64_t* mismatches);
 /* Depth-sort digit passes the last sorted frame ran (1..4; trailing identity
  * passes are skipped on the device), or a negative error code. */
 int gsr_depth_passes(gsr_context* ctx);
+/* Bucket depth sort diagnostics (GSR_TUNE_DEPTH_BUCKETS) of the last sorted frame of the
+ * context (lane 0 of gsr_render_path): its bucket count B, or 0 when that frame was not
+ * bucket-sorted, and each bucket's item count into sizes[0 .. min(B, cap)) (bucket B - 1
+ * holds the items with key 0xFFFFFFFF: the culled ones).  Synchronizes the context. */
+int gsr_bucket_sizes(gsr_context* ctx, uint32_t* sizes, int cap);
 /* Schedule 3: with diagnostics on, the last frame's blend stores per wave
  * (launch order) {start of the 100 MHz s_memrealtime clock, duration (40 bits) |
  * placement << 40 (XCC id, HW_ID)}; read n values. */

@@ -109,9 +109,63 @@ def test_bucket_sort_moving_camera(gpu, orc, torch, tmp_path_factory):
     from gaussianrenderer_amd import multi
     _, soa = scene_soa(gpu, tmp_path_factory, 200_000, 4)
     W, H = 960, 540
+    n = soa.shape[1]
     cams = [multi.orbit_camera(0, W, H), multi.orbit_camera(1, W, H), multi.orbit_camera(3, W, H),
             cam_for(gpu, W, H, pos=(0.0, 0.0, 2.5))]
-    check_bucket_frame(gpu, orc, torch, gpu.Scene.from_soa(soa), soa, cams, W, H)
+    scene = gpu.Scene.from_soa(soa)
+    # every frame's order is exact; a frame after one that sent over n / 8 items through the
+    # global path reseeds the splitters (LSD passes), the others are bucket-sorted with the
+    # previous frame's quantiles
+    r = renderer(gpu)
+    bucketed = 0
+    for i, cam in enumerate(cams):
+        render_frames(gpu, torch, r, scene, [cam], W, H)
+        if i > 0:
+            bucketed += r.depth_passes() == 0
+        assert np.array_equal(r.read_depth_order(n), orc.expected_depth_order(orc.preprocess(soa, cam, W, H, 3.0)))
+    assert bucketed >= 2, "stale splitters were not exercised"
+    r.close()
+    check_bucket_frame(gpu, orc, torch, scene, soa, cams[:2], W, H)
+
+
+def test_bucket_splitters_reseed(gpu, orc, torch, tmp_path_factory):
+    """The splitters belong to a scene and a view: another scene of the same size class, or
+    a frame that sent more than n / 8 items through the global path (a camera cut), makes the
+    next frame take the LSD passes and reseed them (one workgroup would otherwise
+    sort most of the scene); the frame after is bucket-sorted again.  Every order exact."""
+    _, soa_a = scene_soa(gpu, tmp_path_factory, 100_000, 15)
+    _, soa_b = scene_soa(gpu, tmp_path_factory, 100_000, 16)
+    soa_b = soa_b.copy()
+    soa_b[2] *= 0.05                                   # a thin slab: B's depths fill few of A's buckets
+    W, H = 640, 480
+    n = soa_a.shape[1]
+    cam = cam_for(gpu, W, H)
+    a, b = gpu.Scene.from_soa(soa_a), gpu.Scene.from_soa(soa_b)
+    r = renderer(gpu)
+    seq = [(a, soa_a, None), (a, soa_a, 0), (b, soa_b, "lsd"), (b, soa_b, 0), (b, soa_b, 0)]
+    for scene, soa, want in seq:
+        render_frames(gpu, torch, r, scene, [cam], W, H)
+        if want == "lsd":
+            assert r.depth_passes() >= 1, "a new scene did not reseed the splitters"
+        elif want == 0:
+            assert r.depth_passes() == 0
+        assert np.array_equal(r.read_depth_order(n), orc.expected_depth_order(orc.preprocess(soa, cam, W, H, 3.0)))
+    assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER) == 0
+    # a camera cut on one scene: from far behind to close in front, then hold
+    far_cam = cam_for(gpu, W, H, pos=(0, 0, 40))
+    near_cam = cam_for(gpu, W, H, pos=(0, 0, 1.2), fov=90)
+    render_frames(gpu, torch, r, a, [far_cam, far_cam], W, H)
+    assert r.depth_passes() == 0
+    over0 = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER)
+    render_frames(gpu, torch, r, a, [near_cam], W, H)          # stale splitters: a spike
+    assert r.depth_passes() == 0
+    spike = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER) - over0
+    render_frames(gpu, torch, r, a, [near_cam], W, H)
+    assert (r.depth_passes() >= 1) == (spike > n // 8), spike
+    render_frames(gpu, torch, r, a, [near_cam], W, H)
+    assert r.depth_passes() == 0
+    assert np.array_equal(r.read_depth_order(n), orc.expected_depth_order(orc.preprocess(soa_a, near_cam, W, H, 3.0)))
+    r.close()
 
 
 def test_bucket_sort_global_path(gpu, orc, torch, tmp_path_factory):
@@ -294,6 +348,44 @@ def test_bucket_rows_fused_matches_row_count(gpu, orc, torch, tmp_path_factory):
         assert np.array_equal(ranges, base[2]), key
         assert np.array_equal(img.view(np.uint32), base[0].view(np.uint32)), key
     assert_image_parity(base[0], orc.render(soa, cams[-1], W, H, 3.0, threads=THREADS), exact=True)
+
+
+def test_bucket_rows_fused_saturated_keys(gpu, orc, torch, tmp_path_factory):
+    """Live Gaussians whose depth key saturates (depth >= ~4295: gsr_f2u_sat(-Z * 1e6) =
+    0xFFFFFFFF, render.cu:850) under a far clip of 1e4 share the last bucket with the culled
+    items.  The fused row count must bin them like the unfused row pass, the LSD passes and
+    the oracle (the fused row pass used to stop at the last bucket's start)."""
+    _, soa = scene_soa(gpu, tmp_path_factory, 200_000, 14)
+    soa = soa.copy()
+    n = soa.shape[1]
+    far = np.arange(n) % 20 == 7                      # 5 %: large Gaussians ~5,000 units away
+    rng = np.random.default_rng(14)
+    m = int(far.sum())
+    soa[0, far] = rng.uniform(-800, 800, m)
+    soa[1, far] = rng.uniform(-450, 450, m)
+    soa[2, far] = -rng.uniform(4996, 5400, m)
+    soa[4:7, far] = rng.uniform(12, 30, (3, m))
+    W, H = 1280, 720
+    cam = gpu.make_camera(position=(0, 0, 4), look_at=(0, 0, 0), fov_y=50, aspect=W / H, far=1e4)
+    spl = orc.preprocess(soa, cam, W, H, 3.0)
+    sat = int(((spl["status"] == 2) & (spl["depth_key"] == 0xFFFFFFFF)).sum())
+    assert sat > m // 2, f"only {sat} live Gaussians with a saturated key"
+    scene = gpu.Scene.from_soa(soa)
+    got = {}
+    for buckets, fused in ((1, 1), (1, 0), (0, 1)):
+        r = renderer(gpu, buckets)
+        r.set_tuning(gpu.TUNE_BUCKET_ROWS, fused)
+        img = render_frames(gpu, torch, r, scene, [cam] * 2, W, H)
+        assert (r.depth_passes() == 0) == (buckets == 1)
+        assert np.array_equal(r.read_depth_order(n), orc.expected_depth_order(spl))
+        got[(buckets, fused)] = (img, r.read_pairs(), r.read_tile_ranges())
+        r.close()
+    base = got[(0, 1)]
+    for key, (img, pairs, ranges) in got.items():
+        assert np.array_equal(pairs, base[1]), key
+        assert np.array_equal(ranges, base[2]), key
+        assert np.array_equal(img.view(np.uint32), base[0].view(np.uint32)), key
+    assert_image_parity(base[0], orc.render(soa, cam, W, H, 3.0, threads=THREADS), exact=True)
 
 
 def test_bucket_sort_limited_to_2m(gpu, torch, tmp_path_factory):

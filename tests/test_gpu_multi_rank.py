@@ -252,3 +252,11 @@ def test_bench_launches_ranks(gpu, tmp_path):
     res = lines[0]
     assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "frames2"
     assert res["value"] > 0 and res["steps"] == 6
+    # the line explains itself (per-rank render-only rates, gather time per
+    # chunk, DESIGN.md section 8's prediction); 6 frames in chunks of 3: two gathers per rank
+    sc = res["scale"]
+    fps = sc["per_rank_render_fps"]
+    assert len(fps["per_rank"]) == 2 and 0 < fps["min"] <= fps["max"]
+    assert all(c >= 2 for c in sc["gather_ms_per_chunk"]["chunks_per_rank"])
+    assert sc["gather_ms_per_chunk"]["mean"] > 0
+    assert sc["predicted_fps"] == pytest.approx(2 * fps["min"] * (1 - 0.038) * 0.95, rel=1e-3)

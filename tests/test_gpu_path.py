@@ -288,6 +288,47 @@ def test_path_status_word_released_after_error(gpu, orc, torch, c1):
     assert_image_parity(out.view(3, H, W).cpu().numpy(), orc.render(soa, cam, W, H, 3.0))
 
 
+def test_path_error_after_fork_joins_lanes(gpu, orc, torch, tmp_path_factory):
+    """a frame failing after the fork (GSR_TUNE_FAIL_FRAME fails frame 3
+    of 6 on three lanes, so frames 1 and 2 are still running on lanes 1 and 2) must still
+    join those lanes to the caller's stream: a copy queued there right after the error sees
+    frames 0-2 complete (outputs pre-filled with NaN), and the next gsr_render on the
+    context is correct."""
+    _, soa = scene_soa(gpu, tmp_path_factory, 300_000, 21)
+    W, H = 1280, 720
+    cams = orbit_cams(gpu, W, H, 6)
+    scene = gpu.Scene.from_soa(soa)
+    r = gpu.Renderer()
+    r.set_tuning(gpu.TUNE_DEPTH_SPLIT, 0)
+    r.set_frames_in_flight(3)
+    outs = [torch.empty(3 * W * H, device="cuda") for _ in cams]
+    s = torch.cuda.Stream()
+    # warm every lane (workspace high-water marks, bucket splitters) so the failing call
+    # queues real frames, not first-frame allocations
+    for _ in range(2):
+        r.render_path(scene, cams, W, H, [o.data_ptr() for o in outs], stream=s.cuda_stream)
+        assert r.sync() == 0
+    with torch.cuda.stream(s):
+        for o in outs:
+            o.fill_(float("nan"))
+    r.set_tuning(gpu.TUNE_FAIL_FRAME, 3)
+    with pytest.raises(gpu.GsrError):
+        r.render_path(scene, cams, W, H, [o.data_ptr() for o in outs], stream=s.cuda_stream)
+    assert r.get_tuning(gpu.TUNE_FAIL_FRAME) == 0
+    with torch.cuda.stream(s):
+        snap = torch.stack(outs[:3]).clone()      # queued on the caller's stream after the error
+    s.synchronize()
+    for i in range(3):
+        img = snap[i].view(3, H, W).cpu().numpy()
+        assert np.isfinite(img).all(), f"frame {i}'s lane was not joined: the copy saw its output unfinished"
+        assert_image_parity(img, orc.render(soa, cams[i], W, H, 3.0, threads=16))
+    torch.cuda.synchronize()
+    assert r.sync() == 0
+    r.render(scene, cams[4], W, H, outs[4].data_ptr(), stream=s.cuda_stream)
+    assert r.sync() == 0
+    assert_image_parity(outs[4].view(3, H, W).cpu().numpy(), orc.render(soa, cams[4], W, H, 3.0, threads=16))
+
+
 def test_path_bad_arguments(gpu, torch, c1):
     r = gpu.Renderer()
     with pytest.raises(gpu.GsrError):

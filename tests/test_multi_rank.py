@@ -73,3 +73,52 @@ def test_two_rank_orbit_gather(gsr, orc, tmp_path, world):
         assert np.array_equal(frames[r], want)
     for r in range(1, world):
         assert not np.array_equal(frames[0], frames[r])   # different orbit cameras
+
+
+def _scale_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from gaussianrenderer_amd import multi
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    steps = 200
+    render_el = 0.05 + 0.01 * rank                       # rank r renders 200 frames in 50 + 10 r ms
+    headline_el = multi.max_over_ranks(dist, 0.08 + 0.005 * rank, "cpu")   # with gathers: slower
+    gathers = [1.0 + rank, 2.0 + rank, 3.0 + rank]      # ms per chunk on this rank's side stream
+    rep = multi.scale_report(dist, render_el, steps, gathers, world * steps / headline_el, "cpu")
+    if rank == 0:
+        q.put((rep, world * steps / headline_el))
+    else:
+        assert rep is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_scale_report_fields(world):
+    """the N > 1 bench line's 'scale' object (multi.scale_report, a
+    collective) on gloo ranks: per-rank render-only rates (min / max over ranks), the gather
+    time per chunk, and DESIGN.md section 8's prediction, with value <= world * min rate."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scale_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    rep, value = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    fps = rep["per_rank_render_fps"]
+    want = [200 / (0.05 + 0.01 * r) for r in range(world)]
+    assert fps["per_rank"] == pytest.approx(want, rel=1e-6)
+    assert fps["min"] == pytest.approx(min(want)) and fps["max"] == pytest.approx(max(want))
+    g = rep["gather_ms_per_chunk"]
+    assert g["chunks_per_rank"] == [3] * world
+    assert g["per_rank_mean"] == pytest.approx([2.0 + r for r in range(world)])
+    assert g["mean"] == pytest.approx(2.0 + (world - 1) / 2) and g["max"] == pytest.approx(3.0 + world - 1)
+    assert rep["render_bound_fps"] == pytest.approx(world * min(want), rel=1e-6)
+    assert value <= rep["render_bound_fps"]
+    assert rep["value_over_render_bound"] == pytest.approx(value / (world * min(want)), rel=1e-3)
+    assert rep["predicted_fps"] == pytest.approx(world * min(want) * (1 - 0.038) * 0.95, rel=1e-4)
