@@ -530,6 +530,7 @@ TUNE_DEPTH_BUCKETS_OVER = 29
 TUNE_BUCKET_ROWS = 30
 TUNE_COL_CHUNK = 31
 TUNE_FAIL_FRAME = 32
+TUNE_DEPTH_BUCKETS_WORK = 33
 MAX_BUCKETS = 4096             # gsr_internal.h kMaxBuckets: the bucket sort's largest bucket count
 
 

@@ -51,6 +51,8 @@ struct Stats {
                                       // sticky until the host reads it)
     unsigned int bkt_over;            // bucket depth sort: items of buckets over the local capacity,
                                       // sorted through global memory (host copy, sticky diagnostics)
+    unsigned int bkt_over_work;       // ... times the 8-bit passes each needed (their keys' span): the
+                                      // cost of the global path (tied keys cost none; host copy, sticky)
 };
 
 // Depth split (GSR_TUNE_DEPTH_SPLIT): the frame's tiles are binned over the nearest
@@ -149,7 +151,8 @@ hipError_t launch_radix_pass(const uint64_t* in, uint64_t* out, const uint32_t* 
 // 0xFFFFFFFF); s_out: the next frame's (quantiles of this order).  hist: groups x buckets
 // u32 (groups <= kMaxBucketGroups), totals: 2 x buckets + 2 u32 (the totals, then the
 // buckets' first positions and n, then a word raised when a live item has key 0xFFFFFFFF).  cap (<= kMaxBucketCap): largest bucket sorted in LDS (larger
-// ones take the global path; over_host, host-mapped and nullable, counts their items).
+// ones take the global path; over_host, host-mapped and nullable, counts their items, and
+// over_host[1] their items times the passes they took).
 constexpr int kMaxBuckets = 4096;
 constexpr uint32_t kMaxBucketCap = 2048;
 constexpr int kMaxBucketGroups = 512;    // chunks (workgroups) of the scatter; hist: groups x buckets

@@ -2285,6 +2285,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
     kmin = s_mm[0];
     const uint32_t span = s_mm[1] - kmin;
     const int bits = span ? 32 - __clz((int)span) : 0;
+    if (over_host && t == 0 && bits) atomicAdd_system(over_host + 1, count * (uint32_t)((bits + 7) / 8));
     uint64_t* src = seg;
     uint64_t* dst = scratch + start;
     uint32_t* psrc = pseg;

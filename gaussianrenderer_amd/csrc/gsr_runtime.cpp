@@ -445,7 +445,7 @@ struct gsr_context {
     int bkt_par = 0;                 // the half the next bucket-sorted frame reads
     int bkt_B = 0;                   // buckets the splitters were made for (0: none yet)
     const void* bkt_scene = nullptr; // the scene they were made from (another scene reseeds them)
-    unsigned int bkt_over_seen = 0;  // hstats->bkt_over when the last frame was prepared
+    unsigned int bkt_work_seen = 0;  // hstats->bkt_over_work when the last frame was prepared
     bool bds_frame = false;          // this frame's preprocess items went to items[1] for the bucket sort
     bool last_bds = false;           // the last sorted frame was bucket-sorted (order in items[0], no pass plan)
     bool bkt_rows_fused = false;     // its local sorts wrote the row pass's counts (bucket = row chunk): the
@@ -968,15 +968,17 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     // bucket depth sort (splitters exist for this scene size): the items go to items[1], the
     // sort writes the order into items[0]; it keeps culled items apart itself, so it
     // replaces the live partition
-    // the splitters are this scene's and did not just fail: a frame that sent more than an
-    // eighth of the scene through the global path (a camera cut, a zoom) makes the next one
-    // reseed them from the LSD passes (a camera jump could put most of a 2M scene
-    // into one bucket, sorted by one workgroup, a frame of tens of ms).  bkt_over is
+    // the splitters are this scene's and did not just fail: a frame whose global path sorted
+    // more than n / 8 item-passes (a camera cut, a zoom: most of the scene in a few buckets
+    // over capacity, with wide key spans) makes the next one reseed them from the LSD passes
+    // (a camera jump could put most of a 2M scene into one bucket, sorted by one
+    // workgroup, a frame of tens of ms).  Buckets of tied keys cost the global path nothing
+    // (no passes) and do not count: reseeding could not split them.  bkt_over_work is
     // host-mapped and lags by the frames in flight; the test hook 2 (capacity 64) keeps them.
     {
-        const unsigned int over = c->hstats ? ((const volatile Stats*)c->hstats)->bkt_over : 0u;
-        const bool spike = c->bucket_sort == 1 && (int64_t)(over - c->bkt_over_seen) > n / 8;
-        c->bkt_over_seen = over;
+        const unsigned int work = c->hstats ? ((const volatile Stats*)c->hstats)->bkt_over_work : 0u;
+        const bool spike = c->bucket_sort == 1 && (int64_t)(work - c->bkt_work_seen) > n / 8;
+        c->bkt_work_seen = work;
         if (c->bkt_B && (spike || c->bkt_scene != scene)) c->bkt_B = 0;
     }
     c->bds_frame = bkt_applies(n) && !c->split_key && c->bucket_sort && c->bkt_B == bkt_count(n) && c->tile_binning &&
@@ -1955,9 +1957,15 @@ extern "C" int gsr_get_tuning(gsr_context* c, int knob, int* value) {
     case GSR_TUNE_BUCKET_ROWS: *value = c->fuse_rows; break;
     case GSR_TUNE_COL_CHUNK: *value = c->col_chunk; break;
     case GSR_TUNE_FAIL_FRAME: *value = c->fail_frame; break;
-    case GSR_TUNE_DEPTH_BUCKETS_OVER: {
-        int64_t v = c->hstats ? (int64_t)((const volatile Stats*)c->hstats)->bkt_over : 0;
-        for (auto* l : c->lanes) v += l->hstats ? (int64_t)((const volatile Stats*)l->hstats)->bkt_over : 0;
+    case GSR_TUNE_DEPTH_BUCKETS_OVER:
+    case GSR_TUNE_DEPTH_BUCKETS_WORK: {
+        auto get = [&](const gsr_context* x) -> int64_t {
+            if (!x->hstats) return 0;
+            const volatile Stats* h = (const volatile Stats*)x->hstats;
+            return knob == GSR_TUNE_DEPTH_BUCKETS_OVER ? (int64_t)h->bkt_over : (int64_t)h->bkt_over_work;
+        };
+        int64_t v = get(c);
+        for (auto* l : c->lanes) v += get(l);
         *value = (int)std::min<int64_t>(v, INT32_MAX);
         break;
     }
@@ -2076,6 +2084,7 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
     case GSR_TUNE_DEPTH_SPLIT_UNSAT:
     case GSR_TUNE_DEPTH_SPLIT_STATE:
     case GSR_TUNE_DEPTH_BUCKETS_OVER:
+    case GSR_TUNE_DEPTH_BUCKETS_WORK:
         return set_err(GSR_E_ARG, "gsr_set_tuning: knob %d is read-only", knob);
     case GSR_TUNE_TILE_SORT_GROUPS:
     case GSR_TUNE_DEPTH_SORT_GROUPS:

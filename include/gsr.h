@@ -385,8 +385,8 @@ enum {
                                         items are sorted through global memory by their workgroup).  A
                                         context's first frame of a scene size runs the LSD passes and
                                         takes the quantiles from them, and so does the first frame of
-                                        another scene pointer, and the frame after one that sent more
-                                        than n/8 items through the global path (a camera cut).  0 = LSD
+                                        another scene pointer, and the frame after one whose global path
+                                        ran more than n/8 item-passes (a camera cut; knob 33).  0 = LSD
                                         passes only; 2 = test hook: 1 with a 64-item local capacity
                                         (no reseeding on overflow).  Same order, same image;
                                         gsr_depth_passes is 0 after a bucket-sorted frame */
@@ -401,10 +401,14 @@ enum {
     GSR_TUNE_COL_CHUNK = 31,         /* binning path: row items per column-pass chunk.  0 (default) =
                                         1024 for scenes of at most 2,097,152 Gaussians, else 2048;
                                         1024 or 2048 forces it.  Same lists, same image */
-    GSR_TUNE_FAIL_FRAME = 32         /* test hook: v > 0 makes the next gsr_render_path* call fail its
+    GSR_TUNE_FAIL_FRAME = 32,        /* test hook: v > 0 makes the next gsr_render_path* call fail its
                                         frame v with GSR_E_ARG (once; 0 = off, the default).  The
                                         frames queued before it are still joined to the caller's
                                         stream */
+    GSR_TUNE_DEPTH_BUCKETS_WORK = 33 /* read-only: the global path's items times the 8-bit passes each
+                                        took (their bucket's key span; tied keys take none), summed
+                                        over the lanes; sticky, read after gsr_sync.  A frame adding
+                                        more than n/8 makes the next frame reseed the splitters */
 };
 int gsr_set_tuning(gsr_context* ctx, int knob, int value);
 /* Current value of a knob (what gsr_set_tuning last set, else the default). */

@@ -49,7 +49,7 @@ def renderer(gpu, buckets=1):
     return r
 
 
-def check_bucket_frame(gpu, orc, torch, scene, soa, cams, W, H, buckets=1, want_over=None):
+def check_bucket_frame(gpu, orc, torch, scene, soa, cams, W, H, buckets=1, want_over=None, want_work=None):
     """Frames over cams on a bucket-sort renderer and on an LSD-only one; the last frame
     must be bucket-sorted on the first and equal the oracle (order, image) and the LSD
     renderer (order, tile lists)."""
@@ -60,6 +60,8 @@ def check_bucket_frame(gpu, orc, torch, scene, soa, cams, W, H, buckets=1, want_
     order = r.read_depth_order(n)
     pairs = r.read_pairs()
     over = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER)
+    if want_work is not None:       # tied keys: the global path's buckets need (almost) no passes
+        assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_WORK) <= want_work
     ref = renderer(gpu, 0)
     img_lsd = render_frames(gpu, torch, ref, scene, cams[-1:], W, H)
     assert ref.depth_passes() >= 1
@@ -113,8 +115,8 @@ def test_bucket_sort_moving_camera(gpu, orc, torch, tmp_path_factory):
     cams = [multi.orbit_camera(0, W, H), multi.orbit_camera(1, W, H), multi.orbit_camera(3, W, H),
             cam_for(gpu, W, H, pos=(0.0, 0.0, 2.5))]
     scene = gpu.Scene.from_soa(soa)
-    # every frame's order is exact; a frame after one that sent over n / 8 items through the
-    # global path reseeds the splitters (LSD passes), the others are bucket-sorted with the
+    # every frame's order is exact; a frame after one whose global path ran over n / 8
+    # item-passes reseeds the splitters (LSD passes), the others are bucket-sorted with the
     # previous frame's quantiles
     r = renderer(gpu)
     bucketed = 0
@@ -130,7 +132,7 @@ def test_bucket_sort_moving_camera(gpu, orc, torch, tmp_path_factory):
 
 def test_bucket_splitters_reseed(gpu, orc, torch, tmp_path_factory):
     """The splitters belong to a scene and a view: another scene of the same size class, or
-    a frame that sent more than n / 8 items through the global path (a camera cut), makes the
+    a frame whose global path ran more than n / 8 item-passes (a camera cut), makes the
     next frame take the LSD passes and reseed them (one workgroup would otherwise
     sort most of the scene); the frame after is bucket-sorted again.  Every order exact."""
     _, soa_a = scene_soa(gpu, tmp_path_factory, 100_000, 15)
@@ -156,12 +158,13 @@ def test_bucket_splitters_reseed(gpu, orc, torch, tmp_path_factory):
     near_cam = cam_for(gpu, W, H, pos=(0, 0, 1.2), fov=90)
     render_frames(gpu, torch, r, a, [far_cam, far_cam], W, H)
     assert r.depth_passes() == 0
-    over0 = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER)
+    work0 = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_WORK)
     render_frames(gpu, torch, r, a, [near_cam], W, H)          # stale splitters: a spike
     assert r.depth_passes() == 0
-    spike = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER) - over0
+    spike = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_WORK) - work0
+    assert spike > n // 8, f"the cut sent only {spike} item-passes through the global path"
     render_frames(gpu, torch, r, a, [near_cam], W, H)
-    assert (r.depth_passes() >= 1) == (spike > n // 8), spike
+    assert r.depth_passes() >= 1, "the spike did not reseed the splitters"
     render_frames(gpu, torch, r, a, [near_cam], W, H)
     assert r.depth_passes() == 0
     assert np.array_equal(r.read_depth_order(n), orc.expected_depth_order(orc.preprocess(soa_a, near_cam, W, H, 3.0)))
@@ -192,7 +195,7 @@ def test_bucket_sort_tie_heavy(gpu, orc, torch, tmp_path_factory):
     W, H = 1920, 1080
     cams = [cam_for(gpu, W, H)] * 2
     order = check_bucket_frame(gpu, orc, torch, gpu.Scene.from_soa(soa), soa, cams, W, H,
-                               want_over=some_over)
+                               want_over=some_over, want_work=soa.shape[1] // 8)
     keys = (order >> np.uint64(32)).astype(np.uint32)
     assert np.unique(keys[keys != 0xFFFFFFFF]).size <= 7
 
