@@ -2161,8 +2161,8 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
     const uint32_t klo = bounded ? s_in[bkt - 1] : 0u, khi = bounded ? s_in[bkt] : 0u;
     if (bkt == 0 && t == 0) {
         s_next[B - 2] = 0xffffffffu;
-        if (live == 0)
-            for (uint32_t j = 0; j < (uint32_t)B - 2u; j++) s_next[j] = 0;   // any sorted splitters will do
+        if (live == 0)   // no live quantiles (a camera looking away): keep this frame's splitters
+            for (uint32_t j = 0; j < (uint32_t)B - 2u; j++) s_next[j] = s_in[j];
     }
     if (count == 0) {   // uniform; an empty bucket is an empty row-pass chunk
         if (rh.hist) {

@@ -311,17 +311,24 @@ def test_bucket_sort_knob(gpu):
 
 def test_bucket_sort_all_culled_then_visible(gpu, orc, torch, tmp_path_factory):
     """A frame with every Gaussian culled (the camera looks away: every item in the last
-    bucket, no live quantiles) between visible frames: each frame's order is exact."""
+    bucket, no live quantiles, so the frame keeps its splitters) between visible frames:
+    each frame's order is exact, and every frame is bucket-sorted unless the frame before
+    it ran more than n / 8 item-passes through the global path (then it reseeds)."""
     _, soa = scene_soa(gpu, tmp_path_factory, 20_000, 9)
     W, H = 320, 240
     n = soa.shape[1]
     scene = gpu.Scene.from_soa(soa)
     r = renderer(gpu)
     render_frames(gpu, torch, r, scene, [cam_for(gpu, W, H)], W, H)   # the LSD frame: first quantiles
-    for cam in (cam_for(gpu, W, H), cam_for(gpu, W, H, pos=(0, 0, 40), look=(0, 0, 80)), cam_for(gpu, W, H),
-                cam_for(gpu, W, H, pos=(0, 0, 12), fov=90)):
+    spike = False
+    for i, cam in enumerate((cam_for(gpu, W, H), cam_for(gpu, W, H, pos=(0, 0, 40), look=(0, 0, 80)),
+                             cam_for(gpu, W, H), cam_for(gpu, W, H, pos=(0, 0, 12), fov=90))):
+        w0 = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_WORK)
         img = render_frames(gpu, torch, r, scene, [cam], W, H)
-        assert r.depth_passes() == 0
+        assert (r.depth_passes() == 0) == (not spike), i
+        if i == 2:   # after the look-away: its kept splitters are the visible frame's
+            assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_WORK) == w0
+        spike = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_WORK) - w0 > n // 8
         want_spl = orc.preprocess(soa, cam, W, H, 3.0)
         assert np.array_equal(r.read_depth_order(n), orc.expected_depth_order(want_spl))
         assert_image_parity(img, orc.render(soa, cam, W, H, 3.0), exact=True)
