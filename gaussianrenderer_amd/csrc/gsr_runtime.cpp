@@ -514,7 +514,9 @@ int bkt_count(int64_t n) {
 // through five serial tiles (the histogram caps the workgroups at 512) and measured 244 us
 // against the LSD passes' 186 (profiles/r05_kt_c3_orbit.txt): the LSD passes stay there.
 constexpr int64_t kBucketSortMaxN = (int64_t)2048 * 1024;
-bool bkt_applies(int64_t n) { return n > 0 && n <= kBucketSortMaxN; }
+bool bkt_applies(const gsr_context* c, int64_t n) {
+    return n > 0 && (n <= kBucketSortMaxN || c->bucket_sort == 3);   // 3: any size (A/B)
+}
 
 // Row items per column-pass chunk (GSR_TUNE_COL_CHUNK 0): 1,024 up to the same 2M
 // Gaussians (config 2: column scatter 26.0 -> 21.6 us, chain -2 us), 2,048 above (config 3:
@@ -977,11 +979,11 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     // host-mapped and lags by the frames in flight; the test hook 2 (capacity 64) keeps them.
     {
         const unsigned int work = c->hstats ? ((const volatile Stats*)c->hstats)->bkt_over_work : 0u;
-        const bool spike = c->bucket_sort == 1 && (int64_t)(work - c->bkt_work_seen) > n / 8;
+        const bool spike = c->bucket_sort != 2 && (int64_t)(work - c->bkt_work_seen) > n / 8;
         c->bkt_work_seen = work;
         if (c->bkt_B && (spike || c->bkt_scene != scene)) c->bkt_B = 0;
     }
-    c->bds_frame = bkt_applies(n) && !c->split_key && c->bucket_sort && c->bkt_B == bkt_count(n) && c->tile_binning &&
+    c->bds_frame = bkt_applies(c, n) && !c->split_key && c->bucket_sort && c->bkt_B == bkt_count(n) && c->tile_binning &&
                    c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
     c->compact_frame = n > 0 && !c->split_key && !c->bds_frame &&
                        (c->depth_compact == 1 || (c->depth_compact == 2 && layout == GSR_LAYOUT_SCENE_BLOCK_4D)) &&
@@ -1129,7 +1131,7 @@ static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false
     }
     // the bucket sort's first splitters: quantiles of this whole sorted order (the next
     // frame of this scene size is bucket-sorted)
-    if (with_rects && !key && c->bucket_sort && bkt_applies(c->n) && c->bkt_B != bkt_count(c->n)) {
+    if (with_rects && !key && c->bucket_sort && bkt_applies(c, c->n) && c->bkt_B != bkt_count(c->n)) {
         const int B = bkt_count(c->n);
         HIP_TRY(gsr::launch_bkt_splitters(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n,
                                           part ? c->nlive : nullptr, B,
@@ -2065,7 +2067,7 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         c->rank_atomic = value;
         return GSR_OK;
     case GSR_TUNE_DEPTH_BUCKETS:
-        if (value < 0 || value > 2) return set_err(GSR_E_ARG, "gsr_set_tuning: depth buckets must be 0, 1 or 2");
+        if (value < 0 || value > 3) return set_err(GSR_E_ARG, "gsr_set_tuning: depth buckets must be 0..3");
         c->bucket_sort = value;
         return GSR_OK;
     case GSR_TUNE_COL_CHUNK:

@@ -388,7 +388,8 @@ enum {
                                         another scene pointer, and the frame after one whose global path
                                         ran more than n/8 item-passes (a camera cut; knob 33).  0 = LSD
                                         passes only; 2 = test hook: 1 with a 64-item local capacity
-                                        (no reseeding on overflow).  Same order, same image;
+                                        (no reseeding on overflow); 3 = 1 at any scene size (A/B).
+                                        Same order, same image;
                                         gsr_depth_passes is 0 after a bucket-sorted frame */
     GSR_TUNE_DEPTH_BUCKETS_OVER = 29, /* read-only: items the bucket sort's global path has sorted (buckets
                                         over the local capacity), summed over the lanes; sticky, read

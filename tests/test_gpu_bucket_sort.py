@@ -303,7 +303,7 @@ def test_bucket_sort_knob(gpu):
     r = gpu.Renderer()
     assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS) == 1
     with pytest.raises(gpu.GsrError):
-        r.set_tuning(gpu.TUNE_DEPTH_BUCKETS, 3)
+        r.set_tuning(gpu.TUNE_DEPTH_BUCKETS, 4)
     with pytest.raises(gpu.GsrError):
         r.set_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER, 0)
     assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER) == 0

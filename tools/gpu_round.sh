@@ -13,7 +13,8 @@
 #   rehkt      kernel + memory-copy trace of the world-1 RCCL rehearsal, with per-chunk gathers
 #              and without (rank env set directly: no launcher under the profiler)
 #   ktab       kernel trace of the one-frame-at-a-time bench per knob setting (TUNES,
-#              e.g. TUNES="19=0 19=1"; CONFIGS) -> gpurun_out/kt_ab_<tag>/summary.txt
+#              e.g. TUNES="19=0 19=1"; CONFIGS; KT_ARGS, e.g. "--orbit-step 0.25")
+#              -> gpurun_out/kt_ab_<tag>/summary.txt
 #   abtune     interleaved knob A/B in one process (tools/ab_path.py, AB_ARGS)
 #   ablibs     interleaved A/B of two library builds            (tools/ab_libs.sh)
 #
@@ -95,7 +96,7 @@ for step in ${STEPS:-suite smoke bench}; do
   ktab)
     for t in ${TUNES:-19=0 19=1}; do
       tg=$(echo "$t" | tr '=,' '__'); O=gpurun_out/kt_ab_$tg; mkdir -p $O
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 bench.py --config ${CONFIGS:-2} --steps 60 --warmup 5 --no-cpu-baseline --no-sh3-line --inflight 1 --warm-ms 200 --tune "$t" > $O/kt.log 2>&1
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 bench.py --config ${CONFIGS:-2} --steps 60 --warmup 5 --no-cpu-baseline --no-sh3-line --no-orbit-line --inflight 1 --warm-ms 200 --tune "$t" ${KT_ARGS:-} > $O/kt.log 2>&1
       rc=$?; echo "tune $t kt rc=$rc"; fatal $rc ktab; [ $rc = 0 ] || exit $rc
       python3 tools/summarize_prof.py $O > $O/summary.txt 2>&1; echo "== $t"; head -16 $O/summary.txt
     done ;;
