@@ -159,7 +159,8 @@ constexpr int kMaxBucketGroups = 512;    // chunks (workgroups) of the scatter; 
 hipError_t launch_bucket_sort(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int buckets,
                               int groups, const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
                               const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
-                              unsigned int* over_host, hipStream_t s, int row_tiles_y = 0);
+                              unsigned int* over_host, hipStream_t s, int row_tiles_y, uint4* rec);
+// rec: n 16-B records of scratch (the scatter's output, the local sorts' input).
 // row_tiles_y > 0: the local kernel also writes the row pass's count histograms into hist
 // (512 x buckets words: chunk g = bucket g, tile rows < row_tiles_y; the last bucket's chunk
 // is empty unless a live item's key saturated to 0xFFFFFFFF), and the row pass then runs

@@ -1807,20 +1807,23 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_count(const uint64_t* __res
     uint64_t b, e;
     chunk_range(n, groups, blockIdx.x, kBktTile, b, e);
     uint32_t key[kBktItems];
-    auto load = [&](uint64_t i0) {
+    auto load = [&](uint64_t i0, uint32_t (&kk)[kBktItems]) {
 #pragma unroll
         for (int k = 0; k < kBktItems; k++) {
             const uint64_t i = i0 + (uint64_t)k * kBktThreads + t;
-            key[k] = i < e ? (uint32_t)(in[i] >> 32) : 0xffffffffu;
+            kk[k] = i < e ? (uint32_t)(in[i] >> 32) : 0xffffffffu;
         }
     };
-    load(b);   // the first tile's keys travel together with the splitters: one memory round trip
+    load(b, key);   // the first tile's keys travel together with the splitters: one memory round trip
     bkt_load_splitters<B>(s_S, splitters);
     for (uint32_t j = t; j < (uint32_t)B; j += kBktThreads) s_h[j] = 0;
     __syncthreads();
     uint32_t dead = 0;   // culled items all share the last bucket: counted by ballots, not 64-way atomics
     for (uint64_t i0 = b; i0 < e; i0 += kBktTile) {
-        if (i0 != b) load(i0);
+        // the next tile's keys are in flight while this tile walks the tree (scenes above
+        // 1M items give a workgroup several tiles)
+        uint32_t nkey[kBktItems];
+        if (i0 + kBktTile < e) load(i0 + kBktTile, nkey);
         uint32_t bk[kBktItems];
         bkt_of_n<B>(s_S, key, bk);
 #pragma unroll
@@ -1829,6 +1832,10 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_count(const uint64_t* __res
             const bool d = key[k] == 0xffffffffu;
             dead += (uint32_t)__popcll(__ballot(d && i < e));
             if (!d) atomicAdd(&s_h[bk[k]], 1u);
+        }
+        if (i0 + kBktTile < e) {
+#pragma unroll
+            for (int k = 0; k < kBktItems; k++) key[k] = nkey[k];
         }
     }
     if (lane == 0 && dead) atomicAdd(&s_h[B - 1], dead);
@@ -1890,6 +1897,13 @@ __device__ __forceinline__ uint32_t half16(uint32_t v, uint32_t h) { return (v >
 // TH threads (512 from 512 buckets up: twice the waves of 256, half the items per wave, so
 // each wave's latency chain is half as long; the grid is only ~n / 2,048 workgroups:
 // 16.3-16.8 -> 15.6-15.8 us at config 2, profiles/r05_kt_bkt_scatter512.txt).
+// Live items go out as one 16-B record {index, key, rect, 0} into rec (one store request per
+// item: a 4,096-way scatter writes ~one item per bucket per tile, so every store of a wave hits
+// its own cache line and the scatter is bound by the L2's request rate, not by bytes: two
+// arrays, item and rect, were two requests per item); k_bkt_local reads a bucket's records
+// back contiguously.  The last bucket (key 0xFFFFFFFF, never sorted) goes straight to its
+// final place in out / pay_out.  The next tile's items and rects are loaded while this one
+// is ranked.
 template <int B, bool RA, int TH>
 __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__ in,
                                                              uint64_t* __restrict__ out, uint32_t n,
@@ -1898,7 +1912,8 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
                                                              const uint32_t* __restrict__ totals,
                                                              const uint32_t* __restrict__ rect,
                                                              uint32_t* __restrict__ pay_out,
-                                                             uint32_t* __restrict__ bstart) {
+                                                             uint32_t* __restrict__ bstart,
+                                                             uint4* __restrict__ rec) {
     GSR_GEOM_PRIO();
     constexpr int NW = TH / 64, kIt = kBktTile / TH;  // waves; items per thread
     constexpr uint32_t kW = B / 2;                      // packed counter words per wave
@@ -1916,17 +1931,17 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
     const uint32_t wbase = w * 64 * kIt;
     uint64_t it[kIt];
     uint32_t pv[kIt];
-    auto load = [&](uint64_t tb, uint32_t tn) {
+    auto load = [&](uint64_t tb, uint32_t tn, uint64_t (&ii)[kIt], uint32_t (&pp)[kIt]) {
 #pragma unroll
         for (int k = 0; k < kIt; k++) {
             const uint32_t el = wbase + k * 64 + lane;
-            it[k] = el < tn ? in[tb + el] : ~0ull;
-            pv[k] = el < tn ? rect[tb + el] : 0u;   // the input is the preprocess order: rect by position
+            ii[k] = el < tn ? in[tb + el] : ~0ull;
+            pp[k] = el < tn ? rect[tb + el] : 0u;   // the input is the preprocess order: rect by position
         }
     };
     // the first tile's items and rects, the splitters, the bucket totals and this chunk's
     // histogram row are all loaded in one memory round trip
-    load(b, (uint32_t)min((uint64_t)kBktTile, e - b));
+    load(b, (uint32_t)min((uint64_t)kBktTile, e - b), it, pv);
     bkt_load_splitters<B, TH>(s_S, splitters);
     {   // this chunk's first slot in every bucket: the bucket's start + the earlier chunks' items
         uint32_t loc[kPer], hrow[kPer], sum = 0;
@@ -1950,8 +1965,11 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
     if (b >= e) return;   // uniform per workgroup, after the scan's barriers
     for (uint64_t tb = b; tb < e; tb += kBktTile) {
         const uint32_t tn = (uint32_t)min((uint64_t)kBktTile, e - tb);
+        const bool more = tb + kBktTile < e;   // uniform
+        uint64_t nit[kIt];
+        uint32_t npv[kIt];
+        if (more) load(tb + kBktTile, (uint32_t)min((uint64_t)kBktTile, e - tb - kBktTile), nit, npv);
         for (uint32_t j = t; j < NW * kW; j += TH) (&s_wc[0][0])[j] = 0;
-        if (tb != b) load(tb, tn);
         __syncthreads();
         uint32_t dg[kIt], rk[kIt], keys[kIt];
 #pragma unroll
@@ -2023,8 +2041,19 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
             if (el < tn) {
                 const uint32_t d = dg[k];
                 const uint32_t dst = s_gbase[d] + half16(s_wc[w][d >> 1], d & 1u) + rk[k];
-                out[dst] = it[k];
-                pay_out[dst] = pv[k];
+                if (d == (uint32_t)B - 1u) {
+                    out[dst] = it[k];
+                    pay_out[dst] = pv[k];
+                } else {
+                    rec[dst] = make_uint4((uint32_t)it[k], (uint32_t)(it[k] >> 32), pv[k], 0u);
+                }
+            }
+        }
+        if (more) {
+#pragma unroll
+            for (int k = 0; k < kIt; k++) {
+                it[k] = nit[k];
+                pv[k] = npv[k];
             }
         }
         __syncthreads();
@@ -2110,7 +2139,8 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
                                                            uint32_t* __restrict__ bstart,
                                                            const uint32_t* __restrict__ s_in,
                                                            uint32_t* __restrict__ s_next, uint32_t cap,
-                                                           unsigned int* over_host, RowHist rh) {
+                                                           unsigned int* over_host, RowHist rh,
+                                                           const uint4* __restrict__ rec) {
     GSR_GEOM_PRIO();
     __shared__ uint64_t s_items[kBktTile];
     __shared__ uint32_t s_pay[kBktTile];
@@ -2173,6 +2203,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
     }
     uint64_t* const seg = items + start;
     uint32_t* const pseg = pay + start;
+    const uint4* const rseg = rec + start;   // the bucket's records (k_bkt_scatter), index order
     // ---- fast path: the bucket in registers, stable 8-bit passes through LDS.  IT items per
     // thread: 4 for buckets of up to 1,024 (the usual ~n / B: every wave holds a quarter of
     // the bucket), 8 up to the capacity (at 8, buckets under 1,024 left waves 2 and 3 idle
@@ -2185,8 +2216,9 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
 #pragma unroll
         for (int k = 0; k < IT; k++) {
             const uint32_t el = wbase + k * 64 + lane;
-            it[k] = el < count ? seg[el] : ~0ull;
-            pv[k] = el < count ? pseg[el] : 0u;
+            const uint4 r = el < count ? rseg[el] : make_uint4(~0u, ~0u, 0u, 0u);
+            it[k] = ((uint64_t)r.y << 32) | r.x;
+            pv[k] = r.z;
         }
         uint32_t kmin = klo, span = khi - klo - 1u;   // bounded: keys in [klo, khi)
         if (!bounded) {   // the open-ended first and last buckets: their own min and max
@@ -2267,6 +2299,13 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
     const uint32_t wbase = w * 64 * kBktItems;
     // ---- over capacity: stable 8-bit passes through global memory, one tile at a time ----
     if (over_host && t == 0) atomicAdd_system(over_host, count);
+    for (uint32_t i = t; i < count; i += kBktThreads) {   // the records into the item / rect arrays
+        const uint4 r = rseg[i];
+        seg[i] = ((uint64_t)r.y << 32) | r.x;
+        pseg[i] = r.z;
+    }
+    __threadfence();
+    __syncthreads();
     uint32_t kmin = 0xffffffffu, kmax = 0;
     for (uint32_t i = t; i < count; i += kBktThreads) {
         const uint32_t k = (uint32_t)(seg[i] >> 32);
@@ -3976,7 +4015,7 @@ template <int B>
 static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int groups,
                           const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
                           const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
-                          unsigned int* over_host, hipStream_t s, int row_tiles_y) {
+                          unsigned int* over_host, hipStream_t s, int row_tiles_y, uint4* rec) {
     // fused row-pass count: the row hist overwrites the bucket hist, which only the scatter reads
     // (grid B with it: the last bucket is the row pass's last chunk, k_bkt_local)
     const RowHist rh{row_tiles_y > 0 ? hist : nullptr, B, row_tiles_y};
@@ -3987,33 +4026,33 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
     constexpr int kScTh = B >= 512 ? 512 : kBktThreads;   // k_bkt_scatter's workgroup size
     if (rank_atomic) {
         hipLaunchKernelGGL((k_bkt_scatter<B, true, kScTh>), dim3(groups), dim3(kScTh), 0, s, in, items0, n, s_in,
-                           groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart);
+                           groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
         hipLaunchKernelGGL((k_bkt_local<B, true>), dim3(local_grid), dim3(kBktThreads), 0, s, items0, items1, pay0,
-                           pay1, bstart, s_in, s_out, cap, over_host, rh);
+                           pay1, bstart, s_in, s_out, cap, over_host, rh, static_cast<const uint4*>(rec));
     } else {
         hipLaunchKernelGGL((k_bkt_scatter<B, false, kScTh>), dim3(groups), dim3(kScTh), 0, s, in, items0, n, s_in,
-                           groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart);
+                           groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
         hipLaunchKernelGGL((k_bkt_local<B, false>), dim3(local_grid), dim3(kBktThreads), 0, s, items0, items1, pay0,
-                           pay1, bstart, s_in, s_out, cap, over_host, rh);
+                           pay1, bstart, s_in, s_out, cap, over_host, rh, static_cast<const uint4*>(rec));
     }
 }
 
 hipError_t launch_bucket_sort(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int buckets,
                               int groups, const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
                               const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
-                              unsigned int* over_host, hipStream_t s, int row_tiles_y) {
+                              unsigned int* over_host, hipStream_t s, int row_tiles_y, uint4* rec) {
     if (groups < 1 || groups > kBktMaxGroups || (int64_t)groups * buckets > 256 * (int64_t)kMaxSortGroups || cap < 1 ||
         cap > kBktCap ||
-        in == items0 || !rect || !pay0 || !pay1)   // in may be items1: the scratch is used after the scatter
+        in == items0 || !rect || !pay0 || !pay1 || !rec)   // in may be items1: the scratch is used after the scatter
         return hipErrorInvalidValue;
     if (n == 0 || row_tiles_y > 256 || (int64_t)512 * buckets > 256 * (int64_t)kMaxSortGroups)
         return n == 0 ? hipSuccess : hipErrorInvalidValue;
     switch (buckets) {
-    case 256: bucket_sort_b<256>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y); break;
-    case 512: bucket_sort_b<512>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y); break;
-    case 1024: bucket_sort_b<1024>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y); break;
-    case 2048: bucket_sort_b<2048>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y); break;
-    case 4096: bucket_sort_b<4096>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y); break;
+    case 256: bucket_sort_b<256>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y, rec); break;
+    case 512: bucket_sort_b<512>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y, rec); break;
+    case 1024: bucket_sort_b<1024>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y, rec); break;
+    case 2048: bucket_sort_b<2048>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y, rec); break;
+    case 4096: bucket_sort_b<4096>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y, rec); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -442,6 +442,8 @@ struct gsr_context {
                                      // 2 = test hook: as 1 with a local capacity of 64 items (most
                                      // buckets take the global path)
     uint32_t* bkt_split = nullptr;   // 2 x kMaxBuckets splitters (double-buffered: read one, write the other)
+    uint4* bkt_rec = nullptr;        // the scatter's 16-B records (n of them)
+    int64_t bkt_rec_cap = 0;
     int bkt_par = 0;                 // the half the next bucket-sorted frame reads
     int bkt_B = 0;                   // buckets the splitters were made for (0: none yet)
     const void* bkt_scene = nullptr; // the scene they were made from (another scene reseeds them)
@@ -877,7 +879,7 @@ extern "C" void gsr_destroy(gsr_context* c) {
                     (void*)c->ranges, (void*)c->soa_tmp, (void*)c->out_tmp, (void*)c->consumed, (void*)c->binmeta,
                     (void*)c->cbins, (void*)c->srect, (void*)c->spans, (void*)c->nlive, (void*)c->tbuf,
                     (void*)c->bflag, (void*)c->gate, (void*)c->kcut, (void*)c->dstats_far, (void*)c->kcut_frame,
-                    (void*)c->src_items, (void*)c->sat, (void*)c->nfar})
+                    (void*)c->src_items, (void*)c->sat, (void*)c->nfar, (void*)c->bkt_rec})
         if (p) (void)hipFree(p);
     if (c->hstats) (void)hipHostFree(c->hstats);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -1054,6 +1056,11 @@ static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false
     if (with_rects && !c->split_key && c->bds_frame && !c->have_sort && c->pre_out != c->items[0]) {
         const int B = c->bkt_B;
         const int G = std::min(groups_for(c->n, gsr::kMaxBucketCap), gsr::kMaxBucketGroups);
+        if (c->bkt_rec_cap < c->n) {
+            HIP_TRY(hipDeviceSynchronize());
+            if (int rc = realloc_dev(&c->bkt_rec, (size_t)c->n_cap)) return rc;
+            c->bkt_rec_cap = c->n_cap;
+        }
         // a plain frame (one binning over the whole order): the local sorts also count the
         // row pass's items and pairs per bucket, which becomes the row pass's chunk
         const bool fuse = plain && c->fuse_rows && (int64_t)512 * B <= 256 * (int64_t)gsr::kMaxSortGroups;
@@ -1063,7 +1070,7 @@ static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false
                                         c->totals, reinterpret_cast<const uint32_t*>(c->rect), pay_buf(c, 0),
                                         pay_buf(c, 1), rank_atomic_on(c), c->bucket_sort == 2 ? 64u : gsr::kMaxBucketCap,
                                         c->hstats_dev ? &c->hstats_dev->bkt_over : nullptr, c->stream,
-                                        fuse ? c->fr.tiles_y : 0));
+                                        fuse ? c->fr.tiles_y : 0, c->bkt_rec));
         c->bkt_rows_fused = fuse;
         c->bkt_par ^= 1;
         c->last_bds = true;
