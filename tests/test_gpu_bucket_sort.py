@@ -400,7 +400,7 @@ def test_bucket_rows_fused_saturated_keys(gpu, orc, torch, tmp_path_factory):
 
 def test_bucket_sort_large_two_row_chunks(gpu, orc, torch, tmp_path_factory):
     """Knob 28 = 3 (the bucket sort at any size) on 4.4M Gaussians: 4,096 buckets of ~1,070
-    items (n > 4,096 x kRowHalf), so the fused row count gives each bucket two row chunks (its first
+    items, above kRowHalf, so the fused row count gives each bucket two row chunks (its first
     1,024 sorted positions and the rest).  Moving camera (stale splitters), fused / unfused /
     LSD passes: same depth order as the oracle, same tile lists, same image."""
     from gaussianrenderer_amd import multi
@@ -417,7 +417,7 @@ def test_bucket_sort_large_two_row_chunks(gpu, orc, torch, tmp_path_factory):
         assert (r.depth_passes() == 0) == (buckets == 3)
         if buckets == 3:
             sizes = r.bucket_sizes()
-            assert sizes is not None and sizes.size == 4096 and n > 4096 * 1024   # two row chunks per bucket
+            assert sizes is not None and sizes.size == 4096 and sizes[:-1].mean() > 1024
         got[(buckets, fused)] = (img, r.read_pairs(), r.read_tile_ranges(), r.read_depth_order(n))
         r.close()
     spl = orc.preprocess(soa, cams[-1], W, H, 3.0)
