@@ -2091,24 +2091,11 @@ __device__ __forceinline__ void bkt_write_splitters(uint32_t start, uint32_t cou
 // of the bucket this workgroup sorted): per tile row the row items and the pairs of its
 // rects, as difference arrays in LDS (per wave), then a prefix over the rows.
 // hist[row][g] and hist[256 + row][g], rows < tiles_y.
-// Two chunks per bucket (cs != nullptr, scenes whose buckets average more than 1,024 items:
-// the row scatter ranks 1,024 sources at a time, so a 1,220-item bucket as one chunk ran a
-// second, nearly empty round): chunk 2b = the bucket's first kRowHalf sorted positions,
-// chunk 2b + 1 = the rest; the per-wave LDS histograms 0-1 count the first, 2-3 the second
-// (row_slot).  cs: the chunks' first positions (2B + 1 words, written here).
-constexpr uint32_t kRowHalf = 1024;
 struct RowHist {
     uint32_t* hist;      // nullptr: not fused (the row pass counts for itself)
-    int groups;          // the row pass's chunks: B (one per bucket), or 2B with cs
+    int groups;          // the row pass's chunks: the live buckets (B - 1)
     int tiles_y;
-    uint32_t* cs;        // two chunks per bucket: their first positions (nullptr: one chunk)
 };
-
-// The per-wave histogram a sorted position's rect counts into: waves' own (w) with one chunk
-// per bucket; with two, 0-1 for positions below kRowHalf and 2-3 above.
-__device__ __forceinline__ uint32_t row_slot(const RowHist& rh, uint32_t pos, uint32_t w) {
-    return rh.cs ? (pos >= kRowHalf ? 2u : 0u) + (w & 1u) : w;
-}
 
 __device__ __forceinline__ void row_hist_add(uint32_t (*h_items)[256], uint32_t (*h_pairs)[256], uint32_t w,
                                              uint32_t packed) {
@@ -2125,34 +2112,18 @@ __device__ __forceinline__ void row_hist_add(uint32_t (*h_items)[256], uint32_t 
     }
 }
 
-// Bucket g's row histograms (its chunk g, or chunks 2g and 2g + 1 with rh.cs).
 __device__ __forceinline__ void row_hist_write(const RowHist& rh, uint32_t g, uint32_t (*h_items)[256],
                                                uint32_t (*h_pairs)[256], uint32_t* s_scr) {
     const uint32_t t = threadIdx.x;
     __syncthreads();
-    const uint32_t G = (uint32_t)rh.groups;
+    const uint32_t di = h_items[0][t] + h_items[1][t] + h_items[2][t] + h_items[3][t];
+    const uint32_t dp = h_pairs[0][t] + h_pairs[1][t] + h_pairs[2][t] + h_pairs[3][t];
     uint32_t ti, tp;
-    if (!rh.cs) {
-        const uint32_t di = h_items[0][t] + h_items[1][t] + h_items[2][t] + h_items[3][t];
-        const uint32_t dp = h_pairs[0][t] + h_pairs[1][t] + h_pairs[2][t] + h_pairs[3][t];
-        const uint32_t ci = block_exclusive_scan<uint32_t>(di, s_scr, ti) + di;
-        const uint32_t cp = block_exclusive_scan<uint32_t>(dp, s_scr, tp) + dp;
-        if (t < (uint32_t)rh.tiles_y) {
-            rh.hist[t * G + g] = ci;
-            rh.hist[(256 + t) * G + g] = cp;
-        }
-        return;
-    }
-#pragma unroll
-    for (uint32_t h = 0; h < 2; h++) {
-        const uint32_t di = h_items[2 * h][t] + h_items[2 * h + 1][t];
-        const uint32_t dp = h_pairs[2 * h][t] + h_pairs[2 * h + 1][t];
-        const uint32_t ci = block_exclusive_scan<uint32_t>(di, s_scr, ti) + di;
-        const uint32_t cp = block_exclusive_scan<uint32_t>(dp, s_scr, tp) + dp;
-        if (t < (uint32_t)rh.tiles_y) {
-            rh.hist[t * G + 2 * g + h] = ci;
-            rh.hist[(256 + t) * G + 2 * g + h] = cp;
-        }
+    const uint32_t ci = block_exclusive_scan<uint32_t>(di, s_scr, ti) + di;
+    const uint32_t cp = block_exclusive_scan<uint32_t>(dp, s_scr, tp) + dp;
+    if (t < (uint32_t)rh.tiles_y) {
+        rh.hist[t * (uint32_t)rh.groups + g] = ci;
+        rh.hist[(256 + t) * (uint32_t)rh.groups + g] = cp;
     }
 }
 
@@ -2190,7 +2161,6 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
         // raised bstart[B + 1]; then its rects are counted (every live one binned, as the LSD
         // path and render.cu do), else the chunk is emptied (bstart[B] = its start: the
         // row pass reads nothing there).  Only this workgroup reads bstart[B].
-        // (two chunks per bucket: all of it is chunk 2B - 2, chunk 2B - 1 is empty)
         const uint32_t start = bstart[B - 1], end = bstart[B];
         const bool sat = bstart[B + 1] != 0u;
         row_zero();
@@ -2204,20 +2174,11 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
                     p[k] = j < end ? pay[j] : pack_rect(kDeadRect);
                 }
 #pragma unroll
-                for (int k = 0; k < 4; k++) row_hist_add(s_wc, s_hp, rh.cs ? (w & 1u) : w, p[k]);
+                for (int k = 0; k < 4; k++) row_hist_add(s_wc, s_hp, w, p[k]);
             }
         }
         row_hist_write(rh, (uint32_t)B - 1u, s_wc, s_hp, s_scr);
-        if (t == 0) {
-            const uint32_t stop = sat ? end : start;
-            if (rh.cs) {
-                rh.cs[2 * B - 2] = start;
-                rh.cs[2 * B - 1] = stop;
-                rh.cs[2 * B] = stop;
-            } else if (!sat) {
-                bstart[B] = start;
-            }
-        }
+        if (!sat && t == 0) bstart[B] = start;
         return;
     }
     // XCD-contiguous buckets: the fused row count's histogram lines (16 consecutive
@@ -2232,10 +2193,6 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
         s_next[B - 2] = 0xffffffffu;
         if (live == 0)   // no live quantiles (a camera looking away): keep this frame's splitters
             for (uint32_t j = 0; j < (uint32_t)B - 2u; j++) s_next[j] = s_in[j];
-    }
-    if (rh.cs && t == 0) {
-        rh.cs[2 * bkt] = start;
-        rh.cs[2 * bkt + 1] = start + min(count, kRowHalf);
     }
     if (count == 0) {   // uniform; an empty bucket is an empty row-pass chunk
         if (rh.hist) {
@@ -2322,10 +2279,8 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
             row_zero();
             __syncthreads();
 #pragma unroll
-            for (int k = 0; k < IT; k++) {
-                const uint32_t el = wbase + k * 64 + lane;
-                if (el < count) row_hist_add(s_wc, s_hp, row_slot(rh, el, w), pv[k]);
-            }
+            for (int k = 0; k < IT; k++)
+                if (wbase + k * 64 + lane < count) row_hist_add(s_wc, s_hp, w, pv[k]);
             row_hist_write(rh, bkt, s_wc, s_hp, s_scr);
         }
         __syncthreads();
@@ -2439,7 +2394,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
     if (rh.hist) {
         row_zero();
         __syncthreads();
-        for (uint32_t i = t; i < count; i += kBktThreads) row_hist_add(s_wc, s_hp, row_slot(rh, i, w), pseg[i]);
+        for (uint32_t i = t; i < count; i += kBktThreads) row_hist_add(s_wc, s_hp, w, pseg[i]);
         row_hist_write(rh, bkt, s_wc, s_hp, s_scr);
     }
     if (bkt < (uint32_t)B - 1u)
@@ -4062,10 +4017,8 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
                           const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
                           unsigned int* over_host, hipStream_t s, int row_tiles_y, uint4* rec) {
     // fused row-pass count: the row hist overwrites the bucket hist, which only the scatter reads
-    // (grid B with it: the last bucket is the row pass's last chunk, k_bkt_local; two chunks
-    // per bucket when they average over kRowHalf items, their first positions after bstart)
-    const bool two = row_tiles_y > 0 && (uint64_t)n > (uint64_t)B * kRowHalf;
-    const RowHist rh{row_tiles_y > 0 ? hist : nullptr, two ? 2 * B : B, row_tiles_y, two ? totals + 2 * B + 2 : nullptr};
+    // (grid B with it: the last bucket is the row pass's last chunk, k_bkt_local)
+    const RowHist rh{row_tiles_y > 0 ? hist : nullptr, B, row_tiles_y};
     const int local_grid = row_tiles_y > 0 ? B : B - 1;
     uint32_t* bstart = totals + B;   // B + 2 words after the totals
     hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist);
@@ -4092,7 +4045,7 @@ hipError_t launch_bucket_sort(const uint64_t* in, uint64_t* items0, uint64_t* it
         cap > kBktCap ||
         in == items0 || !rect || !pay0 || !pay1 || !rec)   // in may be items1: the scratch is used after the scatter
         return hipErrorInvalidValue;
-    if (n == 0 || row_tiles_y > 256 || (int64_t)512 * 2 * buckets > 512 * (int64_t)kMaxSortGroups)
+    if (n == 0 || row_tiles_y > 256 || (int64_t)512 * buckets > 256 * (int64_t)kMaxSortGroups)
         return n == 0 ? hipSuccess : hipErrorInvalidValue;
     switch (buckets) {
     case 256: bucket_sort_b<256>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y, rec); break;
@@ -4153,8 +4106,7 @@ hipError_t launch_bin_rows(const uint64_t* items0, const uint64_t* items1, const
                            uint32_t* gate, int gate_mode, const uint32_t* cut, const RowSplit* rs,
                            const uint32_t* cstart) {
     const int cut_mode = rs ? rs->cut_mode : 0;
-    // (hist: 512 x groups words; 512 x kMaxSortGroups with bucket chunks, 256 x it otherwise)
-    if (tiles_y < 1 || tiles_y > 256 || groups < 1 || groups > (cstart ? kMaxSortGroups : kMaxSortGroups / 2) ||
+    if (tiles_y < 1 || tiles_y > 256 || groups < 1 || groups > kMaxSortGroups / 2 ||
         (items != 4 && items != 8 && items != 16) || (gate_mode != 0 && !gate) || gate_mode < 0 || gate_mode > 2 ||
         (cut_mode != 0 && !cut) || cut_mode < 0 || cut_mode > 2)
         return hipErrorInvalidValue;

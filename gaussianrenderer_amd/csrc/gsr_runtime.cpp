@@ -583,11 +583,9 @@ int ensure_static(gsr_context* c) {
         if (int rc = rank_check_device(&rk)) return rc;
         c->rank_ok = rk.state == 1;
     }
-    // 512 x kMaxSortGroups: the fused row count's histograms at two chunks per bucket
-    if (int rc = realloc_dev(&c->hist, 512 * (size_t)gsr::kMaxSortGroups)) return rc;
-    // LSD digit totals / bucket totals + bucket starts + n + the saturated-key word + the
-    // two-chunks-per-bucket row chunk starts (2 x buckets + 1)
-    if (int rc = realloc_dev(&c->totals, 4 * (size_t)gsr::kMaxBuckets + 3)) return rc;
+    if (int rc = realloc_dev(&c->hist, 256 * (size_t)gsr::kMaxSortGroups)) return rc;
+    // LSD digit totals / bucket totals + bucket starts
+    if (int rc = realloc_dev(&c->totals, 2 * (size_t)gsr::kMaxBuckets + 2)) return rc;
     if (int rc = realloc_dev(&c->bkt_split, 2 * (size_t)gsr::kMaxBuckets)) return rc;
     if (int rc = realloc_dev(&c->wg, (size_t)gsr::kMaxSortGroups)) return rc;
     if (int rc = realloc_dev(&c->stats, 2)) return rc;
@@ -1065,7 +1063,7 @@ static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false
         }
         // a plain frame (one binning over the whole order): the local sorts also count the
         // row pass's items and pairs per bucket, which becomes the row pass's chunk
-        const bool fuse = plain && c->fuse_rows;
+        const bool fuse = plain && c->fuse_rows && (int64_t)512 * B <= 256 * (int64_t)gsr::kMaxSortGroups;
         uint32_t* s_in = c->bkt_split + (size_t)c->bkt_par * gsr::kMaxBuckets;
         uint32_t* s_out = c->bkt_split + (size_t)(c->bkt_par ^ 1) * gsr::kMaxBuckets;
         HIP_TRY(gsr::launch_bucket_sort(c->pre_out, c->items[0], c->items[1], n, B, G, s_in, s_out, c->hist,
@@ -1212,11 +1210,9 @@ static int bin_locked(gsr_context* c, uint32_t base, uint32_t count, int gate_mo
     // after a bucket-sorted plain frame the buckets are the row chunks and their counts exist
     const bool fused = c->bkt_rows_fused && gate_mode == 0 && base == 0 && !rs && !far && count == (uint32_t)c->n;
     c->bkt_rows_fused = false;
-    // (two row chunks per bucket above an average of 1,024 items: gsr_kernels.hip kRowHalf)
-    const bool two = fused && c->n > (int64_t)c->bkt_B * 1024;
-    const uint32_t* cstart = fused ? c->totals + (two ? 2 * c->bkt_B + 2 : c->bkt_B) : nullptr;
+    const uint32_t* cstart = fused ? c->totals + c->bkt_B : nullptr;
     HIP_TRY(gsr::launch_bin_rows(c->items[0], c->items[1], dst, count, pay_buf(c, 0),
-                                 pay_buf(c, 1), fused ? (two ? 2 : 1) * c->bkt_B : gb,
+                                 pay_buf(c, 1), fused ? c->bkt_B : gb,
                                  c->hist, row_items, row_pairs, cap, c->fr.tiles_y, c->pairs[0], c->bin_row_items,
                                  c->stream, c->spans_frame ? c->spans : nullptr, rank_atomic_on(c), base,
                                  gate_mode ? c->gate : nullptr, gate_mode, rs && rs->cut_mode ? c->nlive : nullptr,

@@ -398,39 +398,6 @@ def test_bucket_rows_fused_saturated_keys(gpu, orc, torch, tmp_path_factory):
     assert_image_parity(base[0], orc.render(soa, cam, W, H, 3.0, threads=THREADS), exact=True)
 
 
-def test_bucket_sort_large_two_row_chunks(gpu, orc, torch, tmp_path_factory):
-    """Knob 28 = 3 (the bucket sort at any size) on 4.4M Gaussians: 4,096 buckets of ~1,070
-    items, above kRowHalf, so the fused row count gives each bucket two row chunks (its first
-    1,024 sorted positions and the rest).  Moving camera (stale splitters), fused / unfused /
-    LSD passes: same depth order as the oracle, same tile lists, same image."""
-    from gaussianrenderer_amd import multi
-    _, soa = scene_soa(gpu, tmp_path_factory, 4_400_000, 17)
-    n = soa.shape[1]
-    W, H = 640, 360
-    scene = gpu.Scene.from_soa(soa)
-    cams = [multi.orbit_camera(0, W, H), gpu.orbit(multi.orbit_camera(0, W, H), 2.0, 0.0)]
-    got = {}
-    for buckets, fused in ((3, 1), (3, 0), (0, 1)):
-        r = renderer(gpu, buckets)
-        r.set_tuning(gpu.TUNE_BUCKET_ROWS, fused)
-        img = render_frames(gpu, torch, r, scene, cams, W, H)
-        assert (r.depth_passes() == 0) == (buckets == 3)
-        if buckets == 3:
-            sizes = r.bucket_sizes()
-            assert sizes is not None and sizes.size == 4096 and sizes[:-1].mean() > 1024
-        got[(buckets, fused)] = (img, r.read_pairs(), r.read_tile_ranges(), r.read_depth_order(n))
-        r.close()
-    spl = orc.preprocess(soa, cams[-1], W, H, 3.0)
-    base = got[(0, 1)]
-    assert np.array_equal(base[3], orc.expected_depth_order(spl))
-    for key, (img, pairs, ranges, order) in got.items():
-        assert np.array_equal(order, base[3]), key
-        assert np.array_equal(pairs, base[1]), key
-        assert np.array_equal(ranges, base[2]), key
-        assert np.array_equal(img.view(np.uint32), base[0].view(np.uint32)), key
-    assert_image_parity(base[0], orc.render(soa, cams[-1], W, H, 3.0, threads=THREADS), exact=True)
-
-
 def test_bucket_sort_limited_to_2m(gpu, torch, tmp_path_factory):
     """Above 2,097,152 Gaussians (config 3's 5M) the LSD passes stay: the bucket sort's
     scatter measured slower there (profiles/r05_kt_c3_orbit.txt)."""
