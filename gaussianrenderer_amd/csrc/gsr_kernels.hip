@@ -2288,8 +2288,18 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
             bkt_write_splitters<B>(start, count, live, s_next,
                                    [&](uint32_t q) { return (uint32_t)(s_items[q] >> 32); });
     };
+    // (5 and 6 items per thread for the 1,025-1,536-item buckets of scenes above 4M items:
+    // at 8 the items of a 1,220-item bucket sat on waves 0-1 and 2-3 idled)
     if (count <= min(cap, (uint32_t)kBktThreads * 4u)) {
         fast(std::integral_constant<int, 4>{});
+        return;
+    }
+    if (count <= min(cap, (uint32_t)kBktThreads * 5u)) {
+        fast(std::integral_constant<int, 5>{});
+        return;
+    }
+    if (count <= min(cap, (uint32_t)kBktThreads * 6u)) {
+        fast(std::integral_constant<int, 6>{});
         return;
     }
     if (count <= cap) {
