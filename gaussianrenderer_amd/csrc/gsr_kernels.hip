@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include <type_traits>
 
@@ -4034,6 +4035,24 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
     hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist);
     hipLaunchKernelGGL(k_bkt_scan<B>, dim3(B / 64), dim3(1024), 0, s, hist, groups, totals);
     constexpr int kScTh = B >= 512 ? 512 : kBktThreads;   // k_bkt_scatter's workgroup size
+    // A/B: GSR_BKT_SCATTER_256=1 runs the 4,096-bucket scatter in 256-thread workgroups (64 KB of
+    // LDS instead of 96: two workgroups per CU)
+    static const bool sc256 = [] { const char* e = std::getenv("GSR_BKT_SCATTER_256"); return e && e[0] == '1'; }();
+    if (B == 4096 && sc256) {
+        if (rank_atomic)
+            hipLaunchKernelGGL((k_bkt_scatter<B, true, kBktThreads>), dim3(groups), dim3(kBktThreads), 0, s, in, items0,
+                               n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
+        else
+            hipLaunchKernelGGL((k_bkt_scatter<B, false, kBktThreads>), dim3(groups), dim3(kBktThreads), 0, s, in, items0,
+                               n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
+        if (rank_atomic)
+            hipLaunchKernelGGL((k_bkt_local<B, true>), dim3(local_grid), dim3(kBktThreads), 0, s, items0, items1, pay0,
+                               pay1, bstart, s_in, s_out, cap, over_host, rh, static_cast<const uint4*>(rec));
+        else
+            hipLaunchKernelGGL((k_bkt_local<B, false>), dim3(local_grid), dim3(kBktThreads), 0, s, items0, items1, pay0,
+                               pay1, bstart, s_in, s_out, cap, over_host, rh, static_cast<const uint4*>(rec));
+        return;
+    }
     if (rank_atomic) {
         hipLaunchKernelGGL((k_bkt_scatter<B, true, kScTh>), dim3(groups), dim3(kScTh), 0, s, in, items0, n, s_in,
                            groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
