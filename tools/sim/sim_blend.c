@@ -160,3 +160,62 @@ void sim(const float* rec /* n x 11 */, const int* lists, const int* offs, int n
     out[3] = loaded;
     out[4] = batches;
 }
+
+/* Two pixels per lane (VERDICT r05 #3 "also price"): one wave per 8-wide x (8 * P)-tall
+ * block, lane l holding pixels (l & 7, (l >> 3) + 8 p) for p < P.  The ideal per-block cull
+ * (cullmode 1): a splat survives a batch iff some unsaturated in-box pixel of the block
+ * reaches alpha >= 1e-3.  Batches of B entries of the tile list, pairs as the kernel.
+ * blocks: bxy (top-left corners) with offs into lists.  out as sim(). */
+void sim_tall(const float* rec, const int* lists, const int* offs, int nblocks, const int* bxy, int P, int B,
+              double* out) {
+    double it = 0, taken = 0, active = 0, loaded = 0, batches = 0;
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : it, taken, active, loaded, batches)
+    for (int blk = 0; blk < nblocks; blk++) {
+        const int bx = bxy[2 * blk], by = bxy[2 * blk + 1];
+        const int np = 64 * P;
+        float T[256];
+        for (int l = 0; l < np; l++) T[l] = 1.0f;
+        const int beg = offs[2 * blk], end = offs[2 * blk + 1];
+        int alive = 1;
+        for (int base = beg; base < end && alive; base += B) {
+            const int cnt = end - base < B ? end - base : B;
+            loaded += cnt;
+            batches += 1;
+            int surv[256], ns = 0;
+            for (int k = 0; k < cnt; k++) {
+                Sp s;
+                const float* r = rec + 11 * (size_t)lists[base + k];
+                s.cx = r[0]; s.cy = r[1]; s.a = r[2]; s.b = r[3]; s.c = r[4]; s.e = r[5]; s.op = r[6];
+                s.x0 = (int)r[7]; s.y0 = (int)r[8]; s.x1 = (int)r[9]; s.y1 = (int)r[10];
+                int ok = 0;
+                for (int l = 0; l < np && !ok; l++) {
+                    const int px = bx + (l & 7), py = by + (l >> 3);
+                    if (px < s.x0 || px > s.x1 || py < s.y0 || py > s.y1 || T[l] < 1e-3f) continue;
+                    if (alpha_at(&s, px, py) >= 1e-3f) ok = 1;
+                }
+                if (ok) surv[ns++] = lists[base + k];
+            }
+            for (int j = 0; j < ns && alive; j += 2) {
+                it += ns - j >= 2 ? 2 : 1;
+                for (int h = 0; h < 2 && j + h < ns; h++) {
+                    const float* r = rec + 11 * (size_t)surv[j + h];
+                    Sp s;
+                    s.cx = r[0]; s.cy = r[1]; s.a = r[2]; s.b = r[3]; s.c = r[4]; s.e = r[5]; s.op = r[6];
+                    s.x0 = (int)r[7]; s.y0 = (int)r[8]; s.x1 = (int)r[9]; s.y1 = (int)r[10];
+                    for (int l = 0; l < np; l++) {
+                        const int px = bx + (l & 7), py = by + (l >> 3);
+                        if (px < s.x0 || px > s.x1 || py < s.y0 || py > s.y1 || T[l] < 1e-3f) continue;
+                        active += 1;
+                        const float a = alpha_at(&s, px, py);
+                        if (a < 1e-3f) continue;
+                        taken += 1;
+                        T[l] *= 1.0f - a;
+                    }
+                }
+                alive = 0;
+                for (int l = 0; l < np; l++) alive |= !(T[l] < 1e-3f);
+            }
+        }
+    }
+    out[0] = it; out[1] = taken; out[2] = active; out[3] = loaded; out[4] = batches;
+}
