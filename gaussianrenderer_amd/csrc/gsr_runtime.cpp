@@ -1204,7 +1204,13 @@ static int bin_locked(gsr_context* c, uint32_t base, uint32_t count, int gate_mo
     // key mode, phase A: about 2 x the split point's items (the count is on the device)
     const int64_t est = rs && rs->cut_mode == 1 ? std::min<int64_t>(count, std::max<int64_t>(2 * (int64_t)rs->na, 65536))
                                                 : (int64_t)count;
-    const int gb = std::min(groups_for(est, 1024), gsr::kMaxSortGroups / 2);
+    // A/B: GSR_ROW_CHUNK = sources per row-pass chunk (default 1,024; the chunk is rounded up
+    // to a multiple of 1,024 and the chunks capped at 4,096)
+    static const int64_t row_chunk = [] {
+        const char* e = std::getenv("GSR_ROW_CHUNK");
+        return e ? std::max<int64_t>(1024, std::atoll(e)) : (int64_t)1024;
+    }();
+    const int gb = std::min(groups_for(est, row_chunk), gsr::kMaxSortGroups / 2);
     // (a bucket-sorted frame has no pass plan: its order is in items[0], its rects in pay_buf 0)
     uint32_t* dst = c->depth_skip && !(c->last_bds && !far) ? (far ? c->dstats_far : c->dstats) : nullptr;
     // after a bucket-sorted plain frame the buckets are the row chunks and their counts exist
