@@ -442,8 +442,7 @@ struct gsr_context {
                                      // 2 = test hook: as 1 with a local capacity of 64 items (most
                                      // buckets take the global path)
     uint32_t* bkt_split = nullptr;   // 2 x kMaxBuckets splitters (double-buffered: read one, write the other)
-    uint4* bkt_rec = nullptr;        // the scatter's 16-B records (n of them)
-    int64_t bkt_rec_cap = 0;
+    uint4* bkt_rec = nullptr;        // the scatter's 16-B records (n_cap of them, with the items)
     int bkt_par = 0;                 // the half the next bucket-sorted frame reads
     int bkt_B = 0;                   // buckets the splitters were made for (0: none yet)
     const void* bkt_scene = nullptr; // the scene they were made from (another scene reseeds them)
@@ -617,6 +616,9 @@ int ensure_n(gsr_context* c, int64_t n) {
     if (int rc = realloc_dev(&c->rect, (size_t)cap)) return rc;
     if (int rc = realloc_dev(&c->srect, (size_t)cap)) return rc;
     if (int rc = realloc_dev(&c->spans, (size_t)cap)) return rc;
+    // the bucket sort's 16-B records (allocated with the items, so gsr_reserve covers them
+    // and a captured frame never allocates)
+    if (int rc = realloc_dev(&c->bkt_rec, (size_t)cap)) return rc;
     c->n_cap = cap;
     if (c->p_cap < 4 * cap) {
         const int64_t pc = std::min<int64_t>(std::max<int64_t>(4 * cap, 1 << 20), 0xffffffffLL);
@@ -1056,11 +1058,6 @@ static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false
     if (with_rects && !c->split_key && c->bds_frame && !c->have_sort && c->pre_out != c->items[0]) {
         const int B = c->bkt_B;
         const int G = std::min(groups_for(c->n, gsr::kMaxBucketCap), gsr::kMaxBucketGroups);
-        if (c->bkt_rec_cap < c->n) {
-            HIP_TRY(hipDeviceSynchronize());
-            if (int rc = realloc_dev(&c->bkt_rec, (size_t)c->n_cap)) return rc;
-            c->bkt_rec_cap = c->n_cap;
-        }
         // a plain frame (one binning over the whole order): the local sorts also count the
         // row pass's items and pairs per bucket, which becomes the row pass's chunk
         const bool fuse = plain && c->fuse_rows && (int64_t)512 * B <= 256 * (int64_t)gsr::kMaxSortGroups;
