@@ -58,19 +58,21 @@ for step in ${STEPS:-suite smoke bench}; do
       line gpurun_out/bench_${TAG}_c$c.log config$c
     done ;;
   kt)
-    OUT=gpurun_out/prof_$TAG SKIP_PMC=1 bash tools/profile.sh
+    # one frame at a time, headline frames only (the orbit / SH-3 objects' frames would mix
+    # other views into the per-kernel means), like the bench's avg_launch_ms
+    OUT=gpurun_out/prof_$TAG BENCH_ARGS=${BENCH_ARGS:---inflight 1 --no-orbit-line --no-sh3-line} SKIP_PMC=1 bash tools/profile.sh
     rc=$?; fatal $rc kt; [ $rc = 0 ] || exit $rc
     python3 tools/summarize_prof.py gpurun_out/prof_$TAG > gpurun_out/prof_$TAG/summary.txt 2>&1; head -30 gpurun_out/prof_$TAG/summary.txt
     slim gpurun_out/prof_$TAG ;;
   pmc)
     # PMC passes of the one-frame-at-a-time bench (BENCH_ARGS default --inflight 1), the
     # per-kernel means written as gpurun_out/pmc_$TAG.json (bench.py reads profiles/pmc_latest.json)
-    OUT=gpurun_out/prof_$TAG BENCH_ARGS=${BENCH_ARGS:---inflight 1} SKIP_KT=1 \
+    OUT=gpurun_out/prof_$TAG BENCH_ARGS=${BENCH_ARGS:---inflight 1 --no-orbit-line --no-sh3-line} SKIP_KT=1 \
       PMC_GROUPS=${PMC_GROUPS:-"FETCH_SIZE;WRITE_SIZE;SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_INSTS_SALU"} \
       bash tools/profile.sh
     rc=$?; fatal $rc pmc; [ $rc = 0 ] || exit $rc
     python3 tools/summarize_prof.py gpurun_out/prof_$TAG --json gpurun_out/pmc_$TAG.json ${PMC_CONFIG:-2} \
-      "rocprofv3 --pmc, separate passes, bench.py --steps 50 ${BENCH_ARGS:---inflight 1}, $TAG"
+      "rocprofv3 --pmc, separate passes, bench.py --steps 50 ${BENCH_ARGS:---inflight 1 --no-orbit-line --no-sh3-line}, $TAG"
     python3 tools/pmc_agg.py gpurun_out/prof_$TAG k_ > gpurun_out/prof_$TAG/pmc_means.txt 2>&1
     # with a kernel trace of the same TAG already there: the table with the PMC columns
     [ -f gpurun_out/prof_$TAG/kt/kt_kernel_stats.csv ] && \
