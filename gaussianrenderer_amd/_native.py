@@ -187,7 +187,12 @@ def lib() -> ctypes.CDLL:
         raise ImportError(f"{LIB_PATH} is missing: run `make` (or __graft_entry__.build()) first")
     L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     for name, res, args in SIGNATURES:
-        fn = getattr(L, name)
+        try:
+            fn = getattr(L, name)
+        except AttributeError:
+            if os.environ.get("GSR_LIBRARY"):   # an older build in an A/B run: its API subset
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     _lib = L
