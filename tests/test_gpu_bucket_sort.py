@@ -130,6 +130,37 @@ def test_bucket_sort_moving_camera(gpu, orc, torch, tmp_path_factory):
     check_bucket_frame(gpu, orc, torch, scene, soa, cams[:2], W, H)
 
 
+def test_bucket_sort_config2_orbit_bounded(gpu, orc, torch, tmp_path_factory):
+    """config 2 (1M, 1920x1080) on a moving camera, 0.25 deg per frame (the
+    bench's orbit object): every frame is bucket-sorted with the previous frame's quantiles,
+    the buckets stay balanced (largest live bucket <= 1.5 x the mean; gsr_bucket_sizes), no
+    item takes the global path, and the last frame's order and image equal the oracle's."""
+    path, soa = scene_soa(gpu, tmp_path_factory, 1_000_000, 2)
+    n = soa.shape[1]
+    W, H = 1920, 1080
+    scene = gpu.Scene.from_ply(path)
+    cams = []
+    for i in range(12):
+        c = gpu.make_camera(position=(0, 0, 4), fov_y=50, aspect=W / H)
+        cams.append(gpu.orbit(c, 0.25 * i, 0.0))
+    r = renderer(gpu)
+    render_frames(gpu, torch, r, scene, cams[:1], W, H)           # LSD: the first quantiles
+    over0 = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER)
+    for cam in cams[1:]:
+        img = render_frames(gpu, torch, r, scene, [cam], W, H)
+        assert r.depth_passes() == 0
+        sizes = r.bucket_sizes()
+        assert sizes is not None and sizes.size == 1024 and int(sizes.sum()) == n
+        live = sizes[:-1].astype(np.float64)
+        assert live.max() <= 1.5 * live.mean(), f"imbalance {live.max() / live.mean():.3f}"
+    assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER) == over0, "an orbit frame took the global path"
+    spl = orc.preprocess(soa, cams[-1], W, H, 3.0)
+    assert int(sizes[-1]) == int((spl["status"] != 2).sum())      # the last bucket: the culled items
+    assert np.array_equal(r.read_depth_order(n), orc.expected_depth_order(spl))
+    assert_image_parity(img, orc.render(soa, cams[-1], W, H, 3.0, threads=THREADS), exact=True)
+    r.close()
+
+
 def test_bucket_splitters_reseed(gpu, orc, torch, tmp_path_factory):
     """The splitters belong to a scene and a view: another scene of the same size class, or
     a frame whose global path ran more than n / 8 item-passes (a camera cut), makes the
