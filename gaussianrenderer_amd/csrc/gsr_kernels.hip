@@ -1737,9 +1737,10 @@ __device__ __forceinline__ void row_range(uint32_t& base, uint32_t& n, const uin
 //                  capacity is sorted by the same workgroup through global memory
 //                  (stable 8-bit passes ping-ponging with the scratch buffer), so any
 //                  splitters give the exact order; they only set the speed
-// Splitters are the previous frame's quantiles: k_bkt_local writes the key at every
-// (j + 1) / (B - 1) of the live order for the next frame (double-buffered), so the
-// buckets hold about n / B items each while the camera moves smoothly.  A context's
+// Splitters are the previous frame's quantiles: k_bkt_local writes the key at each
+// bkt_split_pos of the live order for the next frame (double-buffered; the open first and
+// last live buckets a quarter share, the rest even), so the buckets hold about n / B
+// items each while the camera moves smoothly.  A context's
 // first frame runs the LSD passes and k_bkt_splitters takes the quantiles from them.
 // Stability: the scatter keeps index order inside a bucket, the local passes are stable
 // and buckets are key ranges in order, so ties stay in index order — the same order as
@@ -2073,19 +2074,35 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
 // Next frame's splitters from this bucket's part of the sorted live order: splitter j is
 // the key at live position floor((j + 1) * live / (B - 1)), j < B - 2.  key_at(q) reads
 // the sorted key at bucket-local position q.
+// Where splitter j (j < B - 2) is taken in a sorted live order of `live` items: the open
+// first and last live buckets get a quarter of an interior bucket's share, so a moving
+// camera's drift past the previous frame's nearest and farthest keys (which lands in
+// them) has room under the local capacity (config 2 on a 0.25-deg orbit, the first frames
+// after the LSD quantiles: the last bucket held 2,058 items, over the 2,048 capacity, at
+// an even split).  pos(j) = floor(N(j) live / D), N(j) = (B - 3) + j (4B - 6),
+// D = 4 (B - 3)(B - 1): pos(0) = live / (4 (B - 1)), pos(B - 3) = live (1 - 1 / (4 (B - 1))).
+template <int B>
+__device__ __forceinline__ uint32_t bkt_split_pos(uint32_t j, uint32_t live) {
+    constexpr uint64_t D = 4ull * (uint64_t)(B - 3) * (uint64_t)(B - 1);
+    return (uint32_t)(((uint64_t)(B - 3) + (uint64_t)j * (uint64_t)(4 * B - 6)) * live / D);
+}
+// The smallest j with bkt_split_pos(j, live) >= s (live > 0).
+template <int B>
+__device__ __forceinline__ uint64_t bkt_split_first(uint64_t s, uint32_t live) {
+    constexpr uint64_t D = 4ull * (uint64_t)(B - 3) * (uint64_t)(B - 1);
+    const uint64_t c = (s * D + live - 1) / live;   // pos(j) >= s  <=>  N(j) >= c
+    return c <= (uint64_t)(B - 3) ? 0ull : (c - (uint64_t)(B - 3) + (uint64_t)(4 * B - 7)) / (uint64_t)(4 * B - 6);
+}
+
 template <int B, typename KeyAt>
 __device__ __forceinline__ void bkt_write_splitters(uint32_t start, uint32_t count, uint32_t live,
                                                     uint32_t* __restrict__ s_out, KeyAt key_at) {
     if (live == 0 || count == 0) return;
-    const uint64_t m = (uint64_t)B - 1u;
-    // positions of j in [j0, j1) fall in [start, start + count)
-    const uint64_t j0 = ((uint64_t)start * m + live - 1) / live;            // smallest j + 1 with pos >= start
-    const uint64_t j1 = ((uint64_t)(start + count) * m + live - 1) / live;  // ... with pos >= start + count
-    for (uint64_t jp = j0 + threadIdx.x; jp < j1; jp += kBktThreads) {
-        if (jp == 0 || jp > (uint64_t)B - 2u) continue;   // j = jp - 1 in [0, B - 2)
-        const uint32_t pos = (uint32_t)(jp * live / m);
-        s_out[jp - 1] = key_at(pos - start);
-    }
+    // splitters j in [j0, j1) are taken at positions in [start, start + count)
+    const uint64_t j0 = bkt_split_first<B>(start, live);
+    const uint64_t j1 = min(bkt_split_first<B>((uint64_t)start + count, live), (uint64_t)B - 2u);
+    for (uint64_t j = j0 + threadIdx.x; j < j1; j += kBktThreads)
+        s_out[j] = key_at(bkt_split_pos<B>((uint32_t)j, live) - start);
 }
 
 // Row-pass histograms of one chunk of the depth order (k_bin_rows_count's, for the chunk
@@ -2466,12 +2483,11 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_splitters(const uint64_t* _
     // — must still give sorted splitters: the bucket search assumes them)
     constexpr int kPer = B / kBktThreads;
     __shared__ uint32_t s_wmax[4];
-    const uint64_t m = (uint64_t)B - 1u;
     uint32_t v[kPer], run = 0;
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
         const uint32_t j = t * kPer + k;
-        v[k] = live && j < (uint32_t)B - 2u ? (uint32_t)(sorted[(uint32_t)((uint64_t)(j + 1) * live / m)] >> 32) : 0u;
+        v[k] = live && j < (uint32_t)B - 2u ? (uint32_t)(sorted[bkt_split_pos<B>(j, live)] >> 32) : 0u;
         v[k] = min(v[k], 0xfffffffeu);
         run = max(run, v[k]);
         v[k] = run;
