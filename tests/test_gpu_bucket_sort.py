@@ -133,7 +133,8 @@ def test_bucket_sort_moving_camera(gpu, orc, torch, tmp_path_factory):
 def test_bucket_sort_config2_orbit_bounded(gpu, orc, torch, tmp_path_factory):
     """config 2 (1M, 1920x1080) on a moving camera, 0.25 deg per frame (the
     bench's orbit object): every frame is bucket-sorted with the previous frame's quantiles,
-    the buckets stay balanced (largest live bucket <= 1.5 x the mean; gsr_bucket_sizes), no
+    the buckets stay under the local capacity (largest live bucket <= 2,048 items and <= 2 x
+    the mean; gsr_bucket_sizes; the open edge buckets take a quarter share for the drift), no
     item takes the global path, and the last frame's order and image equal the oracle's."""
     path, soa = scene_soa(gpu, tmp_path_factory, 1_000_000, 2)
     n = soa.shape[1]
@@ -152,7 +153,8 @@ def test_bucket_sort_config2_orbit_bounded(gpu, orc, torch, tmp_path_factory):
         sizes = r.bucket_sizes()
         assert sizes is not None and sizes.size == 1024 and int(sizes.sum()) == n
         live = sizes[:-1].astype(np.float64)
-        assert live.max() <= 1.5 * live.mean(), f"imbalance {live.max() / live.mean():.3f}"
+        # under the 2,048-item local capacity, the edge buckets' drift included
+        assert live.max() <= 2048 and live.max() <= 2.0 * live.mean(), f"imbalance {live.max() / live.mean():.3f}"
     assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER) == over0, "an orbit frame took the global path"
     spl = orc.preprocess(soa, cams[-1], W, H, 3.0)
     assert int(sizes[-1]) == int((spl["status"] != 2).sum())      # the last bucket: the culled items
