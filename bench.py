@@ -640,8 +640,8 @@ def main():
     seq_overflow = r.sync()
 
     # pipelined timed region (the reported value): the same K frames through
-    # gsr_render_path with F frames in flight; blend events on lane 0's launches
-    # measure the kernel while it shares the GPU with the other lanes
+    # gsr_render_path with F frames in flight (no timing events in it: lane 0's blend
+    # launches in flight are sampled in an untimed region after it)
     # Every rank checks its frames for GSR_E_OVERFLOW (an incomplete frame: pair buffer
     # grown, or a depth sort short of passes) and all ranks agree (shard.finish, a
     # collective); a region with one is timed again, once, on the grown buffers.
@@ -652,30 +652,38 @@ def main():
         # per-step gathers carry each frame's validity word: the timed region includes
         # re-rendering and re-gathering exactly the chunks some rank got incomplete
         shard.overflowed, shard.gathers, shard.repaired = False, 0, 0
-        r.set_timing(1, TIMING_STRIDE)
         clean = []
         elapsed = timed(lambda: clean.append(shard.run_checked(args.steps, dev_kind)))
-        blend_times_pipe, timed_frames_pipe = r.stage_times()
-        r.set_timing(0)
         reruns = shard.repaired
         if not clean[0]:
             sys.exit("bench.py: frames still incomplete after repairs")
     elif F > 1:
         for attempt in range(2):
             shard.overflowed, shard.gathers = False, 0
-            r.set_timing(1, TIMING_STRIDE)
             elapsed = timed(lambda: shard.run(args.steps))
-            blend_times_pipe, timed_frames_pipe = r.stage_times()
-            r.set_timing(0)
             if not shard.finish(dev_kind):
                 break
             reruns += 1
     else:
-        elapsed, blend_times_pipe, timed_frames_pipe = seq_elapsed, blend_times, timed_frames
+        elapsed = seq_elapsed
     overflow = r.sync() or seq_overflow
     split_after = (r.get_tuning(26), r.get_tuning(24))   # depth split state and point after the timed frames
     bucket_over = r.get_tuning(29)   # items the bucket sort's global path sorted so far (all lanes, sticky)
     telemetry_after = gpu_telemetry(pci) if rank == 0 else None
+    if F > 1:
+        # lane 0's blend launches while F frames are in flight: K more frames through the
+        # same loop, untimed, with an event pair around every lane-0 blend (a collective at
+        # N > 1: every rank runs it)
+        shard.time_gathers = False
+        r.set_timing(1, 1)
+        shard.run(args.steps)
+        shard.drain()
+        torch.cuda.synchronize()
+        blend_times_pipe, timed_frames_pipe = r.stage_times()
+        r.set_timing(0)
+        shard.finish(dev_kind)
+    else:
+        blend_times_pipe, timed_frames_pipe = blend_times, timed_frames
 
     max_elapsed = multi.max_over_ranks(dist, elapsed, "cpu" if gloo else "cuda")
     max_seq = multi.max_over_ranks(dist, seq_elapsed, "cpu" if gloo else "cuda")
@@ -757,7 +765,8 @@ def main():
                      "algorithmic_bytes_design": algorithmic_blend_bytes(ntiles, consumed, W, H, record=64),
                      "bytes_per_pair": {"survey": 52, "design": 68},
                      "measured_on": "sequential timed segment (K frames one at a time: the kernel does not share "
-                                    "the GPU); avg_launch_ms_inflight = lane 0's launches in the pipelined region",
+                                    "the GPU); avg_launch_ms_inflight = lane 0's launches with F frames in flight "
+                                    "(K more frames after the timed regions, an event pair on each)",
                      "avg_launch_ms_inflight": round(blend_times_pipe["blend"] / max(1, timed_frames_pipe), 4)},
         "frames_in_flight": F,
         "sequential": {"value": round(world * args.steps / max_seq, 3), "unit": "frames/sec",
