@@ -1851,11 +1851,11 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_count(const uint64_t* __res
 // and the bucket's total.  64 buckets per workgroup (one per lane), 16 waves splitting the
 // chunks: every load is a coalesced 256-B row segment.  groups <= kBktMaxGroups.
 constexpr int kBktMaxGroups = kMaxBucketGroups;
-template <int B>
+template <int B, int MAXG = kBktMaxGroups>
 __global__ __launch_bounds__(1024) void k_bkt_scan(uint32_t* __restrict__ hist, int groups,
                                                    uint32_t* __restrict__ totals) {
     GSR_GEOM_PRIO();
-    constexpr int kPerMax = kBktMaxGroups / 16;
+    constexpr int kPerMax = MAXG / 16;
     __shared__ uint32_t s_part[16][64];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint32_t b = blockIdx.x * 64u + lane;
@@ -1906,7 +1906,11 @@ __device__ __forceinline__ uint32_t half16(uint32_t v, uint32_t h) { return (v >
 // back contiguously.  The last bucket (key 0xFFFFFFFF, never sorted) goes straight to its
 // final place in out / pay_out.  The next tile's items and rects are loaded while this one
 // is ranked.
-template <int B, bool RA, int TH>
+// STAGE: the tile is laid out in LDS by bucket first (tile-local position = the bucket's
+// offset in the tile + the item's stable rank in it), then written out by position, so the
+// lanes of a store that hold items of one bucket write consecutive records (a run per bucket
+// and tile: ~4 items at 512 buckets) instead of one store request each.
+template <int B, bool RA, int TH, bool STAGE = false>
 __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__ in,
                                                              uint64_t* __restrict__ out, uint32_t n,
                                                              const uint32_t* __restrict__ splitters, int groups,
@@ -1925,6 +1929,9 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
     __shared__ uint32_t s_S[B], s_gbase[B];
     __shared__ uint32_t s_wc[NW][kW];
     __shared__ uint32_t s_scr[NW];
+    // STAGE: per-word tile counts, per-bucket tile offsets, the tile in bucket order
+    __shared__ uint32_t s_tc[STAGE ? kW : 1], s_tp[STAGE ? B : 1];
+    __shared__ uint4 s_stage[STAGE ? kBktTile : 1];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const int chunk = xcd_chunk((int)blockIdx.x, groups);   // each XCD takes a contiguous run of chunks
@@ -2034,20 +2041,62 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
                     run += c[v];
                 }
                 tc[q] = run;
+                if (STAGE) s_tc[j] = run;
             }
         }
         __syncthreads();
+        if (STAGE) {
+            // the buckets' offsets in the tile: exclusive scan of their tile counts (thread t
+            // owns buckets t * kPer .. + kPer - 1)
+            uint32_t c[kPer], sum = 0;
 #pragma unroll
-        for (int k = 0; k < kIt; k++) {
-            const uint32_t el = wbase + k * 64 + lane;
-            if (el < tn) {
-                const uint32_t d = dg[k];
-                const uint32_t dst = s_gbase[d] + half16(s_wc[w][d >> 1], d & 1u) + rk[k];
+            for (int k = 0; k < kPer; k++) {
+                const uint32_t d = t * kPer + k;
+                c[k] = half16(s_tc[d >> 1], d & 1u);
+                sum += c[k];
+            }
+            uint32_t tot;
+            uint32_t run = block_exclusive_scan<uint32_t, NW>(sum, s_scr, tot);
+#pragma unroll
+            for (int k = 0; k < kPer; k++) {
+                s_tp[t * kPer + k] = run;
+                run += c[k];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kIt; k++) {
+                const uint32_t el = wbase + k * 64 + lane;
+                if (el < tn) {
+                    const uint32_t d = dg[k];
+                    const uint32_t p = s_tp[d] + half16(s_wc[w][d >> 1], d & 1u) + rk[k];
+                    s_stage[p] = make_uint4((uint32_t)it[k], (uint32_t)(it[k] >> 32), pv[k], d);
+                }
+            }
+            __syncthreads();
+            for (uint32_t q = t; q < tn; q += TH) {
+                const uint4 r = s_stage[q];
+                const uint32_t d = r.w;
+                const uint32_t dst = s_gbase[d] + (q - s_tp[d]);
                 if (d == (uint32_t)B - 1u) {
-                    out[dst] = it[k];
-                    pay_out[dst] = pv[k];
+                    out[dst] = ((uint64_t)r.y << 32) | r.x;
+                    pay_out[dst] = r.z;
                 } else {
-                    rec[dst] = make_uint4((uint32_t)it[k], (uint32_t)(it[k] >> 32), pv[k], 0u);
+                    rec[dst] = make_uint4(r.x, r.y, r.z, 0u);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kIt; k++) {
+                const uint32_t el = wbase + k * 64 + lane;
+                if (el < tn) {
+                    const uint32_t d = dg[k];
+                    const uint32_t dst = s_gbase[d] + half16(s_wc[w][d >> 1], d & 1u) + rk[k];
+                    if (d == (uint32_t)B - 1u) {
+                        out[dst] = it[k];
+                        pay_out[dst] = pv[k];
+                    } else {
+                        rec[dst] = make_uint4((uint32_t)it[k], (uint32_t)(it[k] >> 32), pv[k], 0u);
+                    }
                 }
             }
         }
@@ -2094,14 +2143,14 @@ __device__ __forceinline__ uint64_t bkt_split_first(uint64_t s, uint32_t live) {
     return c <= (uint64_t)(B - 3) ? 0ull : (c - (uint64_t)(B - 3) + (uint64_t)(4 * B - 7)) / (uint64_t)(4 * B - 6);
 }
 
-template <int B, typename KeyAt>
+template <int B, int TH = kBktThreads, typename KeyAt>
 __device__ __forceinline__ void bkt_write_splitters(uint32_t start, uint32_t count, uint32_t live,
                                                     uint32_t* __restrict__ s_out, KeyAt key_at) {
     if (live == 0 || count == 0) return;
     // splitters j in [j0, j1) are taken at positions in [start, start + count)
     const uint64_t j0 = bkt_split_first<B>(start, live);
     const uint64_t j1 = min(bkt_split_first<B>((uint64_t)start + count, live), (uint64_t)B - 2u);
-    for (uint64_t j = j0 + threadIdx.x; j < j1; j += kBktThreads)
+    for (uint64_t j = j0 + threadIdx.x; j < j1; j += TH)
         s_out[j] = key_at(bkt_split_pos<B>((uint32_t)j, live) - start);
 }
 
@@ -2158,7 +2207,8 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
                                                            const uint32_t* __restrict__ s_in,
                                                            uint32_t* __restrict__ s_next, uint32_t cap,
                                                            unsigned int* over_host, RowHist rh,
-                                                           const uint4* __restrict__ rec) {
+                                                           const uint4* __restrict__ rec,
+                                                           const uint32_t* __restrict__ only = nullptr) {
     GSR_GEOM_PRIO();
     __shared__ uint64_t s_items[kBktTile];
     __shared__ uint32_t s_pay[kBktTile];
@@ -2203,6 +2253,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
     // buckets of a row) merge in one L2 (12.4 -> 11.95 us at config 2,
     // profiles/r05_kt_xcd_hist.txt)
     const uint32_t bkt = (uint32_t)xcd_chunk((int)blockIdx.x, B - 1);
+    if (only && only[bkt] == 0u) return;   // big buckets: only those k_bbk_local left to this kernel
     const uint32_t start = bstart[bkt], count = bstart[bkt + 1] - start, live = bstart[B - 1];
     // keys of bucket b lie in [s_in[b - 1], s_in[b]) for 0 < b < B - 2
     const bool bounded = bkt > 0 && bkt < (uint32_t)B - 2u;
@@ -2427,6 +2478,198 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
     }
     if (bkt < (uint32_t)B - 1u)
         bkt_write_splitters<B>(start, count, live, s_next, [&](uint32_t q) { return (uint32_t)(seg[q] >> 32); });
+}
+
+// ---- big buckets (scenes above 2M Gaussians: 512 buckets of ~n / 512 items) ----
+//
+// One 1,024-thread workgroup sorts a bucket of up to kBbCap items in LDS: 16 per thread in
+// registers (blocked per wave, so a wave's items are consecutive positions), stable 8-bit
+// LSD passes over key - lo whose exchange carries one u32 per item: the slot (original
+// position, 14 bits) and the key digits the later passes still need (so pass p exchanges
+// (key - lo) >> 8 (p + 1): keys spanning up to 26 bits above lo).  After the last pass each
+// position knows its slot, and the slot's index, rect and key are pulled through the same
+// LDS buffer (written by slot, read by position), then written out coalesced.  Buckets over
+// the capacity or wider than 26 bits are flagged in `left` and sorted by k_bkt_local's paths
+// in a second launch.
+constexpr int kBbThreads = 1024;
+constexpr int kBbItems = 16;
+constexpr uint32_t kBbCap = kBbThreads * kBbItems;     // 16,384
+constexpr int kBbSlot = 14;                             // slot bits of the exchange word
+static_assert(kBbCap == 1u << kBbSlot, "slot field");
+
+template <int B, bool RA>
+__global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__ items, uint32_t* __restrict__ pay,
+                                                          const uint32_t* __restrict__ bstart,
+                                                          const uint32_t* __restrict__ s_in,
+                                                          uint32_t* __restrict__ s_next, uint32_t cap,
+                                                          const uint4* __restrict__ rec, uint32_t* __restrict__ left) {
+    GSR_GEOM_PRIO();
+    constexpr int NW = kBbThreads / 64;
+    __shared__ uint32_t s_buf[kBbCap];                  // the exchange, then the pulls
+    __shared__ uint32_t s_idx[kBbCap];                  // the indices by slot (registers are the limit)
+    __shared__ uint32_t s_wc[NW][256];                  // per-wave digit counts, then their wave prefixes
+    __shared__ uint32_t s_db[256];                      // the digits' first positions
+    __shared__ uint32_t s_scr[NW], s_mm[2];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t bkt = blockIdx.x;
+    const uint32_t start = bstart[bkt], count = bstart[bkt + 1] - start, live = bstart[B - 1];
+    const bool bounded = bkt > 0 && bkt < (uint32_t)B - 2u;
+    const uint32_t klo = bounded ? s_in[bkt - 1] : 0u, khi = bounded ? s_in[bkt] : 0u;
+    if (bkt == 0 && t == 0) {
+        s_next[B - 2] = 0xffffffffu;
+        if (live == 0)   // no live quantiles (a camera looking away): keep this frame's splitters
+            for (uint32_t j = 0; j < (uint32_t)B - 2u; j++) s_next[j] = s_in[j];
+    }
+    if (count == 0) {
+        if (t == 0) left[bkt] = 0u;
+        return;
+    }
+    if (count > min(cap, kBbCap)) {
+        if (t == 0) left[bkt] = 1u;
+        return;
+    }
+    const uint32_t wbase = w * 64 * kBbItems;
+    uint32_t key[kBbItems], rct[kBbItems];
+#pragma unroll
+    for (int k = 0; k < kBbItems; k++) {
+        const uint32_t el = wbase + k * 64 + lane;
+        const uint4 r = el < count ? rec[start + el] : make_uint4(0u, 0xffffffffu, 0u, 0u);
+        s_idx[el] = r.x;
+        key[k] = r.y;
+        rct[k] = r.z;
+    }
+    uint32_t kmin = klo, span = khi - klo - 1u;
+    if (!bounded) {   // the open first and last buckets: their own min and max
+        uint32_t mn = 0xffffffffu, mx = 0;
+#pragma unroll
+        for (int k = 0; k < kBbItems; k++)
+            if (wbase + k * 64 + lane < count) {
+                mn = min(mn, key[k]);
+                mx = max(mx, key[k]);
+            }
+        mn = ~wave_max_u32(~mn);
+        mx = wave_max_u32(mx);
+        if (t < 2) s_mm[t] = t ? 0u : 0xffffffffu;
+        __syncthreads();
+        if (lane == 0) {
+            atomicMin(&s_mm[0], mn);
+            atomicMax(&s_mm[1], mx);
+        }
+        __syncthreads();
+        kmin = s_mm[0];
+        span = s_mm[1] - kmin;
+    }
+    const int bits = span ? 32 - __clz((int)span) : 0;
+    if (bits > 26) {   // uniform: the exchange word cannot carry the digits (k_bkt_local sorts it)
+        if (t == 0) left[bkt] = 1u;
+        return;
+    }
+    if (t == 0) left[bkt] = 0u;
+    // x[k]: the position's exchange word (slot | remaining digits << kBbSlot); before the first
+    // pass position = slot and the digits come from the key
+    uint32_t x[kBbItems];
+#pragma unroll
+    for (int k = 0; k < kBbItems; k++) x[k] = wbase + k * 64 + lane;
+    for (int shift = 0; shift < bits; shift += 8) {   // uniform
+        // (digits recomputed where used: registers are the occupancy limit here)
+        auto digit = [&](int k) { return shift == 0 ? ((key[k] - kmin) & 0xffu) : ((x[k] >> kBbSlot) & 0xffu); };
+        // stable ranks: per-wave counts in (item, lane) order, then wave prefixes and digit bases
+        for (uint32_t j = t; j < (uint32_t)NW * 256u; j += kBbThreads) (&s_wc[0][0])[j] = 0;
+        __syncthreads();
+        uint32_t rk[kBbItems];
+#pragma unroll
+        for (int k = 0; k < kBbItems; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            const bool valid = el < count;
+            const uint32_t dk = digit(k);
+            if (RA) {
+                rk[k] = atomicAdd(&s_wc[w][dk], valid ? 1u : 0u);
+            } else {
+                const uint64_t peers = match_peers<8>(dk, valid, 8);
+                rk[k] = 0;
+                if (valid) {
+                    rk[k] = s_wc[w][dk] + (uint32_t)__popcll(peers & (lane ? (~0ull >> (64 - lane)) : 0ull));
+                    if (lane == (uint32_t)(__ffsll((unsigned long long)peers) - 1))
+                        atomicAdd(&s_wc[w][dk], (uint32_t)__popcll(peers));
+                }
+            }
+        }
+        __syncthreads();
+        uint32_t dtot = 0;
+        if (t < 256u) {
+            uint32_t run = 0;
+#pragma unroll
+            for (int v = 0; v < NW; v++) {
+                const uint32_t c = s_wc[v][t];
+                s_wc[v][t] = run;
+                run += c;
+            }
+            dtot = run;
+        }
+        {
+            uint32_t tot;
+            const uint32_t ex = block_exclusive_scan<uint32_t, NW>(dtot, s_scr, tot);
+            if (t < 256u) s_db[t] = ex;
+        }
+        __syncthreads();
+        const int next = shift + 8;
+#pragma unroll
+        for (int k = 0; k < kBbItems; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            if (el < count) {
+                const uint32_t dk = digit(k);
+                const uint32_t pos = s_db[dk] + s_wc[w][dk] + rk[k];
+                const uint32_t slot = shift == 0 ? el : (x[k] & (kBbCap - 1u));
+                const uint32_t rest = shift == 0 ? ((key[k] - kmin) >> 8) : ((x[k] >> kBbSlot) >> 8);
+                s_buf[pos] = slot | (next < bits ? rest << kBbSlot : 0u);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kBbItems; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            if (el < count) x[k] = s_buf[el];
+        }
+        __syncthreads();
+    }
+    // the slot at every position (x[k] = the slot when no pass ran: the index order is the order)
+#pragma unroll
+    for (int k = 0; k < kBbItems; k++) x[k] &= kBbCap - 1u;
+    // pull index, key and rect by slot (owners write by slot, positions read), write out
+    auto pull = [&](const uint32_t (&src)[kBbItems], uint32_t (&dst)[kBbItems]) {
+#pragma unroll
+        for (int k = 0; k < kBbItems; k++)
+            if (wbase + k * 64 + lane < count) s_buf[wbase + k * 64 + lane] = src[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kBbItems; k++)
+            if (wbase + k * 64 + lane < count) dst[k] = s_buf[x[k]];
+        __syncthreads();
+    };
+    uint64_t* const seg = items + start;
+    uint32_t* const pseg = pay + start;
+    uint32_t o1[kBbItems], o2[kBbItems];
+#pragma unroll
+    for (int k = 0; k < kBbItems; k++)
+        if (wbase + k * 64 + lane < count) o1[k] = s_idx[x[k]];   // (s_idx written before the passes' barriers)
+    pull(key, o2);
+#pragma unroll
+    for (int k = 0; k < kBbItems; k++) {
+        const uint32_t el = wbase + k * 64 + lane;
+        if (el < count) seg[el] = ((uint64_t)o2[k] << 32) | o1[k];
+    }
+    pull(rct, o1);
+#pragma unroll
+    for (int k = 0; k < kBbItems; k++) {
+        const uint32_t el = wbase + k * 64 + lane;
+        if (el < count) {
+            pseg[el] = o1[k];
+            s_buf[el] = o2[k];   // sorted keys, for the next frame's splitters
+        }
+    }
+    __syncthreads();
+    if (bkt < (uint32_t)B - 1u)
+        bkt_write_splitters<B, kBbThreads>(start, count, live, s_next, [&](uint32_t q) { return s_buf[q]; });
 }
 
 // Splitters from a depth order the LSD passes sorted (a context's first frame, or the
@@ -4100,6 +4343,39 @@ hipError_t launch_bucket_sort(const uint64_t* in, uint64_t* items0, uint64_t* it
     case 4096: bucket_sort_b<4096>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1, rank_atomic, cap, over_host, s, row_tiles_y, rec); break;
     default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_bucket_sort_big(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int groups,
+                                  const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
+                                  const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
+                                  unsigned int* over_host, hipStream_t s, uint4* rec, bool stage) {
+    constexpr int B = kBigBuckets;
+    if (groups < 1 || groups > kBigBucketGroups || (int64_t)groups * B > 256 * (int64_t)kMaxSortGroups || cap < 1 ||
+        in == items0 || !rect || !pay0 || !pay1 || !rec)
+        return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    uint32_t* bstart = totals + B;          // B + 2 words after the totals
+    uint32_t* left = totals + 2 * B + 2;    // per bucket: k_bbk_local left it to k_bkt_local
+    const RowHist none{nullptr, B, 0};
+    hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist);
+    hipLaunchKernelGGL((k_bkt_scan<B, kBigBucketGroups>), dim3(B / 64), dim3(1024), 0, s, hist, groups, totals);
+    auto run = [&](auto ra) {
+        constexpr bool RA = decltype(ra)::value;
+        if (stage)
+            hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, true>), dim3(groups), dim3(512), 0, s, in, items0, n, s_in,
+                               groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
+        else
+            hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, false>), dim3(groups), dim3(512), 0, s, in, items0, n, s_in,
+                               groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
+        hipLaunchKernelGGL((k_bbk_local<B, RA>), dim3(B - 1), dim3(kBbThreads), 0, s, items0, pay0,
+                           static_cast<const uint32_t*>(bstart), s_in, s_out, cap, static_cast<const uint4*>(rec), left);
+        hipLaunchKernelGGL((k_bkt_local<B, RA>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0, pay1,
+                           bstart, s_in, s_out, min(cap, kBktCap), over_host, none, static_cast<const uint4*>(rec),
+                           static_cast<const uint32_t*>(left));
+    };
+    if (rank_atomic) run(std::true_type{});
+    else run(std::false_type{});
     return hipGetLastError();
 }
 

@@ -516,8 +516,13 @@ int bkt_count(int64_t n) {
 // against the LSD passes' 186 (profiles/r05_kt_c3_orbit.txt): the LSD passes stay there.
 constexpr int64_t kBucketSortMaxN = (int64_t)2048 * 1024;
 bool bkt_applies(const gsr_context* c, int64_t n) {
-    return n > 0 && (n <= kBucketSortMaxN || c->bucket_sort == 3);   // 3: any size (A/B)
+    // 3: the 4,096-bucket sort at any size (A/B); 4: big buckets above 2M (5: test hook)
+    return n > 0 && (n <= kBucketSortMaxN || c->bucket_sort >= 3);
 }
+// Big buckets (gsr_internal.h launch_bucket_sort_big): scenes above 2M with knob 28 = 4, or 5
+// (test hook: a 64-item capacity, so nearly every bucket takes the second launch's paths).
+bool bkt_big(const gsr_context* c, int64_t n) { return c->bucket_sort >= 4 && n > kBucketSortMaxN; }
+int bkt_count(const gsr_context* c, int64_t n) { return bkt_big(c, n) ? gsr::kBigBuckets : bkt_count(n); }
 
 // Row items per column-pass chunk (GSR_TUNE_COL_CHUNK 0): 1,024 up to the same 2M
 // Gaussians (config 2: column scatter 26.0 -> 21.6 us, chain -2 us), 2,048 above (config 3:
@@ -983,11 +988,11 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     // host-mapped and lags by the frames in flight; the test hook 2 (capacity 64) keeps them.
     {
         const unsigned int work = c->hstats ? ((const volatile Stats*)c->hstats)->bkt_over_work : 0u;
-        const bool spike = c->bucket_sort != 2 && (int64_t)(work - c->bkt_work_seen) > n / 8;
+        const bool spike = c->bucket_sort != 2 && c->bucket_sort != 5 && (int64_t)(work - c->bkt_work_seen) > n / 8;
         c->bkt_work_seen = work;
         if (c->bkt_B && (spike || c->bkt_scene != scene)) c->bkt_B = 0;
     }
-    c->bds_frame = bkt_applies(c, n) && !c->split_key && c->bucket_sort && c->bkt_B == bkt_count(n) && c->tile_binning &&
+    c->bds_frame = bkt_applies(c, n) && !c->split_key && c->bucket_sort && c->bkt_B == bkt_count(c, n) && c->tile_binning &&
                    c->fr.tiles_x <= 256 && c->fr.tiles_y <= 256;
     c->compact_frame = n > 0 && !c->split_key && !c->bds_frame &&
                        (c->depth_compact == 1 || (c->depth_compact == 2 && layout == GSR_LAYOUT_SCENE_BLOCK_4D)) &&
@@ -1057,6 +1062,28 @@ static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false
     // repeated sort of the frame takes the LSD passes over the sorted items[0])
     if (with_rects && !c->split_key && c->bds_frame && !c->have_sort && c->pre_out != c->items[0]) {
         const int B = c->bkt_B;
+        if (bkt_big(c, c->n)) {
+            // 512 buckets of ~n / 512 items, four 2,048-item tiles per scatter workgroup; the row
+            // pass counts for itself (its 2,048-source chunks are cheaper than bucket chunks)
+            static const bool stage = [] { const char* e = std::getenv("GSR_BKT_STAGE"); return !e || e[0] != '0'; }();
+            const int G = std::min(groups_for(c->n, 4 * gsr::kMaxBucketCap), gsr::kBigBucketGroups);
+            uint32_t* s_in = c->bkt_split + (size_t)c->bkt_par * gsr::kMaxBuckets;
+            uint32_t* s_out = c->bkt_split + (size_t)(c->bkt_par ^ 1) * gsr::kMaxBuckets;
+            HIP_TRY(gsr::launch_bucket_sort_big(c->pre_out, c->items[0], c->items[1], n, G, s_in, s_out, c->hist,
+                                                c->totals, reinterpret_cast<const uint32_t*>(c->rect), pay_buf(c, 0),
+                                                pay_buf(c, 1), rank_atomic_on(c), c->bucket_sort == 5 ? 64u : 16384u,
+                                                c->hstats_dev ? &c->hstats_dev->bkt_over : nullptr, c->stream,
+                                                c->bkt_rec, stage));
+            c->bkt_rows_fused = false;
+            c->bkt_par ^= 1;
+            c->last_bds = true;
+            c->last_compact = false;
+            c->last_split_key = false;
+            c->compact_frame = false;
+            c->bds_frame = false;
+            c->passes_launched = 4;
+            return GSR_OK;
+        }
         const int G = std::min(groups_for(c->n, gsr::kMaxBucketCap), gsr::kMaxBucketGroups);
         // a plain frame (one binning over the whole order): the local sorts also count the
         // row pass's items and pairs per bucket, which becomes the row pass's chunk
@@ -1135,8 +1162,8 @@ static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false
     }
     // the bucket sort's first splitters: quantiles of this whole sorted order (the next
     // frame of this scene size is bucket-sorted)
-    if (with_rects && !key && c->bucket_sort && bkt_applies(c, c->n) && c->bkt_B != bkt_count(c->n)) {
-        const int B = bkt_count(c->n);
+    if (with_rects && !key && c->bucket_sort && bkt_applies(c, c->n) && c->bkt_B != bkt_count(c, c->n)) {
+        const int B = bkt_count(c, c->n);
         HIP_TRY(gsr::launch_bkt_splitters(c->items[0], c->items[1], c->depth_skip ? c->dstats : nullptr, n,
                                           part ? c->nlive : nullptr, B,
                                           c->bkt_split + (size_t)c->bkt_par * gsr::kMaxBuckets, c->stream));
@@ -2077,7 +2104,7 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         c->rank_atomic = value;
         return GSR_OK;
     case GSR_TUNE_DEPTH_BUCKETS:
-        if (value < 0 || value > 3) return set_err(GSR_E_ARG, "gsr_set_tuning: depth buckets must be 0..3");
+        if (value < 0 || value > 5) return set_err(GSR_E_ARG, "gsr_set_tuning: depth buckets must be 0..5");
         c->bucket_sort = value;
         return GSR_OK;
     case GSR_TUNE_COL_CHUNK:

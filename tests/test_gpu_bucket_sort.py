@@ -336,7 +336,7 @@ def test_bucket_sort_knob(gpu):
     r = gpu.Renderer()
     assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS) == 1
     with pytest.raises(gpu.GsrError):
-        r.set_tuning(gpu.TUNE_DEPTH_BUCKETS, 4)
+        r.set_tuning(gpu.TUNE_DEPTH_BUCKETS, 6)
     with pytest.raises(gpu.GsrError):
         r.set_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER, 0)
     assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER) == 0
@@ -429,6 +429,59 @@ def test_bucket_rows_fused_saturated_keys(gpu, orc, torch, tmp_path_factory):
         assert np.array_equal(ranges, base[2]), key
         assert np.array_equal(img.view(np.uint32), base[0].view(np.uint32)), key
     assert_image_parity(base[0], orc.render(soa, cam, W, H, 3.0, threads=THREADS), exact=True)
+
+
+@pytest.mark.parametrize("hook", [4, 5])
+def test_big_buckets(gpu, orc, torch, tmp_path_factory, hook):
+    """Knob 28 = 4: above 2M Gaussians, 512 buckets of ~n / 512 items, each sorted by one
+    1,024-thread workgroup in LDS (gsr_kernels.hip k_bbk_local), the scatter writing each tile
+    in bucket order; 5 = the same with a 64-item capacity, so nearly every bucket goes to the
+    second launch (k_bkt_local's paths).  2.3M Gaussians on a moving camera (stale splitters):
+    the order equals the oracle's and the LSD passes', the tile lists and image too."""
+    from gaussianrenderer_amd import multi
+    _, soa = scene_soa(gpu, tmp_path_factory, 2_300_000, 18)
+    n = soa.shape[1]
+    W, H = 960, 540
+    scene = gpu.Scene.from_soa(soa)
+    cams = [multi.orbit_camera(0, W, H), gpu.orbit(multi.orbit_camera(0, W, H), 0.5, 0.0),
+            gpu.orbit(multi.orbit_camera(0, W, H), 1.0, 0.0)]
+    r = renderer(gpu, hook)
+    img = render_frames(gpu, torch, r, scene, cams, W, H)
+    assert r.depth_passes() == 0
+    sizes = r.bucket_sizes()
+    assert sizes is not None and sizes.size == 512 and int(sizes.sum()) == n
+    over = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER)
+    if hook == 5:
+        assert over > n // 2
+    order, pairs = r.read_depth_order(n), r.read_pairs()
+    r.close()
+    ref = renderer(gpu, 0)
+    img_lsd = render_frames(gpu, torch, ref, scene, cams[-1:], W, H)
+    assert ref.depth_passes() >= 1
+    spl = orc.preprocess(soa, cams[-1], W, H, 3.0)
+    assert np.array_equal(order, orc.expected_depth_order(spl)), "big-bucket depth order differs"
+    assert np.array_equal(order, ref.read_depth_order(n))
+    assert np.array_equal(pairs, ref.read_pairs())
+    assert np.array_equal(img.view(np.uint32), img_lsd.view(np.uint32))
+    assert_image_parity(img, orc.render(soa, cams[-1], W, H, 3.0, threads=THREADS), exact=True)
+    ref.close()
+
+
+def test_big_buckets_tie_heavy(gpu, orc, torch, tmp_path_factory):
+    """Knob 28 = 4 on 2.2M Gaussians on 5 depth planes: each plane's bucket is far over the
+    capacity (the second launch's global path, no key bits to sort: index order), ties in
+    index order."""
+    _, soa = scene_soa(gpu, tmp_path_factory, 2_200_000, 19)
+    soa = soa.copy()
+    soa[2] = np.linspace(-0.9, 0.9, 5, dtype=np.float32)[np.arange(soa.shape[1]) % 5]
+    n = soa.shape[1]
+    W, H = 640, 480
+    cam = cam_for(gpu, W, H)
+    r = renderer(gpu, 4)
+    render_frames(gpu, torch, r, gpu.Scene.from_soa(soa), [cam] * 2, W, H)
+    assert r.depth_passes() == 0
+    assert np.array_equal(r.read_depth_order(n), orc.expected_depth_order(orc.preprocess(soa, cam, W, H, 3.0)))
+    r.close()
 
 
 def test_bucket_sort_limited_to_2m(gpu, torch, tmp_path_factory):
