@@ -4297,6 +4297,20 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
     // A/B: GSR_BKT_SCATTER_256=1 runs the 4,096-bucket scatter in 256-thread workgroups (64 KB of
     // LDS instead of 96: two workgroups per CU)
     static const bool sc256 = [] { const char* e = std::getenv("GSR_BKT_SCATTER_256"); return e && e[0] == '1'; }();
+    // A/B: GSR_BKT_STAGE_SMALL=1 writes each scatter tile in bucket order here too
+    static const bool stage = [] { const char* e = std::getenv("GSR_BKT_STAGE_SMALL"); return e && e[0] == '1'; }();
+    if (stage) {
+        auto run = [&](auto ra) {
+            constexpr bool RA = decltype(ra)::value;
+            hipLaunchKernelGGL((k_bkt_scatter<B, RA, kScTh, true>), dim3(groups), dim3(kScTh), 0, s, in, items0, n,
+                               s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
+            hipLaunchKernelGGL((k_bkt_local<B, RA>), dim3(local_grid), dim3(kBktThreads), 0, s, items0, items1, pay0,
+                               pay1, bstart, s_in, s_out, cap, over_host, rh, static_cast<const uint4*>(rec));
+        };
+        if (rank_atomic) run(std::true_type{});
+        else run(std::false_type{});
+        return;
+    }
     if (B == 4096 && sc256) {
         if (rank_atomic)
             hipLaunchKernelGGL((k_bkt_scatter<B, true, kBktThreads>), dim3(groups), dim3(kBktThreads), 0, s, in, items0,
