@@ -1890,6 +1890,40 @@ __global__ __launch_bounds__(1024) void k_bkt_scan(uint32_t* __restrict__ hist, 
     }
 }
 
+// Big buckets (many chunks): one wave per bucket, its lanes splitting the chunks (up to
+// MAXG / 64 each, loads issued together), a wave scan over the lanes.  B / 4 workgroups of
+// four waves: the per-bucket layout of k_bkt_scan put 1.25 MB through 8 workgroups (23 us at
+// 611 chunks).
+template <int B, int MAXG>
+__global__ __launch_bounds__(256) void k_bkt_scan_w(uint32_t* __restrict__ hist, int groups,
+                                                    uint32_t* __restrict__ totals) {
+    GSR_GEOM_PRIO();
+    constexpr int kPerMax = MAXG / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t b = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t per = ((uint32_t)groups + 63u) / 64u;
+    const uint32_t g0 = lane * per;
+    uint32_t v[kPerMax], sum = 0;
+#pragma unroll
+    for (int i = 0; i < kPerMax; i++) {
+        const uint32_t g = g0 + (uint32_t)i;
+        v[i] = (uint32_t)i < per && g < (uint32_t)groups ? hist[(size_t)g * B + b] : 0u;
+        sum += v[i];
+    }
+    const uint32_t incl = wave_incl_scan(sum, OpAdd{});
+    uint32_t run = incl - sum;
+    if (lane == 63) totals[b] = incl;
+    if (b == 0 && lane == 0) totals[2 * B + 1] = 0u;   // bkt_sat_word (as k_bkt_scan)
+#pragma unroll
+    for (int i = 0; i < kPerMax; i++) {
+        const uint32_t g = g0 + (uint32_t)i;
+        if ((uint32_t)i < per && g < (uint32_t)groups) {
+            hist[(size_t)g * B + b] = run;
+            run += v[i];
+        }
+    }
+}
+
 // 16-bit half h of the packed counter word v.
 __device__ __forceinline__ uint32_t half16(uint32_t v, uint32_t h) { return (v >> (16u * h)) & 0xffffu; }
 
@@ -4373,7 +4407,7 @@ hipError_t launch_bucket_sort_big(const uint64_t* in, uint64_t* items0, uint64_t
     uint32_t* left = totals + 2 * B + 2;    // per bucket: k_bbk_local left it to k_bkt_local
     const RowHist none{nullptr, B, 0};
     hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist);
-    hipLaunchKernelGGL((k_bkt_scan<B, kBigBucketGroups>), dim3(B / 64), dim3(1024), 0, s, hist, groups, totals);
+    hipLaunchKernelGGL((k_bkt_scan_w<B, kBigBucketGroups>), dim3(B / 4), dim3(256), 0, s, hist, groups, totals);
     auto run = [&](auto ra) {
         constexpr bool RA = decltype(ra)::value;
         if (stage)
