@@ -2516,19 +2516,19 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
 
 // ---- big buckets (scenes above 2M Gaussians: 512 buckets of ~n / 512 items) ----
 //
-// One 1,024-thread workgroup sorts a bucket of up to kBbCap items in LDS: 16 per thread in
-// registers (blocked per wave, so a wave's items are consecutive positions), stable 8-bit
-// LSD passes over key - lo whose exchange carries one u32 per item: the slot (original
-// position, 14 bits) and the key digits the later passes still need (so pass p exchanges
-// (key - lo) >> 8 (p + 1): keys spanning up to 26 bits above lo).  After the last pass each
-// position knows its slot, and the slot's index, rect and key are pulled through the same
-// LDS buffer (written by slot, read by position), then written out coalesced.  Buckets over
-// the capacity or wider than 26 bits are flagged in `left` and sorted by k_bkt_local's paths
-// in a second launch.
+// One 1,024-thread workgroup sorts a bucket of up to kBbCap items in LDS: 16 per thread
+// (blocked per wave, so a wave's items are consecutive positions), stable 8-bit LSD passes
+// over key - lo whose exchange carries one u32 per item, slot (original position, 14 bits) |
+// (key - lo) << 14, so keys may span 18 bits above lo (config 3's buckets: 12-13).  After
+// the last pass each position knows its slot and key; the index (kept in LDS by slot) and
+// the rect (pulled through the exchange buffer by slot) join them and the bucket is written
+// out coalesced.  Buckets over the capacity or wider than 18 bits are flagged in `left` and
+// sorted by k_bkt_local's paths in a second launch.
 constexpr int kBbThreads = 1024;
 constexpr int kBbItems = 16;
 constexpr uint32_t kBbCap = kBbThreads * kBbItems;     // 16,384
 constexpr int kBbSlot = 14;                             // slot bits of the exchange word
+constexpr int kBbKeyBits = 32 - kBbSlot;                // key bits above lo it carries
 static_assert(kBbCap == 1u << kBbSlot, "slot field");
 
 template <int B, bool RA>
@@ -2539,8 +2539,8 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
                                                           const uint4* __restrict__ rec, uint32_t* __restrict__ left) {
     GSR_GEOM_PRIO();
     constexpr int NW = kBbThreads / 64;
-    __shared__ uint32_t s_buf[kBbCap];                  // the exchange, then the pulls
-    __shared__ uint32_t s_idx[kBbCap];                  // the indices by slot (registers are the limit)
+    __shared__ uint32_t s_buf[kBbCap];                  // the exchange, then the rect pull, then the keys
+    __shared__ uint32_t s_idx[kBbCap];                  // the indices by slot
     __shared__ uint32_t s_wc[NW][256];                  // per-wave digit counts, then their wave prefixes
     __shared__ uint32_t s_db[256];                      // the digits' first positions
     __shared__ uint32_t s_scr[NW], s_mm[2];
@@ -2563,51 +2563,57 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
         return;
     }
     const uint32_t wbase = w * 64 * kBbItems;
-    uint32_t key[kBbItems], rct[kBbItems];
+    uint32_t x[kBbItems], rct[kBbItems];
+    {
+        uint32_t key[kBbItems];
 #pragma unroll
-    for (int k = 0; k < kBbItems; k++) {
-        const uint32_t el = wbase + k * 64 + lane;
-        const uint4 r = el < count ? rec[start + el] : make_uint4(0u, 0xffffffffu, 0u, 0u);
-        s_idx[el] = r.x;
-        key[k] = r.y;
-        rct[k] = r.z;
-    }
-    uint32_t kmin = klo, span = khi - klo - 1u;
-    if (!bounded) {   // the open first and last buckets: their own min and max
-        uint32_t mn = 0xffffffffu, mx = 0;
-#pragma unroll
-        for (int k = 0; k < kBbItems; k++)
-            if (wbase + k * 64 + lane < count) {
-                mn = min(mn, key[k]);
-                mx = max(mx, key[k]);
-            }
-        mn = ~wave_max_u32(~mn);
-        mx = wave_max_u32(mx);
-        if (t < 2) s_mm[t] = t ? 0u : 0xffffffffu;
-        __syncthreads();
-        if (lane == 0) {
-            atomicMin(&s_mm[0], mn);
-            atomicMax(&s_mm[1], mx);
+        for (int k = 0; k < kBbItems; k++) {
+            const uint32_t el = wbase + k * 64 + lane;
+            const uint4 r = el < count ? rec[start + el] : make_uint4(0u, 0xffffffffu, 0u, 0u);
+            s_idx[el] = r.x;
+            key[k] = r.y;
+            rct[k] = r.z;
         }
-        __syncthreads();
-        kmin = s_mm[0];
-        span = s_mm[1] - kmin;
-    }
-    const int bits = span ? 32 - __clz((int)span) : 0;
-    if (bits > 26) {   // uniform: the exchange word cannot carry the digits (k_bkt_local sorts it)
-        if (t == 0) left[bkt] = 1u;
-        return;
-    }
-    if (t == 0) left[bkt] = 0u;
-    // x[k]: the position's exchange word (slot | remaining digits << kBbSlot); before the first
-    // pass position = slot and the digits come from the key
-    uint32_t x[kBbItems];
+        uint32_t kmin = klo, span = khi - klo - 1u;
+        if (!bounded) {   // the open first and last buckets: their own min and max
+            uint32_t mn = 0xffffffffu, mx = 0;
 #pragma unroll
-    for (int k = 0; k < kBbItems; k++) x[k] = wbase + k * 64 + lane;
+            for (int k = 0; k < kBbItems; k++)
+                if (wbase + k * 64 + lane < count) {
+                    mn = min(mn, key[k]);
+                    mx = max(mx, key[k]);
+                }
+            mn = ~wave_max_u32(~mn);
+            mx = wave_max_u32(mx);
+            if (t < 2) s_mm[t] = t ? 0u : 0xffffffffu;
+            __syncthreads();
+            if (lane == 0) {
+                atomicMin(&s_mm[0], mn);
+                atomicMax(&s_mm[1], mx);
+            }
+            __syncthreads();
+            kmin = s_mm[0];
+            span = s_mm[1] - kmin;
+        }
+        if (span >> kBbKeyBits) {   // uniform: wider than the exchange word (k_bkt_local sorts it)
+            if (t == 0) left[bkt] = 1u;
+            return;
+        }
+        // the exchange word of every position (before the first pass: position = slot)
+#pragma unroll
+        for (int k = 0; k < kBbItems; k++) x[k] = (wbase + k * 64 + lane) | ((key[k] - kmin) << kBbSlot);
+        __syncthreads();   // every thread has read s_mm before it is rewritten
+        if (t == 0) {
+            left[bkt] = 0u;
+            s_mm[0] = kmin;
+            s_mm[1] = span;
+        }
+    }
+    __syncthreads();
+    const uint32_t kmin = s_mm[0], span = s_mm[1];
+    const int bits = span ? 32 - __clz((int)span) : 0;   // the passes: the bits the keys span
     for (int shift = 0; shift < bits; shift += 8) {   // uniform
-        // (digits recomputed where used: registers are the occupancy limit here)
-        auto digit = [&](int k) { return shift == 0 ? ((key[k] - kmin) & 0xffu) : ((x[k] >> kBbSlot) & 0xffu); };
-        // stable ranks: per-wave counts in (item, lane) order, then wave prefixes and digit bases
+        auto digit = [&](int k) { return (x[k] >> (kBbSlot + shift)) & 0xffu; };
         for (uint32_t j = t; j < (uint32_t)NW * 256u; j += kBbThreads) (&s_wc[0][0])[j] = 0;
         __syncthreads();
         uint32_t rk[kBbItems];
@@ -2646,16 +2652,12 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
             if (t < 256u) s_db[t] = ex;
         }
         __syncthreads();
-        const int next = shift + 8;
 #pragma unroll
         for (int k = 0; k < kBbItems; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             if (el < count) {
                 const uint32_t dk = digit(k);
-                const uint32_t pos = s_db[dk] + s_wc[w][dk] + rk[k];
-                const uint32_t slot = shift == 0 ? el : (x[k] & (kBbCap - 1u));
-                const uint32_t rest = shift == 0 ? ((key[k] - kmin) >> 8) : ((x[k] >> kBbSlot) >> 8);
-                s_buf[pos] = slot | (next < bits ? rest << kBbSlot : 0u);
+                s_buf[s_db[dk] + s_wc[w][dk] + rk[k]] = x[k];
             }
         }
         __syncthreads();
@@ -2666,39 +2668,29 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
         }
         __syncthreads();
     }
-    // the slot at every position (x[k] = the slot when no pass ran: the index order is the order)
-#pragma unroll
-    for (int k = 0; k < kBbItems; k++) x[k] &= kBbCap - 1u;
-    // pull index, key and rect by slot (owners write by slot, positions read), write out
-    auto pull = [&](const uint32_t (&src)[kBbItems], uint32_t (&dst)[kBbItems]) {
-#pragma unroll
-        for (int k = 0; k < kBbItems; k++)
-            if (wbase + k * 64 + lane < count) s_buf[wbase + k * 64 + lane] = src[k];
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kBbItems; k++)
-            if (wbase + k * 64 + lane < count) dst[k] = s_buf[x[k]];
-        __syncthreads();
-    };
-    uint64_t* const seg = items + start;
-    uint32_t* const pseg = pay + start;
-    uint32_t o1[kBbItems], o2[kBbItems];
+    // rect by slot through the buffer (owners write by slot, positions read), then write out
 #pragma unroll
     for (int k = 0; k < kBbItems; k++)
-        if (wbase + k * 64 + lane < count) o1[k] = s_idx[x[k]];   // (s_idx written before the passes' barriers)
-    pull(key, o2);
-#pragma unroll
-    for (int k = 0; k < kBbItems; k++) {
-        const uint32_t el = wbase + k * 64 + lane;
-        if (el < count) seg[el] = ((uint64_t)o2[k] << 32) | o1[k];
-    }
-    pull(rct, o1);
+        if (wbase + k * 64 + lane < count) s_buf[wbase + k * 64 + lane] = rct[k];
+    __syncthreads();
+    uint64_t* const seg = items + start;
+    uint32_t* const pseg = pay + start;
 #pragma unroll
     for (int k = 0; k < kBbItems; k++) {
         const uint32_t el = wbase + k * 64 + lane;
         if (el < count) {
-            pseg[el] = o1[k];
-            s_buf[el] = o2[k];   // sorted keys, for the next frame's splitters
+            const uint32_t slot = x[k] & (kBbCap - 1u);
+            rct[k] = s_buf[slot];
+            seg[el] = ((uint64_t)(kmin + (x[k] >> kBbSlot)) << 32) | s_idx[slot];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kBbItems; k++) {
+        const uint32_t el = wbase + k * 64 + lane;
+        if (el < count) {
+            pseg[el] = rct[k];
+            s_buf[el] = kmin + (x[k] >> kBbSlot);   // sorted keys, for the next frame's splitters
         }
     }
     __syncthreads();
