@@ -2516,8 +2516,9 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
 
 // ---- big buckets (scenes above 2M Gaussians: 512 buckets of ~n / 512 items) ----
 //
-// One 1,024-thread workgroup sorts a bucket of up to kBbCap items in LDS: 16 per thread
-// (blocked per wave, so a wave's items are consecutive positions), stable 8-bit LSD passes
+// One 1,024-thread workgroup sorts a bucket of up to kBbCap items in LDS: up to 16 per thread
+// (blocked per wave, so a wave's items are consecutive positions; the 16 waves share the
+// bucket evenly, ceil(count / 1,024) rows of 64 each, so all of them work), stable 8-bit LSD passes
 // over key - lo whose exchange carries one u32 per item, slot (original position, 14 bits) |
 // (key - lo) << 14, so keys may span 18 bits above lo (config 3's buckets: 12-13).  After
 // the last pass each position knows its slot and key; the index (kept in LDS by slot) and
@@ -2562,15 +2563,17 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
         if (t == 0) left[bkt] = 1u;
         return;
     }
-    const uint32_t wbase = w * 64 * kBbItems;
+    // the waves split the bucket evenly (kk rows of 64 each) so every wave has work
+    const uint32_t kk = (count + NW * 64u - 1u) / (NW * 64u), wbase = w * kk * 64u;
     uint32_t x[kBbItems], rct[kBbItems];
     {
         uint32_t key[kBbItems];
 #pragma unroll
         for (int k = 0; k < kBbItems; k++) {
             const uint32_t el = wbase + k * 64 + lane;
-            const uint4 r = el < count ? rec[start + el] : make_uint4(0u, 0xffffffffu, 0u, 0u);
-            s_idx[el] = r.x;
+            const bool in = k < (int)kk && el < count;
+            const uint4 r = in ? rec[start + el] : make_uint4(0u, 0xffffffffu, 0u, 0u);
+            if (in) s_idx[el] = r.x;
             key[k] = r.y;
             rct[k] = r.z;
         }
@@ -2579,7 +2582,7 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
             uint32_t mn = 0xffffffffu, mx = 0;
 #pragma unroll
             for (int k = 0; k < kBbItems; k++)
-                if (wbase + k * 64 + lane < count) {
+                if (k < (int)kk && wbase + k * 64 + lane < count) {
                     mn = min(mn, key[k]);
                     mx = max(mx, key[k]);
                 }
@@ -2619,6 +2622,7 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
         uint32_t rk[kBbItems];
 #pragma unroll
         for (int k = 0; k < kBbItems; k++) {
+            if (k >= (int)kk) break;   // uniform
             const uint32_t el = wbase + k * 64 + lane;
             const bool valid = el < count;
             const uint32_t dk = digit(k);
@@ -2655,7 +2659,7 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
 #pragma unroll
         for (int k = 0; k < kBbItems; k++) {
             const uint32_t el = wbase + k * 64 + lane;
-            if (el < count) {
+            if (k < (int)kk && el < count) {
                 const uint32_t dk = digit(k);
                 s_buf[s_db[dk] + s_wc[w][dk] + rk[k]] = x[k];
             }
@@ -2664,21 +2668,21 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
 #pragma unroll
         for (int k = 0; k < kBbItems; k++) {
             const uint32_t el = wbase + k * 64 + lane;
-            if (el < count) x[k] = s_buf[el];
+            if (k < (int)kk && el < count) x[k] = s_buf[el];
         }
         __syncthreads();
     }
     // rect by slot through the buffer (owners write by slot, positions read), then write out
 #pragma unroll
     for (int k = 0; k < kBbItems; k++)
-        if (wbase + k * 64 + lane < count) s_buf[wbase + k * 64 + lane] = rct[k];
+        if (k < (int)kk && wbase + k * 64 + lane < count) s_buf[wbase + k * 64 + lane] = rct[k];
     __syncthreads();
     uint64_t* const seg = items + start;
     uint32_t* const pseg = pay + start;
 #pragma unroll
     for (int k = 0; k < kBbItems; k++) {
         const uint32_t el = wbase + k * 64 + lane;
-        if (el < count) {
+        if (k < (int)kk && el < count) {
             const uint32_t slot = x[k] & (kBbCap - 1u);
             rct[k] = s_buf[slot];
             seg[el] = ((uint64_t)(kmin + (x[k] >> kBbSlot)) << 32) | s_idx[slot];
@@ -2688,7 +2692,7 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
 #pragma unroll
     for (int k = 0; k < kBbItems; k++) {
         const uint32_t el = wbase + k * 64 + lane;
-        if (el < count) {
+        if (k < (int)kk && el < count) {
             pseg[el] = rct[k];
             s_buf[el] = kmin + (x[k] >> kBbSlot);   // sorted keys, for the next frame's splitters
         }

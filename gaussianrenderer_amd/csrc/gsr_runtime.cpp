@@ -1066,7 +1066,8 @@ static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false
             // 512 buckets of ~n / 512 items, four 2,048-item tiles per scatter workgroup; the row
             // pass counts for itself (its 2,048-source chunks are cheaper than bucket chunks)
             static const bool stage = [] { const char* e = std::getenv("GSR_BKT_STAGE"); return !e || e[0] != '0'; }();
-            const int G = std::min(groups_for(c->n, 4 * gsr::kMaxBucketCap), gsr::kBigBucketGroups);
+            static const int g_env = [] { const char* e = std::getenv("GSR_BB_GROUPS"); return e ? std::atoi(e) : 0; }();
+            const int G = std::min(g_env > 0 ? g_env : groups_for(c->n, 4 * gsr::kMaxBucketCap), gsr::kBigBucketGroups);
             uint32_t* s_in = c->bkt_split + (size_t)c->bkt_par * gsr::kMaxBuckets;
             uint32_t* s_out = c->bkt_split + (size_t)(c->bkt_par ^ 1) * gsr::kMaxBuckets;
             HIP_TRY(gsr::launch_bucket_sort_big(c->pre_out, c->items[0], c->items[1], n, G, s_in, s_out, c->hist,
