@@ -1927,6 +1927,26 @@ __global__ __launch_bounds__(256) void k_bkt_scan_w(uint32_t* __restrict__ hist,
 // 16-bit half h of the packed counter word v.
 __device__ __forceinline__ uint32_t half16(uint32_t v, uint32_t h) { return (v >> (16u * h)) & 0xffffu; }
 
+// Bucket records: 16 B {index, key, rect, 0} (R12 false: one store request per item in the
+// unstaged scatter), or 12 B {index, key, rect} (R12: the staged scatter writes runs, where
+// the bytes, not the requests, bound it; a quarter fewer of them).
+struct __attribute__((packed, aligned(4))) BktRec12 {
+    uint32_t i, k, r;
+};
+template <bool R12>
+__device__ __forceinline__ uint4 rec_get(const uint4* __restrict__ rec, uint32_t q) {
+    if (R12) {
+        const BktRec12 v = reinterpret_cast<const BktRec12*>(rec)[q];
+        return make_uint4(v.i, v.k, v.r, 0u);
+    }
+    return rec[q];
+}
+template <bool R12>
+__device__ __forceinline__ void rec_put(uint4* __restrict__ rec, uint32_t q, uint32_t i, uint32_t k, uint32_t r) {
+    if (R12) reinterpret_cast<BktRec12*>(rec)[q] = BktRec12{i, k, r};
+    else rec[q] = make_uint4(i, k, r, 0u);
+}
+
 // bstart (B + 2 words): written by chunk 0's workgroup, the first position of every bucket
 // and bstart[B] = n (k_bkt_local reads its bucket's range there); bstart[B + 1] (cleared by
 // k_bkt_scan) is raised when a live item (a tile rect that covers tiles) has key 0xFFFFFFFF.
@@ -1944,8 +1964,8 @@ __device__ __forceinline__ uint32_t half16(uint32_t v, uint32_t h) { return (v >
 // offset in the tile + the item's stable rank in it), then written out by position, so the
 // lanes of a store that hold items of one bucket write consecutive records (a run per bucket
 // and tile: ~4 items at 512 buckets) instead of one store request each.
-template <int B, bool RA, int TH, bool STAGE = false>
-__global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__ in,
+template <int B, bool RA, int TH, bool STAGE = false, uint32_t TILE = kBktTile, int WPE = 1, bool R12 = false>
+__global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(WPE))) void k_bkt_scatter(const uint64_t* __restrict__ in,
                                                              uint64_t* __restrict__ out, uint32_t n,
                                                              const uint32_t* __restrict__ splitters, int groups,
                                                              const uint32_t* __restrict__ hist,
@@ -1955,22 +1975,22 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
                                                              uint32_t* __restrict__ bstart,
                                                              uint4* __restrict__ rec) {
     GSR_GEOM_PRIO();
-    constexpr int NW = TH / 64, kIt = kBktTile / TH;  // waves; items per thread
+    constexpr int NW = TH / 64, kIt = TILE / TH;  // waves; items per thread
     constexpr uint32_t kW = B / 2;                      // packed counter words per wave
     constexpr int kPer = B / TH;                        // buckets per thread (scan)
     constexpr int kWPer = (kW + TH - 1) / TH;           // counter words per thread
-    static_assert(kPer >= 1 && kIt * TH == kBktTile, "bucket / thread split");
+    static_assert(kPer >= 1 && kIt * TH == TILE && TILE % kBktTile == 0, "bucket / thread split");
     __shared__ uint32_t s_S[B], s_gbase[B];
     __shared__ uint32_t s_wc[NW][kW];
     __shared__ uint32_t s_scr[NW];
     // STAGE: per-word tile counts, per-bucket tile offsets, the tile in bucket order
     __shared__ uint32_t s_tc[STAGE ? kW : 1], s_tp[STAGE ? B : 1];
-    __shared__ uint4 s_stage[STAGE ? kBktTile : 1];
+    __shared__ uint4 s_stage[STAGE ? TILE : 1];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const int chunk = xcd_chunk((int)blockIdx.x, groups);   // each XCD takes a contiguous run of chunks
     uint64_t b, e;
-    chunk_range(n, groups, chunk, kBktTile, b, e);
+    chunk_range(n, groups, chunk, kBktTile, b, e);   // chunks as k_bkt_count's
     const uint32_t wbase = w * 64 * kIt;
     uint64_t it[kIt];
     uint32_t pv[kIt];
@@ -1984,7 +2004,7 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
     };
     // the first tile's items and rects, the splitters, the bucket totals and this chunk's
     // histogram row are all loaded in one memory round trip
-    load(b, (uint32_t)min((uint64_t)kBktTile, e - b), it, pv);
+    load(b, (uint32_t)min((uint64_t)TILE, e - b), it, pv);
     bkt_load_splitters<B, TH>(s_S, splitters);
     {   // this chunk's first slot in every bucket: the bucket's start + the earlier chunks' items
         uint32_t loc[kPer], hrow[kPer], sum = 0;
@@ -2006,12 +2026,12 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
         if (chunk == 0 && t == 0) bstart[B] = n;
     }
     if (b >= e) return;   // uniform per workgroup, after the scan's barriers
-    for (uint64_t tb = b; tb < e; tb += kBktTile) {
-        const uint32_t tn = (uint32_t)min((uint64_t)kBktTile, e - tb);
-        const bool more = tb + kBktTile < e;   // uniform
+    for (uint64_t tb = b; tb < e; tb += TILE) {
+        const uint32_t tn = (uint32_t)min((uint64_t)TILE, e - tb);
+        const bool more = tb + TILE < e;   // uniform
         uint64_t nit[kIt];
         uint32_t npv[kIt];
-        if (more) load(tb + kBktTile, (uint32_t)min((uint64_t)kBktTile, e - tb - kBktTile), nit, npv);
+        if (more) load(tb + TILE, (uint32_t)min((uint64_t)TILE, e - tb - TILE), nit, npv);
         for (uint32_t j = t; j < NW * kW; j += TH) (&s_wc[0][0])[j] = 0;
         __syncthreads();
         uint32_t dg[kIt], rk[kIt], keys[kIt];
@@ -2058,7 +2078,7 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
         if (lane == 0 && dead_run) atomicAdd(&s_wc[w][(B - 1) >> 1], dead_run << 16);   // B - 1 is odd: high half
         __syncthreads();
         // per word (two buckets): exclusive prefix over the waves in place, tile counts kept
-        // (halves <= 2,048: no carry between them)
+        // (halves <= TILE <= 32,768: no carry between them)
         uint32_t tc[kWPer];
 #pragma unroll
         for (int q = 0; q < kWPer; q++) {
@@ -2115,7 +2135,7 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
                     out[dst] = ((uint64_t)r.y << 32) | r.x;
                     pay_out[dst] = r.z;
                 } else {
-                    rec[dst] = make_uint4(r.x, r.y, r.z, 0u);
+                    rec_put<R12>(rec, dst, r.x, r.y, r.z);
                 }
             }
         } else {
@@ -2129,7 +2149,7 @@ __global__ __launch_bounds__(TH) void k_bkt_scatter(const uint64_t* __restrict__
                         out[dst] = it[k];
                         pay_out[dst] = pv[k];
                     } else {
-                        rec[dst] = make_uint4((uint32_t)it[k], (uint32_t)(it[k] >> 32), pv[k], 0u);
+                        rec_put<R12>(rec, dst, (uint32_t)it[k], (uint32_t)(it[k] >> 32), pv[k]);
                     }
                 }
             }
@@ -2234,7 +2254,7 @@ __device__ __forceinline__ void row_hist_write(const RowHist& rh, uint32_t g, ui
 // every bucket but the first and the last (their key span sets the passes).  cap: buckets
 // above it take the global path (kBktCap; smaller only as a test hook).  over_host
 // (host-mapped, nullable): items sorted by the global path, for the diagnostics.
-template <int B, bool RA>
+template <int B, bool RA, bool R12 = false>
 __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict__ items, uint64_t* __restrict__ scratch,
                                                            uint32_t* __restrict__ pay, uint32_t* __restrict__ pay_scratch,
                                                            uint32_t* __restrict__ bstart,
@@ -2306,7 +2326,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
     }
     uint64_t* const seg = items + start;
     uint32_t* const pseg = pay + start;
-    const uint4* const rseg = rec + start;   // the bucket's records (k_bkt_scatter), index order
+    auto rseg = [&](uint32_t q) { return rec_get<R12>(rec, start + q); };   // the bucket's records, index order
     // ---- fast path: the bucket in registers, stable 8-bit passes through LDS.  IT items per
     // thread: 4 for buckets of up to 1,024 (the usual ~n / B: every wave holds a quarter of
     // the bucket), 8 up to the capacity (at 8, buckets under 1,024 left waves 2 and 3 idle
@@ -2319,7 +2339,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
 #pragma unroll
         for (int k = 0; k < IT; k++) {
             const uint32_t el = wbase + k * 64 + lane;
-            const uint4 r = el < count ? rseg[el] : make_uint4(~0u, ~0u, 0u, 0u);
+            const uint4 r = el < count ? rseg(el) : make_uint4(~0u, ~0u, 0u, 0u);
             it[k] = ((uint64_t)r.y << 32) | r.x;
             pv[k] = r.z;
         }
@@ -2413,7 +2433,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
     // ---- over capacity: stable 8-bit passes through global memory, one tile at a time ----
     if (over_host && t == 0) atomicAdd_system(over_host, count);
     for (uint32_t i = t; i < count; i += kBktThreads) {   // the records into the item / rect arrays
-        const uint4 r = rseg[i];
+        const uint4 r = rseg(i);
         seg[i] = ((uint64_t)r.y << 32) | r.x;
         pseg[i] = r.z;
     }
@@ -2532,7 +2552,7 @@ constexpr int kBbSlot = 14;                             // slot bits of the exch
 constexpr int kBbKeyBits = 32 - kBbSlot;                // key bits above lo it carries
 static_assert(kBbCap == 1u << kBbSlot, "slot field");
 
-template <int B, bool RA>
+template <int B, bool RA, bool R12>
 __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__ items, uint32_t* __restrict__ pay,
                                                           const uint32_t* __restrict__ bstart,
                                                           const uint32_t* __restrict__ s_in,
@@ -2572,7 +2592,7 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
         for (int k = 0; k < kBbItems; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             const bool in = k < (int)kk && el < count;
-            const uint4 r = in ? rec[start + el] : make_uint4(0u, 0xffffffffu, 0u, 0u);
+            const uint4 r = in ? rec_get<R12>(rec, start + el) : make_uint4(0u, 0xffffffffu, 0u, 0u);
             if (in) s_idx[el] = r.x;
             key[k] = r.y;
             rct[k] = r.z;
@@ -2622,7 +2642,8 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
         uint32_t rk[kBbItems];
 #pragma unroll
         for (int k = 0; k < kBbItems; k++) {
-            if (k >= (int)kk) break;   // uniform
+            rk[k] = 0;
+            if (k >= (int)kk) continue;   // uniform
             const uint32_t el = wbase + k * 64 + lane;
             const bool valid = el < count;
             const uint32_t dk = digit(k);
@@ -4404,19 +4425,27 @@ hipError_t launch_bucket_sort_big(const uint64_t* in, uint64_t* items0, uint64_t
     const RowHist none{nullptr, B, 0};
     hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist);
     hipLaunchKernelGGL((k_bkt_scan_w<B, kBigBucketGroups>), dim3(B / 4), dim3(256), 0, s, hist, groups, totals);
-    auto run = [&](auto ra) {
-        constexpr bool RA = decltype(ra)::value;
+    // staged: 12-B records (GSR_BB_REC16=1 for the 16-B records, A/B)
+    static const bool rec16 = [] { const char* e = std::getenv("GSR_BB_REC16"); return e && e[0] == '1'; }();
+    auto run2 = [&](auto ra, auto r12) {
+        constexpr bool RA = decltype(ra)::value, R12 = decltype(r12)::value;
         if (stage)
-            hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, true>), dim3(groups), dim3(512), 0, s, in, items0, n, s_in,
-                               groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
+            hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, true, kBktTile, 1, R12>), dim3(groups), dim3(512), 0, s, in,
+                               items0, n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart,
+                               rec);
         else
-            hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, false>), dim3(groups), dim3(512), 0, s, in, items0, n, s_in,
-                               groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
-        hipLaunchKernelGGL((k_bbk_local<B, RA>), dim3(B - 1), dim3(kBbThreads), 0, s, items0, pay0,
+            hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, false, kBktTile, 1, R12>), dim3(groups), dim3(512), 0, s, in,
+                               items0, n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart,
+                               rec);
+        hipLaunchKernelGGL((k_bbk_local<B, RA, R12>), dim3(B - 1), dim3(kBbThreads), 0, s, items0, pay0,
                            static_cast<const uint32_t*>(bstart), s_in, s_out, cap, static_cast<const uint4*>(rec), left);
-        hipLaunchKernelGGL((k_bkt_local<B, RA>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0, pay1,
+        hipLaunchKernelGGL((k_bkt_local<B, RA, R12>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0, pay1,
                            bstart, s_in, s_out, min(cap, kBktCap), over_host, none, static_cast<const uint4*>(rec),
                            static_cast<const uint32_t*>(left));
+    };
+    auto run = [&](auto ra) {
+        if (stage && !rec16) run2(ra, std::true_type{});
+        else run2(ra, std::false_type{});
     };
     if (rank_atomic) run(std::true_type{});
     else run(std::false_type{});
