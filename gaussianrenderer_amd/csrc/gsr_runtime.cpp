@@ -438,9 +438,10 @@ struct gsr_context {
     // bucket depth sort (GSR_TUNE_DEPTH_BUCKETS, gsr_kernels.hip "bucket depth sort")
     int fuse_rows = 1;               // GSR_TUNE_BUCKET_ROWS: the bucket sort's local kernel counts the row pass
     int col_chunk = 0;               // GSR_TUNE_COL_CHUNK: 0 = by scene size (col_chunk_for), 1024, 2048
-    int bucket_sort = 1;             // 0 = LSD passes; 1 = bucket sort after the context's first frame;
-                                     // 2 = test hook: as 1 with a local capacity of 64 items (most
-                                     // buckets take the global path)
+    int bucket_sort = 1;             // 0 = LSD passes; 1 = bucket sort after the context's first frame
+                                     // (big buckets above 2M, bkt_big); 2 = test hook: as 1 with a local
+                                     // capacity of 64 items (most buckets take the global path); 3 = the
+                                     // small-bucket kind at any size (A/B)
     uint32_t* bkt_split = nullptr;   // 2 x kMaxBuckets splitters (double-buffered: read one, write the other)
     uint4* bkt_rec = nullptr;        // the scatter's 16-B records (n_cap of them, with the items)
     int bkt_par = 0;                 // the half the next bucket-sorted frame reads
@@ -510,18 +511,17 @@ int bkt_count(int64_t n) {
     return b;
 }
 
-// The bucket sort pays up to 2,048 buckets (n <= 2M: config 2 one frame at a time +7.7 %,
-// config 5 +9.7 %).  At 5M Gaussians (config 3) its scatter runs ~10K items per workgroup
-// through five serial tiles (the histogram caps the workgroups at 512) and measured 244 us
-// against the LSD passes' 186 (profiles/r05_kt_c3_orbit.txt): the LSD passes stay there.
+// Two kinds of bucket sort.  Up to 2M Gaussians ~n / 1,024 buckets (up to 4,096) of <= 2,048
+// items sorted by 256-thread workgroups (config 2 one frame at a time +7.7 %, config 5 +9.7 %).
+// Above, that kind's scatter measured slower than the LSD passes at 5M (config 3 orbit: 181
+// against 141 us, profiles/r06d_kt_c3_orbit_bucket_it56.txt); there 512 big buckets of ~n / 512
+// items (gsr_internal.h launch_bucket_sort_big), each sorted by one 1,024-thread workgroup in
+// LDS: 124 us, config 3 orbit +2.1 % in flight, +1.7 % one frame at a time
+// (profiles/r06k_big_buckets_c3_orbit.txt).  Knob 28: 1 (default) both kinds by size; 2 the
+// test hook (64-item capacity, either kind); 3 the small-bucket kind at any size (A/B).
 constexpr int64_t kBucketSortMaxN = (int64_t)2048 * 1024;
-bool bkt_applies(const gsr_context* c, int64_t n) {
-    // 3: the 4,096-bucket sort at any size (A/B); 4: big buckets above 2M (5: test hook)
-    return n > 0 && (n <= kBucketSortMaxN || c->bucket_sort >= 3);
-}
-// Big buckets (gsr_internal.h launch_bucket_sort_big): scenes above 2M with knob 28 = 4, or 5
-// (test hook: a 64-item capacity, so nearly every bucket takes the second launch's paths).
-bool bkt_big(const gsr_context* c, int64_t n) { return c->bucket_sort >= 4 && n > kBucketSortMaxN; }
+bool bkt_applies(const gsr_context* c, int64_t n) { return n > 0 && c->bucket_sort != 0; }
+bool bkt_big(const gsr_context* c, int64_t n) { return c->bucket_sort != 3 && n > kBucketSortMaxN; }
 int bkt_count(const gsr_context* c, int64_t n) { return bkt_big(c, n) ? gsr::kBigBuckets : bkt_count(n); }
 
 // Row items per column-pass chunk (GSR_TUNE_COL_CHUNK 0): 1,024 up to the same 2M
@@ -988,7 +988,7 @@ static int preprocess_locked(gsr_context* c, const void* scene, int layout, int6
     // host-mapped and lags by the frames in flight; the test hook 2 (capacity 64) keeps them.
     {
         const unsigned int work = c->hstats ? ((const volatile Stats*)c->hstats)->bkt_over_work : 0u;
-        const bool spike = c->bucket_sort != 2 && c->bucket_sort != 5 && (int64_t)(work - c->bkt_work_seen) > n / 8;
+        const bool spike = c->bucket_sort != 2 && (int64_t)(work - c->bkt_work_seen) > n / 8;
         c->bkt_work_seen = work;
         if (c->bkt_B && (spike || c->bkt_scene != scene)) c->bkt_B = 0;
     }
@@ -1072,7 +1072,7 @@ static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false
             uint32_t* s_out = c->bkt_split + (size_t)(c->bkt_par ^ 1) * gsr::kMaxBuckets;
             HIP_TRY(gsr::launch_bucket_sort_big(c->pre_out, c->items[0], c->items[1], n, G, s_in, s_out, c->hist,
                                                 c->totals, reinterpret_cast<const uint32_t*>(c->rect), pay_buf(c, 0),
-                                                pay_buf(c, 1), rank_atomic_on(c), c->bucket_sort == 5 ? 64u : 16384u,
+                                                pay_buf(c, 1), rank_atomic_on(c), c->bucket_sort == 2 ? 64u : 16384u,
                                                 c->hstats_dev ? &c->hstats_dev->bkt_over : nullptr, c->stream,
                                                 c->bkt_rec, stage));
             c->bkt_rows_fused = false;
@@ -2105,7 +2105,7 @@ extern "C" int gsr_set_tuning(gsr_context* c, int knob, int value) {
         c->rank_atomic = value;
         return GSR_OK;
     case GSR_TUNE_DEPTH_BUCKETS:
-        if (value < 0 || value > 5) return set_err(GSR_E_ARG, "gsr_set_tuning: depth buckets must be 0..5");
+        if (value < 0 || value > 3) return set_err(GSR_E_ARG, "gsr_set_tuning: depth buckets must be 0..3");
         c->bucket_sort = value;
         return GSR_OK;
     case GSR_TUNE_COL_CHUNK:

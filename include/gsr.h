@@ -377,19 +377,21 @@ enum {
        histograms in 512-thread workgroups of 2048 Gaussians, pass 0 without its upsweep launch:
        preprocess 49.4 -> 60.3 us against the 5.7-us upsweep, -1.1 % one frame at a time and
        -1.2 % in flight, profiles/r04_ab_pre_hist.txt) */
-    GSR_TUNE_DEPTH_BUCKETS = 28,     /* binning path, frames not split by a depth threshold, scenes of at
-                                        most 2,097,152 Gaussians (larger ones keep the LSD passes): 1 (default) =
+    GSR_TUNE_DEPTH_BUCKETS = 28,     /* binning path, frames not split by a depth threshold: 1 (default) =
                                         bucket depth sort: one stable scatter of the preprocess order into
-                                        ~n/1024 depth buckets bounded by the previous frame's quantiles,
-                                        then one workgroup per bucket sorts it in LDS (buckets over 2,048
-                                        items are sorted through global memory by their workgroup).  A
-                                        context's first frame of a scene size runs the LSD passes and
-                                        takes the quantiles from them, and so does the first frame of
-                                        another scene pointer, and the frame after one whose global path
-                                        ran more than n/8 item-passes (a camera cut; knob 33).  0 = LSD
-                                        passes only; 2 = test hook: 1 with a 64-item local capacity
-                                        (no reseeding on overflow); 3 = 1 at any scene size (A/B).
-                                        Same order, same image;
+                                        depth buckets bounded by the previous frame's quantiles, then one
+                                        workgroup per bucket sorts it in LDS.  Up to 2,097,152 Gaussians
+                                        ~n/1024 buckets (at most 4,096) of up to 2,048 items per 256-thread
+                                        workgroup (larger buckets are sorted through global memory by their
+                                        workgroup); above, 512 buckets of up to 16,384 items per 1,024-thread
+                                        workgroup (larger or wider-keyed ones go to the first kind's
+                                        paths in a second launch).  A context's first frame of a scene size
+                                        runs the LSD passes and takes the quantiles from them, and so does
+                                        the first frame of another scene pointer, and the frame after one
+                                        whose global path ran more than n/8 item-passes (a camera cut; knob
+                                        33).  0 = LSD passes only; 2 = test hook: 1 with a 64-item local
+                                        capacity in either kind (no reseeding on overflow); 3 = the first
+                                        kind at any scene size (A/B).  Same order, same image;
                                         gsr_depth_passes is 0 after a bucket-sorted frame */
     GSR_TUNE_DEPTH_BUCKETS_OVER = 29, /* read-only: items the bucket sort's global path has sorted (buckets
                                         over the local capacity), summed over the lanes; sticky, read

@@ -336,7 +336,7 @@ def test_bucket_sort_knob(gpu):
     r = gpu.Renderer()
     assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS) == 1
     with pytest.raises(gpu.GsrError):
-        r.set_tuning(gpu.TUNE_DEPTH_BUCKETS, 6)
+        r.set_tuning(gpu.TUNE_DEPTH_BUCKETS, 4)
     with pytest.raises(gpu.GsrError):
         r.set_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER, 0)
     assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER) == 0
@@ -431,12 +431,12 @@ def test_bucket_rows_fused_saturated_keys(gpu, orc, torch, tmp_path_factory):
     assert_image_parity(base[0], orc.render(soa, cam, W, H, 3.0, threads=THREADS), exact=True)
 
 
-@pytest.mark.parametrize("hook", [4, 5])
+@pytest.mark.parametrize("hook", [1, 2])
 def test_big_buckets(gpu, orc, torch, tmp_path_factory, hook):
-    """Knob 28 = 4: above 2M Gaussians, 512 buckets of ~n / 512 items, each sorted by one
-    1,024-thread workgroup in LDS (gsr_kernels.hip k_bbk_local), the scatter writing each tile
-    in bucket order; 5 = the same with a 64-item capacity, so nearly every bucket goes to the
-    second launch (k_bkt_local's paths).  2.3M Gaussians on a moving camera (stale splitters):
+    """Knob 28 = 1 (default) above 2M Gaussians: 512 buckets of ~n / 512 items, each sorted by
+    one 1,024-thread workgroup in LDS (gsr_kernels.hip k_bbk_local), the scatter writing each
+    tile in bucket order as 12-B records; 2 = the same with a 64-item capacity, so nearly every
+    bucket goes to the second launch (k_bkt_local's paths).  2.3M Gaussians on a moving camera (stale splitters):
     the order equals the oracle's and the LSD passes', the tile lists and image too."""
     from gaussianrenderer_amd import multi
     _, soa = scene_soa(gpu, tmp_path_factory, 2_300_000, 18)
@@ -451,7 +451,7 @@ def test_big_buckets(gpu, orc, torch, tmp_path_factory, hook):
     sizes = r.bucket_sizes()
     assert sizes is not None and sizes.size == 512 and int(sizes.sum()) == n
     over = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER)
-    if hook == 5:
+    if hook == 2:
         assert over > n // 2
     order, pairs = r.read_depth_order(n), r.read_pairs()
     r.close()
@@ -468,7 +468,7 @@ def test_big_buckets(gpu, orc, torch, tmp_path_factory, hook):
 
 
 def test_big_buckets_tie_heavy(gpu, orc, torch, tmp_path_factory):
-    """Knob 28 = 4 on 2.2M Gaussians on 5 depth planes: each plane's bucket is far over the
+    """Big buckets (the default above 2M) on 2.2M Gaussians on 5 depth planes: each plane's bucket is far over the
     capacity (the second launch's global path, no key bits to sort: index order), ties in
     index order."""
     _, soa = scene_soa(gpu, tmp_path_factory, 2_200_000, 19)
@@ -477,19 +477,26 @@ def test_big_buckets_tie_heavy(gpu, orc, torch, tmp_path_factory):
     n = soa.shape[1]
     W, H = 640, 480
     cam = cam_for(gpu, W, H)
-    r = renderer(gpu, 4)
+    r = renderer(gpu)
     render_frames(gpu, torch, r, gpu.Scene.from_soa(soa), [cam] * 2, W, H)
     assert r.depth_passes() == 0
     assert np.array_equal(r.read_depth_order(n), orc.expected_depth_order(orc.preprocess(soa, cam, W, H, 3.0)))
     r.close()
 
 
-def test_bucket_sort_limited_to_2m(gpu, torch, tmp_path_factory):
-    """Above 2,097,152 Gaussians (config 3's 5M) the LSD passes stay: the bucket sort's
-    scatter measured slower there (profiles/r05_kt_c3_orbit.txt)."""
+def test_bucket_kind_by_size(gpu, orc, torch, tmp_path_factory):
+    """Above 2,097,152 Gaussians the default sorts 512 big buckets; knob 28 = 3 keeps the
+    small-bucket kind (~n / 1,024 buckets, up to 4,096) there.  Both orders exact."""
     _, soa = scene_soa(gpu, tmp_path_factory, 2_100_000, 13)
+    n = soa.shape[1]
     W, H = 320, 240
     scene = gpu.Scene.from_soa(soa)
-    r = renderer(gpu)
-    render_frames(gpu, torch, r, scene, [cam_for(gpu, W, H)] * 2, W, H)
-    assert r.depth_passes() >= 1
+    cam = cam_for(gpu, W, H)
+    want = orc.expected_depth_order(orc.preprocess(soa, cam, W, H, 3.0))
+    for knob, buckets in ((1, 512), (3, gpu.MAX_BUCKETS)):
+        r = renderer(gpu, knob)
+        render_frames(gpu, torch, r, scene, [cam] * 2, W, H)
+        assert r.depth_passes() == 0
+        assert r.bucket_sizes().size == buckets, knob
+        assert np.array_equal(r.read_depth_order(n), want), knob
+        r.close()

@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
-for b in ${BUCKETS_LIST:-1 4}; do
+for b in ${BUCKETS_LIST:-0 1}; do
   O=gpurun_out/bbkt_$b${KT_TAG:-}; mkdir -p $O
   BUCKETS=$b FRAMES=${FRAMES:-120} timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 tools/bb_probe.py > $O/kt.log 2>&1
   rc=$?; echo "buckets $b rc=$rc"; [ $rc = 0 ] || exit $rc

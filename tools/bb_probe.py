@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Big-bucket probe (analysis only): config 3 on an orbit with knob 28 = 4, per frame the
+"""Big-bucket probe (analysis only): config 3 on an orbit with knob 28 = BUCKETS (default 1: big buckets), per frame the
 largest live bucket, its index, the edge buckets and the items the global path took."""
 import os
 import sys
@@ -21,7 +21,7 @@ def main():
     scene = gsr.Scene.from_ply(ply)
     r = gsr.Renderer()
     r.set_tuning(gsr.TUNE_DEPTH_SPLIT, 0)
-    r.set_tuning(gsr.TUNE_DEPTH_BUCKETS, int(os.environ.get("BUCKETS", "4")))
+    r.set_tuning(gsr.TUNE_DEPTH_BUCKETS, int(os.environ.get("BUCKETS", "1")))
     out = torch.empty(3 * W * H, device="cuda")
     for i in range(int(os.environ.get("FRAMES", "24"))):
         c = gsr.make_camera(position=(0, 0, 4), fov_y=50, aspect=W / H)
