@@ -125,6 +125,26 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* scratch, T& total) {
     return pre + x - v;
 }
 
+// block_exclusive_scan without its trailing barrier: the caller barriers before `scratch`
+// is written again (and before anything it publishes from the result is read).
+template <typename T, int NW = 4>
+__device__ __forceinline__ T block_exclusive_scan_lead(T v, T* scratch, T& total) {
+    const uint32_t lane = lane_id();
+    const uint32_t w = threadIdx.x >> 6;
+    const T x = wave_incl_scan(v, OpAdd{});
+    if (lane == 63) scratch[w] = x;
+    __syncthreads();
+    T pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < NW; k++) {
+        const T s = scratch[k];
+        if ((uint32_t)k < w) pre += s;
+        tot += s;
+    }
+    total = tot;
+    return pre + x - v;
+}
+
 // Wave64-wide max / or (every lane gets the result: lane 63 of the inclusive scan).
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v, OpMax{}), 63);
@@ -1964,7 +1984,8 @@ __device__ __forceinline__ void rec_put(uint4* __restrict__ rec, uint32_t q, uin
 // offset in the tile + the item's stable rank in it), then written out by position, so the
 // lanes of a store that hold items of one bucket write consecutive records (a run per bucket
 // and tile: ~4 items at 512 buckets) instead of one store request each.
-template <int B, bool RA, int TH, bool STAGE = false, uint32_t TILE = kBktTile, int WPE = 1, bool R12 = false>
+template <int B, bool RA, int TH, bool STAGE = false, uint32_t TILE = kBktTile, int WPE = 1, bool R12 = false,
+          bool LEAN = false>
 __global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(WPE))) void k_bkt_scatter(const uint64_t* __restrict__ in,
                                                              uint64_t* __restrict__ out, uint32_t n,
                                                              const uint32_t* __restrict__ splitters, int groups,
@@ -1980,6 +2001,12 @@ __global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     constexpr int kPer = B / TH;                        // buckets per thread (scan)
     constexpr int kWPer = (kW + TH - 1) / TH;           // counter words per thread
     static_assert(kPer >= 1 && kIt * TH == TILE && TILE % kBktTile == 0, "bucket / thread split");
+    // LEAN (staged, one counter word per thread): thread t < kW owns word t (buckets 2t, 2t + 1),
+    // so its wave prefix and the tile offsets' scan are one step (no s_tc, one barrier fewer);
+    // the scan keeps only its first barrier, and the counters are cleared for the next tile
+    // after their last read (the stage writes), so the tile starts without a clear + barrier:
+    // five barriers per tile instead of eight
+    constexpr bool kLean = LEAN && STAGE && kW <= (uint32_t)TH;
     __shared__ uint32_t s_S[B], s_gbase[B];
     __shared__ uint32_t s_wc[NW][kW];
     __shared__ uint32_t s_scr[NW];
@@ -2026,14 +2053,20 @@ __global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         if (chunk == 0 && t == 0) bstart[B] = n;
     }
     if (b >= e) return;   // uniform per workgroup, after the scan's barriers
+    if (kLean) {
+        for (uint32_t j = t; j < NW * kW; j += TH) (&s_wc[0][0])[j] = 0;
+        __syncthreads();
+    }
     for (uint64_t tb = b; tb < e; tb += TILE) {
         const uint32_t tn = (uint32_t)min((uint64_t)TILE, e - tb);
         const bool more = tb + TILE < e;   // uniform
         uint64_t nit[kIt];
         uint32_t npv[kIt];
         if (more) load(tb + TILE, (uint32_t)min((uint64_t)TILE, e - tb - TILE), nit, npv);
-        for (uint32_t j = t; j < NW * kW; j += TH) (&s_wc[0][0])[j] = 0;
-        __syncthreads();
+        if (!kLean) {
+            for (uint32_t j = t; j < NW * kW; j += TH) (&s_wc[0][0])[j] = 0;
+            __syncthreads();
+        }
         uint32_t dg[kIt], rk[kIt], keys[kIt];
 #pragma unroll
         for (int k = 0; k < kIt; k++) keys[k] = (uint32_t)(it[k] >> 32);
@@ -2095,11 +2128,23 @@ __global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                     run += c[v];
                 }
                 tc[q] = run;
-                if (STAGE) s_tc[j] = run;
+                if (STAGE && !kLean) s_tc[j] = run;
             }
         }
-        __syncthreads();
-        if (STAGE) {
+        if (kLean) {
+            // the buckets' offsets in the tile: thread t < kW scans word t's two tile counts
+            const uint32_t lo = tc[0] & 0xffffu, hi = tc[0] >> 16;
+            uint32_t tot;
+            const uint32_t ex = block_exclusive_scan_lead<uint32_t, NW>(t < kW ? lo + hi : 0u, s_scr, tot);
+            if (t < kW) {
+                s_tp[2 * t] = ex;
+                s_tp[2 * t + 1] = ex + lo;
+            }
+            __syncthreads();
+        } else {
+            __syncthreads();
+        }
+        if (STAGE && !kLean) {
             // the buckets' offsets in the tile: exclusive scan of their tile counts (thread t
             // owns buckets t * kPer .. + kPer - 1)
             uint32_t c[kPer], sum = 0;
@@ -2117,6 +2162,8 @@ __global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                 run += c[k];
             }
             __syncthreads();
+        }
+        if (STAGE) {
 #pragma unroll
             for (int k = 0; k < kIt; k++) {
                 const uint32_t el = wbase + k * 64 + lane;
@@ -2127,6 +2174,8 @@ __global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                 }
             }
             __syncthreads();
+            if (kLean)   // the counters' last read is behind: clear them for the next tile
+                for (uint32_t j = t; j < NW * kW; j += TH) (&s_wc[0][0])[j] = 0;
             for (uint32_t q = t; q < tn; q += TH) {
                 const uint4 r = s_stage[q];
                 const uint32_t d = r.w;
@@ -4425,11 +4474,18 @@ hipError_t launch_bucket_sort_big(const uint64_t* in, uint64_t* items0, uint64_t
     const RowHist none{nullptr, B, 0};
     hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist);
     hipLaunchKernelGGL((k_bkt_scan_w<B, kBigBucketGroups>), dim3(B / 4), dim3(256), 0, s, hist, groups, totals);
+    // the barrier-lean staged tile (k_bkt_scatter LEAN: 52.0 -> 50.2 us at config 3 orbit);
+    // GSR_BB_LEAN=0 for the eight-barrier tile (A/B)
+    static const bool lean = [] { const char* e = std::getenv("GSR_BB_LEAN"); return !e || e[0] != '0'; }();
     // staged: 12-B records (GSR_BB_REC16=1 for the 16-B records, A/B)
     static const bool rec16 = [] { const char* e = std::getenv("GSR_BB_REC16"); return e && e[0] == '1'; }();
     auto run2 = [&](auto ra, auto r12) {
         constexpr bool RA = decltype(ra)::value, R12 = decltype(r12)::value;
-        if (stage)
+        if (stage && lean)
+            hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, true, kBktTile, 1, R12, true>), dim3(groups), dim3(512), 0, s,
+                               in, items0, n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0,
+                               bstart, rec);
+        else if (stage)
             hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, true, kBktTile, 1, R12>), dim3(groups), dim3(512), 0, s, in,
                                items0, n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart,
                                rec);

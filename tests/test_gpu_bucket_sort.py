@@ -500,3 +500,36 @@ def test_bucket_kind_by_size(gpu, orc, torch, tmp_path_factory):
         assert r.bucket_sizes().size == buckets, knob
         assert np.array_equal(r.read_depth_order(n), want), knob
         r.close()
+
+
+def test_big_buckets_config3_orbit(gpu, orc, torch, tmp_path_factory):
+    """Config 3 (5M, 1600x1063) on a 0.25-deg orbit with the default
+    bucket sort: the first frame runs the LSD passes, the next three sort 512 big buckets
+    bounded by the previous frame's quantiles.  Every live bucket fits one workgroup's 16,384
+    items and no item takes the global path; the last frame's depth order equals the oracle's,
+    and its order, tile lists and image (exact blend) equal the LSD passes', bit for bit."""
+    path, soa = scene_soa(gpu, tmp_path_factory, 5_000_000, 3)
+    n = soa.shape[1]
+    W, H = 1600, 1063
+    scene = gpu.Scene.from_ply(path)
+    cams = [gpu.orbit(gpu.make_camera(position=(0, 0, 4), fov_y=50, aspect=W / H), 0.25 * i, 0.0)
+            for i in range(4)]
+    r = renderer(gpu)
+    over0 = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER)
+    img = render_frames(gpu, torch, r, scene, cams, W, H)
+    assert r.depth_passes() == 0
+    sizes = r.bucket_sizes()
+    assert sizes.size == 512 and int(sizes.sum()) == n
+    assert int(sizes[:-1].max()) <= 16384, int(sizes[:-1].max())
+    assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER) == over0
+    order, pairs = r.read_depth_order(n), r.read_pairs()
+    r.close()
+    ref = renderer(gpu, 0)
+    img_lsd = render_frames(gpu, torch, ref, scene, cams[-1:], W, H)
+    assert ref.depth_passes() >= 1
+    assert np.array_equal(order, ref.read_depth_order(n))
+    assert np.array_equal(pairs, ref.read_pairs())
+    assert np.array_equal(img.view(np.uint32), img_lsd.view(np.uint32))
+    ref.close()
+    spl = orc.preprocess(soa, cams[-1], W, H, 3.0)
+    assert np.array_equal(order, orc.expected_depth_order(spl)), "config 3 orbit depth order differs"
