@@ -43,6 +43,7 @@ CONFIGS = {
 TIMESTEPS_4D = 120
 TIMING_STRIDE = 8
 STAGE_FRAMES = 10     # untimed frames averaged for stages_ms
+LEAD_IN = 8           # --orbit-step / orbit object: untimed frames per lane just before a timed region
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # the blend (one 64-thread workgroup per 8x8 block): template <DIAG, STAMPS, FX, SPLIT>, FX = the
 # fast-exp blend (GSR_TUNE_BLEND_EXP 1) or the exact one (0, the default); SPLIT 1 = the depth
@@ -357,9 +358,9 @@ ORBIT_STATS_FRAMES = 40       # untimed frames whose bucket sizes give the split
 
 def orbit_line(gsr, torch, multi, args, scene, W, H, F, stream) -> dict:
     """Config 2 on a moving camera: the same seed-2 scene, frame i orbited
-    by 0.25 deg * i (Camera::orbit, camera.cpp:130-158; the orbit continues across every
-    region below, so no frame repeats a view), K frames in flight and one at a time after
-    the same warmup.  The headline repeats one camera, the best case of every temporal cache
+    by 0.25 deg * i (Camera::orbit, camera.cpp:130-158), K frames in flight and one at a time
+    after the same warmup, each timed region preceded by untimed lead-in frames -LEAD_IN..-1
+    (per lane) so it starts from a viewer's history, not a jump.  The headline repeats one camera, the best case of every temporal cache
     in the path (the bucket splitters are the previous frame's depth quantiles, the depth
     pass budget, the depth split's speculation); this object reports the moving viewer's
     rate beside it, the items the bucket sort sent through its global path (buckets over
@@ -396,6 +397,18 @@ def orbit_line(gsr, torch, multi, args, scene, W, H, F, stream) -> dict:
         pos[0] += 4 * F
         torch.cuda.synchronize()
     ro.sync()
+
+    def lead_in(sequential):   # orbit frames -LEAD_IN .. -1 (per lane) before timed frames 0..K-1
+        pos[0] = 0
+        if sequential:
+            for i in range(-LEAD_IN, 0):
+                sh.frame(i)
+        else:
+            sh.path(-LEAD_IN * F, LEAD_IN * F, [j % F for j in range(LEAD_IN * F)])
+        torch.cuda.synchronize()
+        ro.sync()
+
+    lead_in(True)
     over0 = ro.get_tuning(29)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -407,6 +420,9 @@ def orbit_line(gsr, torch, multi, args, scene, W, H, F, stream) -> dict:
     seq_rc = ro.sync()
     timed_frames = args.steps
     for _ in range(2):
+        over1 = ro.get_tuning(29)
+        lead_in(False)
+        over0 += ro.get_tuning(29) - over1   # the lead-in's global-path items are not the timed frames'
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         sh.run(args.steps)
@@ -454,8 +470,9 @@ def orbit_line(gsr, torch, multi, args, scene, W, H, F, stream) -> dict:
             "stages_ms": {k: round(v / max(1, frames), 4) for k, v in sums.items()},
             "overflow_after_timed": seq_rc,
             "note": "config 2 on a moving camera: frame i orbited by 0.25 deg * i around the scene (camera.cpp "
-                    "Camera::orbit), the orbit continuing through warmup, the one-at-a-time and the in-flight "
-                    "regions; same scene, K, warmup as the headline"}
+                    "Camera::orbit); the one-at-a-time and the in-flight regions each show frames 0..K-1 after "
+                    "LEAD_IN untimed frames per lane just before them (-LEAD_IN .. -1), so every timed frame's "
+                    "splitters are a moving viewer's; same scene, K, warmup as the headline"}
 
 
 def frame_time(i: int) -> float:
@@ -520,16 +537,25 @@ def main():
     broadcast_ms = (time.perf_counter() - load_s) * 1e3 if dist else None
     cam = multi.orbit_camera(rank, W, H)      # rank 0: camera (0,0,4); config 4: orbit 45 deg * rank
     frame_cam = None
+    orbit_pos = [0]   # orbit index of region-relative frame 0 (untimed regions continue the orbit)
+
+    def advance(m):
+        orbit_pos[0] += m
+
     if args.orbit_step:
-        # a moving viewer: frame i at azimuth 45 deg * rank + i * step (one Camera::orbit call)
+        # a moving viewer: orbit index j at azimuth 45 deg * rank + j * step (one Camera::orbit
+        # call); region-relative frame i is j = orbit_pos + i.  Each timed region shows frames
+        # 0..K-1 after a lead-in (lead_in below), so its views do not depend on how many
+        # frames the time-based warmups rendered
         cam_cache = {}
 
         def frame_cam(i):
-            if i not in cam_cache:
+            j = orbit_pos[0] + i
+            if j not in cam_cache:
                 c = gsr.make_camera(position=(0, 0, 4), fov_y=50, aspect=W / H)
-                gsr.orbit(c, multi.orbit_azimuth(rank) + args.orbit_step * i, 0.0)
-                cam_cache[i] = c
-            return cam_cache[i]
+                gsr.orbit(c, multi.orbit_azimuth(rank) + args.orbit_step * j, 0.0)
+                cam_cache[j] = c
+            return cam_cache[j]
 
     r = gsr.Renderer()
     for kv in filter(None, args.tune.split(",")):
@@ -546,24 +572,42 @@ def main():
     # warmup (+ grow every lane's pair buffer to the high-water mark)
     for i in range(max(1, args.warmup)):
         frame(i)
+    advance(max(1, args.warmup))
     while r.sync() != 0:
         frame()
+        advance(1)
     for _ in range(3):
         rc = path(0, max(F, args.warmup), [j % min(F, len(outs)) for j in range(max(F, args.warmup))])
+        advance(max(F, args.warmup))
         if r.sync() == 0 and rc == 0:
             break
     torch.cuda.synchronize()
 
-    warm_pos = [0]
+    def lead_in(sequential):
+        """A moving camera's timed region shows orbit frames 0..K-1; untimed frames just
+        before it (-LEAD_IN .. -1 per lane, one at a time or through the lanes) give the
+        temporal caches (bucket splitters, pass budget) a viewer's history instead of a jump
+        from wherever the orbit stood."""
+        if not frame_cam:
+            return
+        orbit_pos[0] = 0
+        if sequential:
+            for i in range(-LEAD_IN, 0):
+                frame(i)
+        else:
+            m = LEAD_IN * F
+            path(-m, m, [j % min(F, len(outs)) for j in range(m)])
+        torch.cuda.synchronize()
+        r.sync()
 
     def warm(ms):
         """Untimed frames in flight for at least `ms` of wall time; returns the count.  A
-        moving camera (--orbit-step) keeps moving through them (frame indices continue)."""
+        moving camera (--orbit-step) keeps moving through them."""
         frames, w0 = 0, time.perf_counter()
         while (time.perf_counter() - w0) * 1e3 < ms:
             m = 4 * F
-            path(warm_pos[0] if frame_cam else 0, m, [j % min(F, len(outs)) for j in range(m)])
-            warm_pos[0] += m
+            path(0, m, [j % min(F, len(outs)) for j in range(m)])
+            advance(m)
             frames += m
             torch.cuda.synchronize()
         r.sync()
@@ -576,14 +620,18 @@ def main():
     # instrumented blend kernel
     t_mid = frame_time(TIMESTEPS_4D // 2) if four_d else None
     r.set_timing(2)
-    for _ in range(STAGE_FRAMES):
-        r.render(scene, cam, W, H, outs[0].data_ptr(), k=args.k, stream=stream, time=t_mid)
+    for i in range(STAGE_FRAMES):
+        r.render(scene, frame_cam(i) if frame_cam else cam, W, H, outs[0].data_ptr(), k=args.k, stream=stream,
+                 time=t_mid)
+    advance(STAGE_FRAMES)
     r.sync()
     stage_sums, stage_frames = r.stage_times()
     stages = {k: v / max(1, stage_frames) for k, v in stage_sums.items()}
     r.set_timing(0)
     r.set_diagnostics(True)
-    r.render(scene, cam, W, H, outs[0].data_ptr(), k=args.k, stream=stream, time=t_mid)
+    r.render(scene, frame_cam(0) if frame_cam else cam, W, H, outs[0].data_ptr(), k=args.k, stream=stream,
+             time=t_mid)
+    advance(1)
     r.sync()
     pairs = r.pair_count()
     row_items = r.row_item_count()
@@ -634,7 +682,9 @@ def main():
     def run_sequential():
         for i in range(args.steps):
             frame(i)
+    lead_in(True)
     seq_elapsed = timed(run_sequential)
+    advance(args.steps)
     blend_times, timed_frames = r.stage_times()
     r.set_timing(0)
     seq_overflow = r.sync()
@@ -653,14 +703,18 @@ def main():
         # re-rendering and re-gathering exactly the chunks some rank got incomplete
         shard.overflowed, shard.gathers, shard.repaired = False, 0, 0
         clean = []
+        lead_in(False)
         elapsed = timed(lambda: clean.append(shard.run_checked(args.steps, dev_kind)))
+        advance(args.steps)
         reruns = shard.repaired
         if not clean[0]:
             sys.exit("bench.py: frames still incomplete after repairs")
     elif F > 1:
         for attempt in range(2):
             shard.overflowed, shard.gathers = False, 0
+            lead_in(False)
             elapsed = timed(lambda: shard.run(args.steps))
+            advance(args.steps)
             if not shard.finish(dev_kind):
                 break
             reruns += 1
@@ -679,6 +733,7 @@ def main():
         shard.run(args.steps)
         shard.drain()
         torch.cuda.synchronize()
+        advance(args.steps)
         blend_times_pipe, timed_frames_pipe = r.stage_times()
         r.set_timing(0)
         shard.finish(dev_kind)
@@ -699,6 +754,7 @@ def main():
                               stream=stream, frame_cam=frame_cam)
         ro.run(args.steps)               # warm: the lanes leave the gathered loop's rhythm
         torch.cuda.synchronize()
+        advance(args.steps)
         r.sync()
         dist.barrier()
         torch.cuda.synchronize()
@@ -706,6 +762,7 @@ def main():
         ro.run(args.steps)
         torch.cuda.synchronize()
         render_el = time.perf_counter() - t0
+        advance(args.steps)
         r.sync()
         scale = multi.scale_report(dist, render_el, args.steps, gms, world * args.steps / max_elapsed,
                                    "cpu" if gloo else "cuda")
@@ -751,7 +808,8 @@ def main():
                                + (f"one orbit camera per GPU, {'RCCL' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'} "
                                   f"gather to rank 0 ({args.gather})" if world > 1
                                   else "camera (0,0,4) fovY 50")
-                               + (f", moving camera: frame i orbited by {args.orbit_step:g} deg * i"
+                               + (f", moving camera: the i-th frame shown orbited by {args.orbit_step:g} deg * i "
+                                  "(the orbit continues across warmup, stage sample and timed regions)"
                                   if args.orbit_step else "")
                                + (", SH degree 3 (opt-in SH-3 mode: 45 f_rest, bands 0-3)" if args.sh3
                                   else ", SH bands 0-2 as the reference evaluates (render.cu:506-530)")
