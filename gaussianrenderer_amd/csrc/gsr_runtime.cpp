@@ -1229,12 +1229,16 @@ static int bin_locked(gsr_context* c, uint32_t base, uint32_t count, int gate_mo
     // key mode, phase A: about 2 x the split point's items (the count is on the device)
     const int64_t est = rs && rs->cut_mode == 1 ? std::min<int64_t>(count, std::max<int64_t>(2 * (int64_t)rs->na, 65536))
                                                 : (int64_t)count;
-    // A/B: GSR_ROW_CHUNK = sources per row-pass chunk (default 1,024; the chunk is rounded up
-    // to a multiple of 1,024 and the chunks capped at 4,096)
-    static const int64_t row_chunk = [] {
+    // Sources per row-pass chunk (rounded up to a multiple of 1,024, the chunks capped at
+    // 4,096): 1,024, and 3,072 for a whole-order pass above 2M Gaussians (config 3 orbit, big
+    // buckets: the row pass 72.8 -> 65.8 us, the count and scan pay per chunk and the scatter
+    // takes 3,072 sources as well as ~1,200; 4,096: 68.7, profiles/r06o_kt_row_chunk_c3.txt).
+    // GSR_ROW_CHUNK forces one size (A/B).
+    static const int64_t row_chunk_env = [] {
         const char* e = std::getenv("GSR_ROW_CHUNK");
-        return e ? std::max<int64_t>(1024, std::atoll(e)) : (int64_t)1024;
+        return e ? std::max<int64_t>(1024, std::atoll(e)) : (int64_t)0;
     }();
+    const int64_t row_chunk = row_chunk_env ? row_chunk_env : (!rs && est > kBucketSortMaxN ? 3072 : 1024);
     const int gb = std::min(groups_for(est, row_chunk), gsr::kMaxSortGroups / 2);
     // (a bucket-sorted frame has no pass plan: its order is in items[0], its rects in pay_buf 0)
     uint32_t* dst = c->depth_skip && !(c->last_bds && !far) ? (far ? c->dstats_far : c->dstats) : nullptr;
