@@ -22,6 +22,9 @@ def main():
     r = gsr.Renderer()
     r.set_tuning(gsr.TUNE_DEPTH_SPLIT, 0)
     r.set_tuning(gsr.TUNE_DEPTH_BUCKETS, int(os.environ.get("BUCKETS", "1")))
+    for kv in filter(None, os.environ.get("TUNE", "").split(",")):   # more knobs: "31=4096,..."
+        k, v = kv.split("=")
+        r.set_tuning(int(k), int(v))
     out = torch.empty(3 * W * H, device="cuda")
     for i in range(int(os.environ.get("FRAMES", "24"))):
         c = gsr.make_camera(position=(0, 0, 4), fov_y=50, aspect=W / H)
