@@ -533,3 +533,32 @@ def test_big_buckets_config3_orbit(gpu, orc, torch, tmp_path_factory):
     ref.close()
     spl = orc.preprocess(soa, cams[-1], W, H, 3.0)
     assert np.array_equal(order, orc.expected_depth_order(spl)), "config 3 orbit depth order differs"
+
+
+def test_big_buckets_camera_cut_reseeds(gpu, orc, torch, tmp_path_factory):
+    """A camera cut above 2M (big buckets): from far behind the scene to close in front, the
+    stale splitters put most items into a few buckets over the 16,384-item capacity; the
+    second launch's global path sorts them (more than n / 8 item-passes), the next frame
+    reseeds from the LSD passes and the one after is bucket-sorted again.  Orders exact."""
+    _, soa = scene_soa(gpu, tmp_path_factory, 2_200_000, 21)
+    n = soa.shape[1]
+    W, H = 640, 480
+    scene = gpu.Scene.from_soa(soa)
+    far_cam = cam_for(gpu, W, H, pos=(0, 0, 40))
+    near_cam = cam_for(gpu, W, H, pos=(0, 0, 1.2), fov=90)
+    r = renderer(gpu)
+    render_frames(gpu, torch, r, scene, [far_cam, far_cam], W, H)
+    assert r.depth_passes() == 0 and r.bucket_sizes().size == 512
+    work0 = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_WORK)
+    render_frames(gpu, torch, r, scene, [near_cam], W, H)          # stale splitters: a spike
+    assert r.depth_passes() == 0
+    spike = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_WORK) - work0
+    assert spike > n // 8, f"the cut sent only {spike} item-passes through the global path"
+    want = orc.expected_depth_order(orc.preprocess(soa, near_cam, W, H, 3.0))
+    assert np.array_equal(r.read_depth_order(n), want)
+    render_frames(gpu, torch, r, scene, [near_cam], W, H)
+    assert r.depth_passes() >= 1, "the spike did not reseed the splitters"
+    render_frames(gpu, torch, r, scene, [near_cam], W, H)
+    assert r.depth_passes() == 0
+    assert np.array_equal(r.read_depth_order(n), want)
+    r.close()
