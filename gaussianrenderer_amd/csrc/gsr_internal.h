@@ -166,16 +166,18 @@ hipError_t launch_bucket_sort(const uint64_t* in, uint64_t* items0, uint64_t* it
 // is empty unless a live item's key saturated to 0xFFFFFFFF), and the row pass then runs
 // with buckets chunks, cstart = totals + buckets (the buckets' first positions) and no count
 // kernel.
-// Big buckets (scenes above 2M Gaussians): kBigBuckets buckets of ~n / 512 items, each sorted
-// by one 1,024-thread workgroup in LDS (up to 16,384 items; larger or wider ones by
-// launch_bucket_sort's local kernel in a second launch).  stage: the scatter writes each tile
-// in bucket order (coalesced records).  groups <= kBigBucketGroups.  No fused row count.
+// Big buckets (scenes above 2M Gaussians): `buckets` (kBigBuckets = 512: ~n / 512 items each,
+// sorted by one 1,024-thread workgroup in LDS, up to 16,384 items; or 1,024: ~n / 1,024 items
+// by 512-thread workgroups, up to 8,192, two per CU) bounded by the previous frame's quantiles;
+// larger or wider-keyed buckets are sorted by launch_bucket_sort's local kernel in a second
+// launch.  The scatter writes each tile in bucket order (coalesced 12-B records).
+// groups <= kBigBucketGroups.  No fused row count.
 constexpr int kBigBuckets = 512;
 constexpr int kBigBucketGroups = 1024;
-hipError_t launch_bucket_sort_big(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int groups,
-                                  const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
+hipError_t launch_bucket_sort_big(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int buckets,
+                                  int groups, const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
                                   const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
-                                  unsigned int* over_host, hipStream_t s, uint4* rec, bool stage);
+                                  unsigned int* over_host, hipStream_t s, uint4* rec);
 // Splitters for launch_bucket_sort from an order the LSD passes sorted (depth_sorted of
 // items0 / items1 under dstats); live_dev (nullable): its visible count.
 hipError_t launch_bkt_splitters(const uint64_t* items0, const uint64_t* items1, const uint32_t* dstats, uint32_t n,

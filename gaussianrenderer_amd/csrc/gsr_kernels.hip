@@ -2585,7 +2585,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
 
 // ---- big buckets (scenes above 2M Gaussians: 512 buckets of ~n / 512 items) ----
 //
-// One 1,024-thread workgroup sorts a bucket of up to kBbCap items in LDS: up to 16 per thread
+// One 1,024-thread workgroup sorts a bucket of up to 16,384 items in LDS: up to 16 per thread
 // (blocked per wave, so a wave's items are consecutive positions; the 16 waves share the
 // bucket evenly, ceil(count / 1,024) rows of 64 each, so all of them work), stable 8-bit LSD passes
 // over key - lo whose exchange carries one u32 per item, slot (original position, 14 bits) |
@@ -2595,22 +2595,22 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_local(uint64_t* __restrict_
 // out coalesced.  Buckets over the capacity or wider than 18 bits are flagged in `left` and
 // sorted by k_bkt_local's paths in a second launch.
 constexpr int kBbThreads = 1024;
-constexpr int kBbItems = 16;
-constexpr uint32_t kBbCap = kBbThreads * kBbItems;     // 16,384
-constexpr int kBbSlot = 14;                             // slot bits of the exchange word
-constexpr int kBbKeyBits = 32 - kBbSlot;                // key bits above lo it carries
-static_assert(kBbCap == 1u << kBbSlot, "slot field");
+constexpr int kBbItems = 16;                            // capacity TH * 16: 16,384 at 1,024 threads
 
-template <int B, bool RA, bool R12>
-__global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__ items, uint32_t* __restrict__ pay,
-                                                          const uint32_t* __restrict__ bstart,
-                                                          const uint32_t* __restrict__ s_in,
-                                                          uint32_t* __restrict__ s_next, uint32_t cap,
-                                                          const uint4* __restrict__ rec, uint32_t* __restrict__ left) {
+// TH threads (1,024: capacity 16,384, one workgroup per CU; 512: 8,192 at half the LDS)
+template <int B, bool RA, bool R12, int TH = kBbThreads>
+__global__ __launch_bounds__(TH) void k_bbk_local(uint64_t* __restrict__ items, uint32_t* __restrict__ pay,
+                                                  const uint32_t* __restrict__ bstart,
+                                                  const uint32_t* __restrict__ s_in,
+                                                  uint32_t* __restrict__ s_next, uint32_t cap,
+                                                  const uint4* __restrict__ rec, uint32_t* __restrict__ left) {
     GSR_GEOM_PRIO();
-    constexpr int NW = kBbThreads / 64;
-    __shared__ uint32_t s_buf[kBbCap];                  // the exchange, then the rect pull, then the keys
-    __shared__ uint32_t s_idx[kBbCap];                  // the indices by slot
+    constexpr int NW = TH / 64;
+    constexpr uint32_t kCap = (uint32_t)TH * kBbItems;
+    constexpr int kBbSlot = __builtin_ctz(kCap);        // slot bits of the exchange word
+    constexpr int kBbKeyBits = 32 - kBbSlot;            // key bits above lo it carries
+    __shared__ uint32_t s_buf[kCap];                    // the exchange, then the rect pull, then the keys
+    __shared__ uint32_t s_idx[kCap];                    // the indices by slot
     __shared__ uint32_t s_wc[NW][256];                  // per-wave digit counts, then their wave prefixes
     __shared__ uint32_t s_db[256];                      // the digits' first positions
     __shared__ uint32_t s_scr[NW], s_mm[2];
@@ -2628,7 +2628,7 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
         if (t == 0) left[bkt] = 0u;
         return;
     }
-    if (count > min(cap, kBbCap)) {
+    if (count > min(cap, kCap)) {
         if (t == 0) left[bkt] = 1u;
         return;
     }
@@ -2686,7 +2686,7 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
     const int bits = span ? 32 - __clz((int)span) : 0;   // the passes: the bits the keys span
     for (int shift = 0; shift < bits; shift += 8) {   // uniform
         auto digit = [&](int k) { return (x[k] >> (kBbSlot + shift)) & 0xffu; };
-        for (uint32_t j = t; j < (uint32_t)NW * 256u; j += kBbThreads) (&s_wc[0][0])[j] = 0;
+        for (uint32_t j = t; j < (uint32_t)NW * 256u; j += TH) (&s_wc[0][0])[j] = 0;
         __syncthreads();
         uint32_t rk[kBbItems];
 #pragma unroll
@@ -2753,7 +2753,7 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
     for (int k = 0; k < kBbItems; k++) {
         const uint32_t el = wbase + k * 64 + lane;
         if (k < (int)kk && el < count) {
-            const uint32_t slot = x[k] & (kBbCap - 1u);
+            const uint32_t slot = x[k] & (kCap - 1u);
             rct[k] = s_buf[slot];
             seg[el] = ((uint64_t)(kmin + (x[k] >> kBbSlot)) << 32) | s_idx[slot];
         }
@@ -2769,7 +2769,7 @@ __global__ __launch_bounds__(kBbThreads) void k_bbk_local(uint64_t* __restrict__
     }
     __syncthreads();
     if (bkt < (uint32_t)B - 1u)
-        bkt_write_splitters<B, kBbThreads>(start, count, live, s_next, [&](uint32_t q) { return s_buf[q]; });
+        bkt_write_splitters<B, TH>(start, count, live, s_next, [&](uint32_t q) { return s_buf[q]; });
 }
 
 // Splitters from a depth order the LSD passes sorted (a context's first frame, or the
@@ -4460,51 +4460,51 @@ hipError_t launch_bucket_sort(const uint64_t* in, uint64_t* items0, uint64_t* it
     return hipGetLastError();
 }
 
-hipError_t launch_bucket_sort_big(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int groups,
-                                  const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
-                                  const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
-                                  unsigned int* over_host, hipStream_t s, uint4* rec, bool stage) {
-    constexpr int B = kBigBuckets;
-    if (groups < 1 || groups > kBigBucketGroups || (int64_t)groups * B > 256 * (int64_t)kMaxSortGroups || cap < 1 ||
-        in == items0 || !rect || !pay0 || !pay1 || !rec)
-        return hipErrorInvalidValue;
-    if (n == 0) return hipSuccess;
+// B buckets, sorted by TH-thread workgroups (512 / 1,024 or 1,024 / 512).  The scatter's tile
+// is staged (bucket runs written coalesced), barrier-lean (52.0 -> 50.2 us at config 3 orbit)
+// and writes 12-B records (16-B: 51.7 -> 50.5 us); the eight-barrier tile, 16-B records and
+// the unstaged scatter measured slower (profiles/r06k_big_buckets_c3_orbit.txt, DESIGN.md
+// section 3).
+template <int B, int TH>
+static void bucket_sort_big_b(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int groups,
+                              const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
+                              const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
+                              unsigned int* over_host, hipStream_t s, uint4* rec) {
     uint32_t* bstart = totals + B;          // B + 2 words after the totals
     uint32_t* left = totals + 2 * B + 2;    // per bucket: k_bbk_local left it to k_bkt_local
     const RowHist none{nullptr, B, 0};
     hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist);
     hipLaunchKernelGGL((k_bkt_scan_w<B, kBigBucketGroups>), dim3(B / 4), dim3(256), 0, s, hist, groups, totals);
-    // the barrier-lean staged tile (k_bkt_scatter LEAN: 52.0 -> 50.2 us at config 3 orbit);
-    // GSR_BB_LEAN=0 for the eight-barrier tile (A/B)
-    static const bool lean = [] { const char* e = std::getenv("GSR_BB_LEAN"); return !e || e[0] != '0'; }();
-    // staged: 12-B records (GSR_BB_REC16=1 for the 16-B records, A/B)
-    static const bool rec16 = [] { const char* e = std::getenv("GSR_BB_REC16"); return e && e[0] == '1'; }();
-    auto run2 = [&](auto ra, auto r12) {
-        constexpr bool RA = decltype(ra)::value, R12 = decltype(r12)::value;
-        if (stage && lean)
-            hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, true, kBktTile, 1, R12, true>), dim3(groups), dim3(512), 0, s,
-                               in, items0, n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0,
-                               bstart, rec);
-        else if (stage)
-            hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, true, kBktTile, 1, R12>), dim3(groups), dim3(512), 0, s, in,
-                               items0, n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart,
-                               rec);
-        else
-            hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, false, kBktTile, 1, R12>), dim3(groups), dim3(512), 0, s, in,
-                               items0, n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart,
-                               rec);
-        hipLaunchKernelGGL((k_bbk_local<B, RA, R12>), dim3(B - 1), dim3(kBbThreads), 0, s, items0, pay0,
-                           static_cast<const uint32_t*>(bstart), s_in, s_out, cap, static_cast<const uint4*>(rec), left);
-        hipLaunchKernelGGL((k_bkt_local<B, RA, R12>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0, pay1,
-                           bstart, s_in, s_out, min(cap, kBktCap), over_host, none, static_cast<const uint4*>(rec),
-                           static_cast<const uint32_t*>(left));
-    };
     auto run = [&](auto ra) {
-        if (stage && !rec16) run2(ra, std::true_type{});
-        else run2(ra, std::false_type{});
+        constexpr bool RA = decltype(ra)::value;
+        hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, true, kBktTile, 1, true, true>), dim3(groups), dim3(512), 0, s,
+                           in, items0, n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart,
+                           rec);
+        hipLaunchKernelGGL((k_bbk_local<B, RA, true, TH>), dim3(B - 1), dim3(TH), 0, s, items0, pay0,
+                           static_cast<const uint32_t*>(bstart), s_in, s_out, cap, static_cast<const uint4*>(rec), left);
+        hipLaunchKernelGGL((k_bkt_local<B, RA, true>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0,
+                           pay1, bstart, s_in, s_out, min(cap, kBktCap), over_host, none,
+                           static_cast<const uint4*>(rec), static_cast<const uint32_t*>(left));
     };
     if (rank_atomic) run(std::true_type{});
     else run(std::false_type{});
+}
+
+hipError_t launch_bucket_sort_big(const uint64_t* in, uint64_t* items0, uint64_t* items1, uint32_t n, int buckets,
+                                  int groups, const uint32_t* s_in, uint32_t* s_out, uint32_t* hist, uint32_t* totals,
+                                  const uint32_t* rect, uint32_t* pay0, uint32_t* pay1, bool rank_atomic, uint32_t cap,
+                                  unsigned int* over_host, hipStream_t s, uint4* rec) {
+    if ((buckets != 512 && buckets != 1024) || groups < 1 || groups > kBigBucketGroups ||
+        (int64_t)groups * buckets > 256 * (int64_t)kMaxSortGroups || cap < 1 || in == items0 || !rect || !pay0 ||
+        !pay1 || !rec)
+        return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    if (buckets == 512)
+        bucket_sort_big_b<512, 1024>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1,
+                                     rank_atomic, cap, over_host, s, rec);
+    else
+        bucket_sort_big_b<1024, 512>(in, items0, items1, n, groups, s_in, s_out, hist, totals, rect, pay0, pay1,
+                                     rank_atomic, cap, over_host, s, rec);
     return hipGetLastError();
 }
 

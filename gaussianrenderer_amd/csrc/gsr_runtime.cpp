@@ -522,7 +522,12 @@ int bkt_count(int64_t n) {
 constexpr int64_t kBucketSortMaxN = (int64_t)2048 * 1024;
 bool bkt_applies(const gsr_context* c, int64_t n) { return n > 0 && c->bucket_sort != 0; }
 bool bkt_big(const gsr_context* c, int64_t n) { return c->bucket_sort != 3 && n > kBucketSortMaxN; }
-int bkt_count(const gsr_context* c, int64_t n) { return bkt_big(c, n) ? gsr::kBigBuckets : bkt_count(n); }
+// A/B: GSR_BIG_BUCKETS=1024 sorts 1,024 big buckets with 512-thread workgroups
+int big_bucket_count() {
+    static const int b = [] { const char* e = std::getenv("GSR_BIG_BUCKETS"); return e && std::atoi(e) == 1024 ? 1024 : gsr::kBigBuckets; }();
+    return b;
+}
+int bkt_count(const gsr_context* c, int64_t n) { return bkt_big(c, n) ? big_bucket_count() : bkt_count(n); }
 
 // Row items per column-pass chunk (GSR_TUNE_COL_CHUNK 0): 1,024 up to the same 2M
 // Gaussians (config 2: column scatter 26.0 -> 21.6 us, chain -2 us), 2,048 above (config 3:
@@ -1065,16 +1070,15 @@ static int depth_sort_locked(gsr_context* c, bool with_rects, bool plain = false
         if (bkt_big(c, c->n)) {
             // 512 buckets of ~n / 512 items, four 2,048-item tiles per scatter workgroup; the row
             // pass counts for itself (its 2,048-source chunks are cheaper than bucket chunks)
-            static const bool stage = [] { const char* e = std::getenv("GSR_BKT_STAGE"); return !e || e[0] != '0'; }();
             static const int g_env = [] { const char* e = std::getenv("GSR_BB_GROUPS"); return e ? std::atoi(e) : 0; }();
             const int G = std::min(g_env > 0 ? g_env : groups_for(c->n, 4 * gsr::kMaxBucketCap), gsr::kBigBucketGroups);
             uint32_t* s_in = c->bkt_split + (size_t)c->bkt_par * gsr::kMaxBuckets;
             uint32_t* s_out = c->bkt_split + (size_t)(c->bkt_par ^ 1) * gsr::kMaxBuckets;
-            HIP_TRY(gsr::launch_bucket_sort_big(c->pre_out, c->items[0], c->items[1], n, G, s_in, s_out, c->hist,
+            HIP_TRY(gsr::launch_bucket_sort_big(c->pre_out, c->items[0], c->items[1], n, B, G, s_in, s_out, c->hist,
                                                 c->totals, reinterpret_cast<const uint32_t*>(c->rect), pay_buf(c, 0),
                                                 pay_buf(c, 1), rank_atomic_on(c), c->bucket_sort == 2 ? 64u : 16384u,
                                                 c->hstats_dev ? &c->hstats_dev->bkt_over : nullptr, c->stream,
-                                                c->bkt_rec, stage));
+                                                c->bkt_rec));
             c->bkt_rows_fused = false;
             c->bkt_par ^= 1;
             c->last_bds = true;

@@ -29,6 +29,11 @@ def torch(gpu):
     return t
 
 
+# big buckets above 2M: 512 (default) or 1,024 (A/B env GSR_BIG_BUCKETS=1024), and their capacity
+BIG = 1024 if os.environ.get("GSR_BIG_BUCKETS") == "1024" else 512
+BIG_CAP = 16384 * 512 // BIG
+
+
 def render_frames(gpu, torch, r, scene, cams, W, H):
     """Render each camera on r (re-rendered after an overflow); returns the last image."""
     out = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
@@ -449,7 +454,7 @@ def test_big_buckets(gpu, orc, torch, tmp_path_factory, hook):
     img = render_frames(gpu, torch, r, scene, cams, W, H)
     assert r.depth_passes() == 0
     sizes = r.bucket_sizes()
-    assert sizes is not None and sizes.size == 512 and int(sizes.sum()) == n
+    assert sizes is not None and sizes.size == BIG and int(sizes.sum()) == n
     over = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER)
     if hook == 2:
         assert over > n // 2
@@ -493,7 +498,7 @@ def test_bucket_kind_by_size(gpu, orc, torch, tmp_path_factory):
     scene = gpu.Scene.from_soa(soa)
     cam = cam_for(gpu, W, H)
     want = orc.expected_depth_order(orc.preprocess(soa, cam, W, H, 3.0))
-    for knob, buckets in ((1, 512), (3, gpu.MAX_BUCKETS)):
+    for knob, buckets in ((1, BIG), (3, gpu.MAX_BUCKETS)):
         r = renderer(gpu, knob)
         render_frames(gpu, torch, r, scene, [cam] * 2, W, H)
         assert r.depth_passes() == 0
@@ -519,8 +524,8 @@ def test_big_buckets_config3_orbit(gpu, orc, torch, tmp_path_factory):
     img = render_frames(gpu, torch, r, scene, cams, W, H)
     assert r.depth_passes() == 0
     sizes = r.bucket_sizes()
-    assert sizes.size == 512 and int(sizes.sum()) == n
-    assert int(sizes[:-1].max()) <= 16384, int(sizes[:-1].max())
+    assert sizes.size == BIG and int(sizes.sum()) == n
+    assert int(sizes[:-1].max()) <= BIG_CAP, int(sizes[:-1].max())
     assert r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_OVER) == over0
     order, pairs = r.read_depth_order(n), r.read_pairs()
     r.close()
@@ -548,7 +553,7 @@ def test_big_buckets_camera_cut_reseeds(gpu, orc, torch, tmp_path_factory):
     near_cam = cam_for(gpu, W, H, pos=(0, 0, 1.2), fov=90)
     r = renderer(gpu)
     render_frames(gpu, torch, r, scene, [far_cam, far_cam], W, H)
-    assert r.depth_passes() == 0 and r.bucket_sizes().size == 512
+    assert r.depth_passes() == 0 and r.bucket_sizes().size == BIG
     work0 = r.get_tuning(gpu.TUNE_DEPTH_BUCKETS_WORK)
     render_frames(gpu, torch, r, scene, [near_cam], W, H)          # stale splitters: a spike
     assert r.depth_passes() == 0
