@@ -1822,7 +1822,8 @@ __device__ __forceinline__ void bkt_of_n(const uint32_t* s_T, const uint32_t (&k
 template <int B>
 __global__ __launch_bounds__(kBktThreads) void k_bkt_count(const uint64_t* __restrict__ in, uint32_t n,
                                                            const uint32_t* __restrict__ splitters, int groups,
-                                                           uint32_t* __restrict__ hist) {
+                                                           uint32_t* __restrict__ hist,
+                                                           uint16_t* __restrict__ bid = nullptr) {
     GSR_GEOM_PRIO();
     __shared__ uint32_t s_S[B], s_h[B];
     const uint32_t t = threadIdx.x, lane = t & 63u;
@@ -1854,6 +1855,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_count(const uint64_t* __res
             const bool d = key[k] == 0xffffffffu;
             dead += (uint32_t)__popcll(__ballot(d && i < e));
             if (!d) atomicAdd(&s_h[bk[k]], 1u);
+            if (bid && i < e) bid[i] = (uint16_t)bk[k];   // the scatter reads it instead of searching again
         }
         if (i0 + kBktTile < e) {
 #pragma unroll
@@ -1985,7 +1987,7 @@ __device__ __forceinline__ void rec_put(uint4* __restrict__ rec, uint32_t q, uin
 // lanes of a store that hold items of one bucket write consecutive records (a run per bucket
 // and tile: ~4 items at 512 buckets) instead of one store request each.
 template <int B, bool RA, int TH, bool STAGE = false, uint32_t TILE = kBktTile, int WPE = 1, bool R12 = false,
-          bool LEAN = false>
+          bool LEAN = false, bool BID = false>
 __global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(WPE))) void k_bkt_scatter(const uint64_t* __restrict__ in,
                                                              uint64_t* __restrict__ out, uint32_t n,
                                                              const uint32_t* __restrict__ splitters, int groups,
@@ -1994,7 +1996,8 @@ __global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                                                              const uint32_t* __restrict__ rect,
                                                              uint32_t* __restrict__ pay_out,
                                                              uint32_t* __restrict__ bstart,
-                                                             uint4* __restrict__ rec) {
+                                                             uint4* __restrict__ rec,
+                                                             const uint16_t* __restrict__ bid) {
     GSR_GEOM_PRIO();
     constexpr int NW = TH / 64, kIt = TILE / TH;  // waves; items per thread
     constexpr uint32_t kW = B / 2;                      // packed counter words per wave
@@ -2020,19 +2023,21 @@ __global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     chunk_range(n, groups, chunk, kBktTile, b, e);   // chunks as k_bkt_count's
     const uint32_t wbase = w * 64 * kIt;
     uint64_t it[kIt];
-    uint32_t pv[kIt];
-    auto load = [&](uint64_t tb, uint32_t tn, uint64_t (&ii)[kIt], uint32_t (&pp)[kIt]) {
+    uint32_t pv[kIt], bv[kIt];
+    // BID: the count kernel's bucket of every item (bid), loaded with the tile
+    auto load = [&](uint64_t tb, uint32_t tn, uint64_t (&ii)[kIt], uint32_t (&pp)[kIt], uint32_t (&bb)[kIt]) {
 #pragma unroll
         for (int k = 0; k < kIt; k++) {
             const uint32_t el = wbase + k * 64 + lane;
             ii[k] = el < tn ? in[tb + el] : ~0ull;
             pp[k] = el < tn ? rect[tb + el] : 0u;   // the input is the preprocess order: rect by position
+            if (BID) bb[k] = el < tn ? (uint32_t)bid[tb + el] : (uint32_t)B - 1u;
         }
     };
     // the first tile's items and rects, the splitters, the bucket totals and this chunk's
     // histogram row are all loaded in one memory round trip
-    load(b, (uint32_t)min((uint64_t)TILE, e - b), it, pv);
-    bkt_load_splitters<B, TH>(s_S, splitters);
+    load(b, (uint32_t)min((uint64_t)TILE, e - b), it, pv, bv);
+    if (!BID) bkt_load_splitters<B, TH>(s_S, splitters);
     {   // this chunk's first slot in every bucket: the bucket's start + the earlier chunks' items
         uint32_t loc[kPer], hrow[kPer], sum = 0;
 #pragma unroll
@@ -2061,8 +2066,8 @@ __global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const uint32_t tn = (uint32_t)min((uint64_t)TILE, e - tb);
         const bool more = tb + TILE < e;   // uniform
         uint64_t nit[kIt];
-        uint32_t npv[kIt];
-        if (more) load(tb + TILE, (uint32_t)min((uint64_t)TILE, e - tb - TILE), nit, npv);
+        uint32_t npv[kIt], nbv[kIt];
+        if (more) load(tb + TILE, (uint32_t)min((uint64_t)TILE, e - tb - TILE), nit, npv, nbv);
         if (!kLean) {
             for (uint32_t j = t; j < NW * kW; j += TH) (&s_wc[0][0])[j] = 0;
             __syncthreads();
@@ -2070,7 +2075,12 @@ __global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         uint32_t dg[kIt], rk[kIt], keys[kIt];
 #pragma unroll
         for (int k = 0; k < kIt; k++) keys[k] = (uint32_t)(it[k] >> 32);
-        bkt_of_n<B>(s_S, keys, dg);   // a key 0xFFFFFFFF (culled) counts every splitter: bucket B - 1
+        if (BID) {
+#pragma unroll
+            for (int k = 0; k < kIt; k++) dg[k] = bv[k];
+        } else {
+            bkt_of_n<B>(s_S, keys, dg);   // a key 0xFFFFFFFF (culled) counts every splitter: bucket B - 1
+        }
         // culled items (the last bucket) rank by ballot against a running wave count, so the
         // live items' returning atomics have no LDS read between them and stay in flight together
         uint32_t dead_run = 0;
@@ -2208,6 +2218,7 @@ __global__ __launch_bounds__(TH) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             for (int k = 0; k < kIt; k++) {
                 it[k] = nit[k];
                 pv[k] = npv[k];
+                if (BID) bv[k] = nbv[k];
             }
         }
         __syncthreads();
@@ -4391,7 +4402,8 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
     const RowHist rh{row_tiles_y > 0 ? hist : nullptr, B, row_tiles_y};
     const int local_grid = row_tiles_y > 0 ? B : B - 1;
     uint32_t* bstart = totals + B;   // B + 2 words after the totals
-    hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist);
+    hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist,
+                       static_cast<uint16_t*>(nullptr));
     hipLaunchKernelGGL(k_bkt_scan<B>, dim3(B / 64), dim3(1024), 0, s, hist, groups, totals);
     constexpr int kScTh = B >= 512 ? 512 : kBktThreads;   // k_bkt_scatter's workgroup size
     // A/B: GSR_BKT_SCATTER_256=1 runs the 4,096-bucket scatter in 256-thread workgroups (64 KB of
@@ -4403,7 +4415,8 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
         auto run = [&](auto ra) {
             constexpr bool RA = decltype(ra)::value;
             hipLaunchKernelGGL((k_bkt_scatter<B, RA, kScTh, true>), dim3(groups), dim3(kScTh), 0, s, in, items0, n,
-                               s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
+                               s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec,
+                               static_cast<const uint16_t*>(nullptr));
             hipLaunchKernelGGL((k_bkt_local<B, RA>), dim3(local_grid), dim3(kBktThreads), 0, s, items0, items1, pay0,
                                pay1, bstart, s_in, s_out, cap, over_host, rh, static_cast<const uint4*>(rec));
         };
@@ -4414,10 +4427,12 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
     if (B == 4096 && sc256) {
         if (rank_atomic)
             hipLaunchKernelGGL((k_bkt_scatter<B, true, kBktThreads>), dim3(groups), dim3(kBktThreads), 0, s, in, items0,
-                               n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
+                               n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec,
+                               static_cast<const uint16_t*>(nullptr));
         else
             hipLaunchKernelGGL((k_bkt_scatter<B, false, kBktThreads>), dim3(groups), dim3(kBktThreads), 0, s, in, items0,
-                               n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
+                               n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec,
+                               static_cast<const uint16_t*>(nullptr));
         if (rank_atomic)
             hipLaunchKernelGGL((k_bkt_local<B, true>), dim3(local_grid), dim3(kBktThreads), 0, s, items0, items1, pay0,
                                pay1, bstart, s_in, s_out, cap, over_host, rh, static_cast<const uint4*>(rec));
@@ -4428,12 +4443,14 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
     }
     if (rank_atomic) {
         hipLaunchKernelGGL((k_bkt_scatter<B, true, kScTh>), dim3(groups), dim3(kScTh), 0, s, in, items0, n, s_in,
-                           groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
+                           groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec,
+                               static_cast<const uint16_t*>(nullptr));
         hipLaunchKernelGGL((k_bkt_local<B, true>), dim3(local_grid), dim3(kBktThreads), 0, s, items0, items1, pay0,
                            pay1, bstart, s_in, s_out, cap, over_host, rh, static_cast<const uint4*>(rec));
     } else {
         hipLaunchKernelGGL((k_bkt_scatter<B, false, kScTh>), dim3(groups), dim3(kScTh), 0, s, in, items0, n, s_in,
-                           groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec);
+                           groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec,
+                               static_cast<const uint16_t*>(nullptr));
         hipLaunchKernelGGL((k_bkt_local<B, false>), dim3(local_grid), dim3(kBktThreads), 0, s, items0, items1, pay0,
                            pay1, bstart, s_in, s_out, cap, over_host, rh, static_cast<const uint4*>(rec));
     }
@@ -4473,13 +4490,22 @@ static void bucket_sort_big_b(const uint64_t* in, uint64_t* items0, uint64_t* it
     uint32_t* bstart = totals + B;          // B + 2 words after the totals
     uint32_t* left = totals + 2 * B + 2;    // per bucket: k_bbk_local left it to k_bkt_local
     const RowHist none{nullptr, B, 0};
-    hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist);
+    // the count hands each item's bucket to the scatter (u16 in pay1, free until the second
+    // launch), which then skips its own splitter search (GSR_BB_BID=0: it searches, A/B)
+    static const bool bids = [] { const char* e = std::getenv("GSR_BB_BID"); return !e || e[0] != '0'; }();
+    uint16_t* bid = bids ? reinterpret_cast<uint16_t*>(pay1) : nullptr;
+    hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist, bid);
     hipLaunchKernelGGL((k_bkt_scan_w<B, kBigBucketGroups>), dim3(B / 4), dim3(256), 0, s, hist, groups, totals);
     auto run = [&](auto ra) {
         constexpr bool RA = decltype(ra)::value;
-        hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, true, kBktTile, 1, true, true>), dim3(groups), dim3(512), 0, s,
-                           in, items0, n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0, bstart,
-                           rec);
+        if (bids)
+            hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, true, kBktTile, 1, true, true, true>), dim3(groups), dim3(512),
+                               0, s, in, items0, n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect,
+                               pay0, bstart, rec, static_cast<const uint16_t*>(bid));
+        else
+            hipLaunchKernelGGL((k_bkt_scatter<B, RA, 512, true, kBktTile, 1, true, true>), dim3(groups), dim3(512), 0,
+                               s, in, items0, n, s_in, groups, hist, static_cast<const uint32_t*>(totals), rect, pay0,
+                               bstart, rec, static_cast<const uint16_t*>(nullptr));
         hipLaunchKernelGGL((k_bbk_local<B, RA, true, TH>), dim3(B - 1), dim3(TH), 0, s, items0, pay0,
                            static_cast<const uint32_t*>(bstart), s_in, s_out, cap, static_cast<const uint4*>(rec), left);
         hipLaunchKernelGGL((k_bkt_local<B, RA, true>), dim3(B - 1), dim3(kBktThreads), 0, s, items0, items1, pay0,
