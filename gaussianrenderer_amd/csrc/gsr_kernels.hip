@@ -4402,15 +4402,18 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
     const RowHist rh{row_tiles_y > 0 ? hist : nullptr, B, row_tiles_y};
     const int local_grid = row_tiles_y > 0 ? B : B - 1;
     uint32_t* bstart = totals + B;   // B + 2 words after the totals
-    hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist,
-                       static_cast<uint16_t*>(nullptr));
-    hipLaunchKernelGGL(k_bkt_scan<B>, dim3(B / 64), dim3(1024), 0, s, hist, groups, totals);
     constexpr int kScTh = B >= 512 ? 512 : kBktThreads;   // k_bkt_scatter's workgroup size
     // A/B: GSR_BKT_SCATTER_256=1 runs the 4,096-bucket scatter in 256-thread workgroups (64 KB of
     // LDS instead of 96: two workgroups per CU)
     static const bool sc256 = [] { const char* e = std::getenv("GSR_BKT_SCATTER_256"); return e && e[0] == '1'; }();
     // A/B: GSR_BKT_STAGE_SMALL=1 writes each scatter tile in bucket order here too
     static const bool stage = [] { const char* e = std::getenv("GSR_BKT_STAGE_SMALL"); return e && e[0] == '1'; }();
+    // A/B: GSR_BKT_BID=1 hands each item's bucket from the count to the scatter (big buckets' scheme)
+    static const bool bids = [] { const char* e = std::getenv("GSR_BKT_BID"); return e && e[0] == '1'; }();
+    const bool bid_on = bids && !stage && !(B == 4096 && sc256);
+    uint16_t* bid = bid_on ? reinterpret_cast<uint16_t*>(pay1) : nullptr;
+    hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist, bid);
+    hipLaunchKernelGGL(k_bkt_scan<B>, dim3(B / 64), dim3(1024), 0, s, hist, groups, totals);
     if (stage) {
         auto run = [&](auto ra) {
             constexpr bool RA = decltype(ra)::value;
@@ -4439,6 +4442,20 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
         else
             hipLaunchKernelGGL((k_bkt_local<B, false>), dim3(local_grid), dim3(kBktThreads), 0, s, items0, items1, pay0,
                                pay1, bstart, s_in, s_out, cap, over_host, rh, static_cast<const uint4*>(rec));
+        return;
+    }
+    if (bid_on) {
+        auto run = [&](auto ra) {
+            constexpr bool RA = decltype(ra)::value;
+            hipLaunchKernelGGL((k_bkt_scatter<B, RA, kScTh, false, kBktTile, 1, false, false, true>), dim3(groups),
+                               dim3(kScTh), 0, s, in, items0, n, s_in, groups, hist,
+                               static_cast<const uint32_t*>(totals), rect, pay0, bstart, rec,
+                               static_cast<const uint16_t*>(bid));
+            hipLaunchKernelGGL((k_bkt_local<B, RA>), dim3(local_grid), dim3(kBktThreads), 0, s, items0, items1, pay0,
+                               pay1, bstart, s_in, s_out, cap, over_host, rh, static_cast<const uint4*>(rec));
+        };
+        if (rank_atomic) run(std::true_type{});
+        else run(std::false_type{});
         return;
     }
     if (rank_atomic) {
