@@ -1946,6 +1946,47 @@ __global__ __launch_bounds__(256) void k_bkt_scan_w(uint32_t* __restrict__ hist,
     }
 }
 
+// Big buckets (A/B, GSR_BB_SCANG=1): 16 buckets per 1,024-thread workgroup, each wave's four
+// 16-lane quarters reading a 64-B row segment of four different chunks (64 chunk slices per
+// workgroup), the slices' sums combined in LDS.  B / 16 workgroups.
+template <int B, int MAXG>
+__global__ __launch_bounds__(1024) void k_bkt_scan_g(uint32_t* __restrict__ hist, int groups,
+                                                     uint32_t* __restrict__ totals) {
+    GSR_GEOM_PRIO();
+    constexpr int kPerMax = (MAXG + 63) / 64;
+    __shared__ uint32_t s_part[64][16];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t bl = lane & 15u, sl = w * 4u + (lane >> 4);   // bucket in the group, chunk slice
+    const uint32_t b = blockIdx.x * 16u + bl;
+    const uint32_t per = ((uint32_t)groups + 63u) / 64u;
+    const uint32_t g0 = sl * per;
+    uint32_t v[kPerMax], sum = 0;
+#pragma unroll
+    for (int i = 0; i < kPerMax; i++) {
+        const uint32_t g = g0 + (uint32_t)i;
+        v[i] = (uint32_t)i < per && g < (uint32_t)groups ? hist[(size_t)g * B + b] : 0u;
+        sum += v[i];
+    }
+    s_part[sl][bl] = sum;
+    __syncthreads();
+    uint32_t run = 0, tot = 0;
+    for (uint32_t k = 0; k < 64u; k++) {
+        const uint32_t p = s_part[k][bl];
+        run += k < sl ? p : 0u;
+        tot += p;
+    }
+    if (sl == 0) totals[b] = tot;
+    if (blockIdx.x == 0 && t == 0) totals[2 * B + 1] = 0u;   // bkt_sat_word (as k_bkt_scan)
+#pragma unroll
+    for (int i = 0; i < kPerMax; i++) {
+        const uint32_t g = g0 + (uint32_t)i;
+        if ((uint32_t)i < per && g < (uint32_t)groups) {
+            hist[(size_t)g * B + b] = run;
+            run += v[i];
+        }
+    }
+}
+
 // 16-bit half h of the packed counter word v.
 __device__ __forceinline__ uint32_t half16(uint32_t v, uint32_t h) { return (v >> (16u * h)) & 0xffffu; }
 
@@ -4413,7 +4454,12 @@ static void bucket_sort_b(const uint64_t* in, uint64_t* items0, uint64_t* items1
     const bool bid_on = bids && !stage && !(B == 4096 && sc256);
     uint16_t* bid = bid_on ? reinterpret_cast<uint16_t*>(pay1) : nullptr;
     hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist, bid);
-    hipLaunchKernelGGL(k_bkt_scan<B>, dim3(B / 64), dim3(1024), 0, s, hist, groups, totals);
+    // A/B: GSR_BKT_SCANG=1 scans 16 buckets per workgroup over 64 chunk slices (the big buckets' scan)
+    static const bool scang = [] { const char* e = std::getenv("GSR_BKT_SCANG"); return e && e[0] == '1'; }();
+    if (scang)
+        hipLaunchKernelGGL((k_bkt_scan_g<B, kBktMaxGroups>), dim3(B / 16), dim3(1024), 0, s, hist, groups, totals);
+    else
+        hipLaunchKernelGGL(k_bkt_scan<B>, dim3(B / 64), dim3(1024), 0, s, hist, groups, totals);
     if (stage) {
         auto run = [&](auto ra) {
             constexpr bool RA = decltype(ra)::value;
@@ -4512,7 +4558,13 @@ static void bucket_sort_big_b(const uint64_t* in, uint64_t* items0, uint64_t* it
     static const bool bids = [] { const char* e = std::getenv("GSR_BB_BID"); return !e || e[0] != '0'; }();
     uint16_t* bid = bids ? reinterpret_cast<uint16_t*>(pay1) : nullptr;
     hipLaunchKernelGGL(k_bkt_count<B>, dim3(groups), dim3(kBktThreads), 0, s, in, n, s_in, groups, hist, bid);
-    hipLaunchKernelGGL((k_bkt_scan_w<B, kBigBucketGroups>), dim3(B / 4), dim3(256), 0, s, hist, groups, totals);
+    // chunk scan: 16 buckets per workgroup over 64 chunk slices (5.9 vs 8.5 us for a wave per
+    // bucket at config 3, profiles/r06sg_kt_big_bucket_scan.txt); GSR_BB_SCANG=0 for the latter
+    static const bool scang = [] { const char* e = std::getenv("GSR_BB_SCANG"); return !e || e[0] != '0'; }();
+    if (scang)
+        hipLaunchKernelGGL((k_bkt_scan_g<B, kBigBucketGroups>), dim3(B / 16), dim3(1024), 0, s, hist, groups, totals);
+    else
+        hipLaunchKernelGGL((k_bkt_scan_w<B, kBigBucketGroups>), dim3(B / 4), dim3(256), 0, s, hist, groups, totals);
     auto run = [&](auto ra) {
         constexpr bool RA = decltype(ra)::value;
         if (bids)
